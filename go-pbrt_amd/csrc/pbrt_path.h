@@ -1,0 +1,711 @@
+// pbrt_path.h — device implementation of go-pbrt's per-path inner loop.
+//
+// One call of path_li() is one Path.Li (pkg/integrator/path.go:32-157);
+// direct_li() is DirectLighting.Li (pkg/integrator/directlighting.go:62-104).
+// Everything below them — BVH traversal (pkg/accelerator/bvh.go:659-765),
+// TransformedPrimitive/GeometricPrimitive (pkg/pbrt/primitive.go:42-115),
+// Sphere (pkg/pbrt/sphere.go) and Disk (pkg/shapes/disk.go) intersection,
+// Matte/Lambertian BSDF (pkg/materials/matte.go, pkg/pbrt/reflection.go),
+// lights (pkg/lights), UniformSampleOneLight / EstimateDirect
+// (pkg/pbrt/integrator.go:23-195) and the Stratified/PCG32 sampler
+// (pkg/sampler, pkg/pbrt/rng.go) — is restated in float64 with the
+// reference's evaluation order and every parity-ledger quirk.
+//
+// Reference panics (EFloat Check, Ld > 10, BVH stack overflow) set
+// Thread::panic; the caller stops the tile and reports PBRT_E_REF_PANIC.
+#pragma once
+#pragma clang fp contract(off)
+
+#include "pbrt_core.h"
+
+namespace pbrt {
+
+// ----------------------------------------------------------------- scene view
+struct DevScene {
+    const pbrt_shape_desc* shapes;
+    const pbrt_material_desc* materials;
+    const pbrt_primitive_desc* prims;
+    const pbrt_bvh_node* nodes;
+    const pbrt_light_desc* lights;
+    const pbrt_camera_desc* camera;
+    const pbrt_film_desc* film;
+    const pbrt_distribution_desc* dist;   // Path light distribution (may be null)
+    int n_prims, n_nodes, n_lights, pad;
+};
+
+// ---------------------------------------------------------------- PCG32 (rng.go)
+struct Pcg {
+    uint64_t state, inc;
+};
+__device__ __forceinline__ uint32_t pcg_next(Pcg& r) {
+    uint64_t old = r.state;
+    r.state = old * 0x5851f42d4c957f2dULL + r.inc;
+    uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
+    uint32_t rot = (uint32_t)(old >> 59);
+    return (xs >> rot) | (xs << ((rot + 1u) & 31u));   // (rot+1)&31, parity ledger #1
+}
+__device__ __forceinline__ void pcg_seed(Pcg& r, uint64_t seed) {   // rng.go:28-34
+    r.state = 0;
+    r.inc = (seed << 1) | 1;
+    pcg_next(r);
+    r.state += 0x853c49e6748fea9bULL;
+    pcg_next(r);
+}
+__device__ __forceinline__ uint32_t pcg_bounded(Pcg& r, uint32_t b) {   // rng.go:44-53
+    uint32_t threshold = (~b + 1u) % b;
+    for (;;) {
+        uint32_t v = pcg_next(r);
+        if (v >= threshold) return v % b;
+    }
+}
+__device__ __forceinline__ double pcg_float(Pcg& r) {   // rng.go:55-57
+    return gomath::min(gomath::kOneMinusEpsilon, (double)pcg_next(r) * 2.3283064365386963e-10);
+}
+
+// ------------------------------------------------------------ per-thread state
+struct Thread {
+    Pcg rng;
+    int32_t spp, ndims, xs, ys, jitter;
+    int32_t sample_index, cur1d, cur2d;
+    double* s1d;              // ndims * spp shuffled stratified values (scratch)
+    uint16_t* stack;          // BVH traversal stack column in LDS (stride kStackStride)
+    int panic;                // PBRT_PANIC_* (sticky)
+    int bounce;
+    uint64_t closest_rays, shadow_rays;
+};
+constexpr int kStackStride = 64;   // one 64-lane wave per workgroup
+
+// Stratified.StartPixel (stratified.go:21-48; sampling.go:101-145)
+__device__ inline void start_pixel(Thread& t) {
+    const int32_t n = t.spp;
+    const double inv = 1.0 / (double)n;
+    for (int d = 0; d < t.ndims; d++) {
+        double* samp = t.s1d + (size_t)d * n;
+        for (int32_t i = 0; i < n; i++) {
+            double delta = t.jitter ? pcg_float(t.rng) : 0.5;
+            samp[i] = gomath::min(((double)i + delta) * inv, gomath::kOneMinusEpsilon);
+        }
+        for (int32_t i = 0; i < n; i++) {
+            int32_t other = i + (int32_t)pcg_bounded(t.rng, (uint32_t)(n - i));
+            double a = samp[i];
+            samp[i] = samp[other];
+            samp[other] = a;
+        }
+    }
+    // StratifiedSample2D writes into a copy (sampling.go:122-124, #3): the 2D
+    // values stay (0,0); only the jitter and shuffle draws advance the stream.
+    for (int d = 0; d < t.ndims; d++) {
+        if (t.jitter)
+            for (int32_t k = 0; k < n; k++) { pcg_next(t.rng); pcg_next(t.rng); }
+        for (int32_t i = 0; i < n; i++) pcg_bounded(t.rng, (uint32_t)(n - i));
+    }
+    t.sample_index = 0;
+    t.cur1d = t.cur2d = 0;
+}
+// sampler.go:29-34 — pre-increment, so sample 0 is never traced (#2)
+__device__ __forceinline__ bool next_sample(Thread& t) {
+    t.cur1d = t.cur2d = 0;
+    t.sample_index += 1;
+    return t.sample_index < t.spp;
+}
+__device__ __forceinline__ double get1d(Thread& t) {   // pixel.go:60-69
+    if (t.cur1d < t.ndims) {
+        double v = t.s1d[(size_t)t.cur1d * t.spp + t.sample_index];
+        t.cur1d++;
+        return v;
+    }
+    return pcg_float(t.rng);
+}
+struct V2 {
+    double x, y;
+};
+__device__ __forceinline__ V2 get2d(Thread& t) {   // pixel.go:71-80
+    if (t.cur2d < t.ndims) {
+        t.cur2d++;
+        return V2{0.0, 0.0};
+    }
+    double x = pcg_float(t.rng);
+    double y = pcg_float(t.rng);
+    return V2{x, y};
+}
+
+// ------------------------------------------------------- surface interaction
+// The reference's SurfaceInteraction shares *interaction (p, perr, n, wo,
+// time) and *Shading by pointer (interaction.go:124-148); dpdu..dndv are its
+// own. Only fields that reach an output are kept.
+struct SI {
+    V3 p, perr, n, wo;
+    double time;
+    V3 sn, sdpdu;
+    int prim;
+};
+
+// NewSurfaceInteractionWith (interaction.go:176-207) + the object-to-world
+// TransformSurfaceInteraction assigned back (*si = *..., sphere.go:185 / disk.go:110)
+__device__ inline void make_si(SI& si, const pbrt_matrix4x4& M, const pbrt_matrix4x4& Mi, V3 p, V3 perr, V3 wo,
+                               V3 dpdu, V3 dpdv, double time, bool flip) {
+    V3 n = normalized(cross(dpdu, dpdv));
+    if (flip) n = muls(n, -1);
+    // transform.go:302-334
+    V3 perr2;
+    si.p = xf_point(M, p, perr, &perr2);
+    si.perr = perr2;
+    si.n = normalized(xf_normal(Mi, n));
+    si.wo = normalized(xf_vector(M, wo));
+    si.time = time;
+    V3 sn = xf_normal(Mi, n);
+    si.sdpdu = xf_vector(M, dpdu);
+    si.sn = face_forward(sn, si.n);
+}
+// TransformedPrimitive: only the shared interaction / Shading objects are
+// mutated; the transformed copy itself is discarded (primitive.go:104-106, #20)
+__device__ inline void transform_si_shared(SI& si, const pbrt_matrix4x4& M, const pbrt_matrix4x4& Mi) {
+    V3 perr2;
+    si.p = xf_point(M, si.p, si.perr, &perr2);
+    si.perr = perr2;
+    si.n = normalized(xf_normal(Mi, si.n));
+    si.wo = normalized(xf_vector(M, si.wo));
+    V3 sn = xf_normal(Mi, si.sn);
+    si.sdpdu = xf_vector(M, si.sdpdu);
+    si.sn = face_forward(sn, si.n);
+}
+
+// -------------------------------------------------------------------- shapes
+// Sphere.Intersect / IntersectP (sphere.go:64-268). world->object = the swap of
+// object_to_world (Transform.Inverse, transform.go:175-177).
+template <bool kFull>
+__device__ inline bool sphere_intersect(const pbrt_shape_desc& s, const Ray& r, SI* si, double& t_hit, int& panic) {
+    V3 oerr, derr;
+    Ray ray = xf_ray(s.object_to_world.m_inv, r, &oerr, &derr);
+    EF ox = ef_new(ray.o.x, oerr.x, panic), oy = ef_new(ray.o.y, oerr.y, panic), oz = ef_new(ray.o.z, oerr.z, panic);
+    EF dx = ef_new(ray.d.x, derr.x, panic), dy = ef_new(ray.d.y, derr.y, panic), dz = ef_new(ray.d.z, derr.z, panic);
+    EF a = ef_add(ef_add(ef_mul(dx, dx, panic), ef_mul(dy, dy, panic), panic), ef_mul(dz, dz, panic), panic);
+    EF b = ef_muls(ef_add(ef_add(ef_mul(dx, ox, panic), ef_mul(dy, oy, panic), panic), ef_mul(dz, oz, panic), panic),
+                   2.0, panic);
+    EF c0 = ef_add(ef_add(ef_mul(ox, ox, panic), ef_mul(oy, oy, panic), panic), ef_mul(oz, oz, panic), panic);
+    EF c = ef_sub(c0, ef_muls(ef_new(s.radius, 0, panic), s.radius, panic), panic);
+    EF t0, t1;
+    if (!ef_quadratic(a, b, c, t0, t1, panic)) return false;
+    if (t0.hi > ray.tmax || t1.lo <= 0) return false;
+    EF ts = t0;
+    bool used_t1 = false;
+    if (ts.lo <= 0) {
+        ts = t1;
+        used_t1 = true;
+        if (ts.hi > ray.tmax) return false;
+    }
+    const double two_pi = 2 * gomath::kPi;
+    V3 ph = ray.o + muls(ray.d, ts.v);
+    ph = muls(ph, s.radius / dist(ph, V3{0, 0, 0}));
+    if (ph.x == 0.0 && ph.y == 0.0) ph.x = 1e-5 * s.radius;
+    double phi = gomath::atan2(ph.y, ph.x);
+    if (phi < 0.0) phi += two_pi;
+    if ((s.z_min > -s.radius && ph.z < s.z_min) || (s.z_max < s.radius && ph.z > s.z_max) || phi > s.phi_max) {
+        if (used_t1) return false;
+        if (t1.hi > ray.tmax) return false;
+        ts = t1;
+        ph = ray.o + muls(ray.d, ts.v);
+        ph = muls(ph, s.radius / dist(ph, V3{0, 0, 0}));
+        if (ph.x == 0.0 && ph.y == 0.0) ph.x = 1e-5 * s.radius;
+        double phi2 = gomath::atan2(ph.y, ph.x);   // sphere.go:127 shadows phi (`:=`)
+        if (phi2 < 0.0) phi2 += two_pi;
+        if ((s.z_min > -s.radius && ph.z < s.z_min) || (s.z_max < s.radius && ph.z > s.z_max) || phi2 > s.phi_max)
+            return false;
+    }
+    t_hit = ts.v;
+    if (!kFull) return true;
+    // parametric representation; only dpdu, dpdv feed the outputs
+    double theta = gomath::acos(gomath::clamp(ph.z / s.radius, -1, 1));
+    double zr = gomath::sqrt(ph.x * ph.x + ph.y * ph.y);
+    double izr = 1.0 / zr;
+    double cos_phi = ph.x * izr, sin_phi = ph.y * izr;
+    V3 dpdu{-s.phi_max * ph.y, s.phi_max * ph.x, 0};
+    double dth = s.theta_max - s.theta_min;
+    V3 dpdv = muls(V3{ph.z * cos_phi, ph.z * sin_phi, -s.radius * gomath::sin(theta)}, dth);
+    V3 perr = muls(vabs(ph), gomath::gamma(5));
+    make_si(*si, s.object_to_world.m, s.object_to_world.m_inv, ph, perr, muls(ray.d, -1), dpdu, dpdv, ray.time,
+            s.reverse_orientation != s.transform_swaps_handedness);
+    (void)phi;
+    return true;
+}
+
+// Disk.Intersect / IntersectP (disk.go:64-159)
+template <bool kFull>
+__device__ inline bool disk_intersect(const pbrt_shape_desc& s, const Ray& r, SI* si, double& t_hit) {
+    Ray ray = xf_ray(s.object_to_world.m_inv, r, nullptr, nullptr);
+    if (ray.d.z == 0) return false;
+    double ts = (s.height - ray.o.z) / ray.d.z;
+    if (ts <= 0 || ts >= ray.tmax) return false;
+    V3 ph = ray.o + muls(ray.d, ts);
+    double d2 = ph.x * ph.x + ph.y * ph.y;
+    if (d2 > s.radius * s.radius || d2 < s.inner_radius * s.inner_radius) return false;
+    double phi = gomath::atan2(ph.y, ph.x);
+    if (phi < 0) phi += 2 * gomath::kPi;
+    if (phi > s.phi_max) return false;
+    t_hit = ts;
+    if (!kFull) return true;
+    double rhit = gomath::sqrt(d2);
+    V3 dpdu{-s.phi_max * ph.y, s.phi_max * ph.x, 0};
+    V3 dpdv = muls(V3{ph.x, ph.y, 0}, (s.radius - s.inner_radius) / rhit);
+    ph.z = s.height;
+    make_si(*si, s.object_to_world.m, s.object_to_world.m_inv, ph, V3{0, 0, 0}, muls(ray.d, -1), dpdu, dpdv, ray.time,
+            s.reverse_orientation != s.transform_swaps_handedness);
+    return true;
+}
+
+template <bool kFull>
+__device__ inline bool shape_intersect(const pbrt_shape_desc& s, const Ray& r, SI* si, double& t_hit, int& panic) {
+    if (s.type == PBRT_SHAPE_SPHERE) return sphere_intersect<kFull>(s, r, si, t_hit, panic);
+    return disk_intersect<kFull>(s, r, si, t_hit);
+}
+
+// GeometricPrimitive / TransformedPrimitive (primitive.go:42-115)
+__device__ inline bool prim_intersect(const DevScene& sc, int pi, Ray& r, SI& si, int& panic) {
+    const pbrt_primitive_desc& p = sc.prims[pi];
+    const pbrt_shape_desc& s = sc.shapes[p.shape];
+    double t_hit;
+    if (p.kind == PBRT_PRIM_TRANSFORMED) {
+        Ray ray = xf_ray(p.prim_to_world.m_inv, r, nullptr, nullptr);
+        if (!shape_intersect<true>(s, ray, &si, t_hit, panic)) return false;
+        si.prim = pi;
+        r.tmax = t_hit;
+        if (!is_identity(p.prim_to_world.m)) transform_si_shared(si, p.prim_to_world.m, p.prim_to_world.m_inv);
+        return true;
+    }
+    if (!shape_intersect<true>(s, r, &si, t_hit, panic)) return false;
+    r.tmax = t_hit;
+    si.prim = pi;
+    return true;
+}
+__device__ inline bool prim_intersect_p(const DevScene& sc, int pi, const Ray& r, int& panic) {
+    const pbrt_primitive_desc& p = sc.prims[pi];
+    const pbrt_shape_desc& s = sc.shapes[p.shape];
+    double t_hit;
+    if (p.kind == PBRT_PRIM_TRANSFORMED) {
+        Ray ray = xf_ray(p.prim_to_world.m_inv, r, nullptr, nullptr);
+        return shape_intersect<false>(s, ray, nullptr, t_hit, panic);
+    }
+    return shape_intersect<false>(s, r, nullptr, t_hit, panic);
+}
+
+// ------------------------------------------------------------------------ BVH
+// Bounds3.IntersectP (bounds.go:149-185); (1 + 2*Gamma(3)) == 1 exactly
+__device__ __forceinline__ bool node_hit(const pbrt_bvh_node& nd, const Ray& r, V3 inv, int nx, int ny, int nz) {
+    const double robust = 1 + 2 * gomath::gamma(3);
+    double tmin = ((nx ? nd.bmax[0] : nd.bmin[0]) - r.o.x) * inv.x;
+    double tmax = ((nx ? nd.bmin[0] : nd.bmax[0]) - r.o.x) * inv.x;
+    double tymin = ((ny ? nd.bmax[1] : nd.bmin[1]) - r.o.y) * inv.y;
+    double tymax = ((ny ? nd.bmin[1] : nd.bmax[1]) - r.o.y) * inv.y;
+    tmax *= robust;
+    tymax *= robust;
+    if (tmin > tymax || tymin > tmax) return false;
+    if (tymin > tmin) tmin = tymin;
+    if (tymax < tmax) tmax = tymax;
+    double tzmin = ((nz ? nd.bmax[2] : nd.bmin[2]) - r.o.z) * inv.z;
+    double tzmax = ((nz ? nd.bmin[2] : nd.bmax[2]) - r.o.z) * inv.z;
+    tzmax *= robust;
+    if (tmin > tzmax || tzmin > tmax) return false;
+    if (tzmin > tmin) tmin = tzmin;
+    if (tzmax < tmax) tmax = tzmax;
+    return tmin < r.tmax && tmax > 0;
+}
+
+// BVH.Intersect (bvh.go:659-712) / IntersectP (:713-765). The [64] node stack
+// lives in LDS (one uint16 column per lane).
+template <bool kAny>
+__device__ inline bool bvh_traverse(const DevScene& sc, Ray& ray, SI* si, uint16_t* stack, int& panic) {
+    if (sc.n_nodes == 0) return false;
+    bool hit = false;
+    V3 inv{1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z};
+    const int nx = inv.x < 0, ny = inv.y < 0, nz = inv.z < 0;
+    const uint32_t negmask = (uint32_t)nx | ((uint32_t)ny << 1) | ((uint32_t)nz << 2);
+    uint32_t to_visit = 0, cur = 0;
+    for (;;) {
+        const pbrt_bvh_node& nd = sc.nodes[cur];
+        if (node_hit(nd, ray, inv, nx, ny, nz)) {
+            if (nd.n_prims > 0) {
+                for (uint32_t i = 0; i < nd.n_prims; i++) {
+                    if (kAny) {
+                        if (prim_intersect_p(sc, (int)(nd.offset + i), ray, panic)) return true;
+                    } else {
+                        if (prim_intersect(sc, (int)(nd.offset + i), ray, *si, panic)) hit = true;
+                    }
+                    if (panic) return hit;
+                }
+                if (to_visit == 0) break;
+                cur = stack[(--to_visit) * kStackStride];
+            } else {
+                if (to_visit >= 64) { panic = PBRT_PANIC_BVH_STACK; return hit; }
+                uint32_t far_node, near_node;
+                if ((negmask >> nd.axis) & 1u) { far_node = cur + 1; near_node = nd.offset; }
+                else { far_node = nd.offset; near_node = cur + 1; }
+                stack[(to_visit++) * kStackStride] = (uint16_t)far_node;
+                cur = near_node;
+            }
+        } else {
+            if (to_visit == 0) break;
+            cur = stack[(--to_visit) * kStackStride];
+        }
+    }
+    return hit;
+}
+
+// ----------------------------------------------------------------- material
+constexpr int BXDF_REFLECTION = 1, BXDF_DIFFUSE = 4, BXDF_SPECULAR = 16, BXDF_ALL = 31;
+constexpr int LAMBERT_TYPE = BXDF_REFLECTION | BXDF_DIFFUSE;
+
+struct BSDF {
+    V3 ns, ng, ss, ts;
+    Spec r;
+    int n_bxdfs;   // 0 or 1 (LambertianReflection)
+};
+__device__ __forceinline__ double inv_pi() { return 1.0 / gomath::kPi; }   // pkg/math InvPi
+
+// MatteMaterial.ComputeScatteringFunctions (matte.go:21-37) + NewBSDF
+// (reflection.go:128-140) + Checkerboard2D/PlanarMapping2D (checkerboard.go:30-40)
+__device__ inline int compute_bsdf(const DevScene& sc, const SI& si, BSDF& b) {
+    const pbrt_material_desc& m = sc.materials[sc.prims[si.prim].material];
+    b.ns = si.sn;
+    b.ng = si.n;
+    b.ss = normalized(si.sdpdu);
+    b.ts = cross(b.ns, b.ss);
+    b.n_bxdfs = 0;
+    Spec r;
+    if (m.kd_type == PBRT_TEX_CHECKERBOARD2D) {
+        double s = m.ds + dot(si.p, load3(m.vs));
+        double t = m.dt + dot(si.p, load3(m.vt));
+        int64_t k = gomath::to_int(gomath::floor(s) + gomath::floor(t));
+        r = (k % 2 == 0) ? spec3(m.tex1) : spec3(m.tex2);
+    } else {
+        r = spec3(m.kd);
+    }
+    r.r = gomath::clamp(r.r, 0, kInf);
+    r.g = gomath::clamp(r.g, 0, kInf);
+    r.b = gomath::clamp(r.b, 0, kInf);
+    double sig = gomath::clamp(m.sigma, 0, 90);
+    if (!is_black(r)) {
+        if (sig != 0) return -1;   // OrenNayar: off the hot path (unsupported)
+        b.n_bxdfs = 1;
+        b.r = r;
+    }
+    return 0;
+}
+__device__ __forceinline__ V3 w2l(const BSDF& b, V3 v) { return V3{dot(v, b.ss), dot(v, b.ts), dot(v, b.ns)}; }
+// BSDF.F (reflection.go:169-186)
+__device__ inline Spec bsdf_f(const BSDF& b, V3 woW, V3 wiW) {
+    V3 wo = w2l(b, woW);
+    if (wo.z == 0.0) return spec(0);
+    bool reflect = dot(wiW, b.ng) * dot(woW, b.ng) > 0;
+    Spec f = spec(0);
+    if (b.n_bxdfs && reflect) f = f + smuls(b.r, inv_pi());
+    return f;
+}
+__device__ __forceinline__ double lambert_pdf(V3 wo, V3 wi) {   // reflection.go:343-348
+    return (wo.z * wi.z > 0) ? gomath::abs(wi.z) * inv_pi() : 0;
+}
+// BSDF.Pdf (reflection.go:255-278)
+__device__ inline double bsdf_pdf(const BSDF& b, V3 woW, V3 wiW) {
+    if (b.n_bxdfs == 0) return 0;
+    V3 wo = w2l(b, woW);
+    V3 wi = w2l(b, wiW);
+    if (wo.z == 0) return 0;
+    double pdf = 0 + lambert_pdf(wo, wi);
+    return pdf / 1.0;
+}
+// sampling.go:173-198
+__device__ inline V2 concentric_sample_disk(V2 u) {
+    V2 uo{u.x * 2.0 - 1, u.y * 2.0 - 1};
+    if (uo.x == 0 && uo.y == 0) return V2{0, 0};
+    double theta, r;
+    if (gomath::abs(uo.x) > gomath::abs(uo.y)) {
+        r = uo.x;
+        theta = (gomath::kPi / 4.0) * (uo.y / uo.x);
+    } else {
+        r = uo.y;
+        theta = (gomath::kPi / 2.0) - (gomath::kPi / 4.0) * (uo.x / uo.y);
+    }
+    return V2{gomath::cos(theta) * r, gomath::sin(theta) * r};
+}
+// BSDF.SampleF (reflection.go:188-253) returning the LOCAL-frame wi (#7)
+__device__ inline Spec bsdf_sample_f(const BSDF& b, V3 woW, V2 u, V3& wi, double& pdf) {
+    wi = V3{0, 0, 0};
+    pdf = 0;
+    if (b.n_bxdfs == 0) return spec(0);
+    double comp = gomath::min(gomath::floor(u.x * 1.0), 1.0 - 1);
+    V2 ur{gomath::min(u.x * 1.0 - comp, gomath::kOneMinusEpsilon), u.y};
+    V3 wo = w2l(b, woW);
+    if (wo.z == 0.0) return spec(0);
+    V2 d = concentric_sample_disk(ur);   // CosineSampleHemisphere (sampling.go:194-198)
+    V3 w{d.x, d.y, gomath::sqrt(gomath::max(0.0, 1.0 - d.x * d.x - d.y * d.y))};
+    if (wo.z < 0) w.z *= -1;
+    double p = lambert_pdf(wo, w);
+    Spec f = smuls(b.r, inv_pi());
+    if (p == 0.0) return spec(0);
+    wi = w;
+    pdf = p;
+    return f;
+}
+
+// ------------------------------------------------------------------- lights
+struct LightSample {
+    Spec Li;
+    V3 wi;
+    double pdf;
+    V3 tp, tperr, tn;   // VisibilityTester p1
+};
+
+// Sphere.SampleAtInteraction (sphere.go:287-344) incl. the inside-sphere branch
+__device__ inline void sphere_sample_at(const pbrt_shape_desc& s, const SI& ref, V2 u, V3& p, V3& perr, V3& n,
+                                        double& pdf) {
+    const pbrt_matrix4x4& M = s.object_to_world.m;
+    V3 pc = xf_point(M, V3{0, 0, 0}, V3{0, 0, 0}, nullptr);
+    V3 po = offset_ray_origin(ref.p, ref.perr, ref.n, pc - ref.p);
+    if (dist2(po, pc) <= s.radius * s.radius) {
+        // Sphere.Sample (sphere.go:270-285) + UniformSampleSphere (sampling.go:158-163)
+        double z = 1.0 - 2.0 * u.x;
+        double rr = gomath::sqrt(gomath::max(0, 1 - z * z));
+        double ph = 2 * gomath::kPi * u.y;
+        V3 pobj = muls(V3{rr * gomath::cos(ph), rr * gomath::sin(ph), z}, s.radius);
+        n = normalized(xf_normal(s.object_to_world.m_inv, pobj));
+        if (s.reverse_orientation) n = muls(n, -1);
+        pobj = muls(pobj, s.radius / dist(pobj, V3{0, 0, 0}));
+        V3 pobj_err = muls(vabs(pobj), gomath::gamma(5));
+        p = xf_point(M, pobj, pobj_err, &perr);
+        pdf = 1.0 / (s.phi_max * s.radius * (s.z_max - s.z_min));
+        V3 wi = p - ref.p;
+        if (len2(wi) == 0) {
+            pdf = 0;
+        } else {
+            wi = normalized(wi);
+            pdf *= dist2(ref.p, p) / absdot(n, muls(wi, -1));
+        }
+        if (gomath::is_inf(pdf)) pdf = 0.0;
+        return;
+    }
+    V3 wc = normalized(pc - ref.p);
+    V3 wcx, wcy;
+    coordinate_system(wc, wcx, wcy);
+    double r2 = s.radius * s.radius;
+    double sin2max = r2 / dist2(ref.p, pc);
+    double cosmax = gomath::sqrt(gomath::max(0, 1.0 - sin2max));
+    double cost = (1.0 - u.x) + u.x * cosmax;
+    double sint = gomath::sqrt(gomath::max(0, 1 - cost * cost));
+    double phi = u.y * 2 * gomath::kPi;
+    double dc = dist(ref.p, pc);
+    double ds = dc * cost - gomath::sqrt(gomath::max(0, r2 - (dc * dc) * (sint * sint)));
+    double cosa = (dc * dc + r2 - ds * ds) / (2.0 * dc * s.radius);
+    double sina = gomath::sqrt(gomath::max(0, 1.0 - cosa * cosa));
+    // SphericalDirectionXYZ (geometry.go:66-70) with -wcX, -wcY, -wc
+    V3 nw = (muls(muls(wcx, -1), sina * gomath::cos(phi)) + muls(muls(wcy, -1), sina * gomath::sin(phi))) +
+            muls(muls(wc, -1), cosa);
+    p = pc + muls(nw, s.radius);
+    perr = muls(vabs(p), gomath::gamma(5.0));
+    n = s.reverse_orientation ? muls(nw, -1) : nw;
+    pdf = 1.0 / (2.0 * gomath::kPi * (1.0 - cosmax));   // UniformConePdf
+}
+
+// Light.SampleLi for Point (point.go:44-49), Distant (distant.go:40-44, #15)
+// and DiffuseAreaLight (diffuse.go:47-59, unnormalized wi #12)
+__device__ inline void sample_li(const DevScene& sc, const pbrt_light_desc& L, const SI& si, V2 u, LightSample& ls) {
+    if (L.type == PBRT_LIGHT_POINT) {
+        V3 pl = load3(L.p_light);
+        ls.wi = normalized(pl - si.p);
+        ls.pdf = 1.0;
+        ls.Li = sdivs(spec3(L.spectrum), dist2(pl, si.p));
+        ls.tp = pl; ls.tperr = V3{0, 0, 0}; ls.tn = V3{0, 0, 0};
+    } else if (L.type == PBRT_LIGHT_DISTANT) {
+        V3 w = load3(L.w_light);
+        ls.tp = muls(w, 2 * L.world_radius);
+        ls.tperr = V3{0, 0, 0}; ls.tn = V3{0, 0, 0};
+        ls.Li = spec3(L.spectrum);
+        ls.wi = w;
+        ls.pdf = 1;
+    } else {
+        V3 p, perr, n;
+        double pdf;
+        sphere_sample_at(sc.shapes[L.shape], si, u, p, perr, n, pdf);
+        if (pdf == 0 || len2(p - si.p) == 0) {
+            ls.Li = spec(0); ls.wi = V3{0, 0, 0}; ls.pdf = 0;
+            ls.tp = ls.tperr = ls.tn = V3{0, 0, 0};
+            return;
+        }
+        ls.wi = p - si.p;
+        ls.pdf = pdf;
+        ls.tp = p; ls.tperr = perr; ls.tn = n;
+        ls.Li = (L.two_sided || dot(n, muls(ls.wi, -1)) > 0) ? spec3(L.spectrum) : spec(0);
+    }
+}
+
+// EstimateDirect, light-sampling half (integrator.go:79-130). The BSDF-sampled
+// MIS half (:132-192) is not executed: no primitive carries an area light
+// (primitive.go:33, GetAreaLight() == nil) so it always contributes 0.
+__device__ inline Spec estimate_direct(const DevScene& sc, Thread& t, const SI& si, const BSDF& b, int li, V2 u_light) {
+    const pbrt_light_desc& L = sc.lights[li];
+    const bool is_delta = L.type != PBRT_LIGHT_DIFFUSE_AREA;
+    Spec Ld = spec(0);
+    LightSample ls;
+    sample_li(sc, L, si, u_light, ls);
+    if (ls.pdf > 0 && !is_black(ls.Li)) {
+        Spec f = bsdf_f(b, si.wo, ls.wi);
+        double wdn = absdot(ls.wi, si.sn);
+        f = smuls(f, wdn);
+        double scat_pdf = bsdf_pdf(b, si.wo, ls.wi);
+        if (!is_black(f)) {
+            // VisibilityTester.Unoccluded -> SpawnRayToInteraction (interaction.go:91-102, #14)
+            V3 origin = offset_ray_origin(si.p, si.perr, si.n, ls.tp - si.p);
+            V3 target = offset_ray_origin(ls.tp, ls.tperr, ls.tn, origin - ls.tp);
+            Ray sr{si.p, target - origin, 1 - 0.0001, si.time};
+            t.shadow_rays++;
+            Spec Li = ls.Li;
+            if (bvh_traverse<true>(sc, sr, nullptr, t.stack, t.panic)) Li = spec(0);
+            if (!is_black(Li)) {
+                if (is_delta) {
+                    Ld = Ld + sdivs(smul(f, Li), ls.pdf);
+                } else {
+                    double fp = 1.0 * ls.pdf, gp = 1.0 * scat_pdf;   // PowerHeuristic(1, lightPdf, 1, scatteringPdf)
+                    double w = (fp * fp) / (fp * fp + gp * gp);
+                    Ld = Ld + sdivs(smuls(smul(f, Li), w), ls.pdf);
+                }
+            }
+        }
+    }
+    return Ld;
+}
+
+// Distribution1D.SampleDiscrete + FindInterval (sampling.go:42-55, math.go:64-80)
+__device__ inline int sample_discrete(const pbrt_distribution_desc& d, double u, double& pdf) {
+    int size = d.count + 1, first = 0, len = size;
+    while (len > 0) {
+        int half = len >> 1, middle = first + half;
+        if (d.cdf[middle] <= u) { first = middle + 1; len -= half + 1; }
+        else len = half;
+    }
+    int off = (int)gomath::clamp((double)(first - 1), 0, (double)(size - 2));
+    pdf = 0;
+    if (d.func_int > 0) pdf = d.func[off] / (d.func_int / (double)d.count);
+    return off;
+}
+
+// UniformSampleOneLight (integrator.go:48-77): no /lightPdf, panic if > 10 (#10)
+__device__ inline Spec uniform_sample_one_light(const DevScene& sc, Thread& t, const SI& si, const BSDF& b,
+                                                const pbrt_distribution_desc* dist) {
+    const int n = sc.n_lights;
+    if (n == 0) return spec(0);
+    int ln;
+    if (dist) {
+        double lpdf;
+        ln = sample_discrete(*dist, get1d(t), lpdf);
+        if (lpdf == 0.0) return spec(0);
+    } else {
+        ln = (int)gomath::to_int(gomath::min(get1d(t) * (double)n, (double)(n - 1)));
+    }
+    V2 ul = get2d(t);
+    get2d(t);   // uScattering: only the (skipped) MIS half reads it
+    Spec s = estimate_direct(sc, t, si, b, ln, ul);
+    if (max_component(s) > 10) t.panic = PBRT_PANIC_LD_GT_10;
+    return s;
+}
+
+// -------------------------------------------------------------- integrators
+// Path.Li (path.go:32-157)
+__device__ inline Spec path_li(const DevScene& sc, Thread& t, Ray ray, int max_depth, double rr_threshold) {
+    Spec L = spec(0), beta = spec(1);
+    int32_t bounces = 0;
+    const double eta_scale = 1.0;
+    for (;;) {
+        bounces++;
+        t.bounce = bounces;
+        if (bounces >= max_depth) break;   // path.go:66 breaks whether or not the ray hits
+        SI isect;
+        t.closest_rays++;
+        if (!bvh_traverse<false>(sc, ray, &isect, t.stack, t.panic)) break;
+        if (t.panic) break;
+        BSDF b;
+        if (compute_bsdf(sc, isect, b) < 0) { t.panic = -1; break; }
+        if (b.n_bxdfs > 0) {   // NumComponents(BSDFAll &^ BSDFSpecular) > 0
+            Spec ld = uniform_sample_one_light(sc, t, isect, b, sc.dist);
+            if (t.panic) break;
+            L = L + smul(beta, ld);
+        }
+        V3 wo = ray.d;   // path.go:91 (#8)
+        V2 u = get2d(t);
+        V3 wi;
+        double pdf;
+        Spec f = bsdf_sample_f(b, wo, u, wi, pdf);
+        if (is_black(f) || pdf == 0.0) break;
+        double wp = absdot(wi, isect.sn) / pdf;
+        beta = smul(beta, smuls(f, wp));
+        // SpawnRay (interaction.go:68-77)
+        ray.o = offset_ray_origin(isect.p, isect.perr, isect.n, wi);
+        ray.d = wi;
+        ray.tmax = kInf;
+        ray.time = isect.time;
+        Spec rr = smuls(beta, eta_scale);
+        if (max_component(rr) < rr_threshold && bounces > 3) {
+            double q = gomath::max(0.05, 1 - max_component(rr));
+            if (get1d(t) < q) break;
+            beta = sdivs(beta, 1 - q);
+        }
+    }
+    return L;
+}
+
+// DirectLighting.Li at depth 0 (directlighting.go:62-104)
+__device__ inline Spec direct_li(const DevScene& sc, Thread& t, Ray ray, int max_depth, int strategy) {
+    Spec L = spec(0);
+    SI si;
+    t.bounce = 1;
+    t.closest_rays++;
+    if (!bvh_traverse<false>(sc, ray, &si, t.stack, t.panic)) {
+        for (int i = 0; i < sc.n_lights; i++) L = L + spec(0);
+        return L;
+    }
+    if (t.panic) return L;
+    BSDF b;
+    if (compute_bsdf(sc, si, b) < 0) { t.panic = -1; return L; }
+    L = L + spec(0);   // si.Le(si.Wo): no primitive carries an area light
+    if (sc.n_lights > 0) {
+        if (strategy == PBRT_DL_UNIFORM_SAMPLE_ALL) {
+            // UniformSampleAllLights (integrator.go:23-46); clones carry no arrays (#23)
+            Spec acc = spec(0);
+            for (int j = 0; j < sc.n_lights; j++) {
+                V2 ul = get2d(t);
+                get2d(t);
+                acc = acc + estimate_direct(sc, t, si, b, j, ul);
+                if (t.panic) return L;
+            }
+            L = L + acc;
+        } else {
+            L = L + uniform_sample_one_light(sc, t, si, b, nullptr);
+        }
+    }
+    if (0 + 1 < max_depth) {
+        // SpecularReflect / SpecularTransmit (integrator.go:352-422): one Get2D
+        // each, black for a Lambertian-only BSDF
+        get2d(t);
+        L = L + spec(0);
+        get2d(t);
+        L = L + spec(0);
+    }
+    return L;
+}
+
+// PerspectiveCamera.GenerateRayDifferential (camera.go:192-242)
+__device__ inline Ray camera_ray(const pbrt_camera_desc& cam, double fx, double fy, double time_u, V2 plens) {
+    V3 pcam = xf_point(cam.raster_to_camera.m, V3{fx, fy, 0}, V3{0, 0, 0}, nullptr);
+    Ray r{V3{0, 0, 0}, normalized(pcam), kInf, 0};
+    if (cam.lens_radius > 0) {
+        V2 pl = concentric_sample_disk(plens);
+        pl.x *= cam.lens_radius;
+        pl.y *= cam.lens_radius;
+        double ft = cam.focal_distance / r.d.z;
+        V3 pf = muls(r.d, ft) + r.o;
+        r.o = V3{pl.x, pl.y, 0};
+        r.d = normalized(pf - r.o);
+    }
+    Ray w = xf_ray(cam.camera_to_world.m, r, nullptr, nullptr);
+    w.time = gomath::lerp(time_u, cam.shutter_open, cam.shutter_close);
+    return w;
+}
+
+}  // namespace pbrt

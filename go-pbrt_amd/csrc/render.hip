@@ -1,0 +1,693 @@
+// render.hip — MI355X (gfx950) kernels and the C ABI of include/pbrt_gpu.h.
+//
+// Kernels
+//   k_render_exact   EXACT mode: one lane per 16-px tile. The lane replays the
+//                    tile's PCG32 stream exactly as pbrt.Render's worker does
+//                    (integrator.go:228-289, 311-340): pixel loop, Stratified
+//                    StartPixel, samples 1..spp-1, Path.Li / DirectLighting.Li,
+//                    NaN guard, FilmTile.AddSample into the tile's film slot.
+//   k_render_decorr  THROUGHPUT mode: same arithmetic, one lane per
+//                    (pixel, sample) path with its own PCG32 stream; paths of
+//                    one pixel are summed in sample order in a second pass.
+//   k_merge_film     Film.MergeFilmTile (film.go:115-132): per output pixel,
+//                    RGBToXYZ of every covering tile film in tile-index order.
+//   k_intersect[_p]  batch BVH closest-hit / any-hit (bvh.go:659-765).
+//
+// Everything is float64 with -ffp-contract=off (bit parity with the Go
+// reference). The scene is a few KB and is read through the scalar/vector L1.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/pbrt_gpu.h"
+#include "../../include/pbrt_scene.h"
+#include "pbrt_path.h"
+
+using namespace pbrt;
+
+namespace {
+
+constexpr int kWave = 64;
+
+struct RenderParams {
+    int64_t film_min_x, film_min_y, film_w, film_h;   // CroppedPixelBounds
+    int64_t tile_size, ntx, nty;
+    int64_t tile_begin, tile_stride, n_slots;
+    int64_t slot_w, slot_h;                            // max tile-film extent
+    int32_t spp, xs, ys, ndims, jitter;
+    int32_t integrator, max_depth, dl_strategy;
+    double rr_threshold;
+    int32_t lanes_per_wave;
+    int32_t pad;
+};
+
+struct PanicRec {
+    int32_t kind;
+    int32_t sample;
+    int32_t bounce;
+    int32_t pad;
+    int64_t px, py;
+};
+
+struct Counters {
+    unsigned long long paths, camera_samples, closest_rays, shadow_rays;
+    int32_t any_panic;
+    int32_t pad;
+};
+
+__device__ __forceinline__ void tile_bounds(const RenderParams& rp, int64_t tile, int64_t& x0, int64_t& y0,
+                                            int64_t& x1, int64_t& y1) {
+    // integrator.go:316-325
+    int64_t tx = tile % rp.ntx, ty = tile / rp.ntx;
+    x0 = rp.film_min_x + tx * rp.tile_size;
+    x1 = gomath::to_int(gomath::min((double)(x0 + rp.tile_size), (double)(rp.film_min_x + rp.film_w)));
+    y0 = rp.film_min_y + ty * rp.tile_size;
+    y1 = gomath::to_int(gomath::min((double)(y0 + rp.tile_size), (double)(rp.film_min_y + rp.film_h)));
+}
+// Film.GetFilmTile (film.go:106-113)
+__device__ __host__ __forceinline__ void film_tile_bounds(const pbrt_film_desc& f, int64_t x0, int64_t y0, int64_t x1,
+                                                          int64_t y1, int64_t& px0, int64_t& py0, int64_t& px1,
+                                                          int64_t& py1) {
+    int64_t p0x = gomath::to_int(gomath::ceil(((double)x0 - 0.5) - f.filter_radius_x));
+    int64_t p0y = gomath::to_int(gomath::ceil(((double)y0 - 0.5) - f.filter_radius_y));
+    int64_t p1x = gomath::to_int(gomath::floor(((double)x1 - 0.5) + f.filter_radius_x)) + 1;
+    int64_t p1y = gomath::to_int(gomath::floor(((double)y1 - 0.5) + f.filter_radius_y)) + 1;
+    px0 = gomath::to_int(gomath::max((double)f.crop_min_x, (double)p0x));
+    py0 = gomath::to_int(gomath::max((double)f.crop_min_y, (double)p0y));
+    px1 = gomath::to_int(gomath::min((double)f.crop_max_x, (double)p1x));
+    py1 = gomath::to_int(gomath::min((double)f.crop_max_y, (double)p1y));
+}
+
+// Footprint of one sample on the tile film (film.go:211-248). pFilm is the
+// pixel corner for every sample of a pixel (2D stratified dims are (0,0), #3),
+// so the footprint and the filter weights are per pixel.
+struct Footprint {
+    int n;               // number of film pixels touched (<= 4 in the register path)
+    int64_t off[4];      // offsets (in pixels) into the tile film slot
+    double w[4];         // sampleWeight * filterWeight
+};
+__device__ inline int footprint(const pbrt_film_desc& f, double pfx, double pfy, int64_t px0, int64_t py0,
+                                int64_t px1, int64_t py1, Footprint& fp, int64_t& p0x, int64_t& p0y, int64_t& p1x,
+                                int64_t& p1y) {
+    double dx = pfx - 0.5, dy = pfy - 0.5;
+    double p0fx = gomath::ceil(dx - f.filter_radius_x), p0fy = gomath::ceil(dy - f.filter_radius_y);
+    double p1fx = gomath::floor(dx + f.filter_radius_x) + 1, p1fy = gomath::floor(dy + f.filter_radius_y) + 1;
+    p0x = gomath::to_int(gomath::max(p0fx, (double)px0));
+    p0y = gomath::to_int(gomath::max(p0fy, (double)py0));
+    p1x = gomath::to_int(gomath::min(p1fx, (double)px1));
+    p1y = gomath::to_int(gomath::min(p1fy, (double)py1));
+    int64_t nx = p1x - p0x, ny = p1y - p0y;
+    if (nx <= 0 || ny <= 0) { fp.n = 0; return 0; }
+    if (nx * ny > 4) return -1;
+    const double ifx = 1.0 / f.filter_radius_x, ify = 1.0 / f.filter_radius_y;
+    int64_t tw = px1 - px0;
+    int k = 0;
+    for (int64_t y = p0y; y < p1y; y++) {
+        int iy = (int)gomath::to_int(gomath::min(gomath::floor(gomath::abs(((double)y - dy) * ify * 16.0)), 16.0 - 1));
+        for (int64_t x = p0x; x < p1x; x++) {
+            int ix =
+                (int)gomath::to_int(gomath::min(gomath::floor(gomath::abs(((double)x - dx) * ifx * 16.0)), 16.0 - 1));
+            fp.off[k] = (x - px0) + (y - py0) * tw;
+            fp.w[k] = 1.0 * f.filter_table[iy * 16 + ix];
+            k++;
+        }
+    }
+    fp.n = k;
+    return 0;
+}
+
+// ----------------------------------------------------------- EXACT kernel
+// One lane per tile; `lanes_per_wave` lanes of each 64-lane workgroup work
+// (fewer busy lanes per wave = less divergence, more waves per SIMD).
+__global__ __launch_bounds__(kWave) void k_render_exact(DevScene sc, RenderParams rp, double* __restrict__ films,
+                                                        double* __restrict__ s1d_scratch, PanicRec* __restrict__ panics,
+                                                        Counters* __restrict__ ctr) {
+    __shared__ uint16_t stack_lds[64 * kStackStride];
+    const int lane = threadIdx.x;
+    if (lane >= rp.lanes_per_wave) return;
+    const int64_t slot = (int64_t)blockIdx.x * rp.lanes_per_wave + lane;
+    if (slot >= rp.n_slots) return;
+    const int64_t tile = rp.tile_begin + slot * rp.tile_stride;
+    const pbrt_film_desc& film = *sc.film;
+
+    int64_t x0, y0, x1, y1, px0, py0, px1, py1;
+    tile_bounds(rp, tile, x0, y0, x1, y1);
+    film_tile_bounds(film, x0, y0, x1, y1, px0, py0, px1, py1);
+    double* tf = films + slot * (rp.slot_w * rp.slot_h * 3);
+    const int64_t npx = (px1 - px0) * (py1 - py0);
+    for (int64_t i = 0; i < npx * 3; i++) tf[i] = 0.0;
+
+    Thread t;
+    t.spp = rp.spp; t.ndims = rp.ndims; t.xs = rp.xs; t.ys = rp.ys; t.jitter = rp.jitter;
+    t.s1d = s1d_scratch + slot * (int64_t)(rp.ndims * rp.spp);
+    t.stack = stack_lds + lane;
+    t.panic = 0;
+    t.bounce = 0;
+    t.closest_rays = t.shadow_rays = 0;
+    pcg_seed(t.rng, (uint64_t)tile);   // Sampler.Clone(seed = tile index), integrator.go:318,328
+    unsigned long long paths = 0;
+    const pbrt_camera_desc& cam = *sc.camera;
+
+    for (int64_t py = y0; py < y1; py++) {
+        for (int64_t px = x0; px < x1; px++) {
+            start_pixel(t);
+            // camera sample: pFilm = pixel + Get2D() == pixel corner; pLens = Get2D() = (0,0)
+            const double fx = (double)px + 0.0, fy = (double)py + 0.0;
+            Footprint fp;
+            int64_t p0x, p0y, p1x, p1y;
+            const bool reg = footprint(film, fx, fy, px0, py0, px1, py1, fp, p0x, p0y, p1x, p1y) == 0;
+            double acc[4][3];
+            if (reg)
+                for (int k = 0; k < fp.n; k++)
+                    for (int c = 0; c < 3; c++) acc[k][c] = tf[fp.off[k] * 3 + c];
+            while (next_sample(t)) {
+                V2 u0 = get2d(t);
+                V2 plens = get2d(t);
+                double tu = get1d(t);
+                Ray ray = camera_ray(cam, (double)px + u0.x, (double)py + u0.y, tu, plens);
+                Spec L = (rp.integrator == PBRT_INTEGRATOR_PATH) ? path_li(sc, t, ray, rp.max_depth, rp.rr_threshold)
+                                                                 : direct_li(sc, t, ray, rp.max_depth, rp.dl_strategy);
+                paths++;
+                if (t.panic) {
+                    PanicRec pr;
+                    pr.kind = t.panic;
+                    pr.sample = t.sample_index;
+                    pr.bounce = t.bounce;
+                    pr.pad = 0;
+                    pr.px = px;
+                    pr.py = py;
+                    panics[slot] = pr;
+                    atomicExch(&ctr->any_panic, 1);
+                    return;
+                }
+                if (has_nans(L)) L = spec(0.1);   // integrator.go:256-262
+                if (0.0 > film.max_sample_luminance) L = smuls(L, film.max_sample_luminance / 0.0);   // L.Y() == 0
+                if (reg) {
+                    for (int k = 0; k < fp.n; k++) {
+                        Spec a = smuls(L, fp.w[k]);
+                        acc[k][0] += a.r; acc[k][1] += a.g; acc[k][2] += a.b;
+                    }
+                } else {
+                    // general filter footprint: AddSample straight into the slot
+                    double dx = fx - 0.5, dy = fy - 0.5;
+                    const double ifx = 1.0 / film.filter_radius_x, ify = 1.0 / film.filter_radius_y;
+                    int64_t tw = px1 - px0;
+                    for (int64_t y = p0y; y < p1y; y++) {
+                        int iy = (int)gomath::to_int(
+                            gomath::min(gomath::floor(gomath::abs(((double)y - dy) * ify * 16.0)), 16.0 - 1));
+                        for (int64_t x = p0x; x < p1x; x++) {
+                            int ix = (int)gomath::to_int(
+                                gomath::min(gomath::floor(gomath::abs(((double)x - dx) * ifx * 16.0)), 16.0 - 1));
+                            Spec a = smuls(L, 1.0 * film.filter_table[iy * 16 + ix]);
+                            double* p = tf + ((x - px0) + (y - py0) * tw) * 3;
+                            p[0] += a.r; p[1] += a.g; p[2] += a.b;
+                        }
+                    }
+                }
+            }
+            if (reg)
+                for (int k = 0; k < fp.n; k++)
+                    for (int c = 0; c < 3; c++) tf[fp.off[k] * 3 + c] = acc[k][c];
+        }
+    }
+    atomicAdd(&ctr->paths, paths);
+    atomicAdd(&ctr->camera_samples, paths);
+    atomicAdd(&ctr->closest_rays, (unsigned long long)t.closest_rays);
+    atomicAdd(&ctr->shadow_rays, (unsigned long long)t.shadow_rays);
+}
+
+// ---------------------------------------------------------- merge kernel
+// Film.MergeFilmTile (film.go:115-132) in tile-index order. A film pixel is
+// covered by at most the 3x3 tiles around its own (filter radius < tile size).
+__global__ __launch_bounds__(256) void k_merge_film(const pbrt_film_desc* __restrict__ film_desc, RenderParams rp,
+                                                    const double* __restrict__ films, double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rp.film_w * rp.film_h) return;
+    const pbrt_film_desc& f = *film_desc;
+    const int64_t x = rp.film_min_x + i % rp.film_w, y = rp.film_min_y + i / rp.film_w;
+    const int64_t tx = (x - rp.film_min_x) / rp.tile_size, ty = (y - rp.film_min_y) / rp.tile_size;
+    double v0 = 0, v1 = 0, v2 = 0;
+    for (int64_t dy = -1; dy <= 1; dy++) {
+        for (int64_t dx = -1; dx <= 1; dx++) {
+            int64_t cx = tx + dx, cy = ty + dy;
+            if (cx < 0 || cy < 0 || cx >= rp.ntx || cy >= rp.nty) continue;
+            int64_t tile = cy * rp.ntx + cx;
+            if (tile < rp.tile_begin || (tile - rp.tile_begin) % rp.tile_stride != 0) continue;
+            int64_t slot = (tile - rp.tile_begin) / rp.tile_stride;
+            if (slot >= rp.n_slots) continue;
+            int64_t x0, y0, x1, y1, px0, py0, px1, py1;
+            tile_bounds(rp, tile, x0, y0, x1, y1);
+            film_tile_bounds(f, x0, y0, x1, y1, px0, py0, px1, py1);
+            if (x < px0 || x >= px1 || y < py0 || y >= py1) continue;
+            const double* c = films + slot * (rp.slot_w * rp.slot_h * 3) + ((x - px0) + (y - py0) * (px1 - px0)) * 3;
+            // spectrum.go:35-41 RGBToXYZ
+            v0 += 0.412453 * c[0] + 0.357580 * c[1] + 0.180423 * c[2];
+            v1 += 0.212671 * c[0] + 0.715160 * c[1] + 0.072169 * c[2];
+            v2 += 0.019334 * c[0] + 0.119193 * c[1] + 0.950227 * c[2];
+        }
+    }
+    out[i * 3 + 0] = v0;
+    out[i * 3 + 1] = v1;
+    out[i * 3 + 2] = v2;
+}
+
+// ------------------------------------------------------- batch intersect
+__global__ __launch_bounds__(kWave) void k_intersect(DevScene sc, int64_t n, const double* __restrict__ rays,
+                                                     double* __restrict__ out, int any_hit) {
+    __shared__ uint16_t stack_lds[64 * kStackStride];
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double* q = rays + 7 * i;
+    Ray r{V3{q[0], q[1], q[2]}, V3{q[3], q[4], q[5]}, q[6], 0};
+    int panic = 0;
+    if (any_hit) {
+        bool h = bvh_traverse<true>(sc, r, nullptr, stack_lds + threadIdx.x, panic);
+        out[i] = panic ? gomath::nan() : (h ? 1.0 : 0.0);
+        return;
+    }
+    SI si;
+    si.p = si.n = V3{0, 0, 0};
+    si.prim = -1;
+    bool h = bvh_traverse<false>(sc, r, &si, stack_lds + threadIdx.x, panic);
+    double* o = out + 9 * i;
+    if (panic) {
+        for (int k = 0; k < 9; k++) o[k] = gomath::nan();
+        return;
+    }
+    o[0] = h ? 1.0 : 0.0;
+    o[1] = r.tmax;
+    o[2] = h ? (double)si.prim : -1.0;
+    o[3] = si.p.x; o[4] = si.p.y; o[5] = si.p.z;
+    o[6] = si.n.x; o[7] = si.n.y; o[8] = si.n.z;
+}
+
+}  // namespace
+
+// =============================================================== C ABI
+struct pbrt_gpu_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int lanes_per_wave = 64;
+    // device scene
+    pbrt_shape_desc* d_shapes = nullptr;
+    pbrt_material_desc* d_materials = nullptr;
+    pbrt_primitive_desc* d_prims = nullptr;
+    pbrt_bvh_node* d_nodes = nullptr;
+    pbrt_light_desc* d_lights = nullptr;
+    pbrt_camera_desc* d_camera = nullptr;
+    pbrt_film_desc* d_film = nullptr;
+    pbrt_distribution_desc* d_dist = nullptr;
+    pbrt_scene_desc host_scene;   // counts + film/camera (pointer fields are not kept)
+    std::vector<pbrt_light_desc> host_lights;
+    // per-render buffers (grown on demand)
+    double* d_films = nullptr;
+    size_t films_cap = 0;
+    double* d_s1d = nullptr;
+    size_t s1d_cap = 0;
+    PanicRec* d_panics = nullptr;
+    size_t panics_cap = 0;
+    Counters* d_ctr = nullptr;
+    double* d_out = nullptr;
+    size_t out_cap = 0;
+    // last render
+    RenderParams rp{};
+    bool rendered = false;
+    std::atomic<int> cancel{0};
+    std::string err;
+    std::chrono::steady_clock::time_point t_start;
+};
+
+namespace {
+
+int set_err(pbrt_gpu_ctx* c, int code, const std::string& m) {
+    if (c) c->err = m;
+    return code;
+}
+#define HIPCHK(ctx, call)                                                                            \
+    do {                                                                                             \
+        hipError_t e_ = (call);                                                                      \
+        if (e_ != hipSuccess)                                                                        \
+            return set_err(ctx, PBRT_E_HIP, std::string(#call ": ") + hipGetErrorString(e_));      \
+    } while (0)
+
+template <class T>
+int upload(pbrt_gpu_ctx* c, T** dst, const T* src, size_t n) {
+    if (n == 0) n = 1;   // keep a valid pointer for empty arrays
+    HIPCHK(c, hipMalloc((void**)dst, sizeof(T) * n));
+    if (src) HIPCHK(c, hipMemcpy(*dst, src, sizeof(T) * n, hipMemcpyHostToDevice));
+    return PBRT_OK;
+}
+template <class T>
+int ensure(pbrt_gpu_ctx* c, T** buf, size_t* cap, size_t n) {
+    if (*cap >= n && *buf) return PBRT_OK;
+    if (*buf) hipFree(*buf);
+    *buf = nullptr;
+    HIPCHK(c, hipMalloc((void**)buf, sizeof(T) * (n ? n : 1)));
+    *cap = n;
+    return PBRT_OK;
+}
+
+DevScene dev_scene(const pbrt_gpu_ctx* c, bool with_dist) {
+    DevScene s;
+    s.shapes = c->d_shapes;
+    s.materials = c->d_materials;
+    s.prims = c->d_prims;
+    s.nodes = c->d_nodes;
+    s.lights = c->d_lights;
+    s.camera = c->d_camera;
+    s.film = c->d_film;
+    s.dist = with_dist ? c->d_dist : nullptr;
+    s.n_prims = c->host_scene.n_prims;
+    s.n_nodes = c->host_scene.n_nodes;
+    s.n_lights = c->host_scene.n_lights;
+    s.pad = 0;
+    return s;
+}
+
+int validate_scene(const pbrt_scene_desc* s) {
+    if (!s) return PBRT_E_INVALID;
+    if (s->n_prims < 0 || s->n_nodes < 0 || s->n_lights < 0 || s->n_shapes < 0 || s->n_materials < 0)
+        return PBRT_E_INVALID;
+    if (s->n_nodes > 65535) return PBRT_E_UNSUPPORTED;   // uint16 LDS stack entries
+    for (int i = 0; i < s->n_prims; i++) {
+        const pbrt_primitive_desc& p = s->prims[i];
+        if (p.shape < 0 || p.shape >= s->n_shapes || p.material < 0 || p.material >= s->n_materials)
+            return PBRT_E_INVALID;
+        if (p.kind != PBRT_PRIM_GEOMETRIC && p.kind != PBRT_PRIM_TRANSFORMED) return PBRT_E_INVALID;
+    }
+    for (int i = 0; i < s->n_shapes; i++)
+        if (s->shapes[i].type != PBRT_SHAPE_SPHERE && s->shapes[i].type != PBRT_SHAPE_DISK) return PBRT_E_UNSUPPORTED;
+    for (int i = 0; i < s->n_nodes; i++) {
+        const pbrt_bvh_node& n = s->nodes[i];
+        if (n.n_prims > 0 && (int64_t)n.offset + n.n_prims > s->n_prims) return PBRT_E_INVALID;
+        if (n.n_prims == 0 && (n.offset >= (uint32_t)s->n_nodes || n.axis > 2)) return PBRT_E_INVALID;
+    }
+    for (int i = 0; i < s->n_lights; i++) {
+        const pbrt_light_desc& l = s->lights[i];
+        if (l.type < PBRT_LIGHT_POINT || l.type > PBRT_LIGHT_DIFFUSE_AREA) return PBRT_E_UNSUPPORTED;
+        if (l.type == PBRT_LIGHT_DIFFUSE_AREA &&
+            (l.shape < 0 || l.shape >= s->n_shapes || s->shapes[l.shape].type != PBRT_SHAPE_SPHERE))
+            return PBRT_E_UNSUPPORTED;
+    }
+    const pbrt_film_desc& f = s->film;
+    if (f.crop_max_x <= f.crop_min_x || f.crop_max_y <= f.crop_min_y) return PBRT_E_INVALID;
+    return PBRT_OK;
+}
+
+int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
+    if (!rd) return set_err(c, PBRT_E_INVALID, "null render desc");
+    if (rd->tile_size <= 0 || rd->sampler_x <= 0 || rd->sampler_y <= 0 || rd->n_dims < 0 || rd->n_dims > 64)
+        return set_err(c, PBRT_E_INVALID, "bad sampler / tile size");
+    if ((int64_t)rd->sampler_x * rd->sampler_y > (1 << 20)) return set_err(c, PBRT_E_INVALID, "spp too large");
+    if (rd->integrator != PBRT_INTEGRATOR_PATH && rd->integrator != PBRT_INTEGRATOR_DIRECT_LIGHTING)
+        return set_err(c, PBRT_E_UNSUPPORTED, "unknown integrator");
+    if (rd->integrator == PBRT_INTEGRATOR_DIRECT_LIGHTING && rd->dl_strategy != PBRT_DL_UNIFORM_SAMPLE_ALL &&
+        rd->dl_strategy != PBRT_DL_UNIFORM_SAMPLE_ONE)
+        return set_err(c, PBRT_E_UNSUPPORTED, "unknown DirectLighting strategy");
+    if (rd->mode != PBRT_MODE_EXACT) return set_err(c, PBRT_E_UNSUPPORTED, "only EXACT mode is implemented");
+    const pbrt_film_desc& f = c->host_scene.film;
+    if (f.filter_radius_x <= 0 || f.filter_radius_y <= 0 || f.filter_radius_x >= (double)rd->tile_size ||
+        f.filter_radius_y >= (double)rd->tile_size)
+        return set_err(c, PBRT_E_UNSUPPORTED, "filter radius must be in (0, tile_size)");
+    RenderParams& rp = c->rp;
+    std::memset(&rp, 0, sizeof(rp));
+    rp.film_min_x = f.crop_min_x;
+    rp.film_min_y = f.crop_min_y;
+    rp.film_w = f.crop_max_x - f.crop_min_x;
+    rp.film_h = f.crop_max_y - f.crop_min_y;
+    rp.tile_size = rd->tile_size;
+    rp.ntx = (rp.film_w + rd->tile_size - 1) / rd->tile_size;
+    rp.nty = (rp.film_h + rd->tile_size - 1) / rd->tile_size;
+    int64_t total = rp.ntx * rp.nty;
+    int64_t begin = rd->tile_begin < 0 ? 0 : rd->tile_begin;
+    int64_t end = rd->tile_end > 0 && rd->tile_end < total ? rd->tile_end : total;
+    int64_t stride = rd->tile_stride > 0 ? rd->tile_stride : 1;
+    rp.tile_begin = begin;
+    rp.tile_stride = stride;
+    rp.n_slots = begin < end ? (end - begin + stride - 1) / stride : 0;
+    rp.slot_w = rd->tile_size + 2 * ((int64_t)f.filter_radius_x + 1);
+    rp.slot_h = rd->tile_size + 2 * ((int64_t)f.filter_radius_y + 1);
+    rp.xs = rd->sampler_x;
+    rp.ys = rd->sampler_y;
+    rp.spp = rd->sampler_x * rd->sampler_y;
+    rp.ndims = rd->n_dims;
+    rp.jitter = rd->jitter ? 1 : 0;
+    rp.integrator = rd->integrator;
+    rp.max_depth = rd->max_depth;
+    rp.dl_strategy = rd->dl_strategy;
+    rp.rr_threshold = rd->rr_threshold;
+    rp.lanes_per_wave = c->lanes_per_wave;
+    if (rd->integrator == PBRT_INTEGRATOR_PATH) {
+        pbrt_distribution_desc dist;
+        int rc = pbrt_scene_light_distribution(&c->host_scene, rd->light_strategy, &dist);
+        if (rc != PBRT_OK) return set_err(c, rc, "unsupported light sample strategy");
+        HIPCHK(c, hipMemcpyAsync(c->d_dist, &dist, sizeof(dist), hipMemcpyHostToDevice, c->stream));
+    }
+    size_t nslot = (size_t)(rp.n_slots > 0 ? rp.n_slots : 1);
+    int rc;
+    if ((rc = ensure(c, &c->d_films, &c->films_cap, nslot * (size_t)(rp.slot_w * rp.slot_h * 3)))) return rc;
+    if ((rc = ensure(c, &c->d_s1d, &c->s1d_cap, nslot * (size_t)(rp.ndims > 0 ? rp.ndims : 1) * (size_t)rp.spp)))
+        return rc;
+    if ((rc = ensure(c, &c->d_panics, &c->panics_cap, nslot))) return rc;
+    if ((rc = ensure(c, &c->d_out, &c->out_cap, (size_t)(rp.film_w * rp.film_h * 3)))) return rc;
+    return PBRT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbrt_gpu_ctx** out) {
+    if (!out) return PBRT_E_INVALID;
+    *out = nullptr;
+    int rc = validate_scene(scene);
+    if (rc != PBRT_OK) return rc;
+    auto* c = new pbrt_gpu_ctx();
+    c->device = (opts && opts->device >= 0) ? opts->device : -1;
+    if (opts && opts->lanes_per_wave > 0 && opts->lanes_per_wave <= 64) c->lanes_per_wave = opts->lanes_per_wave;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        delete c;
+        return PBRT_E_HIP;
+    }
+    if (c->device >= 0) {
+        if (hipSetDevice(c->device) != hipSuccess) { delete c; return PBRT_E_HIP; }
+    } else {
+        hipGetDevice(&c->device);
+    }
+    c->host_scene = *scene;
+    c->host_scene.shapes = nullptr;
+    c->host_scene.materials = nullptr;
+    c->host_scene.prims = nullptr;
+    c->host_scene.nodes = nullptr;
+    c->host_lights.assign(scene->lights, scene->lights + scene->n_lights);
+    c->host_scene.lights = c->host_lights.data();
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        pbrt_gpu_destroy(c);
+        return PBRT_E_HIP;
+    }
+    if ((rc = upload(c, &c->d_shapes, scene->shapes, scene->n_shapes)) ||
+        (rc = upload(c, &c->d_materials, scene->materials, scene->n_materials)) ||
+        (rc = upload(c, &c->d_prims, scene->prims, scene->n_prims)) ||
+        (rc = upload(c, &c->d_nodes, scene->nodes, scene->n_nodes)) ||
+        (rc = upload(c, &c->d_lights, scene->lights, scene->n_lights)) ||
+        (rc = upload(c, &c->d_camera, &scene->camera, 1)) || (rc = upload(c, &c->d_film, &scene->film, 1)) ||
+        (rc = upload<pbrt_distribution_desc>(c, &c->d_dist, nullptr, 1)) ||
+        (rc = upload<Counters>(c, &c->d_ctr, nullptr, 1))) {
+        pbrt_gpu_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return PBRT_OK;
+}
+
+int pbrt_gpu_render_async(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
+    if (!c) return PBRT_E_INVALID;
+    if (c->cancel.load()) return set_err(c, PBRT_E_CANCELLED, "cancelled");
+    HIPCHK(c, hipSetDevice(c->device));
+    c->t_start = std::chrono::steady_clock::now();
+    int rc = prepare(c, rd);
+    if (rc != PBRT_OK) return rc;
+    const RenderParams& rp = c->rp;
+    HIPCHK(c, hipMemsetAsync(c->d_ctr, 0, sizeof(Counters), c->stream));
+    if (rp.n_slots > 0) HIPCHK(c, hipMemsetAsync(c->d_panics, 0, sizeof(PanicRec) * (size_t)rp.n_slots, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    if (rp.n_slots > 0) {
+        DevScene sc = dev_scene(c, rd->integrator == PBRT_INTEGRATOR_PATH);
+        int64_t blocks = (rp.n_slots + rp.lanes_per_wave - 1) / rp.lanes_per_wave;
+        hipLaunchKernelGGL(k_render_exact, dim3((unsigned)blocks), dim3(kWave), 0, c->stream, sc, rp, c->d_films,
+                           c->d_s1d, c->d_panics, c->d_ctr);
+        HIPCHK(c, hipGetLastError());
+    }
+    int64_t npx = rp.film_w * rp.film_h;
+    hipLaunchKernelGGL(k_merge_film, dim3((unsigned)((npx + 255) / 256)), dim3(256), 0, c->stream, c->d_film, rp,
+                       c->d_films, c->d_out);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    c->rendered = true;
+    return PBRT_OK;
+}
+
+int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
+    if (!c) return PBRT_E_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    Counters ctr;
+    HIPCHK(c, hipMemcpy(&ctr, c->d_ctr, sizeof(ctr), hipMemcpyDeviceToHost));
+    float ms = 0;
+    hipEventElapsedTime(&ms, c->ev0, c->ev1);
+    int rc = PBRT_OK;
+    pbrt_gpu_stats st;
+    std::memset(&st, 0, sizeof(st));
+    st.tiles_rendered = (uint64_t)c->rp.n_slots;
+    st.camera_samples = ctr.camera_samples;
+    st.paths_traced = ctr.paths;
+    st.kernel_ms = ms;
+    if (ctr.any_panic) {
+        std::vector<PanicRec> pr((size_t)c->rp.n_slots);
+        HIPCHK(c, hipMemcpy(pr.data(), c->d_panics, sizeof(PanicRec) * pr.size(), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < pr.size(); i++) {
+            if (pr[i].kind == 0) continue;
+            st.panic_kind = pr[i].kind;
+            st.panic_tile = (int32_t)(c->rp.tile_begin + (int64_t)i * c->rp.tile_stride);
+            st.panic_pixel_x = pr[i].px;
+            st.panic_pixel_y = pr[i].py;
+            st.panic_sample = pr[i].sample;
+            st.panic_bounce = pr[i].bounce;
+            break;
+        }
+        if (st.panic_kind == -1) {
+            rc = set_err(c, PBRT_E_UNSUPPORTED, "material not on the hot path (OrenNayar)");
+            st.panic_kind = 0;
+        } else {
+            rc = set_err(c, PBRT_E_REF_PANIC, "the Go reference panics on this input");
+        }
+    }
+    st.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c->t_start).count();
+    if (stats) *stats = st;
+    return rc;
+}
+
+int pbrt_gpu_render(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_xyz, pbrt_gpu_stats* stats) {
+    if (!c) return PBRT_E_INVALID;
+    int rc = pbrt_gpu_render_async(c, rd);
+    if (rc != PBRT_OK) return rc;
+    rc = pbrt_gpu_synchronize(c, stats);
+    if (rc != PBRT_OK) return rc;
+    if (film_xyz) return pbrt_gpu_film_download(c, film_xyz);
+    return PBRT_OK;
+}
+
+double* pbrt_gpu_film_device(pbrt_gpu_ctx* c) { return c ? c->d_out : nullptr; }
+void* pbrt_gpu_stream(pbrt_gpu_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int pbrt_gpu_film_download(pbrt_gpu_ctx* c, double* film_xyz) {
+    if (!c || !film_xyz || !c->rendered) return PBRT_E_INVALID;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpy(film_xyz, c->d_out, sizeof(double) * (size_t)(c->rp.film_w * c->rp.film_h * 3),
+                        hipMemcpyDeviceToHost));
+    return PBRT_OK;
+}
+
+static int intersect_batch(pbrt_gpu_ctx* c, const pbrt_ray_soa* rays, size_t n, int any, pbrt_hit_soa* hits,
+                           uint8_t* occluded) {
+    if (!c || !rays || (!hits && !occluded)) return PBRT_E_INVALID;
+    if (n == 0) return PBRT_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    std::vector<double> packed(n * 7);
+    for (size_t i = 0; i < n; i++) {
+        double* q = &packed[7 * i];
+        q[0] = rays->ox[i]; q[1] = rays->oy[i]; q[2] = rays->oz[i];
+        q[3] = rays->dx[i]; q[4] = rays->dy[i]; q[5] = rays->dz[i];
+        q[6] = rays->tmax ? rays->tmax[i] : gomath::kInf;
+    }
+    size_t nout = any ? n : 9 * n;
+    double *d_in = nullptr, *d_o = nullptr;
+    HIPCHK(c, hipMalloc((void**)&d_in, sizeof(double) * packed.size()));
+    if (hipMalloc((void**)&d_o, sizeof(double) * nout) != hipSuccess) {
+        hipFree(d_in);
+        return set_err(c, PBRT_E_HIP, "hipMalloc");
+    }
+    std::vector<double> o(nout);
+    hipError_t e = hipMemcpyAsync(d_in, packed.data(), sizeof(double) * packed.size(), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) {
+        DevScene sc = dev_scene(c, false);
+        hipLaunchKernelGGL(k_intersect, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave), 0, c->stream, sc,
+                           (int64_t)n, d_in, d_o, any);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(o.data(), d_o, sizeof(double) * nout, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    hipFree(d_in);
+    hipFree(d_o);
+    if (e != hipSuccess) return set_err(c, PBRT_E_HIP, hipGetErrorString(e));
+    int rc = PBRT_OK;
+    for (size_t i = 0; i < n; i++) {
+        if (any) {
+            if (gomath::is_nan(o[i])) rc = PBRT_E_REF_PANIC;
+            occluded[i] = o[i] == 1.0;
+        } else {
+            const double* r = &o[9 * i];
+            if (gomath::is_nan(r[0])) { rc = PBRT_E_REF_PANIC; hits->hit[i] = 0; continue; }
+            hits->hit[i] = r[0] == 1.0;
+            if (hits->t_max) hits->t_max[i] = r[1];
+            if (hits->prim) hits->prim[i] = (int32_t)r[2];
+            if (hits->px) hits->px[i] = r[3];
+            if (hits->py) hits->py[i] = r[4];
+            if (hits->pz) hits->pz[i] = r[5];
+            if (hits->nx) hits->nx[i] = r[6];
+            if (hits->ny) hits->ny[i] = r[7];
+            if (hits->nz) hits->nz[i] = r[8];
+        }
+    }
+    if (rc != PBRT_OK) set_err(c, rc, "the Go reference panics on at least one ray");
+    return rc;
+}
+
+int pbrt_gpu_intersect(pbrt_gpu_ctx* c, const pbrt_ray_soa* rays, size_t n, pbrt_hit_soa* hits) {
+    return intersect_batch(c, rays, n, 0, hits, nullptr);
+}
+int pbrt_gpu_intersect_p(pbrt_gpu_ctx* c, const pbrt_ray_soa* rays, size_t n, uint8_t* occluded) {
+    return intersect_batch(c, rays, n, 1, nullptr, occluded);
+}
+
+void pbrt_gpu_cancel(pbrt_gpu_ctx* c) {
+    if (c) c->cancel.store(1);
+}
+const char* pbrt_gpu_last_error(const pbrt_gpu_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    void* bufs[] = {c->d_shapes, c->d_materials, c->d_prims, c->d_nodes, c->d_lights, c->d_camera, c->d_film,
+                    c->d_dist,   c->d_films,     c->d_s1d,   c->d_panics, c->d_ctr,   c->d_out};
+    for (void* b : bufs)
+        if (b) hipFree(b);
+    if (c->ev0) hipEventDestroy(c->ev0);
+    if (c->ev1) hipEventDestroy(c->ev1);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+// film.go:142-179 WriteImage pixel conversion
+int pbrt_film_to_rgba8(const double* film, int64_t w, int64_t h, uint8_t* rgba) {
+    if (!film || !rgba || w <= 0 || h <= 0) return PBRT_E_INVALID;
+    for (int64_t i = 0; i < w * h; i++) {
+        for (int c = 0; c < 3; c++)
+            rgba[i * 4 + c] = (uint8_t)(gomath::to_int(gomath::clamp(film[i * 3 + c], 0, 1) * 255) & 0xFF);
+        rgba[i * 4 + 3] = 255;
+    }
+    return PBRT_OK;
+}
+
+}  // extern "C"

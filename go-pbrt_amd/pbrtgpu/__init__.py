@@ -1,0 +1,369 @@
+"""pbrtgpu — Python host wrapper over the C ABI of the MI355X hot path.
+
+The product is the C-ABI library lib/libpbrt_gpu.so (include/pbrt_gpu.h,
+include/pbrt_scene.h). This module only loads it with ctypes and mirrors the
+reference's driver-side vocabulary so tests and bench read like go-pbrt:
+
+    scene = Scene.readme(1920, 1080)            # internal/render/server.go:29-164
+    with Renderer(scene) as r:                  # pbrt_gpu_create
+        film, stats = r.render(render_desc())   # pbrt.Render -> fp64 XYZ film
+
+There is deliberately no CPU fallback: if the HIP library is missing or no
+GPU is visible, construction raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+from .abi import *  # noqa: F401,F403  (re-export the ABI constants/structs)
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libpbrt_gpu.so")
+
+_lib = None
+
+
+class PbrtError(RuntimeError):
+    def __init__(self, code, msg, stats=None):
+        super().__init__(f"pbrt status {code}: {msg}")
+        self.code = code
+        self.stats = stats
+
+
+def lib():
+    """Load lib/libpbrt_gpu.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FileNotFoundError(f"{LIB_PATH} missing: run `make -C go-pbrt_amd` (or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    P, d, i64 = C.POINTER, C.c_double, C.c_int64
+    T = P(abi.Transform)
+    L.pbrt_gpu_create.argtypes = [P(abi.SceneDesc), P(abi.GpuOpts), P(C.c_void_p)]
+    L.pbrt_gpu_render.argtypes = [C.c_void_p, P(abi.RenderDesc), P(d), P(abi.GpuStats)]
+    L.pbrt_gpu_render_async.argtypes = [C.c_void_p, P(abi.RenderDesc)]
+    L.pbrt_gpu_synchronize.argtypes = [C.c_void_p, P(abi.GpuStats)]
+    L.pbrt_gpu_film_device.argtypes = [C.c_void_p]
+    L.pbrt_gpu_film_device.restype = C.c_void_p
+    L.pbrt_gpu_film_download.argtypes = [C.c_void_p, P(d)]
+    L.pbrt_gpu_stream.argtypes = [C.c_void_p]
+    L.pbrt_gpu_stream.restype = C.c_void_p
+    L.pbrt_gpu_intersect.argtypes = [C.c_void_p, P(abi.RaySoA), C.c_size_t, P(abi.HitSoA)]
+    L.pbrt_gpu_intersect_p.argtypes = [C.c_void_p, P(abi.RaySoA), C.c_size_t, P(C.c_uint8)]
+    L.pbrt_gpu_cancel.argtypes = [C.c_void_p]
+    L.pbrt_gpu_cancel.restype = None
+    L.pbrt_gpu_last_error.argtypes = [C.c_void_p]
+    L.pbrt_gpu_last_error.restype = C.c_char_p
+    L.pbrt_gpu_destroy.argtypes = [C.c_void_p]
+    L.pbrt_gpu_destroy.restype = None
+    L.pbrt_film_to_rgba8.argtypes = [P(d), i64, i64, P(C.c_uint8)]
+    for name in ("pbrt_translate", "pbrt_scale"):
+        getattr(L, name).argtypes = [d, d, d, T]
+        getattr(L, name).restype = None
+    for name in ("pbrt_rotate_x", "pbrt_rotate_y", "pbrt_rotate_z"):
+        getattr(L, name).argtypes = [d, T]
+        getattr(L, name).restype = None
+    L.pbrt_transform_mul.argtypes = [T, T, T]
+    L.pbrt_transform_mul.restype = None
+    L.pbrt_transform_inverse.argtypes = [T, T]
+    L.pbrt_transform_inverse.restype = None
+    L.pbrt_matrix_inverse.argtypes = [P(abi.Matrix4x4), P(abi.Matrix4x4)]
+    L.pbrt_new_transform.argtypes = [P(abi.Matrix4x4), T]
+    L.pbrt_look_at.argtypes = [P(d), P(d), P(d), T]
+    L.pbrt_perspective.argtypes = [d, d, d, T]
+    L.pbrt_perspective.restype = None
+    L.pbrt_transform_point.argtypes = [T, P(d), P(d), P(d), P(d)]
+    L.pbrt_transform_point.restype = None
+    L.pbrt_transform_ray.argtypes = [T, P(d), P(d), P(d), P(d)]
+    L.pbrt_transform_ray.restype = None
+    L.pbrt_make_sphere.argtypes = [T, C.c_int, d, d, d, d, P(abi.ShapeDesc)]
+    L.pbrt_make_sphere.restype = None
+    L.pbrt_make_disk.argtypes = [T, d, d, d, d, P(abi.ShapeDesc)]
+    L.pbrt_make_disk.restype = None
+    L.pbrt_make_matte_constant.argtypes = [d, d, d, d, P(abi.MaterialDesc)]
+    L.pbrt_make_matte_constant.restype = None
+    L.pbrt_make_matte_checkerboard.argtypes = [P(d), P(d), d, d, P(d), P(d), d, P(abi.MaterialDesc)]
+    L.pbrt_make_matte_checkerboard.restype = None
+    L.pbrt_make_point_light.argtypes = [T, P(d), P(abi.LightDesc)]
+    L.pbrt_make_point_light.restype = None
+    L.pbrt_make_distant_light.argtypes = [T, P(d), P(d), P(abi.LightDesc)]
+    L.pbrt_make_distant_light.restype = None
+    L.pbrt_make_diffuse_area_light.argtypes = [P(d), C.c_int, C.c_int, P(abi.LightDesc)]
+    L.pbrt_make_diffuse_area_light.restype = None
+    L.pbrt_sb_create.restype = C.c_void_p
+    L.pbrt_sb_destroy.argtypes = [C.c_void_p]
+    L.pbrt_sb_destroy.restype = None
+    L.pbrt_sb_add_shape.argtypes = [C.c_void_p, P(abi.ShapeDesc)]
+    L.pbrt_sb_add_material.argtypes = [C.c_void_p, P(abi.MaterialDesc)]
+    L.pbrt_sb_add_primitive.argtypes = [C.c_void_p, P(abi.PrimitiveDesc)]
+    L.pbrt_sb_add_light.argtypes = [C.c_void_p, P(abi.LightDesc)]
+    L.pbrt_sb_set_film.argtypes = [C.c_void_p, i64, i64, P(d), d, d, d]
+    L.pbrt_sb_set_perspective_camera.argtypes = [C.c_void_p, T, P(d), d, d, d, d, d]
+    L.pbrt_sb_build.argtypes = [C.c_void_p, C.c_int, P(P(abi.SceneDesc))]
+    L.pbrt_sb_prim_order.argtypes = [C.c_void_p, P(C.c_int32), C.c_int]
+    L.pbrt_scene_light_distribution.argtypes = [P(abi.SceneDesc), C.c_int, P(abi.DistributionDesc)]
+    L.pbrt_scene_readme.argtypes = [i64, i64, P(C.c_void_p)]
+    L.pbrt_scene_cornell.argtypes = [i64, i64, P(C.c_void_p)]
+    _lib = L
+    return L
+
+
+def _d3(v):
+    return (C.c_double * 3)(*v)
+
+
+# ------------------------------------------------------------------ transforms
+def translate(x, y, z):
+    t = abi.Transform()
+    lib().pbrt_translate(x, y, z, C.byref(t))
+    return t
+
+
+def scale(x, y, z):
+    t = abi.Transform()
+    lib().pbrt_scale(x, y, z, C.byref(t))
+    return t
+
+
+def rotate(axis, degrees):
+    t = abi.Transform()
+    getattr(lib(), "pbrt_rotate_" + "xyz"[axis])(degrees, C.byref(t))
+    return t
+
+
+def mul(a, b):
+    t = abi.Transform()
+    lib().pbrt_transform_mul(C.byref(a), C.byref(b), C.byref(t))
+    return t
+
+
+def look_at(pos, look, up):
+    t = abi.Transform()
+    rc = lib().pbrt_look_at(_d3(pos), _d3(look), _d3(up), C.byref(t))
+    if rc:
+        raise PbrtError(rc, "LookAt: up parallel to view direction")
+    return t
+
+
+def transform_ray(t, o, d):
+    oo, od = (C.c_double * 3)(), (C.c_double * 3)()
+    lib().pbrt_transform_ray(C.byref(t), _d3(o), _d3(d), oo, od)
+    return list(oo), list(od)
+
+
+# ------------------------------------------------------------------------ scene
+class Scene:
+    """A pbrt_scene_builder plus its built pbrt_scene_desc."""
+
+    def __init__(self, handle=None):
+        self.h = handle if handle is not None else lib().pbrt_sb_create()
+        self.desc_ptr = None
+
+    @classmethod
+    def readme(cls, w, h):
+        hb = C.c_void_p()
+        rc = lib().pbrt_scene_readme(w, h, C.byref(hb))
+        if rc:
+            raise PbrtError(rc, "pbrt_scene_readme")
+        s = cls(hb.value)
+        s._fetch()
+        return s
+
+    @classmethod
+    def cornell(cls, w, h):
+        hb = C.c_void_p()
+        rc = lib().pbrt_scene_cornell(w, h, C.byref(hb))
+        if rc:
+            raise PbrtError(rc, "pbrt_scene_cornell")
+        s = cls(hb.value)
+        s._fetch()
+        return s
+
+    # builder API (pbrt_sb_*) -------------------------------------------------
+    def add_sphere(self, o2w, radius, reverse=False, z_min=None, z_max=None, phi_max=360.0):
+        sd = abi.ShapeDesc()
+        lib().pbrt_make_sphere(C.byref(o2w), int(reverse), radius, -radius if z_min is None else z_min,
+                               radius if z_max is None else z_max, phi_max, C.byref(sd))
+        return lib().pbrt_sb_add_shape(self.h, C.byref(sd))
+
+    def add_disk(self, o2w, height, radius, inner=0.0, phi_max=360.0):
+        sd = abi.ShapeDesc()
+        lib().pbrt_make_disk(C.byref(o2w), height, radius, inner, phi_max, C.byref(sd))
+        return lib().pbrt_sb_add_shape(self.h, C.byref(sd))
+
+    def add_matte(self, rgb, sigma=0.0):
+        m = abi.MaterialDesc()
+        lib().pbrt_make_matte_constant(rgb[0], rgb[1], rgb[2], sigma, C.byref(m))
+        return lib().pbrt_sb_add_material(self.h, C.byref(m))
+
+    def add_checker(self, vs, vt, ds, dt, tex1, tex2, sigma=0.0):
+        m = abi.MaterialDesc()
+        lib().pbrt_make_matte_checkerboard(_d3(vs), _d3(vt), ds, dt, _d3(tex1), _d3(tex2), sigma, C.byref(m))
+        return lib().pbrt_sb_add_material(self.h, C.byref(m))
+
+    def add_primitive(self, shape, material, prim_to_world=None):
+        p = abi.PrimitiveDesc()
+        p.shape, p.material = shape, material
+        if prim_to_world is None:
+            p.kind = abi.PBRT_PRIM_GEOMETRIC
+        else:
+            p.kind = abi.PBRT_PRIM_TRANSFORMED
+            p.prim_to_world = prim_to_world
+        return lib().pbrt_sb_add_primitive(self.h, C.byref(p))
+
+    def add_point_light(self, l2w, I):
+        ld = abi.LightDesc()
+        lib().pbrt_make_point_light(C.byref(l2w), _d3(I), C.byref(ld))
+        return lib().pbrt_sb_add_light(self.h, C.byref(ld))
+
+    def add_distant_light(self, l2w, L, w):
+        ld = abi.LightDesc()
+        lib().pbrt_make_distant_light(C.byref(l2w), _d3(L), _d3(w), C.byref(ld))
+        return lib().pbrt_sb_add_light(self.h, C.byref(ld))
+
+    def add_area_light(self, Lemit, shape, two_sided=False):
+        ld = abi.LightDesc()
+        lib().pbrt_make_diffuse_area_light(_d3(Lemit), shape, int(two_sided), C.byref(ld))
+        return lib().pbrt_sb_add_light(self.h, C.byref(ld))
+
+    def set_film(self, w, h, crop=(0, 0, 1, 1), filter_radius=(1.0, 1.0), max_lum=1.0):
+        rc = lib().pbrt_sb_set_film(self.h, w, h, (C.c_double * 4)(*crop), filter_radius[0], filter_radius[1], max_lum)
+        if rc:
+            raise PbrtError(rc, "set_film")
+
+    def set_camera(self, cam2world, screen=(0, 0, 1, 1), shutter=(0.0, 1.0), lens=0.0, focal=20.0, fov=100.0):
+        rc = lib().pbrt_sb_set_perspective_camera(self.h, C.byref(cam2world), (C.c_double * 4)(*screen),
+                                                  shutter[0], shutter[1], lens, focal, fov)
+        if rc:
+            raise PbrtError(rc, "set_camera")
+
+    def build(self, max_prims_in_node=2):
+        """accelerator.NewBVH(prims, maxPrimsInNode, SplitSAH) + pbrt.NewScene."""
+        ptr = C.POINTER(abi.SceneDesc)()
+        rc = lib().pbrt_sb_build(self.h, max_prims_in_node, C.byref(ptr))
+        if rc:
+            raise PbrtError(rc, "pbrt_sb_build")
+        self.desc_ptr = ptr
+        return self
+
+    def _fetch(self):
+        # fixtures are already built (maxPrimsInNode 2); rebuilding is idempotent
+        self.build(2)
+
+    @property
+    def desc(self):
+        return self.desc_ptr.contents
+
+    def prim_order(self):
+        n = self.desc.n_prims
+        out = (C.c_int32 * max(n, 1))()
+        lib().pbrt_sb_prim_order(self.h, out, n)
+        return list(out)[:n]
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.pbrt_sb_destroy(self.h)
+            self.h = None
+
+
+# --------------------------------------------------------------------- renderer
+class Renderer:
+    """pbrt_gpu_ctx: the scene resident on one GPU."""
+
+    def __init__(self, scene, device=-1, lanes_per_wave=0):
+        desc = scene.desc if isinstance(scene, Scene) else scene
+        self._scene = scene  # keep the descriptor alive
+        opts = abi.GpuOpts()
+        opts.device, opts.lanes_per_wave = device, lanes_per_wave
+        h = C.c_void_p()
+        rc = lib().pbrt_gpu_create(C.byref(desc), C.byref(opts), C.byref(h))
+        if rc:
+            raise PbrtError(rc, "pbrt_gpu_create failed (no GPU visible?)")
+        self.h = h.value
+        self.w = desc.film.crop_max_x - desc.film.crop_min_x
+        self.hgt = desc.film.crop_max_y - desc.film.crop_min_y
+
+    def _check(self, rc, stats=None):
+        if rc:
+            raise PbrtError(rc, lib().pbrt_gpu_last_error(self.h).decode(), stats)
+
+    def render(self, rd):
+        film = np.zeros((self.hgt, self.w, 3), dtype=np.float64)
+        st = abi.GpuStats()
+        rc = lib().pbrt_gpu_render(self.h, C.byref(rd), film.ctypes.data_as(C.POINTER(C.c_double)), C.byref(st))
+        self._check(rc, st)
+        return film, st
+
+    def render_async(self, rd):
+        self._check(lib().pbrt_gpu_render_async(self.h, C.byref(rd)))
+
+    def synchronize(self):
+        st = abi.GpuStats()
+        self._check(lib().pbrt_gpu_synchronize(self.h, C.byref(st)), st)
+        return st
+
+    def film(self):
+        film = np.zeros((self.hgt, self.w, 3), dtype=np.float64)
+        self._check(lib().pbrt_gpu_film_download(self.h, film.ctypes.data_as(C.POINTER(C.c_double))))
+        return film
+
+    def film_device_ptr(self):
+        return lib().pbrt_gpu_film_device(self.h)
+
+    def stream(self):
+        return lib().pbrt_gpu_stream(self.h)
+
+    def intersect(self, rays):
+        """rays: (n,7) [ox,oy,oz,dx,dy,dz,tmax] -> (n,9) like the oracle."""
+        rays = np.ascontiguousarray(rays, dtype=np.float64)
+        n = rays.shape[0]
+        cols = [np.ascontiguousarray(rays[:, k]) for k in range(7)]
+        soa = abi.RaySoA(*[c.ctypes.data_as(C.POINTER(C.c_double)) for c in cols])
+        hit = np.zeros(n, np.uint8)
+        tmax = np.zeros(n)
+        prim = np.zeros(n, np.int32)
+        p = [np.zeros(n) for _ in range(6)]
+        hs = abi.HitSoA(hit.ctypes.data_as(C.POINTER(C.c_uint8)), tmax.ctypes.data_as(C.POINTER(C.c_double)),
+                        prim.ctypes.data_as(C.POINTER(C.c_int32)),
+                        *[a.ctypes.data_as(C.POINTER(C.c_double)) for a in p])
+        rc = lib().pbrt_gpu_intersect(self.h, C.byref(soa), n, C.byref(hs))
+        out = np.stack([hit.astype(np.float64), tmax, prim.astype(np.float64)] + p, axis=1)
+        return rc, out
+
+    def intersect_p(self, rays):
+        rays = np.ascontiguousarray(rays, dtype=np.float64)
+        n = rays.shape[0]
+        cols = [np.ascontiguousarray(rays[:, k]) for k in range(7)]
+        soa = abi.RaySoA(*[c.ctypes.data_as(C.POINTER(C.c_double)) for c in cols])
+        occ = np.zeros(n, np.uint8)
+        rc = lib().pbrt_gpu_intersect_p(self.h, C.byref(soa), n, occ.ctypes.data_as(C.POINTER(C.c_uint8)))
+        return rc, occ
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().pbrt_gpu_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        self.close()
+
+
+def film_to_rgba8(film):
+    """film.go:142-179 WriteImage pixel conversion (no XYZ->RGB, no gamma)."""
+    film = np.ascontiguousarray(film, dtype=np.float64)
+    h, w, _ = film.shape
+    out = np.zeros((h, w, 4), np.uint8)
+    rc = lib().pbrt_film_to_rgba8(film.ctypes.data_as(C.POINTER(C.c_double)), w, h,
+                                  out.ctypes.data_as(C.POINTER(C.c_uint8)))
+    if rc:
+        raise PbrtError(rc, "film_to_rgba8")
+    return out

@@ -1,0 +1,277 @@
+/*
+ * pbrt_gpu.h — C ABI of the MI355X-native go-pbrt hot path.
+ *
+ * This is the drop-in boundary for go-pbrt's ray–scene intersection and
+ * path-tracing inner loop. A cgo shim binds exactly these entry points (see
+ * INTEGRATION.md). Every call is frame- or batch-granular: the reference's
+ * per-ray interfaces (pbrt.Integrator.Li, pbrt.Aggregate.Intersect) cost a
+ * cgo hop each and can never be the device boundary.
+ *
+ * Reference interfaces replaced (paths relative to ssttuu/go-pbrt):
+ *   pbrt_gpu_render       <- pbrt.Render(ctx, Integrator, Scene, tileSize)
+ *                            pkg/pbrt/integrator.go:291-350 (with Path.Li
+ *                            pkg/integrator/path.go:32-157 and
+ *                            DirectLighting.Li pkg/integrator/directlighting.go:62-104
+ *                            executed on the device)
+ *   pbrt_gpu_intersect    <- (*accelerator.BVH).Intersect  pkg/accelerator/bvh.go:659-712
+ *   pbrt_gpu_intersect_p  <- (*accelerator.BVH).IntersectP pkg/accelerator/bvh.go:713-765
+ *   pbrt_gpu_cancel       <- ctx.Done() / errgroup cancellation, integrator.go:305-345
+ *   PBRT_E_REF_PANIC      <- the places where the reference panics instead of
+ *                            returning: integrator.go:73-75 (Ld > 10),
+ *                            pkg/efloat/efloat.go:102-111 (EFloat Check)
+ *
+ * Conventions: plain C11, no exceptions across the ABI, caller-owned output
+ * buffers, every function returns a pbrt_status (0 = OK). All arithmetic is
+ * IEEE-754 binary64 with Go (amd64) semantics; descriptors carry matrices
+ * exactly as the Go host computed them.
+ */
+#ifndef PBRT_GPU_H
+#define PBRT_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ status */
+typedef enum pbrt_status {
+    PBRT_OK = 0,
+    PBRT_E_INVALID = 1,      /* bad descriptor / argument                     */
+    PBRT_E_HIP = 2,          /* HIP runtime failure                           */
+    PBRT_E_RCCL = 3,         /* collective failure (multi-GPU film reduce)    */
+    PBRT_E_CANCELLED = 4,    /* pbrt_gpu_cancel() observed                    */
+    PBRT_E_REF_PANIC = 5,    /* the Go reference would have panicked here     */
+    PBRT_E_UNSUPPORTED = 6   /* descriptor uses a feature not on the hot path */
+} pbrt_status;
+
+/* panic kinds reported in pbrt_gpu_stats.panic_kind */
+enum {
+    PBRT_PANIC_NONE = 0,
+    PBRT_PANIC_LD_GT_10 = 1,     /* integrator.go:73-75                      */
+    PBRT_PANIC_EFLOAT = 2,       /* efloat.go:102-111                        */
+    PBRT_PANIC_BVH_STACK = 3     /* bvh.go:670 fixed [64] stack overflow     */
+};
+
+/* --------------------------------------------------------------- transform */
+/* pkg/pbrt/transform.go:27 Matrix4x4, :144 Transform{Matrix, MatrixInverse} */
+typedef struct pbrt_matrix4x4 { double m[4][4]; } pbrt_matrix4x4;
+typedef struct pbrt_transform { pbrt_matrix4x4 m, m_inv; } pbrt_transform;
+
+/* ------------------------------------------------------------------ shapes */
+enum { PBRT_SHAPE_SPHERE = 1, PBRT_SHAPE_DISK = 2 };
+
+/* pkg/pbrt/sphere.go:8-17 Sphere, pkg/shapes/disk.go:14-20 Disk.
+ * world_to_object is object_to_world.Inverse() (matrix/inverse swapped). */
+typedef struct pbrt_shape_desc {
+    int32_t type;
+    int32_t reverse_orientation;
+    int32_t transform_swaps_handedness;
+    int32_t pad0;
+    pbrt_transform object_to_world;
+    double radius;
+    double z_min, z_max, theta_min, theta_max, phi_max;   /* sphere           */
+    double height, inner_radius;                          /* disk             */
+} pbrt_shape_desc;
+
+/* --------------------------------------------------------------- materials */
+enum { PBRT_TEX_CONSTANT = 1, PBRT_TEX_CHECKERBOARD2D = 2 };
+
+/* pkg/materials/matte.go:8-37 MatteMaterial with Kd either a
+ * ConstantSpectrumTexture (pkg/pbrt/texture.go:133-145) or a Checkerboard2D
+ * over PlanarMapping2D (pkg/textures/checkerboard.go, texture.go:105-123) whose
+ * two sub-textures are constants. sigma is a ConstantFloatTexture. */
+typedef struct pbrt_material_desc {
+    int32_t kd_type;
+    int32_t pad0;
+    double kd[3];
+    double vs[3], vt[3], ds, dt;
+    double tex1[3], tex2[3];
+    double sigma;
+} pbrt_material_desc;
+
+/* -------------------------------------------------------------- primitives */
+enum { PBRT_PRIM_GEOMETRIC = 1, PBRT_PRIM_TRANSFORMED = 2 };
+
+/* GeometricPrimitive (pkg/pbrt/primitive.go:22-78), optionally wrapped in a
+ * TransformedPrimitive with a non-animated AnimatedTransform (primitive.go:89-129). */
+typedef struct pbrt_primitive_desc {
+    int32_t kind;
+    int32_t shape;
+    int32_t material;
+    int32_t pad0;
+    pbrt_transform prim_to_world;
+} pbrt_primitive_desc;
+
+/* flattened BVH node, pkg/accelerator/bvh.go:80-87 LinearBVHNode */
+typedef struct pbrt_bvh_node {
+    double bmin[3], bmax[3];
+    uint32_t offset;      /* primitiveOffset (leaf) | secondChildOffset (interior) */
+    uint16_t n_prims;     /* 0 => interior */
+    uint8_t axis;
+    uint8_t pad0;
+} pbrt_bvh_node;
+
+/* ------------------------------------------------------------------ lights */
+enum { PBRT_LIGHT_POINT = 1, PBRT_LIGHT_DISTANT = 2, PBRT_LIGHT_DIFFUSE_AREA = 3 };
+
+/* pkg/lights/{point,distant,diffuse}.go */
+typedef struct pbrt_light_desc {
+    int32_t type;
+    int32_t shape;          /* DIFFUSE_AREA: index into shapes (a sphere)    */
+    int32_t two_sided;      /* DIFFUSE_AREA                                  */
+    int32_t pad0;
+    double spectrum[3];     /* Point.I | Distant.L | DiffuseAreaLight.LEmit  */
+    double p_light[3];      /* Point: lightToWorld(0,0,0)                    */
+    double w_light[3];      /* Distant: normalized world direction           */
+    double world_radius;    /* Distant: set by Preprocess (BoundingSphere)   */
+} pbrt_light_desc;
+
+/* ------------------------------------------------------------------ camera */
+/* PerspectiveCamera (pkg/pbrt/camera.go:128-242). shutter_close is stored as
+ * the reference leaves it: NewProjectiveCamera passes shutterOpen twice
+ * (camera.go:116), so both fields hold shutterOpen. */
+typedef struct pbrt_camera_desc {
+    pbrt_transform camera_to_world;
+    pbrt_transform raster_to_camera;
+    double lens_radius, focal_distance, shutter_open, shutter_close;
+} pbrt_camera_desc;
+
+/* -------------------------------------------------------------------- film */
+/* pkg/pbrt/film.go:27-76 (CroppedPixelBounds, BoxFilter radius, filter table) */
+typedef struct pbrt_film_desc {
+    int64_t res_x, res_y;
+    int64_t crop_min_x, crop_min_y, crop_max_x, crop_max_y;
+    double filter_radius_x, filter_radius_y;
+    double max_sample_luminance;
+    double filter_table[16 * 16];
+} pbrt_film_desc;
+
+/* light-selection distribution (pkg/pbrt/sampling.go:5-55 Distribution1D),
+ * computed by the host from the integrator's LightSampleStrategy
+ * (lightdistribution.go). func has n entries, cdf n+1. */
+#define PBRT_MAX_DIST 64
+typedef struct pbrt_distribution_desc {
+    int32_t count;
+    int32_t pad0;
+    double func_int;
+    double func[PBRT_MAX_DIST];
+    double cdf[PBRT_MAX_DIST + 1];
+} pbrt_distribution_desc;
+
+/* ------------------------------------------------------------------- scene */
+typedef struct pbrt_scene_desc {
+    int32_t n_shapes, n_materials, n_prims, n_nodes, n_lights, pad0;
+    const pbrt_shape_desc* shapes;
+    const pbrt_material_desc* materials;
+    const pbrt_primitive_desc* prims;      /* BVH order (orderedPrims)        */
+    const pbrt_bvh_node* nodes;            /* depth-first, bvh.go:632-651     */
+    const pbrt_light_desc* lights;
+    pbrt_camera_desc camera;
+    pbrt_film_desc film;
+    double world_min[3], world_max[3];     /* Scene.WorldBound (BVH root)     */
+} pbrt_scene_desc;
+
+/* ------------------------------------------------------------------ render */
+enum { PBRT_INTEGRATOR_PATH = 1, PBRT_INTEGRATOR_DIRECT_LIGHTING = 2 };
+enum { PBRT_LIGHT_STRATEGY_UNIFORM = 1, PBRT_LIGHT_STRATEGY_POWER = 2 };
+enum { PBRT_DL_UNIFORM_SAMPLE_ALL = 1, PBRT_DL_UNIFORM_SAMPLE_ONE = 2 };
+
+/* Execution modes.
+ *  EXACT: the reference's per-tile RNG stream replayed bit-for-bit
+ *         (integrator.go:318,328; one sampler clone per 16-px tile).
+ *  THROUGHPUT: identical arithmetic, but every (pixel, sample) path gets its
+ *         own PCG32 stream => statistically (not bitwise) equal images. */
+enum { PBRT_MODE_EXACT = 0, PBRT_MODE_THROUGHPUT = 1 };
+
+typedef struct pbrt_render_desc {
+    /* sampler: sampler.NewStratified(x, y, jitter, nDims) (stratified.go:12-19) */
+    int32_t sampler_x, sampler_y, jitter, n_dims;
+    /* integrator */
+    int32_t integrator;      /* PBRT_INTEGRATOR_*                               */
+    int32_t max_depth;
+    int32_t light_strategy;  /* Path: PBRT_LIGHT_STRATEGY_*                     */
+    int32_t dl_strategy;     /* DirectLighting: PBRT_DL_*                       */
+    double rr_threshold;
+    int64_t tile_size;       /* pbrt.Render tileSize (16 in internal/render)    */
+    /* tile subset (multi-GPU sharding): tiles t = tile_begin, tile_begin +
+     * tile_stride, ... < tile_end (tile_end <= 0 means all tiles). */
+    int64_t tile_begin, tile_end, tile_stride;
+    int32_t mode;            /* PBRT_MODE_*                                     */
+    int32_t flags;           /* reserved, 0                                     */
+} pbrt_render_desc;
+
+typedef struct pbrt_gpu_stats {
+    uint64_t tiles_rendered;
+    uint64_t camera_samples;     /* W*H*(spp-1) over rendered tiles           */
+    uint64_t paths_traced;       /* camera rays that reached Li               */
+    double kernel_ms;            /* device time of the render kernels         */
+    double total_ms;             /* host wall time of the call                */
+    int32_t panic_kind;          /* PBRT_PANIC_*                              */
+    int32_t panic_tile;
+    int64_t panic_pixel_x, panic_pixel_y;
+    int32_t panic_sample, panic_bounce;
+} pbrt_gpu_stats;
+
+/* ----------------------------------------------------------- ray batches */
+typedef struct pbrt_ray_soa {
+    const double *ox, *oy, *oz, *dx, *dy, *dz;
+    const double *tmax;          /* may be NULL => +Inf                      */
+} pbrt_ray_soa;
+
+typedef struct pbrt_hit_soa {
+    uint8_t* hit;
+    double* t_max;               /* ray.TMax after Intersect (tHit if hit)    */
+    int32_t* prim;               /* index into scene prims (BVH order), -1    */
+    double *px, *py, *pz;        /* SurfaceInteraction.Point                  */
+    double *nx, *ny, *nz;        /* SurfaceInteraction.Normal (geometric)     */
+} pbrt_hit_soa;
+
+/* ------------------------------------------------------------------ opts */
+typedef struct pbrt_gpu_opts {
+    int32_t device;              /* HIP device ordinal (-1 => current)       */
+    int32_t lanes_per_wave;      /* EXACT mode: tiles per 64-lane wave (0=auto) */
+    int32_t reserved[6];
+} pbrt_gpu_opts;
+
+typedef struct pbrt_gpu_ctx pbrt_gpu_ctx;
+
+/* Copies the scene to device memory. The descriptor may be freed afterwards. */
+int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts,
+                    pbrt_gpu_ctx** out);
+
+/* Renders the frame (or the tile subset in rd) and writes the fp64 XYZ film,
+ * res_x*res_y*3 doubles in raster order, to film_xyz (host memory) before
+ * returning. Equivalent of pbrt.Render minus WriteImage. */
+int pbrt_gpu_render(pbrt_gpu_ctx* ctx, const pbrt_render_desc* rd,
+                    double* film_xyz, pbrt_gpu_stats* stats);
+
+/* Same, but leaves the film in device memory (pbrt_gpu_film_device) and does
+ * not synchronize with the host: the bench's timed region. */
+int pbrt_gpu_render_async(pbrt_gpu_ctx* ctx, const pbrt_render_desc* rd);
+int pbrt_gpu_synchronize(pbrt_gpu_ctx* ctx, pbrt_gpu_stats* stats);
+/* device pointer to the res_x*res_y*3 fp64 film of the last render */
+double* pbrt_gpu_film_device(pbrt_gpu_ctx* ctx);
+int pbrt_gpu_film_download(pbrt_gpu_ctx* ctx, double* film_xyz);
+/* HIP stream the context launches on (hipStream_t as void*) */
+void* pbrt_gpu_stream(pbrt_gpu_ctx* ctx);
+
+/* Batch closest hit / any hit through the device BVH (Aggregate interface). */
+int pbrt_gpu_intersect(pbrt_gpu_ctx* ctx, const pbrt_ray_soa* rays, size_t n,
+                       pbrt_hit_soa* hits);
+int pbrt_gpu_intersect_p(pbrt_gpu_ctx* ctx, const pbrt_ray_soa* rays, size_t n,
+                         uint8_t* occluded);
+
+void pbrt_gpu_cancel(pbrt_gpu_ctx* ctx);     /* thread-safe                   */
+const char* pbrt_gpu_last_error(const pbrt_gpu_ctx* ctx);
+void pbrt_gpu_destroy(pbrt_gpu_ctx* ctx);
+
+/* PNG-byte conversion of film.go:142-179 WriteImage: uint8(clamp(XYZ,0,1)*255),
+ * no XYZ->RGB and no gamma, exactly as the reference. rgba: w*h*4 bytes. */
+int pbrt_film_to_rgba8(const double* film_xyz, int64_t w, int64_t h, uint8_t* rgba);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PBRT_GPU_H */

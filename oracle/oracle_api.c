@@ -1,0 +1,125 @@
+/*
+ * oracle/oracle_api.c — TEST INFRASTRUCTURE (oracle). Not part of the product.
+ *
+ * C exports used from tests/ (ctypes), __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg. Nothing in go-pbrt_amd/ links or loads this library.
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "oracle_render.h"
+#include "oracle_scene.h"
+
+/* ------------------------------------------------------------ Go math KATs */
+double oracle_go_sin(double x) { return go_sin(x); }
+double oracle_go_cos(double x) { return go_cos(x); }
+double oracle_go_tan(double x) { return go_tan(x); }
+double oracle_go_atan(double x) { return go_atan(x); }
+double oracle_go_atan2(double y, double x) { return go_atan2(y, x); }
+double oracle_go_asin(double x) { return go_asin(x); }
+double oracle_go_acos(double x) { return go_acos(x); }
+double oracle_go_nextafter(double x, double y) { return go_nextafter(x, y); }
+double oracle_go_max(double x, double y) { return go_max(x, y); }
+double oracle_go_min(double x, double y) { return go_min(x, y); }
+double oracle_go_radians(double d) { return go_radians(d); }
+int64_t oracle_go_f2i(double x) { return go_f2i(x); }
+
+/* ray.go:57-74 */
+void oracle_offset_ray_origin(const double p[3], const double e[3], const double n[3], const double w[3],
+                              double out[3]) {
+    v3 r = offset_ray_origin(V3(p[0], p[1], p[2]), V3(e[0], e[1], e[2]), V3(n[0], n[1], n[2]),
+                             V3(w[0], w[1], w[2]));
+    out[0] = r.x; out[1] = r.y; out[2] = r.z;
+}
+/* efloat.go:10-40: returns 0 on success, 1 if Check() would panic */
+int oracle_efloat_add(double v1, double e1, double v2, double e2, double out[3]) {
+    panic_ctx pc;
+    if (setjmp(pc.jb)) return 1;
+    ef_t a = ef_new(&pc, v1, e1), b = ef_new(&pc, v2, e2);
+    ef_t r = ef_add(&pc, a, b);
+    out[0] = r.v; out[1] = r.lo; out[2] = r.hi;
+    return 0;
+}
+/* transform.go */
+void oracle_translate(double x, double y, double z, pbrt_transform* out) { *out = orc_translate(x, y, z); }
+void oracle_scale(double x, double y, double z, pbrt_transform* out) { *out = orc_scale(x, y, z); }
+void oracle_rotate(int axis, double deg, pbrt_transform* out) { *out = orc_rotate(axis, deg); }
+void oracle_xf_mul(const pbrt_transform* a, const pbrt_transform* b, pbrt_transform* out) { *out = orc_xf_mul(a, b); }
+int oracle_matrix_inverse(const pbrt_matrix4x4* m, pbrt_matrix4x4* out) { return orc_m_inverse(m, out); }
+int oracle_look_at(const double pos[3], const double look[3], const double up[3], pbrt_transform* out) {
+    return orc_look_at(V3(pos[0], pos[1], pos[2]), V3(look[0], look[1], look[2]), V3(up[0], up[1], up[2]), out);
+}
+void oracle_perspective(double fov, double n, double f, pbrt_transform* out) { *out = orc_perspective(fov, n, f); }
+void oracle_transform_point(const pbrt_transform* t, const double p[3], const double e[3], double op[3], double oe[3]) {
+    v3 err;
+    v3 r = xf_point(t, V3(p[0], p[1], p[2]), V3(e[0], e[1], e[2]), &err);
+    op[0] = r.x; op[1] = r.y; op[2] = r.z;
+    oe[0] = err.x; oe[1] = err.y; oe[2] = err.z;
+}
+void oracle_transform_ray(const pbrt_transform* t, const double o[3], const double d[3], double oo[3], double od[3]) {
+    ray_t r;
+    r.o = V3(o[0], o[1], o[2]); r.d = V3(d[0], d[1], d[2]); r.tmax = INFINITY; r.time = 0;
+    ray_t w = xf_ray(t, &r, NULL, NULL);
+    oo[0] = w.o.x; oo[1] = w.o.y; oo[2] = w.o.z;
+    od[0] = w.d.x; od[1] = w.d.y; od[2] = w.d.z;
+}
+void oracle_make_sphere(const pbrt_transform* o2w, int rev, double r, double zmin, double zmax, double phimax,
+                        pbrt_shape_desc* out) {
+    *out = orc_sphere(*o2w, rev, r, zmin, zmax, phimax);
+}
+void oracle_make_disk(const pbrt_transform* o2w, double h, double r, double ri, double phimax, pbrt_shape_desc* out) {
+    *out = orc_disk(*o2w, h, r, ri, phimax);
+}
+
+/* ------------------------------------------------------------------ RNG */
+void oracle_pcg_stream(uint64_t seed, int n, uint32_t* out) {
+    orc_pcg r;
+    orc_pcg_set_sequence(&r, seed);
+    for (int i = 0; i < n; i++) out[i] = orc_pcg_next(&r);
+}
+void oracle_pcg_floats(uint64_t seed, int n, double* out) {
+    orc_pcg r;
+    orc_pcg_set_sequence(&r, seed);
+    for (int i = 0; i < n; i++) out[i] = orc_pcg_float(&r);
+}
+
+/* ---------------------------------------------------------------- scenes */
+void* oracle_scene_new(void) { return calloc(1, sizeof(orc_scene)); }
+void* oracle_scene_readme(int64_t w, int64_t h) { return orc_scene_readme(w, h); }
+void* oracle_scene_cornell(int64_t w, int64_t h) { return orc_scene_cornell(w, h); }
+int oracle_scene_add_shape(void* s, const pbrt_shape_desc* d) { return orc_add_shape((orc_scene*)s, *d); }
+int oracle_scene_add_material(void* s, const pbrt_material_desc* d) { return orc_add_material((orc_scene*)s, *d); }
+int oracle_scene_add_primitive(void* s, const pbrt_primitive_desc* d) {
+    orc_scene* sc = (orc_scene*)s;
+    sc->prims_in[sc->n_prims_in] = *d;
+    return sc->n_prims_in++;
+}
+int oracle_scene_add_light(void* s, const pbrt_light_desc* d) {
+    orc_scene* sc = (orc_scene*)s;
+    sc->lights[sc->n_lights] = *d;
+    return sc->n_lights++;
+}
+void oracle_scene_set_camera_film(void* s, const pbrt_camera_desc* c, const pbrt_film_desc* f) {
+    orc_scene* sc = (orc_scene*)s;
+    sc->camera = *c; sc->film = *f;
+}
+int oracle_scene_finalize(void* s, int max_prims) { return orc_scene_finalize((orc_scene*)s, max_prims); }
+void oracle_scene_desc(void* s, pbrt_scene_desc* out) { orc_scene_desc((orc_scene*)s, out); }
+void oracle_scene_order(void* s, int32_t* out) {
+    orc_scene* sc = (orc_scene*)s;
+    for (int i = 0; i < sc->n_prims_in; i++) out[i] = sc->order[i];
+}
+void oracle_scene_free(void* s) { orc_scene_free((orc_scene*)s); }
+
+/* ---------------------------------------------------------------- render */
+int oracle_render(const pbrt_scene_desc* sc, const pbrt_render_desc* rd, int n_threads, int flags,
+                  double* film_xyz, orc_stats* stats) {
+    return orc_render(sc, rd, n_threads, flags, film_xyz, stats);
+}
+int64_t oracle_num_tiles(const pbrt_scene_desc* sc, const pbrt_render_desc* rd) { return orc_num_tiles(sc, rd); }
+int oracle_intersect(const pbrt_scene_desc* sc, const double* rays, size_t n, int closest, double* out) {
+    return orc_intersect(sc, rays, n, closest, out);
+}
+void oracle_light_distribution(const pbrt_scene_desc* sc, const pbrt_render_desc* rd, pbrt_distribution_desc* d) {
+    orc_light_distribution(sc, rd, d);
+}
