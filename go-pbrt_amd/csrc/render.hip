@@ -162,7 +162,11 @@ __global__ __launch_bounds__(kWave) void k_render_exact(DevScene sc, RenderParam
             const double fx = (double)px + 0.0, fy = (double)py + 0.0;
             Footprint fp;
             int64_t p0x, p0y, p1x, p1y;
-            const bool reg = footprint(film, fx, fy, px0, py0, px1, py1, fp, p0x, p0y, p1x, p1y) == 0;
+            // With n_dims >= 1 the camera's Get2D is stratified 2D dim 0 == (0,0) for every
+            // sample, so pFilm is the pixel corner and the footprint is per pixel; with
+            // n_dims == 0 it comes from the RNG and the footprint is per sample.
+            const bool reg = rp.ndims >= 1 &&
+                             footprint(film, fx, fy, px0, py0, px1, py1, fp, p0x, p0y, p1x, p1y) == 0;
             double acc[4][3];
             if (reg)
                 for (int k = 0; k < fp.n; k++)
@@ -195,8 +199,13 @@ __global__ __launch_bounds__(kWave) void k_render_exact(DevScene sc, RenderParam
                         acc[k][0] += a.r; acc[k][1] += a.g; acc[k][2] += a.b;
                     }
                 } else {
-                    // general filter footprint: AddSample straight into the slot
-                    double dx = fx - 0.5, dy = fy - 0.5;
+                    // general footprint: FilmTile.AddSample straight into the slot
+                    const double sfx = (double)px + u0.x, sfy = (double)py + u0.y;
+                    double dx = sfx - 0.5, dy = sfy - 0.5;
+                    p0x = gomath::to_int(gomath::max(gomath::ceil(dx - film.filter_radius_x), (double)px0));
+                    p0y = gomath::to_int(gomath::max(gomath::ceil(dy - film.filter_radius_y), (double)py0));
+                    p1x = gomath::to_int(gomath::min(gomath::floor(dx + film.filter_radius_x) + 1, (double)px1));
+                    p1y = gomath::to_int(gomath::min(gomath::floor(dy + film.filter_radius_y) + 1, (double)py1));
                     const double ifx = 1.0 / film.filter_radius_x, ify = 1.0 / film.filter_radius_y;
                     int64_t tw = px1 - px0;
                     for (int64_t y = p0y; y < p1y; y++) {
@@ -348,7 +357,7 @@ int upload(pbrt_gpu_ctx* c, T** dst, const T* src, size_t n) {
 template <class T>
 int ensure(pbrt_gpu_ctx* c, T** buf, size_t* cap, size_t n) {
     if (*cap >= n && *buf) return PBRT_OK;
-    if (*buf) hipFree(*buf);
+    if (*buf) (void)hipFree(*buf);
     *buf = nullptr;
     HIPCHK(c, hipMalloc((void**)buf, sizeof(T) * (n ? n : 1)));
     *cap = n;
@@ -481,7 +490,7 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
     if (c->device >= 0) {
         if (hipSetDevice(c->device) != hipSuccess) { delete c; return PBRT_E_HIP; }
     } else {
-        hipGetDevice(&c->device);
+        (void)hipGetDevice(&c->device);
     }
     c->host_scene = *scene;
     c->host_scene.shapes = nullptr;
@@ -544,7 +553,7 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
     Counters ctr;
     HIPCHK(c, hipMemcpy(&ctr, c->d_ctr, sizeof(ctr), hipMemcpyDeviceToHost));
     float ms = 0;
-    hipEventElapsedTime(&ms, c->ev0, c->ev1);
+    (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
     int rc = PBRT_OK;
     pbrt_gpu_stats st;
     std::memset(&st, 0, sizeof(st));
@@ -614,7 +623,7 @@ static int intersect_batch(pbrt_gpu_ctx* c, const pbrt_ray_soa* rays, size_t n, 
     double *d_in = nullptr, *d_o = nullptr;
     HIPCHK(c, hipMalloc((void**)&d_in, sizeof(double) * packed.size()));
     if (hipMalloc((void**)&d_o, sizeof(double) * nout) != hipSuccess) {
-        hipFree(d_in);
+        (void)hipFree(d_in);
         return set_err(c, PBRT_E_HIP, "hipMalloc");
     }
     std::vector<double> o(nout);
@@ -627,8 +636,8 @@ static int intersect_batch(pbrt_gpu_ctx* c, const pbrt_ray_soa* rays, size_t n, 
     }
     if (e == hipSuccess) e = hipMemcpyAsync(o.data(), d_o, sizeof(double) * nout, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    hipFree(d_in);
-    hipFree(d_o);
+    (void)hipFree(d_in);
+    (void)hipFree(d_o);
     if (e != hipSuccess) return set_err(c, PBRT_E_HIP, hipGetErrorString(e));
     int rc = PBRT_OK;
     for (size_t i = 0; i < n; i++) {
@@ -667,15 +676,15 @@ const char* pbrt_gpu_last_error(const pbrt_gpu_ctx* c) { return c ? c->err.c_str
 
 void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
     if (!c) return;
-    hipSetDevice(c->device);
-    if (c->stream) hipStreamSynchronize(c->stream);
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_shapes, c->d_materials, c->d_prims, c->d_nodes, c->d_lights, c->d_camera, c->d_film,
                     c->d_dist,   c->d_films,     c->d_s1d,   c->d_panics, c->d_ctr,   c->d_out};
     for (void* b : bufs)
-        if (b) hipFree(b);
-    if (c->ev0) hipEventDestroy(c->ev0);
-    if (c->ev1) hipEventDestroy(c->ev1);
-    if (c->stream) hipStreamDestroy(c->stream);
+        if (b) (void)hipFree(b);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
@@ -691,3 +700,100 @@ int pbrt_film_to_rgba8(const double* film, int64_t w, int64_t h, uint8_t* rgba) 
 }
 
 }  // extern "C"
+
+// ============================================================ diagnostics
+#include "../../include/pbrt_diag.h"
+
+namespace {
+__global__ void k_probe(int op, const double* __restrict__ in, int64_t n, int in_stride, double* __restrict__ out,
+                        int out_stride) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double* a = in + i * in_stride;
+    double* o = out + i * out_stride;
+    switch (op) {
+        case PBRT_PROBE_SIN: o[0] = gomath::sin(a[0]); break;
+        case PBRT_PROBE_COS: o[0] = gomath::cos(a[0]); break;
+        case PBRT_PROBE_TAN: o[0] = gomath::tan(a[0]); break;
+        case PBRT_PROBE_ATAN: o[0] = gomath::atan(a[0]); break;
+        case PBRT_PROBE_ATAN2: o[0] = gomath::atan2(a[0], a[1]); break;
+        case PBRT_PROBE_ASIN: o[0] = gomath::asin(a[0]); break;
+        case PBRT_PROBE_ACOS: o[0] = gomath::acos(a[0]); break;
+        case PBRT_PROBE_SQRT: o[0] = gomath::sqrt(a[0]); break;
+        case PBRT_PROBE_DIV: o[0] = a[0] / a[1]; break;
+        case PBRT_PROBE_NEXTAFTER: o[0] = gomath::nextafter(a[0], a[1]); break;
+        case PBRT_PROBE_MAX: o[0] = gomath::max(a[0], a[1]); break;
+        case PBRT_PROBE_MIN: o[0] = gomath::min(a[0], a[1]); break;
+        case PBRT_PROBE_OFFSET_RAY_ORIGIN: {
+            V3 r = offset_ray_origin(load3(a), load3(a + 3), load3(a + 6), load3(a + 9));
+            o[0] = r.x; o[1] = r.y; o[2] = r.z;
+            break;
+        }
+        case PBRT_PROBE_EFLOAT_ADD: {
+            int panic = 0;
+            EF r = ef_add(ef_new(a[0], a[1], panic), ef_new(a[2], a[3], panic), panic);
+            o[0] = r.v; o[1] = r.lo; o[2] = r.hi; o[3] = panic;
+            break;
+        }
+        case PBRT_PROBE_TRANSFORM_RAY: {
+            pbrt_matrix4x4 m;
+            for (int k = 0; k < 16; k++) m.m[k / 4][k % 4] = a[k];
+            Ray r{load3(a + 16), load3(a + 19), gomath::kInf, 0};
+            Ray w = xf_ray(m, r, nullptr, nullptr);
+            o[0] = w.o.x; o[1] = w.o.y; o[2] = w.o.z; o[3] = w.d.x; o[4] = w.d.y; o[5] = w.d.z;
+            break;
+        }
+        case PBRT_PROBE_SPAWN_RAY_TO: {
+            V3 p0 = load3(a), e0 = load3(a + 3), n0 = load3(a + 6), p1 = load3(a + 9), e1 = load3(a + 12),
+               n1 = load3(a + 15);
+            V3 origin = offset_ray_origin(p0, e0, n0, p1 - p0);
+            V3 target = offset_ray_origin(p1, e1, n1, origin - p1);
+            V3 d = target - origin;
+            o[0] = p0.x; o[1] = p0.y; o[2] = p0.z; o[3] = d.x; o[4] = d.y; o[5] = d.z; o[6] = 1 - 0.0001;
+            break;
+        }
+        case PBRT_PROBE_PCG: {
+            Pcg r;
+            pcg_seed(r, (uint64_t)a[0]);
+            for (int k = 0; k < out_stride; k++) o[k] = pcg_float(r);
+            break;
+        }
+        default: o[0] = gomath::nan();
+    }
+}
+}  // namespace
+
+extern "C" int pbrt_gpu_probe(int device, int op, const double* in, size_t n, int in_stride, double* out,
+                              int out_stride) {
+    if (!in || !out || in_stride <= 0 || out_stride <= 0) return PBRT_E_INVALID;
+    if (n == 0) return PBRT_OK;
+    if (device >= 0 && hipSetDevice(device) != hipSuccess) return PBRT_E_HIP;
+    double *d_in = nullptr, *d_out = nullptr;
+    if (hipMalloc((void**)&d_in, sizeof(double) * n * in_stride) != hipSuccess) return PBRT_E_HIP;
+    if (hipMalloc((void**)&d_out, sizeof(double) * n * out_stride) != hipSuccess) {
+        (void)hipFree(d_in);
+        return PBRT_E_HIP;
+    }
+    hipError_t e = hipMemcpy(d_in, in, sizeof(double) * n * in_stride, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_probe, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, op, d_in, (int64_t)n,
+                           in_stride, d_out, out_stride);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(out, d_out, sizeof(double) * n * out_stride, hipMemcpyDeviceToHost);
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    return e == hipSuccess ? PBRT_OK : PBRT_E_HIP;
+}
+
+extern "C" int pbrt_abi_sizes(size_t* out, int n) {
+    const size_t s[] = {sizeof(pbrt_matrix4x4),   sizeof(pbrt_transform),    sizeof(pbrt_shape_desc),
+                        sizeof(pbrt_material_desc), sizeof(pbrt_primitive_desc), sizeof(pbrt_bvh_node),
+                        sizeof(pbrt_light_desc),  sizeof(pbrt_camera_desc),  sizeof(pbrt_film_desc),
+                        sizeof(pbrt_distribution_desc), sizeof(pbrt_scene_desc), sizeof(pbrt_render_desc),
+                        sizeof(pbrt_gpu_stats),   sizeof(pbrt_ray_soa),      sizeof(pbrt_hit_soa),
+                        sizeof(pbrt_gpu_opts)};
+    int m = (int)(sizeof(s) / sizeof(s[0]));
+    for (int i = 0; i < n && i < m; i++) out[i] = s[i];
+    return m;
+}

@@ -1,0 +1,48 @@
+/*
+ * pbrt_diag.h — diagnostics of the device path (not part of the reference
+ * interface). Evaluates individual device functions on a batch of inputs so
+ * the reference's known-answer tests and large random sweeps can be checked
+ * against the oracle on the GPU itself (Go-math trig, correctly rounded
+ * division / sqrt, OffsetRayOrigin, EFloat, TransformRay, SpawnRayToInteraction,
+ * PCG32 stream).
+ */
+#ifndef PBRT_DIAG_H
+#define PBRT_DIAG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    PBRT_PROBE_SIN = 1,        /* in a          -> out Sin(a)                 */
+    PBRT_PROBE_COS = 2,
+    PBRT_PROBE_TAN = 3,
+    PBRT_PROBE_ATAN = 4,
+    PBRT_PROBE_ATAN2 = 5,      /* in y, x                                    */
+    PBRT_PROBE_ASIN = 6,
+    PBRT_PROBE_ACOS = 7,
+    PBRT_PROBE_SQRT = 8,
+    PBRT_PROBE_DIV = 9,        /* in a, b       -> a / b                      */
+    PBRT_PROBE_NEXTAFTER = 10, /* in x, y                                    */
+    PBRT_PROBE_MAX = 11,
+    PBRT_PROBE_MIN = 12,
+    PBRT_PROBE_OFFSET_RAY_ORIGIN = 13, /* in p[3] perr[3] n[3] w[3] -> out[3]    */
+    PBRT_PROBE_EFLOAT_ADD = 14,        /* in v1 e1 v2 e2 -> value low high panic */
+    PBRT_PROBE_TRANSFORM_RAY = 15,     /* in m[16] o[3] d[3] -> o'[3] d'[3]      */
+    PBRT_PROBE_SPAWN_RAY_TO = 16,      /* in p0 perr0 n0 p1 perr1 n1 -> o d tmax */
+    PBRT_PROBE_PCG = 17                /* in seed -> out[out_stride] first floats */
+};
+
+/* Inputs: n records of in_stride doubles; outputs: n records of out_stride. */
+int pbrt_gpu_probe(int device, int op, const double* in, size_t n, int in_stride, double* out, int out_stride);
+
+/* sizeof() of every ABI struct, for binding checks (index order as in pbrt_gpu.h). */
+int pbrt_abi_sizes(size_t* out, int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

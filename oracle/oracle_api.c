@@ -123,3 +123,15 @@ int oracle_intersect(const pbrt_scene_desc* sc, const double* rays, size_t n, in
 void oracle_light_distribution(const pbrt_scene_desc* sc, const pbrt_render_desc* rd, pbrt_distribution_desc* d) {
     orc_light_distribution(sc, rd, d);
 }
+
+/* interaction.go:91-102 SpawnRayToInteraction: in p0 perr0 n0 p1 perr1 n1; out o d tmax */
+void oracle_spawn_ray_to(const double in[18], double out[7]) {
+    v3 p0 = V3(in[0], in[1], in[2]), e0 = V3(in[3], in[4], in[5]), n0 = V3(in[6], in[7], in[8]);
+    v3 p1 = V3(in[9], in[10], in[11]), e1 = V3(in[12], in[13], in[14]), n1 = V3(in[15], in[16], in[17]);
+    v3 origin = offset_ray_origin(p0, e0, n0, v_sub(p1, p0));
+    v3 target = offset_ray_origin(p1, e1, n1, v_sub(origin, p1));
+    v3 d = v_sub(target, origin);
+    out[0] = p0.x; out[1] = p0.y; out[2] = p0.z;
+    out[3] = d.x; out[4] = d.y; out[5] = d.z;
+    out[6] = 1 - 0.0001;
+}

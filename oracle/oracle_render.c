@@ -674,6 +674,7 @@ static spec estimate_direct(orc_ctx* oc, const si_t* si, const bsdf_t* b, v2 u_s
             r2.o = offset_ray_origin(si->p, si->perr, si->n, wi2);
             r2.d = wi2; r2.tmax = INFINITY; r2.time = si->time;
             si_t tmp;
+            oc->closest_rays++;
             orc_bvh_intersect(&oc->pc, sc, &r2, &tmp);
         }
     }

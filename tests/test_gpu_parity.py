@@ -1,0 +1,316 @@
+"""Parity of the HIP path (through the C ABI) with the CPU oracle.
+
+Bar: bit-identical fp64 films (integer-exact comparison of the IEEE bits) for
+every configuration the oracle finishes in seconds, plus the committed golden
+fixtures; at full 1080p size, size-independent properties and a bit-exact
+check of a sample of tiles.
+"""
+import ctypes as C
+import hashlib
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import pbrtgpu as G
+from pbrtgpu import abi
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = json.load(open(os.path.join(HERE, "golden", "golden.json")))
+
+
+def same_bits(a, b):
+    return np.array_equal(np.ascontiguousarray(a).view(np.uint64), np.ascontiguousarray(b).view(np.uint64))
+
+
+def gpu_render(scene, rd, lanes_per_wave=0):
+    with G.Renderer(scene, lanes_per_wave=lanes_per_wave) as r:
+        return r.render(rd)
+
+
+def oracle_render(scene, rd):
+    rc, film, st = O.render(scene.desc, rd, threads=min(16, os.cpu_count() or 1))
+    assert rc == 0
+    return film, st
+
+
+def check(scene, rd, **kw):
+    film, st = gpu_render(scene, rd, **kw)
+    ofilm, ost = oracle_render(scene, rd)
+    assert st.paths_traced == ost.paths
+    assert same_bits(film, ofilm), f"{int((film != ofilm).sum())} film values differ"
+    return film, st
+
+
+# ----------------------------------------------------------- device math KATs
+def probe(op, inp, out_stride=1):
+    inp = np.ascontiguousarray(inp, dtype=np.float64)
+    if inp.ndim == 1:
+        inp = inp[:, None]
+    out = np.zeros((inp.shape[0], out_stride))
+    rc = G.lib().pbrt_gpu_probe(-1, op, inp.ctypes.data_as(C.POINTER(C.c_double)), inp.shape[0], inp.shape[1],
+                                out.ctypes.data_as(C.POINTER(C.c_double)), out_stride)
+    assert rc == 0
+    return out
+
+
+def setup_module(module):
+    G.lib().pbrt_gpu_probe.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_double), C.c_size_t, C.c_int,
+                                       C.POINTER(C.c_double), C.c_int]
+
+
+def test_device_go_cos_golden():
+    """transform_test.go:80 on the device: Cos(Pi/180*90) == 6.123233995736757e-17."""
+    out = probe(abi.PBRT_PROBE_COS if hasattr(abi, "PBRT_PROBE_COS") else 2, np.array([math.pi / 180.0 * 90]))
+    assert out[0, 0] == 6.123233995736757e-17
+
+
+def test_device_trig_matches_oracle():
+    """Go-math trig on the device equals the oracle bit for bit on 2e5 inputs per
+    function over the ranges the hot path uses (phi, theta, concentric-disk angles)."""
+    rng = np.random.default_rng(1)
+    L = O.lib()
+    n = 200_000
+    xs = np.concatenate([rng.uniform(-7, 7, n // 2), rng.uniform(-1, 1, n // 4), rng.uniform(-1e3, 1e3, n // 4)])
+    for op, f in ((1, L.oracle_go_sin), (2, L.oracle_go_cos), (4, L.oracle_go_atan)):
+        got = probe(op, xs)[:, 0]
+        want = np.array([f(x) for x in xs])
+        assert same_bits(got, want), op
+    u = rng.uniform(-1, 1, n)
+    for op, f in ((6, L.oracle_go_asin), (7, L.oracle_go_acos)):
+        got = probe(op, u)[:, 0]
+        want = np.array([f(x) for x in u])
+        assert same_bits(got, want), op
+    yx = rng.normal(size=(n, 2)) * rng.choice([1e-3, 1, 1e3], size=(n, 1))
+    got = probe(5, yx)[:, 0]
+    want = np.array([L.oracle_go_atan2(y, x) for y, x in yx])
+    assert same_bits(got, want)
+
+
+def test_device_div_sqrt_correctly_rounded():
+    """gfx950 fp64 '/' and sqrt must be correctly rounded (SURVEY §9 'verify on
+    gfx950'): 2e6 random operands incl. denormals vs the host (IEEE)."""
+    rng = np.random.default_rng(2)
+    n = 1_000_000
+    a = rng.normal(size=n) * np.exp2(rng.integers(-1070, 1000, n))
+    b = rng.normal(size=n) * np.exp2(rng.integers(-60, 60, n))
+    got = probe(9, np.stack([a, b], 1))[:, 0]
+    with np.errstate(over="ignore", under="ignore"):
+        assert same_bits(got, a / b)
+    s = np.abs(rng.normal(size=n)) * np.exp2(rng.integers(-1074, 1000, n))
+    got = probe(8, s)[:, 0]
+    assert same_bits(got, np.sqrt(s))
+
+
+def test_device_offset_ray_origin_golden():
+    """ray_test.go:10-19 on the device (fp64 denormals preserved)."""
+    eps = 5e-324
+    out = probe(13, np.array([[0, 0, 0, eps, eps, eps, 1, 1, 1, 1, 1, 1]]), 3)
+    assert list(out[0]) == [1.5183e-320] * 3
+
+
+def test_device_efloat_add_golden():
+    """efloat_test.go:9-13 on the device."""
+    out = probe(14, np.array([[1.0, 0.0, 1.0, 0.0]]), 4)
+    assert list(out[0]) == [2.0, 1.9999999999999998, 2.0000000000000004, 0.0]
+
+
+def test_device_transform_ray_golden():
+    """transform_test.go:77-81 on the device."""
+    x = G.mul(G.rotate(1, 90), G.translate(5, 4, 3))
+    m = [x.m.m[i][j] for i in range(4) for j in range(4)]
+    out = probe(15, np.array([m + [0, 0, 0, 1, 0, 0]]), 6)
+    assert list(out[0]) == [3.0000000000000004, 4, -5, 6.123233995736757e-17, 0, -1]
+
+
+def test_device_visibility_tester_golden():
+    """light_test.go:10-44 on the device."""
+    out = probe(16, np.array([[0, 0, 0, 0, 0, 0, 0, 0, 0, 10, 0, 0, 0, 0, 0, 0, 0, 0]]), 7)
+    assert list(out[0]) == [0, 0, 0, 10, 0, 0, 0.9999]
+
+
+def test_device_pcg_matches_golden():
+    gold = GOLDEN["pcg32_first16"]
+    L = O.lib()
+    for seed in (0, 1, 8159):
+        buf = (C.c_double * 16)()
+        L.oracle_pcg_floats(seed, 16, buf)
+        out = probe(17, np.array([float(seed)]), 16)
+        assert same_bits(out[0], np.array(list(buf)))
+        # and the oracle floats derive from the committed u32 golden stream
+        assert list(buf) == [min(0.9999999999999999, u * 2.3283064365386963e-10) for u in gold[str(seed)]]
+
+
+# ---------------------------------------------------------------- film parity
+@pytest.mark.parametrize("name", sorted(GOLDEN["cases"]))
+def test_golden_fixtures(name):
+    case = GOLDEN["cases"][name]
+    w, h = case["w"], case["h"]
+    scene = G.Scene.readme(w, h) if case["scene"] == "readme" else G.Scene.cornell(w, h)
+    rd = abi.render_desc(**case["render"])
+    film, st = gpu_render(scene, rd)
+    gold = np.load(os.path.join(HERE, "golden", name + ".npz"))["film"]
+    assert same_bits(film, gold)
+    assert hashlib.sha256(film.tobytes()).hexdigest() == case["sha256"]
+    assert st.paths_traced == case["paths"]
+
+
+def test_readme_256_path_bitexact():
+    check(G.Scene.readme(256, 256), abi.render_desc(2, 2))
+
+
+def test_config_A_traces_nothing():
+    """Config A: Stratified(1,1) traces 0 paths (sampler.go:29-34): all-zero film."""
+    film, st = gpu_render(G.Scene.readme(256, 256),
+                          abi.render_desc(1, 1, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING))
+    assert st.paths_traced == 0 and st.tiles_rendered == 256
+    assert not film.any()
+
+
+def test_config_A_prime_direct_lighting():
+    check(G.Scene.readme(256, 256), abi.render_desc(2, 2, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING))
+
+
+def test_direct_lighting_sample_one():
+    check(G.Scene.readme(64, 64), abi.render_desc(2, 2, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING,
+                                                  dl_strategy=abi.PBRT_DL_UNIFORM_SAMPLE_ONE))
+
+
+@pytest.mark.parametrize("kw", [
+    dict(spp_x=4, spp_y=4),
+    dict(spp_x=3, spp_y=5, jitter=True),
+    dict(spp_x=2, spp_y=2, n_dims=0),
+    dict(spp_x=2, spp_y=2, n_dims=7),
+    dict(spp_x=2, spp_y=2, max_depth=1),
+    dict(spp_x=2, spp_y=2, max_depth=2),
+    dict(spp_x=2, spp_y=2, max_depth=5, rr_threshold=0.0),
+    dict(spp_x=2, spp_y=2, rr_threshold=1e9),
+    dict(spp_x=2, spp_y=2, light_strategy=abi.PBRT_LIGHT_STRATEGY_POWER),
+    dict(spp_x=2, spp_y=2, tile_size=8),
+    dict(spp_x=2, spp_y=2, tile_size=13),
+])
+def test_readme_variants_bitexact(kw):
+    check(G.Scene.readme(72, 40), abi.render_desc(**kw))
+
+
+@pytest.mark.parametrize("w,h", [(1, 1), (17, 3), (37, 23), (16, 16)])
+def test_ragged_images(w, h):
+    check(G.Scene.readme(w, h), abi.render_desc(3, 3))
+
+
+@pytest.mark.parametrize("lpw", [1, 4, 16, 64])
+def test_lanes_per_wave_invariant(lpw):
+    check(G.Scene.readme(96, 48), abi.render_desc(2, 2), lanes_per_wave=lpw)
+
+
+def test_cornell_bitexact():
+    check(G.Scene.cornell(64, 48), abi.render_desc(3, 3, max_depth=8))
+
+
+def test_tile_shards_sum_to_full_frame():
+    """Multi-GPU sharding (tile t -> rank t mod N): the sum of the shard films
+    equals the single-device film; only pixels covered by tiles of different
+    shards can differ, and then only by float association order."""
+    scene = G.Scene.readme(80, 48)
+    full, _ = gpu_render(scene, abi.render_desc(2, 2))
+    for n in (2, 3):
+        parts = [gpu_render(scene, abi.render_desc(2, 2, tile_begin=r, tile_stride=n))[0] for r in range(n)]
+        acc = np.zeros_like(full)
+        for p in parts:
+            acc += p
+        np.testing.assert_allclose(acc, full, rtol=1e-14, atol=0)
+        # each shard equals the oracle's render of the same shard, bit for bit
+        for r in range(n):
+            ofilm, _ = oracle_render(scene, abi.render_desc(2, 2, tile_begin=r, tile_stride=n))
+            assert same_bits(parts[r], ofilm)
+
+
+def test_tile_range_subset():
+    scene = G.Scene.readme(64, 64)
+    rd = abi.render_desc(2, 2, tile_begin=3, tile_end=11, tile_stride=1)
+    film, st = gpu_render(scene, rd)
+    assert st.tiles_rendered == 8
+    ofilm, _ = oracle_render(scene, rd)
+    assert same_bits(film, ofilm)
+
+
+# --------------------------------------------------------- batch intersection
+def random_rays(n, seed):
+    rng = np.random.default_rng(seed)
+    o = rng.uniform(-60, 140, size=(n, 3))
+    o[:, 1] = rng.uniform(-5, 120, size=n)
+    d = rng.normal(size=(n, 3))
+    tmax = np.where(rng.uniform(size=n) < 0.2, rng.uniform(1, 200, size=n), np.inf)
+    return np.concatenate([o, d, tmax[:, None]], axis=1)
+
+
+def test_intersect_matches_oracle():
+    """Aggregate.Intersect/IntersectP (bvh.go:659-765) on 2e4 random rays, bit-exact
+    hit flags, hit prim, TMax, point and normal."""
+    scene = G.Scene.readme(64, 64)
+    rays = random_rays(20_000, 3)
+    with G.Renderer(scene) as r:
+        rc, got = r.intersect(rays)
+        rc_p, occ = r.intersect_p(rays)
+    assert rc == 0 and rc_p == 0
+    want = O.intersect(scene.desc, rays, closest=True)
+    wocc = O.intersect(scene.desc, rays, closest=False)
+    assert same_bits(got, want)
+    assert np.array_equal(occ.astype(bool), wocc.astype(bool))
+    assert 0.2 < got[:, 0].mean() < 0.95   # the sample exercises hits and misses
+
+
+# ------------------------------------------------------------ reference panics
+def panic_scene():
+    """A point light so bright that EstimateDirect returns > 10 on the first
+    lit hit: UniformSampleOneLight panics (integrator.go:73-75)."""
+    s = G.Scene()
+    chk = s.add_matte((0.8, 0.8, 0.8))
+    t = G.mul(G.translate(0, 0, 0), G.rotate(0, 90))
+    d = s.add_disk(t, 0.0, 100.0)
+    s.add_primitive(d, chk)
+    s.add_point_light(G.translate(0, 5, 0), (1e5, 1e5, 1e5))
+    s.set_film(32, 32)
+    s.set_camera(G.look_at((0, 20, 20), (0, 0, 0), (0, 1, 0)), fov=60)
+    return s.build()
+
+
+def test_reference_panic_is_reported_like_the_oracle():
+    scene = panic_scene()
+    rd = abi.render_desc(2, 2)
+    rc, _, ost = O.render(scene.desc, rd, threads=1)
+    assert rc == abi.PBRT_E_REF_PANIC and ost.panic_kind == abi.PBRT_PANIC_LD_GT_10
+    with G.Renderer(scene) as r:
+        with pytest.raises(G.PbrtError) as ei:
+            r.render(rd)
+    st = ei.value.stats
+    assert ei.value.code == abi.PBRT_E_REF_PANIC
+    assert st.panic_kind == abi.PBRT_PANIC_LD_GT_10
+    assert (st.panic_tile, st.panic_pixel_x, st.panic_pixel_y, st.panic_sample, st.panic_bounce) == (
+        ost.panic_tile, ost.panic_px, ost.panic_py, ost.panic_sample, ost.panic_bounce)
+
+
+# ------------------------------------------------------------ full-size (1080p)
+@pytest.mark.slow
+def test_1080p_64spp_properties_and_sampled_tiles():
+    """BASELINE config B at full size: 8160 tiles, W*H*63 paths, finite film;
+    a sample of tiles is re-rendered by the oracle and must match bit for bit."""
+    scene = G.Scene.readme(1920, 1080)
+    rd = abi.render_desc(8, 8)
+    with G.Renderer(scene) as r:
+        film, st = r.render(rd)
+    assert st.tiles_rendered == 8160
+    assert st.paths_traced == 1920 * 1080 * 63
+    assert np.isfinite(film).all()
+    # tiles 0, 4080, 8159 (first, middle, last) alone, oracle vs GPU
+    for t in (0, 4080, 8159):
+        one = abi.render_desc(8, 8, tile_begin=t, tile_end=t + 1)
+        with G.Renderer(scene) as r:
+            g, _ = r.render(one)
+        o, _ = oracle_render(scene, one)
+        assert same_bits(g, o), t
