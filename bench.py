@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X hot path on BASELINE.json's headline workload.
+
+One step = one full frame of config B: the README sphere scene
+(internal/render/server.go:29-164) at 1920x1080, Stratified(8,8) (63 traced
+paths per pixel: sample 0 is never traced, sampler.go:29-34), Path(maxDepth 10,
+rr 1, Uniform), 16-px tiles, EXACT mode (the reference's per-tile RNG replayed
+bit for bit). Inputs (scene, BVH) are resident on the GPU before timing.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Multi-GPU: one process per GPU; tiles are sharded t -> rank (t mod N) and the
+per-rank fp64 XYZ films are summed on rank 0 with one RCCL reduce (the
+additive Film.MergeFilmTile, film.go:115-132). Total work is fixed -> "strong".
+
+Prints ONE JSON line on rank 0 (value = Mpaths/s over all GPUs).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "go-pbrt_amd"))
+
+METRIC = ("Mpaths/s (samples×pixels/s) at 1920×1080, 64 spp; 1/2/4/8-GPU scaling + HBM GB/s vs "
+          "roofline")
+FP64_PEAK_TFLOPS = 78.6     # MI355X fp64 vector peak (datasheet); the path is fp64-VALU bound
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=8, help="Stratified(spp, spp)")
+    ap.add_argument("--lanes-per-wave", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall budget of the CPU baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, nproc)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def load_json(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(args, rd_kwargs):
+    """The oracle (C restatement of the Go path, oracle/) on a bounded, evenly
+    spread sample of the same frame's tiles, on this box's host cores."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib as O
+    from pbrtgpu import abi
+
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    sc = O.OracleScene.readme(args.width, args.height)
+    n_tiles = int(O.lib().oracle_num_tiles(sc.desc, abi.render_desc(**rd_kwargs)))
+    stride = 64
+    # bit-reversed offsets: every prefix of batches is an evenly spread tile subset
+    offsets = [int(format(i, "06b")[::-1], 2) for i in range(stride)]
+    paths = tiles = 0
+    t0 = time.perf_counter()
+    for off in offsets:
+        rd = abi.render_desc(**dict(rd_kwargs, tile_begin=off, tile_stride=stride))
+        rc, _, st = O.render(sc.desc, rd, threads=threads)
+        if rc != 0:
+            raise RuntimeError(f"oracle rc {rc}")
+        paths += st.paths
+        tiles += st.tiles
+        if time.perf_counter() - t0 >= args.cpu_seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {
+        "value": paths / dt / 1e6,
+        "unit": "Mpaths/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{tiles} of {n_tiles} tiles of the same frame (evenly spread, stride {stride}), "
+                  f"{paths} paths in {dt:.2f} s on {threads} threads; oracle/ C restatement of the Go path",
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)   # RCCL over xGMI
+
+    import pbrtgpu as G
+
+    W, H, S = args.width, args.height, args.spp
+    rd_kwargs = dict(spp_x=S, spp_y=S)
+    scene = G.Scene.readme(W, H)
+    renderer = G.Renderer(scene, device=local, lanes_per_wave=args.lanes_per_wave)
+    rd = G.render_desc(**rd_kwargs, tile_begin=rank, tile_stride=world)
+    film = torch.zeros((H, W, 3), dtype=torch.float64, device=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local])
+
+    def step():
+        renderer.render_async(rd, film.data_ptr())
+        st = renderer.synchronize()
+        if world > 1:
+            dist.reduce(film, dst=0, op=dist.ReduceOp.SUM)
+        return st
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stats = [step() for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    paths_local = sum(int(s.paths_traced) for s in stats)
+    kern_ms = sum(s.kernel_ms for s in stats) / len(stats)
+    merge_ms = sum(s.merge_ms for s in stats) / len(stats)
+    agg = torch.tensor([elapsed, float(paths_local), kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = agg.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = agg.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed, paths_total, kern_ms_max = float(mx[0]), float(sm[1]), float(mx[2])
+    else:
+        paths_total, kern_ms_max = float(paths_local), kern_ms
+
+    if rank == 0:
+        value = paths_total / elapsed / 1e6
+        # roofline of the dominant kernel (k_render_exact): fp64 VALU bound.
+        fl = load_json(os.path.join(REPO, "profiles", f"flops_readme_{W}x{H}_s{S}x{S}.json"))
+        roof = None
+        if fl:
+            flops_per_launch = fl["flops_per_path"] * (paths_local / len(stats))
+            achieved = flops_per_launch / (kern_ms / 1e3) / 1e12
+            pmc = load_json(os.path.join(REPO, "profiles", f"pmc_readme_{W}x{H}_s{S}x{S}.json"))
+            roof = {"bound": "fp64-valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": achieved / FP64_PEAK_TFLOPS,
+                    "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
+                    "kernel": "k_render_exact", "kernel_ms": kern_ms, "merge_ms": merge_ms,
+                    "flops_per_path": fl["flops_per_path"]}
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "Mpaths/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (the reference's hard-coded README scene; no external data)",
+            "config": {
+                "workload": f"README sphere scene {W}x{H}, Stratified({S},{S}) = {S * S - 1} traced paths/px, "
+                            "Path(maxDepth 10, rr 1, Uniform), tile 16, EXACT per-tile RNG",
+                "width": W, "height": H, "spp": S * S, "traced_spp": S * S - 1,
+                "paths_per_frame": int(paths_total / args.steps), "mode": "exact",
+                "parallelism": f"tiles mod {world}" + (" + RCCL film reduce" if world > 1 else ""),
+                "lanes_per_wave": args.lanes_per_wave or 64,
+            },
+            "roofline": roof,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(args, rd_kwargs)
+        print(json.dumps(out), flush=True)
+    renderer.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

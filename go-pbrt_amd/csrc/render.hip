@@ -303,7 +303,8 @@ __global__ __launch_bounds__(kWave) void k_intersect(DevScene sc, int64_t n, con
 struct pbrt_gpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    double* film_target = nullptr;   // caller buffer of the last render_async_into
     int lanes_per_wave = 64;
     // device scene
     pbrt_shape_desc* d_shapes = nullptr;
@@ -500,7 +501,8 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
     c->host_lights.assign(scene->lights, scene->lights + scene->n_lights);
     c->host_scene.lights = c->host_lights.data();
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipEventCreate(&c->ev2) != hipSuccess) {
         pbrt_gpu_destroy(c);
         return PBRT_E_HIP;
     }
@@ -519,7 +521,7 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
     return PBRT_OK;
 }
 
-int pbrt_gpu_render_async(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
+int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_device) {
     if (!c) return PBRT_E_INVALID;
     if (c->cancel.load()) return set_err(c, PBRT_E_CANCELLED, "cancelled");
     HIPCHK(c, hipSetDevice(c->device));
@@ -527,6 +529,8 @@ int pbrt_gpu_render_async(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
     int rc = prepare(c, rd);
     if (rc != PBRT_OK) return rc;
     const RenderParams& rp = c->rp;
+    double* out = film_device ? film_device : c->d_out;
+    c->film_target = out;
     HIPCHK(c, hipMemsetAsync(c->d_ctr, 0, sizeof(Counters), c->stream));
     if (rp.n_slots > 0) HIPCHK(c, hipMemsetAsync(c->d_panics, 0, sizeof(PanicRec) * (size_t)rp.n_slots, c->stream));
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
@@ -537,13 +541,18 @@ int pbrt_gpu_render_async(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
                            c->d_s1d, c->d_panics, c->d_ctr);
         HIPCHK(c, hipGetLastError());
     }
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     int64_t npx = rp.film_w * rp.film_h;
     hipLaunchKernelGGL(k_merge_film, dim3((unsigned)((npx + 255) / 256)), dim3(256), 0, c->stream, c->d_film, rp,
-                       c->d_films, c->d_out);
+                       c->d_films, out);
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev2, c->stream));
     c->rendered = true;
     return PBRT_OK;
+}
+
+int pbrt_gpu_render_async(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
+    return pbrt_gpu_render_async_into(c, rd, nullptr);
 }
 
 int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
@@ -552,8 +561,9 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     Counters ctr;
     HIPCHK(c, hipMemcpy(&ctr, c->d_ctr, sizeof(ctr), hipMemcpyDeviceToHost));
-    float ms = 0;
+    float ms = 0, ms_merge = 0;
     (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
+    (void)hipEventElapsedTime(&ms_merge, c->ev1, c->ev2);
     int rc = PBRT_OK;
     pbrt_gpu_stats st;
     std::memset(&st, 0, sizeof(st));
@@ -561,6 +571,7 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
     st.camera_samples = ctr.camera_samples;
     st.paths_traced = ctr.paths;
     st.kernel_ms = ms;
+    st.merge_ms = ms_merge;
     if (ctr.any_panic) {
         std::vector<PanicRec> pr((size_t)c->rp.n_slots);
         HIPCHK(c, hipMemcpy(pr.data(), c->d_panics, sizeof(PanicRec) * pr.size(), hipMemcpyDeviceToHost));
@@ -602,7 +613,8 @@ void* pbrt_gpu_stream(pbrt_gpu_ctx* c) { return c ? (void*)c->stream : nullptr; 
 int pbrt_gpu_film_download(pbrt_gpu_ctx* c, double* film_xyz) {
     if (!c || !film_xyz || !c->rendered) return PBRT_E_INVALID;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipMemcpy(film_xyz, c->d_out, sizeof(double) * (size_t)(c->rp.film_w * c->rp.film_h * 3),
+    HIPCHK(c, hipMemcpy(film_xyz, c->film_target ? c->film_target : c->d_out,
+                        sizeof(double) * (size_t)(c->rp.film_w * c->rp.film_h * 3),
                         hipMemcpyDeviceToHost));
     return PBRT_OK;
 }
@@ -684,6 +696,7 @@ void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
         if (b) (void)hipFree(b);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->ev2) (void)hipEventDestroy(c->ev2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }

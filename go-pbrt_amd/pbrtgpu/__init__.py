@@ -45,6 +45,7 @@ def lib():
     L.pbrt_gpu_create.argtypes = [P(abi.SceneDesc), P(abi.GpuOpts), P(C.c_void_p)]
     L.pbrt_gpu_render.argtypes = [C.c_void_p, P(abi.RenderDesc), P(d), P(abi.GpuStats)]
     L.pbrt_gpu_render_async.argtypes = [C.c_void_p, P(abi.RenderDesc)]
+    L.pbrt_gpu_render_async_into.argtypes = [C.c_void_p, P(abi.RenderDesc), C.c_void_p]
     L.pbrt_gpu_synchronize.argtypes = [C.c_void_p, P(abi.GpuStats)]
     L.pbrt_gpu_film_device.argtypes = [C.c_void_p]
     L.pbrt_gpu_film_device.restype = C.c_void_p
@@ -297,8 +298,12 @@ class Renderer:
         self._check(rc, st)
         return film, st
 
-    def render_async(self, rd):
-        self._check(lib().pbrt_gpu_render_async(self.h, C.byref(rd)))
+    def render_async(self, rd, film_device_ptr=None):
+        """Enqueue a frame; film_device_ptr = caller device buffer (e.g. tensor.data_ptr())."""
+        if film_device_ptr is None:
+            self._check(lib().pbrt_gpu_render_async(self.h, C.byref(rd)))
+        else:
+            self._check(lib().pbrt_gpu_render_async_into(self.h, C.byref(rd), C.c_void_p(film_device_ptr)))
 
     def synchronize(self):
         st = abi.GpuStats()

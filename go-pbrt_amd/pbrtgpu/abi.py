@@ -197,6 +197,7 @@ class GpuStats(C.Structure):
         ("camera_samples", C.c_uint64),
         ("paths_traced", C.c_uint64),
         ("kernel_ms", C.c_double),
+        ("merge_ms", C.c_double),
         ("total_ms", C.c_double),
         ("panic_kind", C.c_int32),
         ("panic_tile", C.c_int32),

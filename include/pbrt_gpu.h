@@ -206,7 +206,8 @@ typedef struct pbrt_gpu_stats {
     uint64_t tiles_rendered;
     uint64_t camera_samples;     /* W*H*(spp-1) over rendered tiles           */
     uint64_t paths_traced;       /* camera rays that reached Li               */
-    double kernel_ms;            /* device time of the render kernels         */
+    double kernel_ms;            /* device time of the tile render kernel      */
+    double merge_ms;             /* device time of the film merge kernel       */
     double total_ms;             /* host wall time of the call                */
     int32_t panic_kind;          /* PBRT_PANIC_*                              */
     int32_t panic_tile;
@@ -250,6 +251,9 @@ int pbrt_gpu_render(pbrt_gpu_ctx* ctx, const pbrt_render_desc* rd,
 /* Same, but leaves the film in device memory (pbrt_gpu_film_device) and does
  * not synchronize with the host: the bench's timed region. */
 int pbrt_gpu_render_async(pbrt_gpu_ctx* ctx, const pbrt_render_desc* rd);
+/* Same, merging the film into a caller-owned device buffer of res_x*res_y*3
+ * doubles (e.g. a torch tensor that is then reduced over RCCL). */
+int pbrt_gpu_render_async_into(pbrt_gpu_ctx* ctx, const pbrt_render_desc* rd, double* film_device);
 int pbrt_gpu_synchronize(pbrt_gpu_ctx* ctx, pbrt_gpu_stats* stats);
 /* device pointer to the res_x*res_y*3 fp64 film of the last render */
 double* pbrt_gpu_film_device(pbrt_gpu_ctx* ctx);

@@ -25,6 +25,16 @@
 #include <stdint.h>
 #include <string.h>
 
+/* Algorithmic-FLOP accounting (bench.py roofline): one fp64 add, sub, mul, div
+ * or sqrt = 1; comparisons, Max/Min, abs, negation and Nextafter's bit steps = 0.
+ * Compiled in only for _build/liboracle_flops.so (-DORACLE_COUNT_FLOPS). */
+#ifdef ORACLE_COUNT_FLOPS
+extern __thread uint64_t orc_flops;
+#define FL(n) (orc_flops += (uint64_t)(n))
+#else
+#define FL(n) ((void)0)
+#endif
+
 static inline uint64_t gm_bits(double x) { uint64_t u; memcpy(&u, &x, 8); return u; }
 static inline double gm_from_bits(uint64_t u) { double x; memcpy(&x, &u, 8); return x; }
 static inline int gm_isnan(double x) { return x != x; }
@@ -63,8 +73,8 @@ static inline double go_nextafter(double x, double y) {
 }
 
 /* pkg/math/math.go:122-128 */
-static inline double go_next_float_up(double v) { return go_nextafter(v, v + 1); }
-static inline double go_next_float_down(double v) { return go_nextafter(v, v - 1); }
+static inline double go_next_float_up(double v) { FL(1); return go_nextafter(v, v + 1); }
+static inline double go_next_float_down(double v) { FL(1); return go_nextafter(v, v - 1); }
 
 /* pkg/math/math.go:17-19: MachineEpsilon = NextFloatUp(0) (smallest denormal) */
 #define GO_MACHINE_EPSILON 4.9406564584124654e-324
@@ -72,6 +82,7 @@ static inline double go_next_float_down(double v) { return go_nextafter(v, v - 1
 #define GO_ONE_MINUS_EPSILON 0.99999999999999988898
 /* pkg/math/math.go:82-84 */
 static inline double go_gamma(double n) {
+    FL(4);
     return (n * GO_MACHINE_EPSILON) / (1 - n * GO_MACHINE_EPSILON);
 }
 /* pkg/math/math.go:42-51 */
@@ -80,7 +91,7 @@ static inline double go_clamp(double v, double lo, double hi) {
     if (v > hi) return hi;
     return v;
 }
-static inline double go_lerp(double t, double v1, double v2) { return (1.0 - t) * v1 + t * v2; }
+static inline double go_lerp(double t, double v1, double v2) { FL(4); return (1.0 - t) * v1 + t * v2; }
 
 /* int(float64) / int64(float64) on amd64: CVTTSD2SQ, NaN / out of range -> INT64_MIN */
 static inline int64_t go_f2i(double x) {
@@ -109,15 +120,18 @@ static inline void gm_trig_reduce(double x, uint64_t* jo, double* zo) {
     /* arguments on the hot path are far below reduceThreshold (1<<29) */
     uint64_t j = (uint64_t)(x * gm_4_over_pi);
     double y = (double)j;
-    if (j & 1) { j++; y++; }
+    FL(7);
+    if (j & 1) { j++; y++; FL(1); }
     j &= 7;
     *zo = ((x - y * gm_PI4A) - y * gm_PI4B) - y * gm_PI4C;
     *jo = j;
 }
 static inline double gm_sin_poly(double z, double zz) {
+    FL(14);
     return z + z * zz * ((((((gm_sin[0] * zz) + gm_sin[1]) * zz + gm_sin[2]) * zz + gm_sin[3]) * zz + gm_sin[4]) * zz + gm_sin[5]);
 }
 static inline double gm_cos_poly(double zz) {
+    FL(16);
     return 1.0 - 0.5 * zz + zz * zz * ((((((gm_cos[0] * zz) + gm_cos[1]) * zz + gm_cos[2]) * zz + gm_cos[3]) * zz + gm_cos[4]) * zz + gm_cos[5]);
 }
 
@@ -131,6 +145,7 @@ static inline double go_cos(double x) {
     if (j > 3) { j -= 4; sign = !sign; }
     if (j > 1) sign = !sign;
     double zz = z * z, y;
+    FL(1);
     if (j == 1 || j == 2) y = gm_sin_poly(z, zz);
     else y = gm_cos_poly(zz);
     return sign ? -y : y;
@@ -145,6 +160,7 @@ static inline double go_sin(double x) {
     gm_trig_reduce(x, &j, &z);
     if (j > 3) { sign = !sign; j -= 4; }
     double zz = z * z, y;
+    FL(1);
     if (j == 1 || j == 2) y = gm_cos_poly(zz);
     else y = gm_sin_poly(z, zz);
     return sign ? -y : y;
@@ -162,11 +178,13 @@ static inline double go_tan(double x) {
     uint64_t j; double z;
     gm_trig_reduce(x, &j, &z);   /* tan.go does not mask j&7; j&2 is unaffected */
     double zz = z * z, y;
+    FL(1);
+    if (zz > 1e-14) FL(15);
     if (zz > 1e-14)
         y = z + z * (zz * (((P[0] * zz) + P[1]) * zz + P[2]) / ((((zz + Q1) * zz + Q2) * zz + Q3) * zz + Q4));
     else
         y = z;
-    if (j & 2) y = -1 / y;
+    if (j & 2) { y = -1 / y; FL(1); }
     return sign ? -y : y;
 }
 
@@ -177,6 +195,7 @@ static inline double gm_xatan(double x) {
                  P4 = -6.485021904942025371773e+01, Q0 = +2.485846490142306297962e+01,
                  Q1 = +1.650270098316988542046e+02, Q2 = +4.328810604912902668951e+02,
                  Q3 = +4.853903996359136964868e+02, Q4 = +1.945506571482613964425e+02;
+    FL(22);
     double z = x * x;
     z = z * ((((P0 * z + P1) * z + P2) * z + P3) * z + P4) / (((((z + Q0) * z + Q1) * z + Q2) * z + Q3) * z + Q4);
     z = x * z + x;
@@ -186,7 +205,8 @@ static inline double gm_satan(double x) {
     const double Morebits = 6.123233995736765886130e-17;
     const double Tan3pio8 = 2.41421356237309504880;
     if (x <= 0.66) return gm_xatan(x);
-    if (x > Tan3pio8) return GO_PI / 2 - gm_xatan(1 / x) + Morebits;
+    if (x > Tan3pio8) { FL(3); return GO_PI / 2 - gm_xatan(1 / x) + Morebits; }
+    FL(5);
     return GO_PI / 4 + gm_xatan((x - 1) / (x + 1)) + 0.5 * Morebits;
 }
 /* src/math/atan.go */
@@ -213,7 +233,9 @@ static inline double go_atan2(double y, double x) {
     }
     if (gm_isinf(y, 0)) return gm_copysign(GO_PI / 2, y);
     double q = go_atan(y / x);
+    FL(1);
     if (x < 0) {
+        FL(1);
         if (q <= 0) return q + GO_PI;
         return q - GO_PI;
     }
@@ -226,13 +248,14 @@ static inline double go_asin(double x) {
     if (x < 0) { x = -x; sign = 1; }
     if (x > 1) return NAN;
     double temp = sqrt(1 - x * x);
-    if (x > 0.7) temp = GO_PI / 2 - gm_satan(temp / x);
-    else temp = gm_satan(x / temp);
+    FL(3);
+    if (x > 0.7) { temp = GO_PI / 2 - gm_satan(temp / x); FL(2); }
+    else { temp = gm_satan(x / temp); FL(1); }
     return sign ? -temp : temp;
 }
-static inline double go_acos(double x) { return GO_PI / 2 - go_asin(x); }
+static inline double go_acos(double x) { FL(1); return GO_PI / 2 - go_asin(x); }
 
 /* pkg/math/math.go:113-115: Radians(deg) = Pi / 180.0 * deg (float64 vars) */
-static inline double go_radians(double deg) { return go_Pi / 180.0 * deg; }
+static inline double go_radians(double deg) { FL(2); return go_Pi / 180.0 * deg; }
 
 #endif

@@ -19,6 +19,18 @@
  */
 #include "oracle_render.h"
 
+#ifdef ORACLE_COUNT_FLOPS
+__thread uint64_t orc_flops;
+static __thread uint64_t orc_flops_saved;
+/* bracket reference computations whose results never reach an output (the
+ * device path does not execute them) */
+#define FL_OFF_BEGIN (orc_flops_saved = orc_flops)
+#define FL_OFF_END (orc_flops = orc_flops_saved)
+#else
+#define FL_OFF_BEGIN ((void)0)
+#define FL_OFF_END ((void)0)
+#endif
+
 #include <pthread.h>
 #include <stdatomic.h>
 #include <stdio.h>
@@ -52,6 +64,7 @@ uint32_t orc_pcg_bounded(orc_pcg* r, uint32_t b) {
     }
 }
 double orc_pcg_float(orc_pcg* r) {
+    FL(1);
     return go_min(GO_ONE_MINUS_EPSILON, (double)orc_pcg_next(r) * 2.3283064365386963e-10);
 }
 
@@ -69,6 +82,7 @@ static void sampler_start_pixel(sampler_t* s) {
     for (int d = 0; d < s->ndims; d++) {
         double* samp = s->s1d + (size_t)d * n;
         double inv = 1.0 / (double)n;
+        FL(1 + 2 * n);
         for (int32_t i = 0; i < n; i++) {
             double delta = 0.5;
             if (s->jitter) delta = orc_pcg_float(&s->rng);
@@ -197,9 +211,10 @@ static int sphere_intersect(panic_ctx* pc, const pbrt_shape_desc* s, const ray_t
     }
     v3 ph = v_add(ray.o, v_muls(ray.d, ts.v));
     ph = v_muls(ph, s->radius / v_dist(ph, V3(0, 0, 0)));
-    if (ph.x == 0.0 && ph.y == 0.0) ph.x = 1e-5 * s->radius;
+    FL(1);
+    if (ph.x == 0.0 && ph.y == 0.0) { ph.x = 1e-5 * s->radius; FL(1); }
     double phi = go_atan2(ph.y, ph.x);
-    if (phi < 0.0) phi += 2 * go_Pi;
+    if (phi < 0.0) { phi += 2 * go_Pi; FL(2); }
     if ((s->z_min > -s->radius && ph.z < s->z_min) || (s->z_max < s->radius && ph.z > s->z_max) ||
         phi > s->phi_max) {
         if (used_t1) return 0;
@@ -207,10 +222,11 @@ static int sphere_intersect(panic_ctx* pc, const pbrt_shape_desc* s, const ray_t
         ts = t1;
         ph = v_add(ray.o, v_muls(ray.d, ts.v));
         ph = v_muls(ph, s->radius / v_dist(ph, V3(0, 0, 0)));
-        if (ph.x == 0.0 && ph.y == 0.0) ph.x = 1e-5 * s->radius;
+        FL(1);
+        if (ph.x == 0.0 && ph.y == 0.0) { ph.x = 1e-5 * s->radius; FL(1); }
         /* sphere.go:127 declares a NEW phi (`phi :=`): the outer phi is kept */
         double phi2 = go_atan2(ph.y, ph.x);
-        if (phi2 < 0.0) phi2 += 2 * go_Pi;
+        if (phi2 < 0.0) { phi2 += 2 * go_Pi; FL(2); }
         if ((s->z_min > -s->radius && ph.z < s->z_min) || (s->z_max < s->radius && ph.z > s->z_max) ||
             phi2 > s->phi_max)
             return 0;
@@ -219,15 +235,19 @@ static int sphere_intersect(panic_ctx* pc, const pbrt_shape_desc* s, const ray_t
         *t_hit = ts.v;
         return 1;
     }
-    double u = phi / s->phi_max;
+    /* live part: reaches SurfaceInteraction fields the path reads */
     double theta = go_acos(go_clamp(ph.z / s->radius, -1, 1));
-    double v = (theta - s->theta_min) / (s->theta_max - s->theta_min);
     double zr = sqrt(ph.x * ph.x + ph.y * ph.y);
     double izr = 1.0 / zr;
     double cos_phi = ph.x * izr, sin_phi = ph.y * izr;
     v3 dpdu = V3(-s->phi_max * ph.y, s->phi_max * ph.x, 0);
     double dth = s->theta_max - s->theta_min;
     v3 dpdv = v_muls(V3(ph.z * cos_phi, ph.z * sin_phi, -s->radius * go_sin(theta)), dth);
+    FL(1 + 4 + 1 + 2 + 2 + 1 + 3);   /* ph.z/r, zr, 1/zr, cos/sin phi, dpdu, dth, dpdv comps */
+    /* dead part: uv and dndu/dndv never reach an output (not executed on the device) */
+    FL_OFF_BEGIN;
+    double u = phi / s->phi_max;
+    double v = (theta - s->theta_min) / (s->theta_max - s->theta_min);
     v3 d2uu = v_muls(V3(ph.x, ph.y, 0.0), -s->phi_max * s->phi_max);
     v3 d2uv = v_muls(V3(-sin_phi, cos_phi, 0.0), dth * ph.z * s->phi_max);
     v3 d2vv = v_muls(ph, -dth * dth);
@@ -237,6 +257,7 @@ static int sphere_intersect(panic_ctx* pc, const pbrt_shape_desc* s, const ray_t
     double inv = 1.0 / (E * G - F * F);
     v3 dndu = v_add(v_muls(dpdu, (f * F - e * G) * inv), v_muls(dpdv, (e * F - f * E) * inv));
     v3 dndv = v_add(v_muls(dpdu, (g * F - f * G) * inv), v_muls(dpdv, (f * F - g * E) * inv));
+    FL_OFF_END;
     v3 perr = v_muls(v_abs(ph), go_gamma(5));
     *si = si_new_with(ph, perr, u, v, v_muls(ray.d, -1), dpdu, dpdv, dndu, dndv, ray.time,
                       s->reverse_orientation, s->transform_swaps_handedness);
@@ -251,21 +272,26 @@ static int disk_intersect(const pbrt_shape_desc* s, const ray_t* r, si_t* si, do
     ray_t ray = xf_ray(&w2o, r, NULL, NULL);
     if (ray.d.z == 0) return 0;
     double ts = (s->height - ray.o.z) / ray.d.z;
+    FL(2);
     if (ts <= 0 || ts >= ray.tmax) return 0;
     v3 ph = v_add(ray.o, v_muls(ray.d, ts));
     double dist2 = ph.x * ph.x + ph.y * ph.y;
+    FL(5);
     if (dist2 > s->radius * s->radius || dist2 < s->inner_radius * s->inner_radius) return 0;
     double phi = go_atan2(ph.y, ph.x);
-    if (phi < 0) phi += 2 * go_Pi;
+    if (phi < 0) { phi += 2 * go_Pi; FL(2); }
     if (phi > s->phi_max) return 0;
     if (!si) {
         *t_hit = ts;
         return 1;
     }
-    double u = phi / s->phi_max;
     double rhit = sqrt(dist2);
+    FL(1 + 2 + 2);   /* sqrt, dpdu comps, (r - inner)/rhit */
+    FL_OFF_BEGIN;   /* uv: never reaches an output */
+    double u = phi / s->phi_max;
     double omv = (rhit - s->inner_radius) / (s->radius - s->inner_radius);
     double v = 1 - omv;
+    FL_OFF_END;
     v3 dpdu = V3(-s->phi_max * ph.y, s->phi_max * ph.x, 0);
     v3 dpdv = v_muls(V3(ph.x, ph.y, 0), (s->radius - s->inner_radius) / rhit);
     ph.z = s->height;
@@ -326,12 +352,14 @@ static int bounds_intersect_p(const pbrt_bvh_node* nd, const ray_t* r, v3 inv, c
     double robust = 1 + 2 * go_gamma(3);
     tmax *= robust;
     tymax *= robust;
+    FL(8 + 2 + 2);
     if (tmin > tymax || tymin > tmax) return 0;
     if (tymin > tmin) tmin = tymin;
     if (tymax < tmax) tmax = tymax;
     double tzmin = (bx[neg[2]][2] - r->o.z) * inv.z;
     double tzmax = (bx[1 - neg[2]][2] - r->o.z) * inv.z;
     tzmax *= robust;
+    FL(4 + 2 + 1);
     if (tmin > tzmax || tzmin > tmax) return 0;
     if (tzmin > tmin) tmin = tzmin;
     if (tzmax < tmax) tmax = tzmax;
@@ -343,6 +371,7 @@ int orc_bvh_intersect(panic_ctx* pc, const pbrt_scene_desc* sc, ray_t* ray, si_t
     if (sc->n_nodes == 0) return 0;
     int hit = 0;
     v3 inv = V3(1 / ray->d.x, 1 / ray->d.y, 1 / ray->d.z);
+    FL(3);
     int neg[3] = {inv.x < 0, inv.y < 0, inv.z < 0};
     uint64_t to_visit = 0, cur = 0;
     uint64_t stack[64];
@@ -375,6 +404,7 @@ int orc_bvh_intersect(panic_ctx* pc, const pbrt_scene_desc* sc, ray_t* ray, si_t
 int orc_bvh_intersect_p(panic_ctx* pc, const pbrt_scene_desc* sc, const ray_t* ray) {
     if (sc->n_nodes == 0) return 0;
     v3 inv = V3(1 / ray->d.x, 1 / ray->d.y, 1 / ray->d.z);
+    FL(3);
     int neg[3] = {inv.x < 0, inv.y < 0, inv.z < 0};
     uint64_t to_visit = 0, cur = 0;
     uint64_t stack[64];
@@ -418,7 +448,7 @@ typedef struct {
 #define BXDF_ALL 31
 #define LAMBERT_TYPE (BXDF_REFLECTION | BXDF_DIFFUSE)
 
-static double inv_pi(void) { return 1.0 / go_Pi; }   /* pkg/math InvPi = 1.0 / Pi */
+static double inv_pi(void) { FL(1); return 1.0 / go_Pi; }   /* pkg/math InvPi = 1.0 / Pi */
 static int matches_flags(int t, int flags) { return (t & flags) == t; }
 
 /* matte.go:21-37 + reflection.go:128-140 + checkerboard.go:30-40 */
@@ -434,6 +464,7 @@ static int material_bsdf(const pbrt_scene_desc* sc, const si_t* si, bsdf_t* b) {
         double s = m->ds + v_dot(si->p, V3(m->vs[0], m->vs[1], m->vs[2]));
         double t = m->dt + v_dot(si->p, V3(m->vt[0], m->vt[1], m->vt[2]));
         int64_t k = go_f2i(floor(s) + floor(t));
+        FL(3);
         if (k % 2 == 0) r = S3(m->tex1[0], m->tex1[1], m->tex1[2]);
         else r = S3(m->tex2[0], m->tex2[1], m->tex2[2]);
     } else {
@@ -452,11 +483,14 @@ static v3 bsdf_w2l(const bsdf_t* b, v3 v) { return V3(v_dot(v, b->ss), v_dot(v, 
 
 /* reflection.go:169-186 */
 static spec bsdf_f(const bsdf_t* b, v3 woW, v3 wiW, int flags) {
-    v3 wi = bsdf_w2l(b, wiW);
+    FL_OFF_BEGIN;
+    v3 wi = bsdf_w2l(b, wiW);   /* dead for Lambertian */
+    FL_OFF_END;
     v3 wo = bsdf_w2l(b, woW);
     (void)wi;
     if (wo.z == 0.0) return S3(0, 0, 0);
     int reflect = v_dot(wiW, b->ng) * v_dot(woW, b->ng) > 0;
+    FL(1);
     spec f = S3(0, 0, 0);
     if (b->n_bxdfs && matches_flags(LAMBERT_TYPE, flags) && reflect)
         f = s_add(f, s_muls(b->r, inv_pi()));
@@ -464,7 +498,8 @@ static spec bsdf_f(const bsdf_t* b, v3 woW, v3 wiW, int flags) {
 }
 /* reflection.go:343-348 */
 static double lambert_pdf(v3 wo, v3 wi) {
-    if (wo.z * wi.z > 0) return gm_abs(wi.z) * inv_pi();
+    FL(1);
+    if (wo.z * wi.z > 0) { FL(1); return gm_abs(wi.z) * inv_pi(); }
     return 0;
 }
 /* reflection.go:255-278 */
@@ -475,29 +510,35 @@ static double bsdf_pdf(const bsdf_t* b, v3 woW, v3 wiW, int flags) {
     if (wo.z == 0) return 0;
     double pdf = 0;
     int matching = 0;
-    if (matches_flags(LAMBERT_TYPE, flags)) { matching++; pdf += lambert_pdf(wo, wi); }
+    if (matches_flags(LAMBERT_TYPE, flags)) { matching++; pdf += lambert_pdf(wo, wi); FL(1); }
     if (matching <= 0) return 0;
+    FL(1);
     return pdf / (double)matching;
 }
 /* sampling.go:173-198 */
 static v2 concentric_sample_disk(v2 u) {
     v2 uo = {u.x * 2.0 - 1, u.y * 2.0 - 1};
+    FL(4);
     v2 z = {0, 0};
     if (uo.x == 0 && uo.y == 0) return z;
     double theta, r;
     if (gm_abs(uo.x) > gm_abs(uo.y)) {
         r = uo.x;
         theta = (go_Pi / 4.0) * (uo.y / uo.x);
+        FL(3);
     } else {
         r = uo.y;
         theta = (go_Pi / 2.0) - (go_Pi / 4.0) * (uo.x / uo.y);
+        FL(5);
     }
     v2 p = {go_cos(theta) * r, go_sin(theta) * r};
+    FL(2);
     return p;
 }
 static v3 cosine_sample_hemisphere(v2 u) {
     v2 d = concentric_sample_disk(u);
     double z = sqrt(go_max(0.0, 1.0 - d.x * d.x - d.y * d.y));
+    FL(5);
     return V3(d.x, d.y, z);
 }
 /* reflection.go:188-253; returns the LOCAL-frame wi (#7) */
@@ -508,11 +549,12 @@ static spec bsdf_sample_f(const bsdf_t* b, v3 woW, v2 u, int t, v3* wi_out, doub
     if (matching == 0) return S3(0, 0, 0);
     double comp = go_min(floor(u.x * (double)matching), (double)matching - 1);
     v2 ur = {go_min(u.x * (double)matching - comp, GO_ONE_MINUS_EPSILON), u.y};
+    FL(4);
     v3 wo = bsdf_w2l(b, woW);
     if (wo.z == 0.0) return S3(0, 0, 0);
     /* reflection.go:305-314 sampleF */
     v3 wi = cosine_sample_hemisphere(ur);
-    if (wo.z < 0) wi.z *= -1;
+    if (wo.z < 0) { wi.z *= -1; FL(1); }
     double pdf = lambert_pdf(wo, wi);
     spec f = s_muls(b->r, inv_pi());
     if (pdf == 0.0) return S3(0, 0, 0);
@@ -530,6 +572,7 @@ static intr_t sphere_sample(const pbrt_shape_desc* s, v2 u, double* pdf) {
     double z = 1.0 - 2.0 * u.x;
     double rr = sqrt(go_max(0, 1 - z * z));
     double phi = 2 * go_Pi * u.y;
+    FL(2 + 3 + 2 + 2 + 1);   /* z, rr, phi, rr*cos/sin, radius/dist */
     v3 pobj = v_muls(V3(rr * go_cos(phi), rr * go_sin(phi), z), s->radius);
     intr_t it;
     it.n = v_normalized(xf_normal(&s->object_to_world, pobj));
@@ -540,6 +583,7 @@ static intr_t sphere_sample(const pbrt_shape_desc* s, v2 u, double* pdf) {
     it.time = 0;
     double area = s->phi_max * s->radius * (s->z_max - s->z_min);
     *pdf = 1.0 / area;
+    FL(4);
     return it;
 }
 /* sphere.go:287-344 */
@@ -554,8 +598,9 @@ static intr_t sphere_sample_at(const pbrt_shape_desc* s, const si_t* ref, v2 u, 
         } else {
             /* Normalize() in place (xyz.go:587-594) */
             double n2 = v_len2(wi);
-            if (n2 > 0) { double invn = 1.0 / sqrt(n2); wi.x *= invn; wi.y *= invn; wi.z *= invn; }
+            if (n2 > 0) { double invn = 1.0 / sqrt(n2); wi.x *= invn; wi.y *= invn; wi.z *= invn; FL(5); }
             *pdf *= v_dist2(ref->p, it.p) / v_absdot(it.n, v_muls(wi, -1));
+            FL(2);
         }
         if (gm_isinf(*pdf, 0)) *pdf = 0.0;
         return it;
@@ -573,6 +618,7 @@ static intr_t sphere_sample_at(const pbrt_shape_desc* s, const si_t* ref, v2 u, 
     double ds = dc * cost - sqrt(go_max(0, r2 - (dc * dc) * (sint * sint)));
     double cosa = (dc * dc + r2 - ds * ds) / (2.0 * dc * s->radius);
     double sina = sqrt(go_max(0, 1.0 - cosa * cosa));
+    FL(1 + 1 + 2 + 3 + 3 + 2 + 6 + 7 + 3 + 2);
     /* geometry.go:66-70 SphericalDirectionXYZ */
     v3 x = v_muls(wcx, -1), y = v_muls(wcy, -1), zz = v_muls(wc, -1);
     v3 nw = v_add(v_add(v_muls(x, sina * go_cos(phi)), v_muls(y, sina * go_sin(phi))), v_muls(zz, cosa));
@@ -584,6 +630,7 @@ static intr_t sphere_sample_at(const pbrt_shape_desc* s, const si_t* ref, v2 u, 
     if (s->reverse_orientation) it.n = v_muls(it.n, -1);
     it.time = 0;
     *pdf = 1.0 / (2.0 * go_Pi * (1.0 - cosmax));
+    FL(4);
     return it;
 }
 
@@ -596,6 +643,7 @@ static ray_t spawn_ray_to(const si_t* from, v3 to_p, v3 to_perr, v3 to_n) {
     r.d = v_sub(target, origin);
     r.tmax = 1 - 0.0001;
     r.time = from->time;
+    FL(1);
     return r;
 }
 
@@ -658,6 +706,7 @@ static spec estimate_direct(orc_ctx* oc, const si_t* si, const bsdf_t* b, v2 u_s
                 } else {
                     double fp = 1.0 * light_pdf, gp = 1.0 * scat_pdf;
                     double weight = (fp * fp) / (fp * fp + gp * gp);
+                    FL(7);
                     Ld = s_add(Ld, s_divs(s_muls(s_mul(f, Li), weight), light_pdf));
                 }
             }
@@ -692,7 +741,7 @@ static int sample_discrete(const pbrt_distribution_desc* d, double u, double* pd
     }
     int off = (int)go_clamp((double)(first - 1), 0, (double)(size - 2));
     *pdf = 0;
-    if (d->func_int > 0) *pdf = d->func[off] / (d->func_int / (double)d->count);
+    if (d->func_int > 0) { *pdf = d->func[off] / (d->func_int / (double)d->count); FL(2); }
     return off;
 }
 
@@ -709,6 +758,7 @@ static spec uniform_sample_one_light(orc_ctx* oc, sampler_t* smp, const si_t* si
     } else {
         ln = (int)go_f2i(go_min(sampler_get1d(smp) * (double)n, (double)(n - 1)));
         lpdf = 1.0 / (double)n;
+        FL(2);
     }
     v2 ul = sampler_get2d(smp);
     v2 us = sampler_get2d(smp);
@@ -749,6 +799,7 @@ static spec path_li(orc_ctx* oc, sampler_t* smp, ray_t ray) {
         if (s_is_black(f) || pdf == 0.0) break;
         double wabs = v_absdot(wi, isect.sn);
         double wp = wabs / pdf;
+        FL(1);
         spec fm = s_muls(f, wp);
         beta = s_mul(beta, fm);
         /* interaction.go:68-77 SpawnRay */
@@ -759,8 +810,10 @@ static spec path_li(orc_ctx* oc, sampler_t* smp, ray_t ray) {
         spec rr = s_muls(beta, eta_scale);
         if (s_max_component(rr) < rd->rr_threshold && bounces > 3) {
             double q = go_max(0.05, 1 - s_max_component(rr));
+            FL(1);
             if (sampler_get1d(smp) < q) break;
             beta = s_divs(beta, 1 - q);
+            FL(1);
         }
     }
     return L;
@@ -819,6 +872,7 @@ static ray_t camera_ray(const pbrt_camera_desc* cam, double fx, double fy, doubl
         v2 pl = concentric_sample_disk(plens);
         pl.x *= cam->lens_radius; pl.y *= cam->lens_radius;
         double ft = cam->focal_distance / r.d.z;
+        FL(3);
         v3 pf = v_add(v_muls(r.d, ft), r.o);
         r.o = V3(pl.x, pl.y, 0);
         r.d = v_normalized(v_sub(pf, r.o));
@@ -873,6 +927,7 @@ static void film_tile_add(const pbrt_film_desc* fm, film_tile_t* ft, double pfx,
                           double w) {
     if (0.0 > fm->max_sample_luminance) L = s_muls(L, fm->max_sample_luminance / 0.0); /* L.Y() == 0 (#5) */
     double dx = pfx - 0.5, dy = pfy - 0.5;
+    FL(2);
     double p0fx = ceil(dx - fm->filter_radius_x), p0fy = ceil(dy - fm->filter_radius_y);
     double p1fx = floor(dx + fm->filter_radius_x) + 1, p1fy = floor(dy + fm->filter_radius_y) + 1;
     int64_t p0x = go_f2i(go_max(p0fx, (double)ft->px0)), p0y = go_f2i(go_max(p0fy, (double)ft->py0));
@@ -894,6 +949,7 @@ static void film_tile_add(const pbrt_film_desc* fm, film_tile_t* ft, double pfx,
             double* px = ft->contrib + ((x - ft->px0) + (y - ft->py0) * tw) * 3;
             spec add = s_muls(L, w * fw);
             px[0] += add.c[0]; px[1] += add.c[1]; px[2] += add.c[2];
+            FL(4);
         }
 }
 
@@ -954,7 +1010,7 @@ typedef struct {
     int* panic_kind;
     int64_t* panic_info;    /* 4 per tile: px, py, sample, bounce */
     int flags;
-    atomic_ullong paths, samples, closest, shadow;
+    atomic_ullong paths, samples, closest, shadow, flops;
 } job_t;
 
 static void* worker(void* arg) {
@@ -962,6 +1018,9 @@ static void* worker(void* arg) {
     orc_ctx oc;
     memset(&oc, 0, sizeof(oc));
     oc.scene = j->sc; oc.rd = j->rd; oc.flags = j->flags;
+#ifdef ORACLE_COUNT_FLOPS
+    orc_flops = 0;
+#endif
     orc_light_distribution(j->sc, j->rd, &oc.dist);
     int spp = j->rd->sampler_x * j->rd->sampler_y;
     double* s1d = (double*)malloc(sizeof(double) * (size_t)spp * (size_t)(j->rd->n_dims > 0 ? j->rd->n_dims : 1));
@@ -983,6 +1042,9 @@ static void* worker(void* arg) {
     atomic_fetch_add(&j->samples, oc.camera_samples);
     atomic_fetch_add(&j->closest, oc.closest_rays);
     atomic_fetch_add(&j->shadow, oc.shadow_rays);
+#ifdef ORACLE_COUNT_FLOPS
+    atomic_fetch_add(&j->flops, orc_flops);
+#endif
     free(s1d);
     return NULL;
 }
@@ -1083,6 +1145,7 @@ int orc_render(const pbrt_scene_desc* sc, const pbrt_render_desc* rd, int n_thre
         stats->camera_samples = atomic_load(&j.samples);
         stats->closest_rays = atomic_load(&j.closest);
         stats->shadow_rays = atomic_load(&j.shadow);
+        stats->flops = atomic_load(&j.flops);
     }
     free(pool); free(j.films); free(j.status); free(j.panic_kind); free(j.panic_info); free(tiles);
     return rc;

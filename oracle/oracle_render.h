@@ -29,6 +29,7 @@ typedef struct {
 
 typedef struct {
     uint64_t tiles, paths, camera_samples, closest_rays, shadow_rays;
+    uint64_t flops;   /* fp64 add/sub/mul/div/sqrt executed (liboracle_flops.so only) */
     int32_t panic_kind;
     int64_t panic_tile, panic_px, panic_py, panic_sample, panic_bounce;
 } orc_stats;

@@ -16,8 +16,10 @@ from pbrtgpu import abi  # noqa: E402
 
 ORACLE_DIR = os.path.join(REPO, "oracle")
 ORACLE_SO = os.path.join(ORACLE_DIR, "_build", "liboracle.so")
+ORACLE_FLOPS_SO = os.path.join(ORACLE_DIR, "_build", "liboracle_flops.so")
 
 _lib = None
+_lib_flops = None
 
 
 class OracleStats(C.Structure):
@@ -27,6 +29,7 @@ class OracleStats(C.Structure):
         ("camera_samples", C.c_uint64),
         ("closest_rays", C.c_uint64),
         ("shadow_rays", C.c_uint64),
+        ("flops", C.c_uint64),
         ("panic_kind", C.c_int32),
         ("panic_tile", C.c_int64),
         ("panic_px", C.c_int64),
@@ -40,12 +43,24 @@ def build():
     subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
 
 
-def lib():
-    global _lib
+def lib(flops=False):
+    """The oracle library; flops=True loads the FLOP-accounting build."""
+    global _lib, _lib_flops
+    if flops:
+        if _lib_flops is None:
+            if not os.path.exists(ORACLE_FLOPS_SO):
+                build()
+            _lib_flops = _bind(C.CDLL(ORACLE_FLOPS_SO))
+        return _lib_flops
     if _lib is None:
         if not os.path.exists(ORACLE_SO):
             build()
-        L = C.CDLL(ORACLE_SO)
+        _lib = _bind(C.CDLL(ORACLE_SO))
+    return _lib
+
+
+def _bind(L):
+    if True:
         d = C.c_double
         P = C.POINTER
         for name in ("sin", "cos", "tan", "atan", "asin", "acos", "radians"):
@@ -91,8 +106,8 @@ def lib():
         L.oracle_num_tiles.restype = C.c_int64
         L.oracle_intersect.argtypes = [P(abi.SceneDesc), P(d), C.c_size_t, C.c_int, P(d)]
         L.oracle_light_distribution.argtypes = [P(abi.SceneDesc), P(abi.RenderDesc), P(abi.DistributionDesc)]
-        _lib = L
-    return _lib
+        L.oracle_spawn_ray_to.argtypes = [P(d), P(d)]
+    return L
 
 
 def dptr(a):
@@ -126,14 +141,14 @@ class OracleScene:
             self.h = None
 
 
-def render(desc, rd, threads=None, flags=0):
+def render(desc, rd, threads=None, flags=0, flops=False):
     """Returns (rc, film[H,W,3] float64, OracleStats)."""
     threads = threads or os.cpu_count() or 1
     W = desc.film.crop_max_x - desc.film.crop_min_x
     H = desc.film.crop_max_y - desc.film.crop_min_y
     film = np.zeros((H, W, 3), dtype=np.float64)
     st = OracleStats()
-    rc = lib().oracle_render(C.byref(desc), C.byref(rd), threads, flags, dptr(film), C.byref(st))
+    rc = lib(flops).oracle_render(C.byref(desc), C.byref(rd), threads, flags, dptr(film), C.byref(st))
     return rc, film, st
 
 
