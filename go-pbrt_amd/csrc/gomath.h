@@ -34,18 +34,22 @@ GO_HD double copysign(double x, double s) {
 }
 GO_HD double nan() { return from_bits(0x7FF8000000000001ULL); }
 
-// src/math/dim.go Max/Min (+Inf / -Inf win over NaN; +0 > -0)
+// src/math/dim.go Max/Min (+Inf / -Inf win over NaN; +0 > -0). Written as
+// selects (no early returns) so 64-lane waves do not branch on them; the
+// results are bit-identical to the Go code path by path:
+//   x == y (incl. +0 vs -0): Max -> bits(x) & bits(y)  (+0 unless both -0)
+//                            Min -> bits(x) | bits(y)  (-0 unless both +0)
 GO_HD double max(double x, double y) {
-    if (x == kInf || y == kInf) return kInf;
-    if (is_nan(x) || is_nan(y)) return nan();
-    if (x == 0 && x == y) return signbit(x) ? y : x;
-    return x > y ? x : y;
+    double r = x > y ? x : y;
+    r = x == y ? from_bits(bits(x) & bits(y)) : r;
+    r = (is_nan(x) || is_nan(y)) ? nan() : r;
+    return (x == kInf || y == kInf) ? kInf : r;
 }
 GO_HD double min(double x, double y) {
-    if (x == -kInf || y == -kInf) return -kInf;
-    if (is_nan(x) || is_nan(y)) return nan();
-    if (x == 0 && x == y) return signbit(x) ? x : y;
-    return x < y ? x : y;
+    double r = x < y ? x : y;
+    r = x == y ? from_bits(bits(x) | bits(y)) : r;
+    r = (is_nan(x) || is_nan(y)) ? nan() : r;
+    return (x == -kInf || y == -kInf) ? -kInf : r;
 }
 
 // src/math/nextafter.go
@@ -56,9 +60,24 @@ GO_HD double nextafter(double x, double y) {
     if ((y > x) == (x > 0)) return from_bits(bits(x) + 1);
     return from_bits(bits(x) - 1);
 }
-// pkg/math/math.go:122-128 (no-op for |v| >= 2^53, parity ledger #24)
-GO_HD double next_up(double v) { return nextafter(v, v + 1); }
-GO_HD double next_down(double v) { return nextafter(v, v - 1); }
+// pkg/math/math.go:122-128: Nextafter(v, v+1) / Nextafter(v, v-1); no-op for
+// |v| >= 2^53 (v == v±1, parity ledger #24). Branch-free forms of the above.
+GO_HD double next_up(double v) {
+    const uint64_t u = bits(v);
+    uint64_t r = v > 0 ? u + 1 : u - 1;
+    r = v == 0 ? 1ULL : r;
+    double d = from_bits(r);
+    d = v == v + 1 ? v : d;
+    return is_nan(v) ? nan() : d;
+}
+GO_HD double next_down(double v) {
+    const uint64_t u = bits(v);
+    uint64_t r = v > 0 ? u - 1 : u + 1;
+    r = v == 0 ? 0x8000000000000001ULL : r;
+    double d = from_bits(r);
+    d = v == v - 1 ? v : d;
+    return is_nan(v) ? nan() : d;
+}
 
 // pkg/math/math.go:82-84: Gamma(n) = n*eps/(1-n*eps) with eps a denormal
 GO_HD double gamma(double n) { return (n * kMachineEpsilon) / (1 - n * kMachineEpsilon); }

@@ -167,9 +167,9 @@ struct EF {
 };
 // efloat.go:102-111 Check(): Inf/NaN bounds or Low > High panics in Go
 GO_HD void ef_check(const EF& f, int& panic) {
-    if (gomath::is_inf(f.lo) || gomath::is_nan(f.lo) || gomath::is_inf(f.hi) || gomath::is_nan(f.hi) ||
-        f.lo > f.hi)
-        panic = 1;
+    // !(|lo| < Inf) is true for ±Inf and NaN
+    const bool bad = !(gomath::abs(f.lo) < kInf) | !(gomath::abs(f.hi) < kInf) | (f.lo > f.hi);
+    panic = bad ? 1 : panic;
 }
 GO_HD EF ef_new(double v, double err, int& panic) {
     EF f{v, v, v};

@@ -259,33 +259,32 @@ __device__ inline bool shape_intersect(const pbrt_shape_desc& s, const Ray& r, S
     return disk_intersect<kFull>(s, r, si, t_hit);
 }
 
+// Shape test without the SurfaceInteraction: the hit parameter only.
+__device__ inline bool prim_hit_t(const DevScene& sc, int pi, const Ray& r, double& t_hit, int& panic) {
+    const pbrt_primitive_desc& p = sc.prims[pi];
+    const pbrt_shape_desc& s = sc.shapes[p.shape];
+    Ray ray = r;
+    if (p.kind == PBRT_PRIM_TRANSFORMED) ray = xf_ray(p.prim_to_world.m_inv, r, nullptr, nullptr);
+    return shape_intersect<false>(s, ray, nullptr, t_hit, panic);
+}
+
 // GeometricPrimitive / TransformedPrimitive (primitive.go:42-115)
 __device__ inline bool prim_intersect(const DevScene& sc, int pi, Ray& r, SI& si, int& panic) {
     const pbrt_primitive_desc& p = sc.prims[pi];
     const pbrt_shape_desc& s = sc.shapes[p.shape];
+    const bool xformed = p.kind == PBRT_PRIM_TRANSFORMED;
+    Ray ray = r;
+    if (xformed) ray = xf_ray(p.prim_to_world.m_inv, r, nullptr, nullptr);
     double t_hit;
-    if (p.kind == PBRT_PRIM_TRANSFORMED) {
-        Ray ray = xf_ray(p.prim_to_world.m_inv, r, nullptr, nullptr);
-        if (!shape_intersect<true>(s, ray, &si, t_hit, panic)) return false;
-        si.prim = pi;
-        r.tmax = t_hit;
-        if (!is_identity(p.prim_to_world.m)) transform_si_shared(si, p.prim_to_world.m, p.prim_to_world.m_inv);
-        return true;
-    }
-    if (!shape_intersect<true>(s, r, &si, t_hit, panic)) return false;
-    r.tmax = t_hit;
+    if (!shape_intersect<true>(s, ray, &si, t_hit, panic)) return false;
     si.prim = pi;
+    r.tmax = t_hit;
+    if (xformed && !is_identity(p.prim_to_world.m)) transform_si_shared(si, p.prim_to_world.m, p.prim_to_world.m_inv);
     return true;
 }
 __device__ inline bool prim_intersect_p(const DevScene& sc, int pi, const Ray& r, int& panic) {
-    const pbrt_primitive_desc& p = sc.prims[pi];
-    const pbrt_shape_desc& s = sc.shapes[p.shape];
     double t_hit;
-    if (p.kind == PBRT_PRIM_TRANSFORMED) {
-        Ray ray = xf_ray(p.prim_to_world.m_inv, r, nullptr, nullptr);
-        return shape_intersect<false>(s, ray, nullptr, t_hit, panic);
-    }
-    return shape_intersect<false>(s, r, nullptr, t_hit, panic);
+    return prim_hit_t(sc, pi, r, t_hit, panic);
 }
 
 // ------------------------------------------------------------------------ BVH
@@ -310,44 +309,81 @@ __device__ __forceinline__ bool node_hit(const pbrt_bvh_node& nd, const Ray& r, 
     return tmin < r.tmax && tmax > 0;
 }
 
+
 // BVH.Intersect (bvh.go:659-712) / IntersectP (:713-765). The [64] node stack
 // lives in LDS (one uint16 column per lane).
+//
+// Structured "while-while" for 64-lane waves: loop A walks interior nodes
+// until the lane reaches a leaf whose box it hits (or empties its stack),
+// loop B then tests that leaf's primitives, so the wave runs the expensive
+// shape code once per leaf round instead of once per node step. Node order,
+// box tests and TMax updates are exactly the reference's.
+//
+// Closest hit: each accepted primitive only shrinks TMax; the interaction of
+// the LAST accepted one is computed once after the walk. This equals the
+// reference's per-hit SurfaceInteraction: a shape's chosen root (t0 or t1)
+// never depends on TMax (TMax only rejects), so re-running the accepted
+// primitive with the unchanged ray gives the same hit and the same fields.
 template <bool kAny>
 __device__ inline bool bvh_traverse(const DevScene& sc, Ray& ray, SI* si, uint16_t* stack, int& panic) {
     if (sc.n_nodes == 0) return false;
-    bool hit = false;
+    const double ray_tmax0 = ray.tmax;
     V3 inv{1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z};
     const int nx = inv.x < 0, ny = inv.y < 0, nz = inv.z < 0;
     const uint32_t negmask = (uint32_t)nx | ((uint32_t)ny << 1) | ((uint32_t)nz << 2);
     uint32_t to_visit = 0, cur = 0;
+    int best = -1;
     for (;;) {
-        const pbrt_bvh_node& nd = sc.nodes[cur];
-        if (node_hit(nd, ray, inv, nx, ny, nz)) {
-            if (nd.n_prims > 0) {
-                for (uint32_t i = 0; i < nd.n_prims; i++) {
-                    if (kAny) {
-                        if (prim_intersect_p(sc, (int)(nd.offset + i), ray, panic)) return true;
-                    } else {
-                        if (prim_intersect(sc, (int)(nd.offset + i), ray, *si, panic)) hit = true;
-                    }
-                    if (panic) return hit;
+        // A: interior nodes
+        bool leaf = false, done = false;
+        for (;;) {
+            const pbrt_bvh_node& nd = sc.nodes[cur];
+            if (node_hit(nd, ray, inv, nx, ny, nz)) {
+                if (nd.n_prims > 0) {
+                    leaf = true;
+                    break;
                 }
-                if (to_visit == 0) break;
-                cur = stack[(--to_visit) * kStackStride];
-            } else {
-                if (to_visit >= 64) { panic = PBRT_PANIC_BVH_STACK; return hit; }
+                if (to_visit >= 64) {
+                    panic = PBRT_PANIC_BVH_STACK;
+                    return kAny ? false : best >= 0;
+                }
                 uint32_t far_node, near_node;
                 if ((negmask >> nd.axis) & 1u) { far_node = cur + 1; near_node = nd.offset; }
                 else { far_node = nd.offset; near_node = cur + 1; }
                 stack[(to_visit++) * kStackStride] = (uint16_t)far_node;
                 cur = near_node;
+            } else {
+                if (to_visit == 0) {
+                    done = true;
+                    break;
+                }
+                cur = stack[(--to_visit) * kStackStride];
             }
-        } else {
-            if (to_visit == 0) break;
-            cur = stack[(--to_visit) * kStackStride];
         }
+        if (done) break;
+        (void)leaf;
+        // B: the leaf's primitives
+        const pbrt_bvh_node& nd = sc.nodes[cur];
+        const uint32_t first = nd.offset, np = nd.n_prims;
+        for (uint32_t i = 0; i < np; i++) {
+            double t_hit;
+            const bool h = prim_hit_t(sc, (int)(first + i), ray, t_hit, panic);
+            if (panic) return kAny ? false : best >= 0;
+            if (h) {
+                if (kAny) return true;
+                ray.tmax = t_hit;
+                best = (int)(first + i);
+            }
+        }
+        if (to_visit == 0) break;
+        cur = stack[(--to_visit) * kStackStride];
     }
-    return hit;
+    if (!kAny && best >= 0) {
+        Ray r = ray;
+        r.tmax = ray_tmax0;
+        prim_intersect(sc, best, r, *si, panic);
+    }
+    return best >= 0;
 }
 
 // ----------------------------------------------------------------- material
@@ -539,7 +575,8 @@ __device__ inline void sample_li(const DevScene& sc, const pbrt_light_desc& L, c
 // EstimateDirect, light-sampling half (integrator.go:79-130). The BSDF-sampled
 // MIS half (:132-192) is not executed: no primitive carries an area light
 // (primitive.go:33, GetAreaLight() == nil) so it always contributes 0.
-__device__ inline Spec estimate_direct(const DevScene& sc, Thread& t, const SI& si, const BSDF& b, int li, V2 u_light) {
+__device__ inline Spec estimate_direct(const DevScene& sc, uint16_t* stack, int& panic, const SI& si, const BSDF& b,
+                                       int li, V2 u_light) {
     const pbrt_light_desc& L = sc.lights[li];
     const bool is_delta = L.type != PBRT_LIGHT_DIFFUSE_AREA;
     Spec Ld = spec(0);
@@ -555,9 +592,8 @@ __device__ inline Spec estimate_direct(const DevScene& sc, Thread& t, const SI& 
             V3 origin = offset_ray_origin(si.p, si.perr, si.n, ls.tp - si.p);
             V3 target = offset_ray_origin(ls.tp, ls.tperr, ls.tn, origin - ls.tp);
             Ray sr{si.p, target - origin, 1 - 0.0001, si.time};
-            t.shadow_rays++;
             Spec Li = ls.Li;
-            if (bvh_traverse<true>(sc, sr, nullptr, t.stack, t.panic)) Li = spec(0);
+            if (bvh_traverse<true>(sc, sr, nullptr, stack, panic)) Li = spec(0);
             if (!is_black(Li)) {
                 if (is_delta) {
                     Ld = Ld + sdivs(smul(f, Li), ls.pdf);
@@ -601,7 +637,8 @@ __device__ inline Spec uniform_sample_one_light(const DevScene& sc, Thread& t, c
     }
     V2 ul = get2d(t);
     get2d(t);   // uScattering: only the (skipped) MIS half reads it
-    Spec s = estimate_direct(sc, t, si, b, ln, ul);
+    t.shadow_rays++;
+    Spec s = estimate_direct(sc, t.stack, t.panic, si, b, ln, ul);
     if (max_component(s) > 10) t.panic = PBRT_PANIC_LD_GT_10;
     return s;
 }
@@ -671,7 +708,8 @@ __device__ inline Spec direct_li(const DevScene& sc, Thread& t, Ray ray, int max
             for (int j = 0; j < sc.n_lights; j++) {
                 V2 ul = get2d(t);
                 get2d(t);
-                acc = acc + estimate_direct(sc, t, si, b, j, ul);
+                t.shadow_rays++;
+                acc = acc + estimate_direct(sc, t.stack, t.panic, si, b, j, ul);
                 if (t.panic) return L;
             }
             L = L + acc;

@@ -1,0 +1,196 @@
+// pbrt_spec.h — pieces of the wave-parallel EXACT kernel (k_render_spec).
+//
+// The reference renders a tile with ONE sampler clone whose PCG32 stream is
+// consumed path after path (integrator.go:311-340), so path k+1 starts at the
+// RNG offset where path k stopped. Two facts make that chain parallel:
+//
+//  1. Within a pixel, with n_dims >= 3, the camera ray, the first hit, its
+//     BSDF and the bounce-1 light sample are the same for every sample: the
+//     2D stratified values are always (0,0) (sampling.go:122-124, ledger #3)
+//     and ray time never reaches an output. Only the bounce-1 light INDEX
+//     varies (stratified 1D dim 1), so bounce-1 NEE is cached per light.
+//  2. The number of PCG draws D a path consumes depends only on its RNG
+//     offset, never on the sample index k, as long as the stratified 1D
+//     values it reads do not steer control flow (light selection is
+//     Uniform, or Power with every light pdf > 0; a Russian-roulette draw
+//     that lands on a stratified dim marks the lane k-dependent).
+//
+// So a wave evaluates path TRAJECTORIES (no NEE) at 64 candidate offsets
+// (head + 2j) in parallel, follows the exact chain head -> head + D(head) ->
+// ... through the evaluated offsets, and repeats from where the chain left
+// the window. When all of a pixel's offsets are known, the pixel's samples
+// run as full paths (with NEE) one per lane, and their radiance is added to
+// the tile film in sample order. Lane 0 of every window evaluates the exact
+// head, so every window makes progress. Results are bit-identical to the
+// serial replay (k_render_exact) — only the schedule changes.
+#pragma once
+#pragma clang fp contract(off)
+
+#include "pbrt_path.h"
+
+namespace pbrt {
+
+// PCG32 jump-ahead: state after 2^i steps = a[i] * state + inc * b[i] (mod 2^64)
+struct PcgJump {
+    uint64_t a[64];
+    uint64_t b[64];
+};
+__device__ __forceinline__ uint64_t pcg_advance(const PcgJump& J, uint64_t s, uint64_t inc, uint64_t n) {
+    for (int i = 0; n; ++i, n >>= 1)
+        if (n & 1) s = J.a[i] * s + inc * J.b[i];
+    return s;
+}
+__device__ __forceinline__ uint32_t pcg_output(uint64_t old) {   // rng.go:36-42 (#1)
+    uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
+    uint32_t rot = (uint32_t)(old >> 59);
+    return (xs >> rot) | (xs << ((rot + 1u) & 31u));
+}
+
+// Stratified sampler of one path (pixel.go:60-80) positioned at an RNG
+// offset; k < 0 while the sample index is still unknown (speculation).
+struct SpecSampler {
+    const double* s1d;   // ndims x spp shuffled 1D values of the pixel (LDS)
+    int spp, ndims;
+};
+struct Cursor {
+    Pcg rng;
+    uint32_t draws;
+    int cur1d, cur2d;
+    int k;
+    int kdep;   // a stratified value was needed while k < 0
+};
+__device__ __forceinline__ double c_get1d(Cursor& c, const SpecSampler& s) {
+    if (c.cur1d < s.ndims) {
+        const int d = c.cur1d++;
+        if (c.k < 0) {
+            c.kdep = 1;
+            return 0.5;
+        }
+        return s.s1d[d * s.spp + c.k];
+    }
+    c.draws++;
+    return pcg_float(c.rng);
+}
+// a 1D value whose only effect is on radiance (light index): consume it
+__device__ __forceinline__ void c_skip1d(Cursor& c, const SpecSampler& s) {
+    if (c.cur1d < s.ndims) {
+        c.cur1d++;
+        return;
+    }
+    c.draws++;
+    pcg_next(c.rng);
+}
+__device__ __forceinline__ V2 c_get2d(Cursor& c, const SpecSampler& s) {
+    if (c.cur2d < s.ndims) {
+        c.cur2d++;
+        return V2{0.0, 0.0};
+    }
+    c.draws += 2;
+    double x = pcg_float(c.rng);
+    double y = pcg_float(c.rng);
+    return V2{x, y};
+}
+
+constexpr int kMaxCachedLights = 16;
+
+// Per-pixel bounce-1 state shared by all samples of the pixel (LDS).
+struct PixelCache {
+    SI si;
+    BSDF b;
+    V3 wo;                            // camera ray direction (path.go:91, #8)
+    Spec ld[kMaxCachedLights];        // EstimateDirect(light l, uLight = (0,0))
+    int ld_panic[kMaxCachedLights];   // panic kind of that estimate (incl. Ld > 10)
+    int hit;                          // first hit exists and maxDepth > 1
+    int first_panic;                  // panic of the camera-ray traversal
+};
+
+// Path.Li (path.go:32-157) from bounce 1 on, with bounce 1 taken from the
+// pixel cache. kNEE = false: trajectory only (no light sampling; the draws
+// are still consumed), used to learn D for an RNG offset. One body serves
+// both uses (runtime flag) so the kernel carries a single copy of the
+// traversal code.
+__device__ inline Spec spec_path(const DevScene& sc, const PixelCache& pc, const SpecSampler& ss, Cursor& c,
+                                 int max_depth, double rr_threshold, uint16_t* stack, int& panic, int& bounce,
+                                 const bool kNEE) {
+    Spec L = spec(0), beta = spec(1);
+    int32_t bounces = 1;
+    bounce = 1;
+    SI isect = pc.si;
+    BSDF b = pc.b;
+    V3 wo = pc.wo;
+    Ray ray;
+    bool first = true;
+    const int nl = sc.n_lights;
+    for (;;) {
+        if (!first) {
+            bounces++;
+            bounce = bounces;
+            if (bounces >= max_depth) break;
+            if (!bvh_traverse<false>(sc, ray, &isect, stack, panic)) break;
+            if (panic) break;
+            if (compute_bsdf(sc, isect, b) < 0) {
+                panic = -1;
+                break;
+            }
+            wo = ray.d;
+        }
+        if (b.n_bxdfs > 0) {   // UniformSampleOneLight (integrator.go:48-77)
+            if (nl == 0) {
+                if (kNEE) L = L + smul(beta, spec(0));
+            } else if (kNEE) {
+                int ln;
+                if (sc.dist) {
+                    double lpdf;   // > 0 for every light (launch precondition)
+                    ln = sample_discrete(*sc.dist, c_get1d(c, ss), lpdf);
+                } else {
+                    ln = (int)gomath::to_int(gomath::min(c_get1d(c, ss) * (double)nl, (double)(nl - 1)));
+                }
+                V2 ul = c_get2d(c, ss);
+                c_get2d(c, ss);
+                Spec ld;
+                if (first) {
+                    ld = pc.ld[ln];
+                    if (pc.ld_panic[ln]) {
+                        panic = pc.ld_panic[ln];
+                        break;
+                    }
+                } else {
+                    ld = estimate_direct(sc, stack, panic, isect, b, ln, ul);
+                    if (panic) break;
+                    if (max_component(ld) > 10) {
+                        panic = PBRT_PANIC_LD_GT_10;
+                        break;
+                    }
+                }
+                L = L + smul(beta, ld);
+            } else {
+                c_skip1d(c, ss);
+                c_get2d(c, ss);
+                c_get2d(c, ss);
+            }
+        }
+        first = false;
+        V2 u = c_get2d(c, ss);
+        V3 wi;
+        double pdf;
+        Spec f = bsdf_sample_f(b, wo, u, wi, pdf);
+        if (is_black(f) || pdf == 0.0) break;
+        double wp = absdot(wi, isect.sn) / pdf;
+        beta = smul(beta, smuls(f, wp));
+        ray.o = offset_ray_origin(isect.p, isect.perr, isect.n, wi);
+        ray.d = wi;
+        ray.tmax = kInf;
+        ray.time = isect.time;
+        Spec rr = smuls(beta, 1.0);
+        if (max_component(rr) < rr_threshold && bounces > 3) {
+            double q = gomath::max(0.05, 1 - max_component(rr));
+            double u1 = c_get1d(c, ss);
+            if (c.kdep) break;
+            if (u1 < q) break;
+            beta = sdivs(beta, 1 - q);
+        }
+    }
+    return L;
+}
+
+}  // namespace pbrt

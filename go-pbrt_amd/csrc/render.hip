@@ -28,7 +28,7 @@
 
 #include "../../include/pbrt_gpu.h"
 #include "../../include/pbrt_scene.h"
-#include "pbrt_path.h"
+#include "pbrt_spec.h"
 
 using namespace pbrt;
 
@@ -45,7 +45,7 @@ struct RenderParams {
     int32_t integrator, max_depth, dl_strategy;
     double rr_threshold;
     int32_t lanes_per_wave;
-    int32_t pad;
+    int32_t flags;   // pbrt_render_desc.flags
 };
 
 struct PanicRec {
@@ -60,7 +60,11 @@ struct Counters {
     unsigned long long paths, camera_samples, closest_rays, shadow_rays;
     int32_t any_panic;
     int32_t pad;
+    // wave kernel diagnostics (pbrt_gpu_counters): speculation windows, and
+    // lane-0 clock64 cycles in StartPixel / bounce 1 / chain / full paths / film add
+    unsigned long long windows, phase[5];
 };
+constexpr int kNumCounters = 6 + 5;
 
 __device__ __forceinline__ void tile_bounds(const RenderParams& rp, int64_t tile, int64_t& x0, int64_t& y0,
                                             int64_t& x1, int64_t& y1) {
@@ -126,7 +130,8 @@ __device__ inline int footprint(const pbrt_film_desc& f, double pfx, double pfy,
 // ----------------------------------------------------------- EXACT kernel
 // One lane per tile; `lanes_per_wave` lanes of each 64-lane workgroup work
 // (fewer busy lanes per wave = less divergence, more waves per SIMD).
-__global__ __launch_bounds__(kWave) void k_render_exact(DevScene sc, RenderParams rp, double* __restrict__ films,
+template <int kMinWaves>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kMinWaves, 8))) void k_render_exact(DevScene sc, RenderParams rp, double* __restrict__ films,
                                                         double* __restrict__ s1d_scratch, PanicRec* __restrict__ panics,
                                                         Counters* __restrict__ ctr) {
     __shared__ uint16_t stack_lds[64 * kStackStride];
@@ -232,6 +237,317 @@ __global__ __launch_bounds__(kWave) void k_render_exact(DevScene sc, RenderParam
     atomicAdd(&ctr->shadow_rays, (unsigned long long)t.shadow_rays);
 }
 
+// ------------------------------------------------------ EXACT, wave-parallel
+// One 64-lane wave per tile; see pbrt_spec.h for why this is the same
+// computation as k_render_exact. Per pixel:
+//   1. StartPixel: the ~ndims*2*spp draws are computed lane-parallel by PCG
+//      jump-ahead (assuming pcg_bounded never rejects, checked; on a
+//      rejection lane 0 replays StartPixel serially), then one lane per dim
+//      runs the Fisher-Yates swaps.
+//   2. Bounce 1: camera ray, first hit and BSDF (wave-uniform); lane l
+//      computes EstimateDirect for light l with uLight = (0,0).
+//   3. Chain: trajectories at offsets head + 2j (j = lane) give D per offset;
+//      lane 0 walks head -> head + D -> ... to assign each sample its offset.
+//   4. Samples 1..spp-1 run as full paths, one per lane (batches of 64), and
+//      are added to the tile film (LDS) in sample order.
+struct SpecLayout {   // byte offsets into the dynamic LDS block
+    int film, s1d, other, memb, lbuf, sbuf, dbuf, pbuf, total;
+};
+constexpr uint32_t kBadD = 0xFFFFFFFFu;
+
+__device__ __forceinline__ double pcg_float_of(uint32_t v) {
+    return gomath::min(gomath::kOneMinusEpsilon, (double)v * 2.3283064365386963e-10);
+}
+
+// Bounce 1 of a pixel (camera ray, first hit, BSDF; EstimateDirect per light
+// with uLight = (0,0), lane l computing light l) into the LDS cache. Returns
+// 1 = hit, 0 = no traced bounce, or kind - 1000 (< 0) when the first hit
+// panics (kind = PBRT_PANIC_* or -1 for an unsupported material). Out of line:
+// it runs once per pixel.
+__device__ __noinline__ int pixel_setup(DevScene sc, const RenderParams& rp, const pbrt_camera_desc& cam, int64_t px,
+                                        int64_t py, double time_u, PixelCache* pc, uint16_t* stack, int lane) {
+    Ray ray = camera_ray(cam, (double)px + 0.0, (double)py + 0.0, time_u, V2{0.0, 0.0});
+    int panic0 = 0;
+    SI si0;
+    BSDF b0;
+    b0.n_bxdfs = 0;
+    int hit0 = 0;
+    if (1 < rp.max_depth) {
+        hit0 = bvh_traverse<false>(sc, ray, &si0, stack, panic0) ? 1 : 0;
+        if (!panic0 && hit0 && compute_bsdf(sc, si0, b0) < 0) panic0 = -1;
+    }
+    if (panic0) return panic0 - 1000;
+    if (lane == 0) {
+        pc->si = si0;
+        pc->b = b0;
+        pc->wo = ray.d;
+        pc->hit = hit0;
+    }
+    if (hit0 && b0.n_bxdfs > 0 && lane < sc.n_lights) {
+        int pl = 0;
+        Spec ld = estimate_direct(sc, stack, pl, si0, b0, lane, V2{0.0, 0.0});
+        if (!pl && max_component(ld) > 10) pl = PBRT_PANIC_LD_GT_10;
+        pc->ld[lane] = ld;
+        pc->ld_panic[lane] = pl;
+    }
+    return hit0;
+}
+
+template <int kWaves>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8))) void k_render_spec(DevScene sc, RenderParams rp, SpecLayout lay,
+                                                       const PcgJump* __restrict__ jump,
+                                                       double* __restrict__ films, PanicRec* __restrict__ panics,
+                                                       Counters* __restrict__ ctr) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ uint16_t stack_lds[64 * kStackStride];
+    __shared__ PixelCache pc;
+    __shared__ uint64_t sh_state;
+    __shared__ int sh_k, sh_flag, sh_trunc, sh_stop, sh_tkind, sh_tbounce;
+    const int lane = threadIdx.x;
+    const int64_t slot = blockIdx.x;
+    const int64_t tile = rp.tile_begin + slot * rp.tile_stride;
+    const pbrt_film_desc& film = *sc.film;
+    const PcgJump& J = *jump;
+    double* film_l = (double*)(lds + lay.film);
+    double* s1d = (double*)(lds + lay.s1d);
+    uint16_t* other = (uint16_t*)(lds + lay.other);
+    uint64_t* memb = (uint64_t*)(lds + lay.memb);
+    double* lbuf = (double*)(lds + lay.lbuf);
+    uint64_t* sbuf = (uint64_t*)(lds + lay.sbuf);
+    uint32_t* dbuf = (uint32_t*)(lds + lay.dbuf);
+    int* pbuf = (int*)(lds + lay.pbuf);
+    uint16_t* stack = stack_lds + lane;
+
+    int64_t x0, y0, x1, y1, px0, py0, px1, py1;
+    tile_bounds(rp, tile, x0, y0, x1, y1);
+    film_tile_bounds(film, x0, y0, x1, y1, px0, py0, px1, py1);
+    const int64_t npx = (px1 - px0) * (py1 - py0);
+    for (int64_t i = lane; i < npx * 3; i += kWave) film_l[i] = 0.0;
+
+    const int n = rp.spp, ndims = rp.ndims, nl = sc.n_lights;
+    const double inv_n = 1.0 / (double)n;
+    const int s1 = rp.jitter ? 2 * n : n, s2 = rp.jitter ? 3 * n : n;
+    const int64_t T = (int64_t)ndims * (s1 + s2);   // StartPixel draws without rejections
+    Pcg seed;
+    pcg_seed(seed, (uint64_t)tile);   // Sampler.Clone(seed = tile index), integrator.go:318,328
+    const uint64_t inc = seed.inc;
+    uint64_t S = seed.state;
+    const SpecSampler ss{s1d, n, ndims};
+    const pbrt_camera_desc& cam = *sc.camera;
+    unsigned long long paths = 0, windows = 0;
+    unsigned long long ph[5] = {0, 0, 0, 0, 0};
+    long long tprev = clock64();
+    auto mark = [&](int i) {
+        long long now = clock64();
+        ph[i] += (unsigned long long)(now - tprev);
+        tprev = now;
+    };
+    __syncthreads();
+
+    for (int64_t py = y0; py < y1; py++) {
+        for (int64_t px = x0; px < x1; px++) {
+            // ---- 1. StartPixel (stratified.go:21-48)
+            if (lane == 0) sh_flag = 0;
+            __syncthreads();
+            int rej = 0;
+            for (int64_t idx = lane; idx < T; idx += kWave) {
+                const uint32_t v = pcg_output(pcg_advance(J, S, inc, (uint64_t)idx));
+                int d, r, i;
+                if (idx < (int64_t)ndims * s1) {
+                    d = (int)(idx / s1);
+                    r = (int)(idx % s1);
+                    if (rp.jitter && r < n) {
+                        s1d[d * n + r] = gomath::min(((double)r + pcg_float_of(v)) * inv_n, gomath::kOneMinusEpsilon);
+                        continue;
+                    }
+                    i = r - (rp.jitter ? n : 0);
+                    other[d * n + i] = (uint16_t)(i + (int)(v % (uint32_t)(n - i)));
+                } else {
+                    const int64_t q = idx - (int64_t)ndims * s1;
+                    r = (int)(q % s2);
+                    if (rp.jitter && r < 2 * n) continue;
+                    i = r - (rp.jitter ? 2 * n : 0);
+                }
+                const uint32_t b = (uint32_t)(n - i);
+                if (v < (~b + 1u) % b) rej = 1;
+            }
+            if (!rp.jitter)
+                for (int idx = lane; idx < ndims * n; idx += kWave)
+                    s1d[idx] = gomath::min(((double)(idx % n) + 0.5) * inv_n, gomath::kOneMinusEpsilon);
+            if (rej) atomicOr(&sh_flag, 1);
+            __syncthreads();
+            if (sh_flag || (rp.flags & PBRT_FLAG_SERIAL_START_PIXEL)) {
+                if (lane == 0) {   // a pcg_bounded rejection: serial replay
+                    Thread t;
+                    t.rng.state = S;
+                    t.rng.inc = inc;
+                    t.spp = n; t.ndims = ndims; t.xs = rp.xs; t.ys = rp.ys; t.jitter = rp.jitter;
+                    t.s1d = s1d;
+                    start_pixel(t);
+                    sh_state = t.rng.state;
+                }
+            } else {
+                if (lane < ndims) {
+                    double* samp = s1d + lane * n;
+                    const uint16_t* oth = other + lane * n;
+                    for (int i = 0; i < n; i++) {
+                        const int o = oth[i];
+                        double a = samp[i];
+                        samp[i] = samp[o];
+                        samp[o] = a;
+                    }
+                }
+                if (lane == 0) sh_state = pcg_advance(J, S, inc, (uint64_t)T);
+            }
+            __syncthreads();
+            S = sh_state;
+            mark(0);
+            if (n <= 1) continue;   // sample 0 is never traced (#2)
+
+            // ---- 2. bounce 1, shared by every sample of the pixel
+            const int hit0 = pixel_setup(sc, rp, cam, px, py, s1d[1 < n ? 1 : 0], &pc, stack, lane);
+            if (hit0 < 0) {   // the first traced sample panics at bounce 1
+                if (lane == 0) {
+                    PanicRec pr{hit0 + 1000, 1, 1, 0, px, py};
+                    panics[slot] = pr;
+                    atomicExch(&ctr->any_panic, 1);
+                }
+                return;
+            }
+            if (lane == 0) {
+                sh_trunc = 0;
+                sh_stop = 0;
+            }
+            __syncthreads();
+            mark(1);
+            // ---- 3. offsets of samples 1..n-1 (chain through speculative trajectories)
+            int kend = n;
+            if (hit0) {
+                uint64_t Sh = S;
+                int kh = 1;
+                while (kh < n) {
+                    const uint64_t st = pcg_advance(J, Sh, inc, 2 * (uint64_t)lane);
+                    Cursor c;
+                    c.rng.state = st;
+                    c.rng.inc = inc;
+                    c.draws = 0;
+                    c.cur1d = 1;   // camera: Get2D pFilm, Get2D pLens, Get1D time (stratified)
+                    c.cur2d = 2;
+                    c.k = lane == 0 ? kh : -1;
+                    c.kdep = 0;
+                    int pnc = 0, bnc = 0;
+                    (void)spec_path(sc, pc, ss, c, rp.max_depth, rp.rr_threshold, stack, pnc, bnc, false);
+                    windows++;
+                    sbuf[lane] = st;
+                    dbuf[lane] = (pnc || c.kdep) ? kBadD : c.draws;
+                    __syncthreads();
+                    if (lane == 0) {
+                        uint64_t x = 0;
+                        int k = kh;
+                        while (k < n) {
+                            if ((x & 1) || (x >> 1) >= (uint64_t)kWave) break;
+                            const uint32_t d = dbuf[x >> 1];
+                            if (d == kBadD) break;
+                            memb[k++] = sbuf[x >> 1];
+                            x += d;
+                        }
+                        if (k == kh) {   // the exact head itself panicked
+                            memb[kh] = Sh;
+                            sh_trunc = kh;
+                            sh_tkind = pnc;
+                            sh_tbounce = bnc;
+                        }
+                        sh_k = k;
+                        sh_state = pcg_advance(J, Sh, inc, x);
+                    }
+                    __syncthreads();
+                    kh = sh_k;
+                    Sh = sh_state;
+                    if (sh_trunc) break;
+                }
+                S = Sh;
+                if (sh_trunc) kend = sh_trunc + 1;
+            }
+
+            mark(2);
+            // ---- 4. full paths, one sample per lane, added in sample order
+            const double fx = (double)px + 0.0, fy = (double)py + 0.0;
+            Footprint fp;
+            int64_t p0x, p0y, p1x, p1y;
+            footprint(film, fx, fy, px0, py0, px1, py1, fp, p0x, p0y, p1x, p1y);
+            for (int kb = 1; kb < kend; kb += kWave) {
+                const int k = kb + lane;
+                Spec L = spec(0);
+                int pnc = 0, bnc = 0;
+                if (k < kend && hit0) {
+                    Cursor c;
+                    c.rng.state = memb[k];
+                    c.rng.inc = inc;
+                    c.draws = 0;
+                    c.cur1d = 1;
+                    c.cur2d = 2;
+                    c.k = k;
+                    c.kdep = 0;
+                    L = spec_path(sc, pc, ss, c, rp.max_depth, rp.rr_threshold, stack, pnc, bnc, true);
+                }
+                lbuf[lane * 3 + 0] = L.r;
+                lbuf[lane * 3 + 1] = L.g;
+                lbuf[lane * 3 + 2] = L.b;
+                pbuf[lane * 2 + 0] = (k < kend) ? pnc : 0;
+                pbuf[lane * 2 + 1] = bnc;
+                __syncthreads();
+                if (lane == 0) {
+                    for (int m = 0; m < kWave && kb + m < kend; m++) {
+                        if (pbuf[m * 2]) {
+                            PanicRec pr{pbuf[m * 2], kb + m, pbuf[m * 2 + 1], 0, px, py};
+                            panics[slot] = pr;
+                            atomicExch(&ctr->any_panic, 1);
+                            sh_stop = 1;
+                            break;
+                        }
+                    }
+                }
+                __syncthreads();
+                if (sh_stop) return;
+                mark(3);
+                const int kn = (kend - kb < kWave) ? kend - kb : kWave;
+                if (lane < fp.n * 3) {
+                    const int f = lane / 3, ch = lane - f * 3;
+                    const double w = fp.w[f];
+                    double acc = film_l[fp.off[f] * 3 + ch];
+                    for (int m = 0; m < kn; m++) {
+                        Spec Ls{lbuf[m * 3 + 0], lbuf[m * 3 + 1], lbuf[m * 3 + 2]};
+                        if (has_nans(Ls)) Ls = spec(0.1);   // integrator.go:256-262
+                        if (0.0 > film.max_sample_luminance) Ls = smuls(Ls, film.max_sample_luminance / 0.0);
+                        const double v = ch == 0 ? Ls.r : (ch == 1 ? Ls.g : Ls.b);
+                        acc += v * w;
+                    }
+                    film_l[fp.off[f] * 3 + ch] = acc;
+                }
+                __syncthreads();
+                mark(4);
+            }
+            if (sh_trunc) {   // head panicked in the trajectory but no full path did: report it
+                if (lane == 0) {
+                    PanicRec pr{sh_tkind, sh_trunc, sh_tbounce, 0, px, py};
+                    panics[slot] = pr;
+                    atomicExch(&ctr->any_panic, 1);
+                }
+                return;
+            }
+            paths += (unsigned long long)(n - 1);
+        }
+    }
+    double* tf = films + slot * (rp.slot_w * rp.slot_h * 3);
+    for (int64_t i = lane; i < npx * 3; i += kWave) tf[i] = film_l[i];
+    if (lane == 0) {
+        atomicAdd(&ctr->paths, paths);
+        atomicAdd(&ctr->camera_samples, paths);
+        atomicAdd(&ctr->windows, windows);
+        for (int i = 0; i < 5; i++) atomicAdd(&ctr->phase[i], ph[i]);
+    }
+}
+
 // ---------------------------------------------------------- merge kernel
 // Film.MergeFilmTile (film.go:115-132) in tile-index order. A film pixel is
 // covered by at most the 3x3 tiles around its own (filter radius < tile size).
@@ -306,6 +622,13 @@ struct pbrt_gpu_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     double* film_target = nullptr;   // caller buffer of the last render_async_into
     int lanes_per_wave = 64;
+    int min_waves = 1;      // amdgpu_waves_per_eu variant of k_render_exact
+    int kernel_req = PBRT_KERNEL_AUTO;
+    int last_kernel = 0;    // PBRT_KERNEL_SERIAL / PBRT_KERNEL_WAVE
+    PcgJump* d_jump = nullptr;
+    pbrt_distribution_desc host_dist;
+    SpecLayout lay{};
+    bool use_spec = false;
     // device scene
     pbrt_shape_desc* d_shapes = nullptr;
     pbrt_material_desc* d_materials = nullptr;
@@ -412,6 +735,54 @@ int validate_scene(const pbrt_scene_desc* s) {
     return PBRT_OK;
 }
 
+const PcgJump& pcg_jump_table() {
+    static PcgJump J = [] {
+        PcgJump t;
+        uint64_t a = 0x5851f42d4c957f2dULL, b = 1;   // one step: s' = a*s + inc*1
+        for (int i = 0; i < 64; i++) {
+            t.a[i] = a;
+            t.b[i] = b;
+            b = b * (a + 1);   // two applications of the 2^i jump
+            a = a * a;
+        }
+        return t;
+    }();
+    return J;
+}
+
+// Can k_render_spec replay this render exactly? (see pbrt_spec.h for the conditions)
+bool spec_layout(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const RenderParams& rp, SpecLayout& L) {
+    if (rd->integrator != PBRT_INTEGRATOR_PATH || rd->n_dims < 3) return false;
+    const int nl = c->host_scene.n_lights;
+    if (nl > kMaxCachedLights) return false;
+    if (nl > 0) {
+        const pbrt_distribution_desc& d = c->host_dist;
+        if (!(d.func_int > 0)) return false;
+        for (int i = 0; i < d.count; i++)
+            if (!(d.func[i] > 0)) return false;   // a zero-pdf light changes the draw count
+    }
+    const pbrt_film_desc& f = c->host_scene.film;
+    if (!(f.filter_radius_x < 1.5 && f.filter_radius_y < 1.5)) return false;   // <= 2x2 pixel footprint
+    const int64_t n = rp.spp, nd = rp.ndims;
+    if (n > 4096 || nd * n > 8192) return false;
+    int64_t off = 0;
+    auto put = [&](int64_t bytes) {
+        int64_t o = off;
+        off += (bytes + 15) & ~int64_t(15);
+        return (int)o;
+    };
+    L.film = put(rp.slot_w * rp.slot_h * 3 * 8);
+    L.s1d = put(nd * n * 8);
+    L.other = put(nd * n * 2);
+    L.memb = put(n * 8);
+    L.lbuf = put(kWave * 3 * 8);
+    L.sbuf = put(kWave * 8);
+    L.dbuf = put(kWave * 4);
+    L.pbuf = put(kWave * 2 * 4);
+    L.total = (int)off;
+    return off <= 48 * 1024;
+}
+
 int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
     if (!rd) return set_err(c, PBRT_E_INVALID, "null render desc");
     if (rd->tile_size <= 0 || rd->sampler_x <= 0 || rd->sampler_y <= 0 || rd->n_dims < 0 || rd->n_dims > 64)
@@ -455,12 +826,17 @@ int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
     rp.dl_strategy = rd->dl_strategy;
     rp.rr_threshold = rd->rr_threshold;
     rp.lanes_per_wave = c->lanes_per_wave;
+    rp.flags = rd->flags;
+    pbrt_distribution_desc& dist = c->host_dist;
+    std::memset(&dist, 0, sizeof(dist));
     if (rd->integrator == PBRT_INTEGRATOR_PATH) {
-        pbrt_distribution_desc dist;
         int rc = pbrt_scene_light_distribution(&c->host_scene, rd->light_strategy, &dist);
         if (rc != PBRT_OK) return set_err(c, rc, "unsupported light sample strategy");
         HIPCHK(c, hipMemcpyAsync(c->d_dist, &dist, sizeof(dist), hipMemcpyHostToDevice, c->stream));
     }
+    c->use_spec = c->kernel_req != PBRT_KERNEL_SERIAL && spec_layout(c, rd, rp, c->lay);
+    if (c->kernel_req == PBRT_KERNEL_WAVE && !c->use_spec)
+        return set_err(c, PBRT_E_UNSUPPORTED, "render not eligible for the wave-parallel kernel");
     size_t nslot = (size_t)(rp.n_slots > 0 ? rp.n_slots : 1);
     int rc;
     if ((rc = ensure(c, &c->d_films, &c->films_cap, nslot * (size_t)(rp.slot_w * rp.slot_h * 3)))) return rc;
@@ -483,6 +859,12 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
     auto* c = new pbrt_gpu_ctx();
     c->device = (opts && opts->device >= 0) ? opts->device : -1;
     if (opts && opts->lanes_per_wave > 0 && opts->lanes_per_wave <= 64) c->lanes_per_wave = opts->lanes_per_wave;
+    if (opts && (opts->occupancy == 2 || opts->occupancy == 4 || opts->occupancy == 8)) c->min_waves = opts->occupancy;
+    if (opts && (opts->kernel < PBRT_KERNEL_AUTO || opts->kernel > PBRT_KERNEL_WAVE)) {
+        delete c;
+        return PBRT_E_INVALID;
+    }
+    if (opts) c->kernel_req = opts->kernel;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
         delete c;
@@ -513,7 +895,8 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
         (rc = upload(c, &c->d_lights, scene->lights, scene->n_lights)) ||
         (rc = upload(c, &c->d_camera, &scene->camera, 1)) || (rc = upload(c, &c->d_film, &scene->film, 1)) ||
         (rc = upload<pbrt_distribution_desc>(c, &c->d_dist, nullptr, 1)) ||
-        (rc = upload<Counters>(c, &c->d_ctr, nullptr, 1))) {
+        (rc = upload<Counters>(c, &c->d_ctr, nullptr, 1)) ||
+        (rc = upload<PcgJump>(c, &c->d_jump, &pcg_jump_table(), 1))) {
         pbrt_gpu_destroy(c);
         return rc;
     }
@@ -536,9 +919,21 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     if (rp.n_slots > 0) {
         DevScene sc = dev_scene(c, rd->integrator == PBRT_INTEGRATOR_PATH);
-        int64_t blocks = (rp.n_slots + rp.lanes_per_wave - 1) / rp.lanes_per_wave;
-        hipLaunchKernelGGL(k_render_exact, dim3((unsigned)blocks), dim3(kWave), 0, c->stream, sc, rp, c->d_films,
-                           c->d_s1d, c->d_panics, c->d_ctr);
+        if (c->use_spec) {
+            c->last_kernel = PBRT_KERNEL_WAVE;
+            auto kern = c->min_waves >= 2 ? k_render_spec<2> : k_render_spec<1>;
+            hipLaunchKernelGGL(kern, dim3((unsigned)rp.n_slots), dim3(kWave), (unsigned)c->lay.total,
+                               c->stream, sc, rp, c->lay, c->d_jump, c->d_films, c->d_panics, c->d_ctr);
+        } else {
+            c->last_kernel = PBRT_KERNEL_SERIAL;
+            int64_t blocks = (rp.n_slots + rp.lanes_per_wave - 1) / rp.lanes_per_wave;
+            auto kern = k_render_exact<1>;
+            if (c->min_waves == 2) kern = k_render_exact<2>;
+            else if (c->min_waves == 4) kern = k_render_exact<4>;
+            else if (c->min_waves == 8) kern = k_render_exact<8>;
+            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kWave), 0, c->stream, sc, rp, c->d_films,
+                               c->d_s1d, c->d_panics, c->d_ctr);
+        }
         HIPCHK(c, hipGetLastError());
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
@@ -572,6 +967,7 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
     st.paths_traced = ctr.paths;
     st.kernel_ms = ms;
     st.merge_ms = ms_merge;
+    st.kernel = c->last_kernel;
     if (ctr.any_panic) {
         std::vector<PanicRec> pr((size_t)c->rp.n_slots);
         HIPCHK(c, hipMemcpy(pr.data(), c->d_panics, sizeof(PanicRec) * pr.size(), hipMemcpyDeviceToHost));
@@ -691,7 +1087,7 @@ void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_shapes, c->d_materials, c->d_prims, c->d_nodes, c->d_lights, c->d_camera, c->d_film,
-                    c->d_dist,   c->d_films,     c->d_s1d,   c->d_panics, c->d_ctr,   c->d_out};
+                    c->d_dist,   c->d_films,     c->d_s1d,   c->d_panics, c->d_ctr,   c->d_out,    c->d_jump};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -771,6 +1167,8 @@ __global__ void k_probe(int op, const double* __restrict__ in, int64_t n, int in
             for (int k = 0; k < out_stride; k++) o[k] = pcg_float(r);
             break;
         }
+        case PBRT_PROBE_NEXT_FLOAT_UP: o[0] = gomath::next_up(a[0]); break;
+        case PBRT_PROBE_NEXT_FLOAT_DOWN: o[0] = gomath::next_down(a[0]); break;
         default: o[0] = gomath::nan();
     }
 }
@@ -797,6 +1195,18 @@ extern "C" int pbrt_gpu_probe(int device, int op, const double* in, size_t n, in
     (void)hipFree(d_in);
     (void)hipFree(d_out);
     return e == hipSuccess ? PBRT_OK : PBRT_E_HIP;
+}
+
+extern "C" int pbrt_gpu_counters(pbrt_gpu_ctx* c, uint64_t* out, int n) {
+    if (!c || !out) return PBRT_E_INVALID;
+    if (hipSetDevice(c->device) != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) return PBRT_E_HIP;
+    Counters ctr;
+    if (hipMemcpy(&ctr, c->d_ctr, sizeof(ctr), hipMemcpyDeviceToHost) != hipSuccess) return PBRT_E_HIP;
+    const uint64_t v[kNumCounters] = {ctr.paths, ctr.camera_samples, ctr.closest_rays, ctr.shadow_rays,
+                                      (uint64_t)ctr.any_panic, ctr.windows, ctr.phase[0], ctr.phase[1],
+                                      ctr.phase[2], ctr.phase[3], ctr.phase[4]};
+    for (int i = 0; i < n && i < kNumCounters; i++) out[i] = v[i];
+    return kNumCounters;
 }
 
 extern "C" int pbrt_abi_sizes(size_t* out, int n) {

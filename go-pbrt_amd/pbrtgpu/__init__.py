@@ -274,11 +274,14 @@ class Scene:
 class Renderer:
     """pbrt_gpu_ctx: the scene resident on one GPU."""
 
-    def __init__(self, scene, device=-1, lanes_per_wave=0):
+    KERNELS = {"auto": abi.PBRT_KERNEL_AUTO, "serial": abi.PBRT_KERNEL_SERIAL, "wave": abi.PBRT_KERNEL_WAVE}
+
+    def __init__(self, scene, device=-1, lanes_per_wave=0, occupancy=0, kernel="auto"):
         desc = scene.desc if isinstance(scene, Scene) else scene
         self._scene = scene  # keep the descriptor alive
         opts = abi.GpuOpts()
         opts.device, opts.lanes_per_wave = device, lanes_per_wave
+        opts.occupancy, opts.kernel = occupancy, self.KERNELS[kernel]
         h = C.c_void_p()
         rc = lib().pbrt_gpu_create(C.byref(desc), C.byref(opts), C.byref(h))
         if rc:

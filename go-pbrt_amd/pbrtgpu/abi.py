@@ -31,6 +31,10 @@ PBRT_DL_UNIFORM_SAMPLE_ALL = 1
 PBRT_DL_UNIFORM_SAMPLE_ONE = 2
 PBRT_MODE_EXACT = 0
 PBRT_MODE_THROUGHPUT = 1
+PBRT_KERNEL_AUTO = 0
+PBRT_KERNEL_SERIAL = 1
+PBRT_KERNEL_WAVE = 2
+PBRT_FLAG_SERIAL_START_PIXEL = 1
 
 PBRT_PANIC_NONE = 0
 PBRT_PANIC_LD_GT_10 = 1
@@ -205,6 +209,8 @@ class GpuStats(C.Structure):
         ("panic_pixel_y", C.c_int64),
         ("panic_sample", C.c_int32),
         ("panic_bounce", C.c_int32),
+        ("kernel", C.c_int32),
+        ("pad0", C.c_int32),
     ]
 
 
@@ -227,13 +233,14 @@ class HitSoA(C.Structure):
 
 
 class GpuOpts(C.Structure):
-    _fields_ = [("device", C.c_int32), ("lanes_per_wave", C.c_int32), ("reserved", C.c_int32 * 6)]
+    _fields_ = [("device", C.c_int32), ("lanes_per_wave", C.c_int32), ("occupancy", C.c_int32),
+                ("kernel", C.c_int32), ("reserved", C.c_int32 * 4)]
 
 
 def render_desc(spp_x=8, spp_y=8, jitter=False, n_dims=4, integrator=PBRT_INTEGRATOR_PATH,
                 max_depth=10, rr_threshold=1.0, light_strategy=PBRT_LIGHT_STRATEGY_UNIFORM,
                 dl_strategy=PBRT_DL_UNIFORM_SAMPLE_ALL, tile_size=16, tile_begin=0, tile_end=0,
-                tile_stride=1, mode=PBRT_MODE_EXACT):
+                tile_stride=1, mode=PBRT_MODE_EXACT, flags=0):
     """RenderDesc with the defaults of internal/render/server.go:142,162,164."""
     rd = RenderDesc()
     rd.sampler_x, rd.sampler_y, rd.jitter, rd.n_dims = spp_x, spp_y, int(bool(jitter)), n_dims
@@ -241,5 +248,5 @@ def render_desc(spp_x=8, spp_y=8, jitter=False, n_dims=4, integrator=PBRT_INTEGR
     rd.light_strategy, rd.dl_strategy = light_strategy, dl_strategy
     rd.rr_threshold = rr_threshold
     rd.tile_size, rd.tile_begin, rd.tile_end, rd.tile_stride = tile_size, tile_begin, tile_end, tile_stride
-    rd.mode, rd.flags = mode, 0
+    rd.mode, rd.flags = mode, flags
     return rd

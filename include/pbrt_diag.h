@@ -33,11 +33,21 @@ enum {
     PBRT_PROBE_EFLOAT_ADD = 14,        /* in v1 e1 v2 e2 -> value low high panic */
     PBRT_PROBE_TRANSFORM_RAY = 15,     /* in m[16] o[3] d[3] -> o'[3] d'[3]      */
     PBRT_PROBE_SPAWN_RAY_TO = 16,      /* in p0 perr0 n0 p1 perr1 n1 -> o d tmax */
-    PBRT_PROBE_PCG = 17                /* in seed -> out[out_stride] first floats */
+    PBRT_PROBE_PCG = 17,               /* in seed -> out[out_stride] first floats */
+    PBRT_PROBE_NEXT_FLOAT_UP = 18,     /* in v -> NextFloatUp(v)   (math.go:122-124) */
+    PBRT_PROBE_NEXT_FLOAT_DOWN = 19    /* in v -> NextFloatDown(v) (math.go:126-128) */
 };
 
 /* Inputs: n records of in_stride doubles; outputs: n records of out_stride. */
 int pbrt_gpu_probe(int device, int op, const double* in, size_t n, int in_stride, double* out, int out_stride);
+
+/* Device counters of the last render (after it completed), in this order:
+ * paths, camera_samples, closest_rays, shadow_rays, any_panic, windows
+ * (WAVE kernel speculation rounds), then lane-0 clock64 cycles summed over
+ * tiles in: StartPixel, bounce 1, offset chain, full paths, film add.
+ * Returns the number of counters available. */
+struct pbrt_gpu_ctx;
+int pbrt_gpu_counters(struct pbrt_gpu_ctx* ctx, uint64_t* out, int n);
 
 /* sizeof() of every ABI struct, for binding checks (index order as in pbrt_gpu.h). */
 int pbrt_abi_sizes(size_t* out, int n);

@@ -199,7 +199,7 @@ typedef struct pbrt_render_desc {
      * tile_stride, ... < tile_end (tile_end <= 0 means all tiles). */
     int64_t tile_begin, tile_end, tile_stride;
     int32_t mode;            /* PBRT_MODE_*                                     */
-    int32_t flags;           /* reserved, 0                                     */
+    int32_t flags;           /* PBRT_FLAG_* (diagnostics), normally 0           */
 } pbrt_render_desc;
 
 typedef struct pbrt_gpu_stats {
@@ -213,6 +213,8 @@ typedef struct pbrt_gpu_stats {
     int32_t panic_tile;
     int64_t panic_pixel_x, panic_pixel_y;
     int32_t panic_sample, panic_bounce;
+    int32_t kernel;          /* PBRT_KERNEL_SERIAL or PBRT_KERNEL_WAVE (last render) */
+    int32_t pad0;
 } pbrt_gpu_stats;
 
 /* ----------------------------------------------------------- ray batches */
@@ -232,9 +234,23 @@ typedef struct pbrt_hit_soa {
 /* ------------------------------------------------------------------ opts */
 typedef struct pbrt_gpu_opts {
     int32_t device;              /* HIP device ordinal (-1 => current)       */
-    int32_t lanes_per_wave;      /* EXACT mode: tiles per 64-lane wave (0=auto) */
-    int32_t reserved[6];
+    int32_t lanes_per_wave;      /* serial kernel: tiles per 64-lane wave (0=auto) */
+    int32_t occupancy;           /* serial kernel: waves/SIMD build variant (0,1,2,4,8) */
+    int32_t kernel;              /* PBRT_KERNEL_*                               */
+    int32_t reserved[4];
 } pbrt_gpu_opts;
+
+/* EXACT-mode kernels. Both replay the reference bit for bit:
+ *  SERIAL  one lane per tile, the tile's PCG32 stream consumed in order;
+ *  WAVE    one 64-lane wave per tile: per-pixel shared bounce 1, path
+ *          offsets found by speculative trajectories + jump-ahead, the
+ *          pixel's samples traced in parallel (Path integrator, n_dims >= 3,
+ *          every light pdf > 0, filter radius < 1.5; else SERIAL is used). */
+/* WAVE kernel: always replay StartPixel serially (the path normally taken
+ * only after a pcg_bounded rejection); results are identical. */
+#define PBRT_FLAG_SERIAL_START_PIXEL 1
+
+enum { PBRT_KERNEL_AUTO = 0, PBRT_KERNEL_SERIAL = 1, PBRT_KERNEL_WAVE = 2 };
 
 typedef struct pbrt_gpu_ctx pbrt_gpu_ctx;
 

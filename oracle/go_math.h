@@ -38,6 +38,11 @@ extern __thread uint64_t orc_flops;
 static inline uint64_t gm_bits(double x) { uint64_t u; memcpy(&u, &x, 8); return u; }
 static inline double gm_from_bits(uint64_t u) { double x; memcpy(&x, &u, 8); return x; }
 static inline int gm_isnan(double x) { return x != x; }
+/* math.NaN() = Float64frombits(0x7FF8000000000001) (src/math/bits.go) */
+static inline double go_nan(void) {
+    union { uint64_t u; double d; } v = {0x7FF8000000000001ULL};
+    return v.d;
+}
 static inline int gm_isinf(double x, int sign) {
     if (sign > 0) return x == INFINITY;
     if (sign < 0) return x == -INFINITY;
@@ -52,20 +57,20 @@ static inline double gm_abs(double x) { return gm_from_bits(gm_bits(x) & ~(1ULL 
 /* math.Max / math.Min (src/math/dim.go; amd64 asm has the same special cases) */
 static inline double go_max(double x, double y) {
     if (gm_isinf(x, 1) || gm_isinf(y, 1)) return INFINITY;
-    if (gm_isnan(x) || gm_isnan(y)) return NAN;
+    if (gm_isnan(x) || gm_isnan(y)) return go_nan();
     if (x == 0 && x == y) return gm_signbit(x) ? y : x;
     return x > y ? x : y;
 }
 static inline double go_min(double x, double y) {
     if (gm_isinf(x, -1) || gm_isinf(y, -1)) return -INFINITY;
-    if (gm_isnan(x) || gm_isnan(y)) return NAN;
+    if (gm_isnan(x) || gm_isnan(y)) return go_nan();
     if (x == 0 && x == y) return gm_signbit(x) ? x : y;
     return x < y ? x : y;
 }
 
 /* math.Nextafter (src/math/nextafter.go) */
 static inline double go_nextafter(double x, double y) {
-    if (gm_isnan(x) || gm_isnan(y)) return NAN;
+    if (gm_isnan(x) || gm_isnan(y)) return go_nan();
     if (x == y) return x;
     if (x == 0) return gm_copysign(gm_from_bits(1), y);
     if ((y > x) == (x > 0)) return gm_from_bits(gm_bits(x) + 1);
@@ -137,7 +142,7 @@ static inline double gm_cos_poly(double zz) {
 
 /* src/math/sin.go cos() */
 static inline double go_cos(double x) {
-    if (gm_isnan(x) || gm_isinf(x, 0)) return NAN;
+    if (gm_isnan(x) || gm_isinf(x, 0)) return go_nan();
     int sign = 0;
     x = gm_abs(x);
     uint64_t j; double z;
@@ -153,7 +158,7 @@ static inline double go_cos(double x) {
 /* src/math/sin.go sin() */
 static inline double go_sin(double x) {
     if (x == 0 || gm_isnan(x)) return x;
-    if (gm_isinf(x, 0)) return NAN;
+    if (gm_isinf(x, 0)) return go_nan();
     int sign = 0;
     if (x < 0) { x = -x; sign = 1; }
     uint64_t j; double z;
@@ -172,7 +177,7 @@ static inline double go_tan(double x) {
     static const double Q1 = 1.36812963470692954678e4, Q2 = -1.32089234440210967447e6,
                         Q3 = 2.50083801823357915839e7, Q4 = -5.38695755929454629881e7;
     if (x == 0 || gm_isnan(x)) return x;
-    if (gm_isinf(x, 0)) return NAN;
+    if (gm_isinf(x, 0)) return go_nan();
     int sign = 0;
     if (x < 0) { x = -x; sign = 1; }
     uint64_t j; double z;
@@ -217,7 +222,7 @@ static inline double go_atan(double x) {
 }
 /* src/math/atan2.go */
 static inline double go_atan2(double y, double x) {
-    if (gm_isnan(y) || gm_isnan(x)) return NAN;
+    if (gm_isnan(y) || gm_isnan(x)) return go_nan();
     if (y == 0) {
         if (x >= 0 && !gm_signbit(x)) return gm_copysign(0, y);
         return gm_copysign(GO_PI, y);
@@ -246,7 +251,7 @@ static inline double go_asin(double x) {
     if (x == 0) return x;
     int sign = 0;
     if (x < 0) { x = -x; sign = 1; }
-    if (x > 1) return NAN;
+    if (x > 1) return go_nan();
     double temp = sqrt(1 - x * x);
     FL(3);
     if (x > 0.7) { temp = GO_PI / 2 - gm_satan(temp / x); FL(2); }

@@ -28,9 +28,22 @@ def same_bits(a, b):
     return np.array_equal(np.ascontiguousarray(a).view(np.uint64), np.ascontiguousarray(b).view(np.uint64))
 
 
-def gpu_render(scene, rd, lanes_per_wave=0):
-    with G.Renderer(scene, lanes_per_wave=lanes_per_wave) as r:
-        return r.render(rd)
+KERNELS = ["serial", "auto"]   # auto = the wave-parallel kernel wherever it is eligible
+
+
+def gpu_render(scene, rd, lanes_per_wave=0, kernel="auto"):
+    with G.Renderer(scene, lanes_per_wave=lanes_per_wave, kernel=kernel) as r:
+        film, st = r.render(rd)
+    if kernel == "serial":
+        assert st.kernel == abi.PBRT_KERNEL_SERIAL
+    elif kernel == "wave":
+        assert st.kernel == abi.PBRT_KERNEL_WAVE
+    return film, st
+
+
+def wave_eligible(rd):
+    return (rd.integrator == abi.PBRT_INTEGRATOR_PATH and rd.n_dims >= 3
+            and rd.light_strategy == abi.PBRT_LIGHT_STRATEGY_UNIFORM)
 
 
 def oracle_render(scene, rd):
@@ -41,6 +54,9 @@ def oracle_render(scene, rd):
 
 def check(scene, rd, **kw):
     film, st = gpu_render(scene, rd, **kw)
+    if kw.get("kernel", "auto") == "auto":
+        want = abi.PBRT_KERNEL_WAVE if wave_eligible(rd) else abi.PBRT_KERNEL_SERIAL
+        assert st.kernel == want
     ofilm, ost = oracle_render(scene, rd)
     assert st.paths_traced == ost.paths
     assert same_bits(film, ofilm), f"{int((film != ofilm).sum())} film values differ"
@@ -90,6 +106,35 @@ def test_device_trig_matches_oracle():
     got = probe(5, yx)[:, 0]
     want = np.array([L.oracle_go_atan2(y, x) for y, x in yx])
     assert same_bits(got, want)
+
+
+def special_values(n, seed):
+    rng = np.random.default_rng(seed)
+    sp = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 5e-324, -5e-324, 2.2250738585072014e-308,
+                   1.0, -1.0, 2.0 ** 53, -(2.0 ** 53), 2.0 ** 53 - 1, 2.0 ** 60, 1.7976931348623157e308,
+                   -1.7976931348623157e308, 0.5, 1e-300, -1e-300])
+    rnd = rng.standard_normal(n) * 10.0 ** rng.integers(-320, 300, n)
+    return np.concatenate([sp, rnd])
+
+
+def test_device_next_float_up_down_and_go_max_min_special_values():
+    """Branch-free device forms of NextFloatUp/Down (pkg/math/math.go:122-128 =
+    math.Nextafter(v, v±1)) and Go math.Max/Min: bit-identical to the oracle's
+    Go restatement on ±0, ±Inf, NaN, denormals, |v| >= 2^53 and random values."""
+    L = O.lib()
+    v = special_values(4000, 11)
+    up = probe(18, v)[:, 0]
+    dn = probe(19, v)[:, 0]
+    want_up = np.array([L.oracle_go_nextafter(x, x + 1) for x in v])
+    want_dn = np.array([L.oracle_go_nextafter(x, x - 1) for x in v])
+    assert same_bits(up, want_up) and same_bits(dn, want_dn)
+    a = np.repeat(v[:60], 60)
+    b = np.tile(v[:60], 60)
+    pairs = np.stack([np.concatenate([a, v]), np.concatenate([b, v[::-1]])], axis=1)
+    mx = probe(11, pairs)[:, 0]
+    mn = probe(12, pairs)[:, 0]
+    assert same_bits(mx, np.array([L.oracle_go_max(x, y) for x, y in pairs]))
+    assert same_bits(mn, np.array([L.oracle_go_min(x, y) for x, y in pairs]))
 
 
 def test_device_div_sqrt_correctly_rounded():
@@ -147,21 +192,23 @@ def test_device_pcg_matches_golden():
 
 
 # ---------------------------------------------------------------- film parity
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("name", sorted(GOLDEN["cases"]))
-def test_golden_fixtures(name):
+def test_golden_fixtures(name, kernel):
     case = GOLDEN["cases"][name]
     w, h = case["w"], case["h"]
     scene = G.Scene.readme(w, h) if case["scene"] == "readme" else G.Scene.cornell(w, h)
     rd = abi.render_desc(**case["render"])
-    film, st = gpu_render(scene, rd)
+    film, st = gpu_render(scene, rd, kernel=kernel)
     gold = np.load(os.path.join(HERE, "golden", name + ".npz"))["film"]
     assert same_bits(film, gold)
     assert hashlib.sha256(film.tobytes()).hexdigest() == case["sha256"]
     assert st.paths_traced == case["paths"]
 
 
-def test_readme_256_path_bitexact():
-    check(G.Scene.readme(256, 256), abi.render_desc(2, 2))
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_readme_256_path_bitexact(kernel):
+    check(G.Scene.readme(256, 256), abi.render_desc(2, 2), kernel=kernel)
 
 
 def test_config_A_traces_nothing():
@@ -194,13 +241,39 @@ def test_direct_lighting_sample_one():
     dict(spp_x=2, spp_y=2, tile_size=8),
     dict(spp_x=2, spp_y=2, tile_size=13),
 ])
-def test_readme_variants_bitexact(kw):
-    check(G.Scene.readme(72, 40), abi.render_desc(**kw))
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_readme_variants_bitexact(kw, kernel):
+    check(G.Scene.readme(72, 40), abi.render_desc(**kw), kernel=kernel)
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("w,h", [(1, 1), (17, 3), (37, 23), (16, 16)])
-def test_ragged_images(w, h):
-    check(G.Scene.readme(w, h), abi.render_desc(3, 3))
+def test_ragged_images(w, h, kernel):
+    check(G.Scene.readme(w, h), abi.render_desc(3, 3), kernel=kernel)
+
+
+@pytest.mark.parametrize("kw", [
+    dict(spp_x=9, spp_y=9),                      # 80 traced samples: two 64-lane batches
+    dict(spp_x=8, spp_y=8, n_dims=3),            # bounce-1 uScattering from the RNG
+    dict(spp_x=5, spp_y=5, n_dims=5),            # bounce-1 BSDF sample stratified (0,0)
+    dict(spp_x=4, spp_y=6, jitter=True),
+    dict(spp_x=6, spp_y=6, flags=abi.PBRT_FLAG_SERIAL_START_PIXEL),
+    dict(spp_x=4, spp_y=4, max_depth=3),
+    dict(spp_x=4, spp_y=4, max_depth=12, rr_threshold=0.0),
+])
+def test_wave_kernel_variants(kw):
+    check(G.Scene.readme(48, 40), abi.render_desc(**kw), kernel="wave")
+
+
+def test_wave_kernel_cornell_64spp():
+    check(G.Scene.cornell(32, 32), abi.render_desc(8, 8, max_depth=10), kernel="wave")
+
+
+def test_wave_kernel_rejects_ineligible_render():
+    with G.Renderer(G.Scene.readme(16, 16), kernel="wave") as r:
+        with pytest.raises(G.PbrtError) as ei:
+            r.render(abi.render_desc(2, 2, n_dims=2))
+    assert ei.value.code == abi.PBRT_E_UNSUPPORTED
 
 
 @pytest.mark.parametrize("lpw", [1, 4, 16, 64])
@@ -208,8 +281,9 @@ def test_lanes_per_wave_invariant(lpw):
     check(G.Scene.readme(96, 48), abi.render_desc(2, 2), lanes_per_wave=lpw)
 
 
-def test_cornell_bitexact():
-    check(G.Scene.cornell(64, 48), abi.render_desc(3, 3, max_depth=8))
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_cornell_bitexact(kernel):
+    check(G.Scene.cornell(64, 48), abi.render_desc(3, 3, max_depth=8), kernel=kernel)
 
 
 def test_tile_shards_sum_to_full_frame():
@@ -280,12 +354,13 @@ def panic_scene():
     return s.build()
 
 
-def test_reference_panic_is_reported_like_the_oracle():
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_reference_panic_is_reported_like_the_oracle(kernel):
     scene = panic_scene()
     rd = abi.render_desc(2, 2)
     rc, _, ost = O.render(scene.desc, rd, threads=1)
     assert rc == abi.PBRT_E_REF_PANIC and ost.panic_kind == abi.PBRT_PANIC_LD_GT_10
-    with G.Renderer(scene) as r:
+    with G.Renderer(scene, kernel=kernel) as r:
         with pytest.raises(G.PbrtError) as ei:
             r.render(rd)
     st = ei.value.stats

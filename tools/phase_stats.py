@@ -1,0 +1,43 @@
+"""Render one frame and print the wave kernel's phase counters (diagnostics).
+
+    python tools/phase_stats.py [--width W --height H --spp S --kernel auto|serial]
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "go-pbrt_amd"))
+import pbrtgpu as G  # noqa: E402
+from pbrtgpu import abi  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--width", type=int, default=1920)
+ap.add_argument("--height", type=int, default=1080)
+ap.add_argument("--spp", type=int, default=8)
+ap.add_argument("--kernel", default="auto")
+ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--occupancy", type=int, default=0)
+a = ap.parse_args()
+
+scene = G.Scene.readme(a.width, a.height)
+names = ["paths", "camera_samples", "closest_rays", "shadow_rays", "any_panic", "windows",
+         "cyc_start_pixel", "cyc_bounce1", "cyc_chain", "cyc_full_paths", "cyc_film_add"]
+with G.Renderer(scene, kernel=a.kernel, occupancy=a.occupancy) as r:
+    rd = abi.render_desc(a.spp, a.spp)
+    for i in range(a.reps):
+        t0 = time.perf_counter()
+        r.render_async(rd)
+        st = r.synchronize()
+        dt = time.perf_counter() - t0
+        out = (C.c_uint64 * 16)()
+        n = G.lib().pbrt_gpu_counters(C.c_void_p(r.h), out, 16)
+        vals = dict(zip(names, list(out)[:n]))
+        tot = sum(vals[k] for k in names[6:]) or 1
+        print(f"rep {i}: {dt * 1e3:.1f} ms kernel {st.kernel_ms:.1f} ms kernel={st.kernel} "
+              f"Mpaths/s={st.paths_traced / dt / 1e6:.2f}")
+        px = a.width * a.height
+        print("  windows/pixel %.2f" % (vals["windows"] / px))
+        for k in names[6:]:
+            print(f"  {k:16s} {vals[k] / tot * 100:5.1f}%  {vals[k] / px:10.0f} cyc/pixel")
