@@ -46,6 +46,7 @@ struct RenderParams {
     double rr_threshold;
     int32_t lanes_per_wave;
     int32_t flags;   // pbrt_render_desc.flags
+    int32_t sp_events, sp_draws, sp_serial, pad1;   // wave kernel StartPixel: events, raw draws buffered
 };
 
 struct PanicRec {
@@ -62,9 +63,9 @@ struct Counters {
     int32_t pad;
     // wave kernel diagnostics (pbrt_gpu_counters): speculation windows, and
     // lane-0 clock64 cycles in StartPixel / bounce 1 / chain / full paths / film add
-    unsigned long long windows, phase[5];
+    unsigned long long windows, phase[8];
 };
-constexpr int kNumCounters = 6 + 5;
+constexpr int kNumCounters = 6 + 8;
 
 __device__ __forceinline__ void tile_bounds(const RenderParams& rp, int64_t tile, int64_t& x0, int64_t& y0,
                                             int64_t& x1, int64_t& y1) {
@@ -251,7 +252,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kMinWaves
 //   4. Samples 1..spp-1 run as full paths, one per lane (batches of 64), and
 //      are added to the tile film (LDS) in sample order.
 struct SpecLayout {   // byte offsets into the dynamic LDS block
-    int film, s1d, other, memb, lbuf, sbuf, dbuf, pbuf, total;
+    int film, s1d, other, memb, lbuf, sbuf, dbuf, pbuf, vbuf, total;
 };
 constexpr uint32_t kBadD = 0xFFFFFFFFu;
 
@@ -316,6 +317,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8
     uint64_t* sbuf = (uint64_t*)(lds + lay.sbuf);
     uint32_t* dbuf = (uint32_t*)(lds + lay.dbuf);
     int* pbuf = (int*)(lds + lay.pbuf);
+    uint32_t* vbuf = (uint32_t*)(lds + lay.vbuf);
     uint16_t* stack = stack_lds + lane;
 
     int64_t x0, y0, x1, y1, px0, py0, px1, py1;
@@ -326,8 +328,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8
 
     const int n = rp.spp, ndims = rp.ndims, nl = sc.n_lights;
     const double inv_n = 1.0 / (double)n;
-    const int s1 = rp.jitter ? 2 * n : n, s2 = rp.jitter ? 3 * n : n;
-    const int64_t T = (int64_t)ndims * (s1 + s2);   // StartPixel draws without rejections
+    const int s1 = rp.jitter ? 2 * n : n, s2 = rp.jitter ? 3 * n : n;   // StartPixel draws per 1D / 2D dim
     Pcg seed;
     pcg_seed(seed, (uint64_t)tile);   // Sampler.Clone(seed = tile index), integrator.go:318,328
     const uint64_t inc = seed.inc;
@@ -335,7 +336,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8
     const SpecSampler ss{s1d, n, ndims};
     const pbrt_camera_desc& cam = *sc.camera;
     unsigned long long paths = 0, windows = 0;
-    unsigned long long ph[5] = {0, 0, 0, 0, 0};
+    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     long long tprev = clock64();
     auto mark = [&](int i) {
         long long now = clock64();
@@ -347,37 +348,81 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8
     for (int64_t py = y0; py < y1; py++) {
         for (int64_t px = x0; px < x1; px++) {
             // ---- 1. StartPixel (stratified.go:21-48)
-            if (lane == 0) sh_flag = 0;
-            __syncthreads();
-            int rej = 0;
-            for (int64_t idx = lane; idx < T; idx += kWave) {
-                const uint32_t v = pcg_output(pcg_advance(J, S, inc, (uint64_t)idx));
-                int d, r, i;
-                if (idx < (int64_t)ndims * s1) {
-                    d = (int)(idx / s1);
-                    r = (int)(idx % s1);
-                    if (rp.jitter && r < n) {
-                        s1d[d * n + r] = gomath::min(((double)r + pcg_float_of(v)) * inv_n, gomath::kOneMinusEpsilon);
-                        continue;
-                    }
-                    i = r - (rp.jitter ? n : 0);
-                    other[d * n + i] = (uint16_t)(i + (int)(v % (uint32_t)(n - i)));
-                } else {
-                    const int64_t q = idx - (int64_t)ndims * s1;
-                    r = (int)(q % s2);
-                    if (rp.jitter && r < 2 * n) continue;
-                    i = r - (rp.jitter ? 2 * n : 0);
+            // The pixel's draws form a fixed list of E events (jitter floats and
+            // pcg_bounded shuffle picks, sampling.go:101-145). A bounded pick
+            // retries on v < 2^32 mod b, which the reference's (rot+1)&31 output
+            // rotation makes common (v < 4 has probability ~1/64), so event e
+            // lands on draw e + R(e), R(e) = rejections before it. Lanes fill
+            // the raw stream by jump-ahead, then resolve R chunk by chunk: one
+            // ballot per rejection shifts every later event by one draw.
+            bool serial_sp = rp.sp_serial != 0;
+            if (!serial_sp) {
+                const int E = rp.sp_events, V = rp.sp_draws;
+                uint64_t st = pcg_advance(J, S, inc, (uint64_t)lane);
+                for (int t = lane; t < V; t += kWave) {
+                    vbuf[t] = pcg_output(st);
+                    st = J.a[6] * st + inc * J.b[6];   // +64 draws
                 }
-                const uint32_t b = (uint32_t)(n - i);
-                if (v < (~b + 1u) % b) rej = 1;
+                __syncthreads();
+                mark(5);
+                int R = 0;
+                bool overflow = false;
+                for (int cb = 0; cb < E; cb += kWave) {
+                    const int e = cb + lane;
+                    int kind = 0, slot = 0, i = 0;   // kind 0 none, 1 1D float, 2 1D pick, 3 2D pick
+                    if (e < E) {
+                        if (e < ndims * s1) {
+                            const int d = e / s1, q = e - d * s1;
+                            if (rp.jitter && q < n) { kind = 1; slot = d * n + q; }
+                            else { kind = 2; i = q - (rp.jitter ? n : 0); slot = d * n + i; }
+                        } else {
+                            const int e2 = e - ndims * s1, d = e2 / s2, q = e2 - d * s2;
+                            if (!(rp.jitter && q < 2 * n)) { kind = 3; i = q - (rp.jitter ? 2 * n : 0); }
+                        }
+                    }
+                    const uint32_t b = (uint32_t)(n - i);
+                    const uint32_t thr = kind >= 2 ? (~b + 1u) % b : 0u;
+                    int local = 0;
+                    for (;;) {
+                        const int t = e + R + local;
+                        const bool out = kind != 0 && t >= V;
+                        const bool bad = !out && kind >= 2 && vbuf[t] < thr;
+                        if (__any(out)) { overflow = true; break; }
+                        const unsigned long long m = __ballot(bad);
+                        if (m == 0) break;
+                        const int first = __ffsll((long long)m) - 1;
+                        if (lane >= first) local++;
+                    }
+                    if (overflow) break;
+                    const uint32_t v = kind != 0 ? vbuf[e + R + local] : 0u;
+                    if (kind == 1)
+                        s1d[slot] = gomath::min(((double)(slot % n) + pcg_float_of(v)) * inv_n, gomath::kOneMinusEpsilon);
+                    else if (kind == 2)
+                        other[slot] = (uint16_t)(i + (int)(v % b));
+                    R += __shfl(local, kWave - 1);
+                }
+                serial_sp = overflow;
+                if (!serial_sp) {
+                    if (!rp.jitter)
+                        for (int idx = lane; idx < ndims * n; idx += kWave)
+                            s1d[idx] = gomath::min(((double)(idx % n) + 0.5) * inv_n, gomath::kOneMinusEpsilon);
+                    __syncthreads();
+                    if (lane < ndims) {
+                        double* samp = s1d + lane * n;
+                        const uint16_t* oth = other + lane * n;
+                        for (int k = 0; k < n; k++) {
+                            const int o = oth[k];
+                            double a = samp[k];
+                            samp[k] = samp[o];
+                            samp[o] = a;
+                        }
+                    }
+                    if (lane == 0) sh_state = pcg_advance(J, S, inc, (uint64_t)(E + R));
+                }
             }
-            if (!rp.jitter)
-                for (int idx = lane; idx < ndims * n; idx += kWave)
-                    s1d[idx] = gomath::min(((double)(idx % n) + 0.5) * inv_n, gomath::kOneMinusEpsilon);
-            if (rej) atomicOr(&sh_flag, 1);
-            __syncthreads();
-            if (sh_flag || (rp.flags & PBRT_FLAG_SERIAL_START_PIXEL)) {
-                if (lane == 0) {   // a pcg_bounded rejection: serial replay
+            if (serial_sp || (rp.flags & PBRT_FLAG_SERIAL_START_PIXEL)) {
+                ph[7]++;
+                if (lane == 0) {   // serial replay (huge sample counts, or forced)
                     Thread t;
                     t.rng.state = S;
                     t.rng.inc = inc;
@@ -386,18 +431,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8
                     start_pixel(t);
                     sh_state = t.rng.state;
                 }
-            } else {
-                if (lane < ndims) {
-                    double* samp = s1d + lane * n;
-                    const uint16_t* oth = other + lane * n;
-                    for (int i = 0; i < n; i++) {
-                        const int o = oth[i];
-                        double a = samp[i];
-                        samp[i] = samp[o];
-                        samp[o] = a;
-                    }
-                }
-                if (lane == 0) sh_state = pcg_advance(J, S, inc, (uint64_t)T);
             }
             __syncthreads();
             S = sh_state;
@@ -441,6 +474,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8
                     sbuf[lane] = st;
                     dbuf[lane] = (pnc || c.kdep) ? kBadD : c.draws;
                     __syncthreads();
+                    mark(2);
                     if (lane == 0) {
                         uint64_t x = 0;
                         int k = kh;
@@ -463,6 +497,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8
                     __syncthreads();
                     kh = sh_k;
                     Sh = sh_state;
+                    mark(6);
                     if (sh_trunc) break;
                 }
                 S = Sh;
@@ -544,7 +579,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8
         atomicAdd(&ctr->paths, paths);
         atomicAdd(&ctr->camera_samples, paths);
         atomicAdd(&ctr->windows, windows);
-        for (int i = 0; i < 5; i++) atomicAdd(&ctr->phase[i], ph[i]);
+        for (int i = 0; i < 8; i++) atomicAdd(&ctr->phase[i], ph[i]);
     }
 }
 
@@ -779,6 +814,10 @@ bool spec_layout(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Render
     L.sbuf = put(kWave * 8);
     L.dbuf = put(kWave * 4);
     L.pbuf = put(kWave * 2 * 4);
+    const int64_t s1 = rd->jitter ? 2 * n : n, s2 = rd->jitter ? 3 * n : n;
+    const int64_t E = nd * (s1 + s2), V = E + 64 + E / 8;
+    const bool buffered = V * 4 <= 16 * 1024;
+    L.vbuf = put(buffered ? V * 4 : 4);
     L.total = (int)off;
     return off <= 48 * 1024;
 }
@@ -835,6 +874,13 @@ int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
         HIPCHK(c, hipMemcpyAsync(c->d_dist, &dist, sizeof(dist), hipMemcpyHostToDevice, c->stream));
     }
     c->use_spec = c->kernel_req != PBRT_KERNEL_SERIAL && spec_layout(c, rd, rp, c->lay);
+    {
+        const int64_t n = rp.spp, s1 = rp.jitter ? 2 * n : n, s2 = rp.jitter ? 3 * n : n;
+        const int64_t E = (int64_t)rp.ndims * (s1 + s2), V = E + 64 + E / 8;
+        rp.sp_events = (int32_t)E;
+        rp.sp_draws = (int32_t)V;
+        rp.sp_serial = V * 4 <= 16 * 1024 ? 0 : 1;
+    }
     if (c->kernel_req == PBRT_KERNEL_WAVE && !c->use_spec)
         return set_err(c, PBRT_E_UNSUPPORTED, "render not eligible for the wave-parallel kernel");
     size_t nslot = (size_t)(rp.n_slots > 0 ? rp.n_slots : 1);
@@ -1202,9 +1248,10 @@ extern "C" int pbrt_gpu_counters(pbrt_gpu_ctx* c, uint64_t* out, int n) {
     if (hipSetDevice(c->device) != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) return PBRT_E_HIP;
     Counters ctr;
     if (hipMemcpy(&ctr, c->d_ctr, sizeof(ctr), hipMemcpyDeviceToHost) != hipSuccess) return PBRT_E_HIP;
-    const uint64_t v[kNumCounters] = {ctr.paths, ctr.camera_samples, ctr.closest_rays, ctr.shadow_rays,
+    const uint64_t v[kNumCounters] = {ctr.paths,    ctr.camera_samples, ctr.closest_rays, ctr.shadow_rays,
                                       (uint64_t)ctr.any_panic, ctr.windows, ctr.phase[0], ctr.phase[1],
-                                      ctr.phase[2], ctr.phase[3], ctr.phase[4]};
+                                      ctr.phase[2], ctr.phase[3], ctr.phase[4], ctr.phase[5],
+                                      ctr.phase[6], ctr.phase[7]};
     for (int i = 0; i < n && i < kNumCounters; i++) out[i] = v[i];
     return kNumCounters;
 }

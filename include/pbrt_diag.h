@@ -44,7 +44,8 @@ int pbrt_gpu_probe(int device, int op, const double* in, size_t n, int in_stride
 /* Device counters of the last render (after it completed), in this order:
  * paths, camera_samples, closest_rays, shadow_rays, any_panic, windows
  * (WAVE kernel speculation rounds), then lane-0 clock64 cycles summed over
- * tiles in: StartPixel, bounce 1, offset chain, full paths, film add.
+ * tiles in: StartPixel swaps, bounce 1, speculative trajectories, full paths,
+ * film add, StartPixel draws, chain walk, (spare).
  * Returns the number of counters available. */
 struct pbrt_gpu_ctx;
 int pbrt_gpu_counters(struct pbrt_gpu_ctx* ctx, uint64_t* out, int n);

@@ -23,7 +23,8 @@ a = ap.parse_args()
 
 scene = G.Scene.readme(a.width, a.height)
 names = ["paths", "camera_samples", "closest_rays", "shadow_rays", "any_panic", "windows",
-         "cyc_start_pixel", "cyc_bounce1", "cyc_chain", "cyc_full_paths", "cyc_film_add"]
+         "cyc_sp_swaps", "cyc_bounce1", "cyc_trajectories", "cyc_full_paths", "cyc_film_add",
+         "cyc_sp_draws", "cyc_chain_walk", "n_serial_start_pixel"]
 with G.Renderer(scene, kernel=a.kernel, occupancy=a.occupancy) as r:
     rd = abi.render_desc(a.spp, a.spp)
     for i in range(a.reps):
@@ -31,13 +32,14 @@ with G.Renderer(scene, kernel=a.kernel, occupancy=a.occupancy) as r:
         r.render_async(rd)
         st = r.synchronize()
         dt = time.perf_counter() - t0
-        out = (C.c_uint64 * 16)()
-        n = G.lib().pbrt_gpu_counters(C.c_void_p(r.h), out, 16)
+        out = (C.c_uint64 * 32)()
+        n = G.lib().pbrt_gpu_counters(C.c_void_p(r.h), out, 32)
         vals = dict(zip(names, list(out)[:n]))
-        tot = sum(vals[k] for k in names[6:]) or 1
+        tot = sum(vals[k] for k in names[6:13]) or 1
         print(f"rep {i}: {dt * 1e3:.1f} ms kernel {st.kernel_ms:.1f} ms kernel={st.kernel} "
               f"Mpaths/s={st.paths_traced / dt / 1e6:.2f}")
         px = a.width * a.height
         print("  windows/pixel %.2f" % (vals["windows"] / px))
-        for k in names[6:]:
+        print("  serial StartPixel fallbacks", vals["n_serial_start_pixel"])
+        for k in names[6:13]:
             print(f"  {k:16s} {vals[k] / tot * 100:5.1f}%  {vals[k] / px:10.0f} cyc/pixel")
