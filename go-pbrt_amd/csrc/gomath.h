@@ -15,6 +15,11 @@
 #include <stdint.h>
 
 #define GO_HD __host__ __device__ __forceinline__
+// Go's trig routines are long polynomial sequences; GO_TRIG lets a build keep
+// one out-of-line copy of each instead of inlining them at every call site.
+#ifndef GO_TRIG
+#define GO_TRIG GO_HD
+#endif
 
 namespace gomath {
 
@@ -120,7 +125,7 @@ GO_HD double reduce(double x, uint64_t& j) {
 }
 }  // namespace detail
 
-GO_HD double cos(double x) {
+GO_TRIG double cos(double x) {
     if (is_nan(x) || is_inf(x)) return nan();
     bool sign = false;
     x = abs(x);
@@ -132,7 +137,7 @@ GO_HD double cos(double x) {
     double y = (j == 1 || j == 2) ? detail::sin_poly(z, zz) : detail::cos_poly(zz);
     return sign ? -y : y;
 }
-GO_HD double sin(double x) {
+GO_TRIG double sin(double x) {
     if (x == 0 || is_nan(x)) return x;
     if (is_inf(x)) return nan();
     bool sign = false;
@@ -145,7 +150,7 @@ GO_HD double sin(double x) {
     return sign ? -y : y;
 }
 // src/math/tan.go (host-side camera setup)
-GO_HD double tan(double x) {
+GO_TRIG double tan(double x) {
     if (x == 0 || is_nan(x)) return x;
     if (is_inf(x)) return nan();
     bool sign = false;
@@ -188,7 +193,7 @@ GO_HD double atan(double x) {
     return x > 0 ? detail::satan(x) : -detail::satan(-x);
 }
 // src/math/atan2.go
-GO_HD double atan2(double y, double x) {
+GO_TRIG double atan2(double y, double x) {
     if (is_nan(y) || is_nan(x)) return nan();
     if (y == 0) return (x >= 0 && !signbit(x)) ? copysign(0, y) : copysign(kPi, y);
     if (x == 0) return copysign(kPi / 2, y);
@@ -202,7 +207,7 @@ GO_HD double atan2(double y, double x) {
     return q;
 }
 // src/math/asin.go
-GO_HD double asin(double x) {
+GO_TRIG double asin(double x) {
     if (x == 0) return x;
     bool sign = false;
     if (x < 0) { x = -x; sign = true; }
@@ -211,7 +216,7 @@ GO_HD double asin(double x) {
     t = (x > 0.7) ? kPi / 2 - detail::satan(t / x) : detail::satan(x / t);
     return sign ? -t : t;
 }
-GO_HD double acos(double x) { return kPi / 2 - asin(x); }
+GO_TRIG double acos(double x) { return kPi / 2 - asin(x); }
 GO_HD double sqrt(double x) { return __builtin_sqrt(x); }
 GO_HD double floor(double x) { return __builtin_floor(x); }
 GO_HD double ceil(double x) { return __builtin_ceil(x); }

@@ -168,7 +168,7 @@ struct EF {
 // efloat.go:102-111 Check(): Inf/NaN bounds or Low > High panics in Go
 GO_HD void ef_check(const EF& f, int& panic) {
     // !(|lo| < Inf) is true for ±Inf and NaN
-    const bool bad = !(gomath::abs(f.lo) < kInf) | !(gomath::abs(f.hi) < kInf) | (f.lo > f.hi);
+    const bool bad = (int)!(gomath::abs(f.lo) < kInf) | (int)!(gomath::abs(f.hi) < kInf) | (int)(f.lo > f.hi);
     panic = bad ? 1 : panic;
 }
 GO_HD EF ef_new(double v, double err, int& panic) {

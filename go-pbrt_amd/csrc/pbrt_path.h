@@ -25,7 +25,7 @@ struct DevScene {
     const pbrt_shape_desc* shapes;
     const pbrt_material_desc* materials;
     const pbrt_primitive_desc* prims;
-    const pbrt_bvh_node* nodes;
+    const struct DevNode* nodes;   // device copy of pbrt_bvh_node[], 64-byte records
     const pbrt_light_desc* lights;
     const pbrt_camera_desc* camera;
     const pbrt_film_desc* film;
@@ -171,6 +171,19 @@ __device__ inline void transform_si_shared(SI& si, const pbrt_matrix4x4& M, cons
 }
 
 // -------------------------------------------------------------------- shapes
+// `phi > phiMax` of the partial-shape tests (sphere.go:115-131, disk.go:90-95)
+// with phi = Atan2(y, x) (+2*Pi if negative). Go's Atan2 lies in [-Pi, Pi], so
+// phi <= 2*Pi after rounding and the test is false whenever phiMax >= 2*Pi
+// (every full sphere / disk): the Atan2 is skipped there, with the same result
+// (a NaN phi compares false either way).
+__device__ __forceinline__ bool phi_beyond(double y, double x, double phi_max) {
+    const double two_pi = 2 * gomath::kPi;
+    if (phi_max >= two_pi) return false;
+    double phi = gomath::atan2(y, x);
+    if (phi < 0.0) phi += two_pi;
+    return phi > phi_max;
+}
+
 // Sphere.Intersect / IntersectP (sphere.go:64-268). world->object = the swap of
 // object_to_world (Transform.Inverse, transform.go:175-177).
 template <bool kFull>
@@ -194,22 +207,20 @@ __device__ inline bool sphere_intersect(const pbrt_shape_desc& s, const Ray& r, 
         used_t1 = true;
         if (ts.hi > ray.tmax) return false;
     }
-    const double two_pi = 2 * gomath::kPi;
     V3 ph = ray.o + muls(ray.d, ts.v);
     ph = muls(ph, s.radius / dist(ph, V3{0, 0, 0}));
     if (ph.x == 0.0 && ph.y == 0.0) ph.x = 1e-5 * s.radius;
-    double phi = gomath::atan2(ph.y, ph.x);
-    if (phi < 0.0) phi += two_pi;
-    if ((s.z_min > -s.radius && ph.z < s.z_min) || (s.z_max < s.radius && ph.z > s.z_max) || phi > s.phi_max) {
+    if ((s.z_min > -s.radius && ph.z < s.z_min) || (s.z_max < s.radius && ph.z > s.z_max) ||
+        phi_beyond(ph.y, ph.x, s.phi_max)) {
         if (used_t1) return false;
         if (t1.hi > ray.tmax) return false;
         ts = t1;
         ph = ray.o + muls(ray.d, ts.v);
         ph = muls(ph, s.radius / dist(ph, V3{0, 0, 0}));
         if (ph.x == 0.0 && ph.y == 0.0) ph.x = 1e-5 * s.radius;
-        double phi2 = gomath::atan2(ph.y, ph.x);   // sphere.go:127 shadows phi (`:=`)
-        if (phi2 < 0.0) phi2 += two_pi;
-        if ((s.z_min > -s.radius && ph.z < s.z_min) || (s.z_max < s.radius && ph.z > s.z_max) || phi2 > s.phi_max)
+        // sphere.go:127 shadows phi (`:=`): the new phi is only tested here
+        if ((s.z_min > -s.radius && ph.z < s.z_min) || (s.z_max < s.radius && ph.z > s.z_max) ||
+            phi_beyond(ph.y, ph.x, s.phi_max))
             return false;
     }
     t_hit = ts.v;
@@ -225,7 +236,6 @@ __device__ inline bool sphere_intersect(const pbrt_shape_desc& s, const Ray& r, 
     V3 perr = muls(vabs(ph), gomath::gamma(5));
     make_si(*si, s.object_to_world.m, s.object_to_world.m_inv, ph, perr, muls(ray.d, -1), dpdu, dpdv, ray.time,
             s.reverse_orientation != s.transform_swaps_handedness);
-    (void)phi;
     return true;
 }
 
@@ -239,9 +249,7 @@ __device__ inline bool disk_intersect(const pbrt_shape_desc& s, const Ray& r, SI
     V3 ph = ray.o + muls(ray.d, ts);
     double d2 = ph.x * ph.x + ph.y * ph.y;
     if (d2 > s.radius * s.radius || d2 < s.inner_radius * s.inner_radius) return false;
-    double phi = gomath::atan2(ph.y, ph.x);
-    if (phi < 0) phi += 2 * gomath::kPi;
-    if (phi > s.phi_max) return false;
+    if (phi_beyond(ph.y, ph.x, s.phi_max)) return false;
     t_hit = ts;
     if (!kFull) return true;
     double rhit = gomath::sqrt(d2);
@@ -288,27 +296,59 @@ __device__ inline bool prim_intersect_p(const DevScene& sc, int pi, const Ray& r
 }
 
 // ------------------------------------------------------------------------ BVH
-// Bounds3.IntersectP (bounds.go:149-185); (1 + 2*Gamma(3)) == 1 exactly
-__device__ __forceinline__ bool node_hit(const pbrt_bvh_node& nd, const Ray& r, V3 inv, int nx, int ny, int nz) {
+// BVH node as stored on the device: pbrt_bvh_node widened to 64 bytes so a
+// node is fetched with four 16-byte loads issued together (the 56-byte ABI
+// layout let the compiler sink each field load behind the previous test,
+// one memory round trip per field).
+struct alignas(16) DevNode {
+    double bmin[3];
+    double bmax[3];
+    uint32_t offset;     // primitivesOffset (leaf) / secondChildOffset (interior)
+    uint32_t nprims_axis;   // nPrimitives | axis << 16
+    uint64_t pad;
+};
+static_assert(sizeof(DevNode) == 64, "DevNode is four 16-byte loads");
+struct NodeView {
+    double b[6];
+    uint32_t offset, n_prims, axis;
+};
+__device__ __forceinline__ NodeView load_node(const DevNode* nodes, uint32_t i) {
+    const ulonglong2* q = reinterpret_cast<const ulonglong2*>(nodes + i);
+    const ulonglong2 a = q[0], b = q[1], c = q[2], d = q[3];
+    NodeView v;
+    v.b[0] = __builtin_bit_cast(double, a.x);
+    v.b[1] = __builtin_bit_cast(double, a.y);
+    v.b[2] = __builtin_bit_cast(double, b.x);
+    v.b[3] = __builtin_bit_cast(double, b.y);
+    v.b[4] = __builtin_bit_cast(double, c.x);
+    v.b[5] = __builtin_bit_cast(double, c.y);
+    v.offset = (uint32_t)d.x;
+    v.n_prims = (uint32_t)(d.x >> 32) & 0xFFFFu;
+    v.axis = (uint32_t)(d.x >> 48) & 0xFFu;
+    return v;
+}
+// Bounds3.IntersectP (bounds.go:149-185); (1 + 2*Gamma(3)) == 1 exactly.
+// Branch-free: the same comparisons as the reference's early returns, folded
+// into one flag (values computed after a failed test are ignored).
+__device__ __forceinline__ bool node_hit(const NodeView& nd, const Ray& r, V3 inv, int nx, int ny, int nz) {
     const double robust = 1 + 2 * gomath::gamma(3);
-    double tmin = ((nx ? nd.bmax[0] : nd.bmin[0]) - r.o.x) * inv.x;
-    double tmax = ((nx ? nd.bmin[0] : nd.bmax[0]) - r.o.x) * inv.x;
-    double tymin = ((ny ? nd.bmax[1] : nd.bmin[1]) - r.o.y) * inv.y;
-    double tymax = ((ny ? nd.bmin[1] : nd.bmax[1]) - r.o.y) * inv.y;
+    double tmin = ((nx ? nd.b[3] : nd.b[0]) - r.o.x) * inv.x;
+    double tmax = ((nx ? nd.b[0] : nd.b[3]) - r.o.x) * inv.x;
+    const double tymin = ((ny ? nd.b[4] : nd.b[1]) - r.o.y) * inv.y;
+    double tymax = ((ny ? nd.b[1] : nd.b[4]) - r.o.y) * inv.y;
     tmax *= robust;
     tymax *= robust;
-    if (tmin > tymax || tymin > tmax) return false;
-    if (tymin > tmin) tmin = tymin;
-    if (tymax < tmax) tmax = tymax;
-    double tzmin = ((nz ? nd.bmax[2] : nd.bmin[2]) - r.o.z) * inv.z;
-    double tzmax = ((nz ? nd.bmin[2] : nd.bmax[2]) - r.o.z) * inv.z;
+    int hit = (int)!(tmin > tymax) & (int)!(tymin > tmax);
+    tmin = tymin > tmin ? tymin : tmin;
+    tmax = tymax < tmax ? tymax : tmax;
+    const double tzmin = ((nz ? nd.b[5] : nd.b[2]) - r.o.z) * inv.z;
+    double tzmax = ((nz ? nd.b[2] : nd.b[5]) - r.o.z) * inv.z;
     tzmax *= robust;
-    if (tmin > tzmax || tzmin > tmax) return false;
-    if (tzmin > tmin) tmin = tzmin;
-    if (tzmax < tmax) tmax = tzmax;
-    return tmin < r.tmax && tmax > 0;
+    hit &= (int)!(tmin > tzmax) & (int)!(tzmin > tmax);
+    tmin = tzmin > tmin ? tzmin : tmin;
+    tmax = tzmax < tmax ? tzmax : tmax;
+    return (hit & (int)(tmin < r.tmax) & (int)(tmax > 0)) != 0;
 }
-
 
 // BVH.Intersect (bvh.go:659-712) / IntersectP (:713-765). The [64] node stack
 // lives in LDS (one uint16 column per lane).
@@ -337,7 +377,7 @@ __device__ inline bool bvh_traverse(const DevScene& sc, Ray& ray, SI* si, uint16
         // A: interior nodes
         bool leaf = false, done = false;
         for (;;) {
-            const pbrt_bvh_node& nd = sc.nodes[cur];
+            const NodeView nd = load_node(sc.nodes, cur);
             if (node_hit(nd, ray, inv, nx, ny, nz)) {
                 if (nd.n_prims > 0) {
                     leaf = true;
@@ -363,7 +403,7 @@ __device__ inline bool bvh_traverse(const DevScene& sc, Ray& ray, SI* si, uint16
         if (done) break;
         (void)leaf;
         // B: the leaf's primitives
-        const pbrt_bvh_node& nd = sc.nodes[cur];
+        const NodeView nd = load_node(sc.nodes, cur);
         const uint32_t first = nd.offset, np = nd.n_prims;
         for (uint32_t i = 0; i < np; i++) {
             double t_hit;

@@ -106,12 +106,20 @@ struct PixelCache {
 
 // Path.Li (path.go:32-157) from bounce 1 on, with bounce 1 taken from the
 // pixel cache. kNEE = false: trajectory only (no light sampling; the draws
-// are still consumed), used to learn D for an RNG offset. One body serves
-// both uses (runtime flag) so the kernel carries a single copy of the
-// traversal code.
-__device__ inline Spec spec_path(const DevScene& sc, const PixelCache& pc, const SpecSampler& ss, Cursor& c,
-                                 int max_depth, double rr_threshold, uint16_t* stack, int& panic, int& bounce,
-                                 const bool kNEE) {
+// are still consumed), used to learn D for an RNG offset (k_chain);
+// kNEE = true: the full path (k_paths). Each kernel instantiates one.
+// Bounce-1 state without the per-light estimates (what trajectories need).
+struct ChainCache {
+    SI si;
+    BSDF b;
+    V3 wo;
+    int hit;
+    int pad;
+};
+
+template <bool kNEE, class Cache>
+__device__ inline Spec spec_path(const DevScene& sc, const Cache& pc, const SpecSampler& ss, Cursor& c,
+                                 int max_depth, double rr_threshold, uint16_t* stack, int& panic, int& bounce) {
     Spec L = spec(0), beta = spec(1);
     int32_t bounces = 1;
     bounce = 1;
@@ -148,13 +156,16 @@ __device__ inline Spec spec_path(const DevScene& sc, const PixelCache& pc, const
                 V2 ul = c_get2d(c, ss);
                 c_get2d(c, ss);
                 Spec ld;
-                if (first) {
-                    ld = pc.ld[ln];
-                    if (pc.ld_panic[ln]) {
-                        panic = pc.ld_panic[ln];
-                        break;
+                if constexpr (kNEE) {
+                    if (first) {
+                        ld = pc.ld[ln];
+                        if (pc.ld_panic[ln]) {
+                            panic = pc.ld_panic[ln];
+                            break;
+                        }
                     }
-                } else {
+                }
+                if (!first) {
                     ld = estimate_direct(sc, stack, panic, isect, b, ln, ul);
                     if (panic) break;
                     if (max_component(ld) > 10) {

@@ -239,103 +239,93 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kMinWaves
 }
 
 // ------------------------------------------------------ EXACT, wave-parallel
-// One 64-lane wave per tile; see pbrt_spec.h for why this is the same
-// computation as k_render_exact. Per pixel:
-//   1. StartPixel: the ~ndims*2*spp draws are computed lane-parallel by PCG
-//      jump-ahead (assuming pcg_bounded never rejects, checked; on a
-//      rejection lane 0 replays StartPixel serially), then one lane per dim
-//      runs the Fisher-Yates swaps.
-//   2. Bounce 1: camera ray, first hit and BSDF (wave-uniform); lane l
-//      computes EstimateDirect for light l with uLight = (0,0).
-//   3. Chain: trajectories at offsets head + 2j (j = lane) give D per offset;
-//      lane 0 walks head -> head + D -> ... to assign each sample its offset.
-//   4. Samples 1..spp-1 run as full paths, one per lane (batches of 64), and
-//      are added to the tile film (LDS) in sample order.
-struct SpecLayout {   // byte offsets into the dynamic LDS block
-    int film, s1d, other, memb, lbuf, sbuf, dbuf, pbuf, vbuf, total;
+// Three kernels replace the serial tile replay (see pbrt_spec.h for why the
+// results are the same bits):
+//   k_chain  one 64-lane wave per tile. Per pixel: StartPixel (lane-parallel,
+//            with pcg_bounded rejections resolved), bounce 1 (camera ray,
+//            first hit, BSDF), then windows of speculative trajectories at
+//            RNG offsets head + 2j until every sample's offset is known.
+//            Writes a PixelRec, the stratified 1D values and the RNG state of
+//            each sample. The only serial dependency of the reference (the
+//            per-tile PCG32 stream) lives here, and only trajectories run here.
+//   k_paths  one wave per pixel: bounce-1 EstimateDirect per light (lane l ->
+//            light l), then the pixel's samples as full paths, one per lane.
+//            Writes L per sample and the pixel's first panic.
+//   k_film   one thread per tile-film pixel: FilmTile.AddSample contributions
+//            summed in the reference's order (pixels row-major, samples in
+//            order), i.e. the same floating-point sums as the serial replay.
+struct PixelRec {
+    SI si;
+    BSDF b;
+    V3 wo;
+    int32_t hit;      // first hit exists and maxDepth > 1
+    int32_t nvalid;   // samples 1 .. nvalid-1 have offsets (spp unless a panic cut the chain)
+    int32_t panic0;   // the camera ray's traversal panics (kind), else 0
+    int32_t pad;
+};
+struct WaveBufs {
+    PixelRec* prec;     // [slot][ppt]
+    double* s1d;        // [slot][ppt][ndims * spp]
+    uint64_t* memb;     // [slot][ppt][spp]   PCG32 state at sample k's offset
+    double* L;          // [slot][ppt][spp][3]
+    PanicRec* ppanic;   // [slot][ppt]        first panic of the pixel in sample order
+    int32_t* tile_npx;  // [slot]             pixels with records (a panic ends the tile)
+    int64_t ppt;        // pixel records per tile slot (tile_size^2)
+    int64_t s1d_stride; // ndims * spp
+};
+struct ChainLayout {   // byte offsets into k_chain's dynamic LDS block
+    int s1d, other, sbuf, dbuf, vbuf, total;
 };
 constexpr uint32_t kBadD = 0xFFFFFFFFu;
 
 __device__ __forceinline__ double pcg_float_of(uint32_t v) {
     return gomath::min(gomath::kOneMinusEpsilon, (double)v * 2.3283064365386963e-10);
 }
-
-// Bounce 1 of a pixel (camera ray, first hit, BSDF; EstimateDirect per light
-// with uLight = (0,0), lane l computing light l) into the LDS cache. Returns
-// 1 = hit, 0 = no traced bounce, or kind - 1000 (< 0) when the first hit
-// panics (kind = PBRT_PANIC_* or -1 for an unsupported material). Out of line:
-// it runs once per pixel.
-__device__ __noinline__ int pixel_setup(DevScene sc, const RenderParams& rp, const pbrt_camera_desc& cam, int64_t px,
-                                        int64_t py, double time_u, PixelCache* pc, uint16_t* stack, int lane) {
-    Ray ray = camera_ray(cam, (double)px + 0.0, (double)py + 0.0, time_u, V2{0.0, 0.0});
-    int panic0 = 0;
-    SI si0;
-    BSDF b0;
-    b0.n_bxdfs = 0;
-    int hit0 = 0;
-    if (1 < rp.max_depth) {
-        hit0 = bvh_traverse<false>(sc, ray, &si0, stack, panic0) ? 1 : 0;
-        if (!panic0 && hit0 && compute_bsdf(sc, si0, b0) < 0) panic0 = -1;
-    }
-    if (panic0) return panic0 - 1000;
-    if (lane == 0) {
-        pc->si = si0;
-        pc->b = b0;
-        pc->wo = ray.d;
-        pc->hit = hit0;
-    }
-    if (hit0 && b0.n_bxdfs > 0 && lane < sc.n_lights) {
-        int pl = 0;
-        Spec ld = estimate_direct(sc, stack, pl, si0, b0, lane, V2{0.0, 0.0});
-        if (!pl && max_component(ld) > 10) pl = PBRT_PANIC_LD_GT_10;
-        pc->ld[lane] = ld;
-        pc->ld_panic[lane] = pl;
-    }
-    return hit0;
+__device__ __forceinline__ int64_t tile_of_slot(const RenderParams& rp, int64_t slot) {
+    return rp.tile_begin + slot * rp.tile_stride;
 }
 
+// k_chain runs G = 64 / L tiles per wave: lane group g (L lanes) owns tile
+// slot blockIdx.x * G + g and speculates with L candidate offsets per window
+// (fewer lanes per tile = less speculation waste; more tiles per wave keeps
+// every SIMD busy with ~one wave). Per iteration: (1) groups that need a new
+// pixel run StartPixel and bounce 1 one at a time, with all 64 lanes; (2) one
+// trajectory window for every group; (3) each group leader walks its chain.
+struct GroupState {
+    uint64_t S;     // PCG32 state at the group's chain head
+    int64_t pi;     // current pixel (row-major index in the tile)
+    int64_t npx;    // pixels of the tile
+    int kh;         // next sample without an offset
+    int phase;      // 0 needs a pixel, 1 resolving offsets, 2 tile finished
+    int stop;       // a reference panic ended the tile
+    int pad;
+};
+constexpr int kMaxGroups = 16;
+
 template <int kWaves>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8))) void k_render_spec(DevScene sc, RenderParams rp, SpecLayout lay,
-                                                       const PcgJump* __restrict__ jump,
-                                                       double* __restrict__ films, PanicRec* __restrict__ panics,
-                                                       Counters* __restrict__ ctr) {
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8))) void k_chain(
+    DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
+    int64_t nslots_batch, int lanes_per_tile, Counters* __restrict__ ctr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ uint16_t stack_lds[64 * kStackStride];
-    __shared__ PixelCache pc;
+    __shared__ ChainCache pcs[kMaxGroups];
+    __shared__ GroupState gs[kMaxGroups];
     __shared__ uint64_t sh_state;
-    __shared__ int sh_k, sh_flag, sh_trunc, sh_stop, sh_tkind, sh_tbounce;
     const int lane = threadIdx.x;
-    const int64_t slot = blockIdx.x;
-    const int64_t tile = rp.tile_begin + slot * rp.tile_stride;
-    const pbrt_film_desc& film = *sc.film;
+    const int L = lanes_per_tile, G = kWave / L;
+    const int g = lane / L, gl = lane - g * L;
     const PcgJump& J = *jump;
-    double* film_l = (double*)(lds + lay.film);
-    double* s1d = (double*)(lds + lay.s1d);
+    double* s1d = (double*)(lds + lay.s1d);            // StartPixel staging (one group at a time)
     uint16_t* other = (uint16_t*)(lds + lay.other);
-    uint64_t* memb = (uint64_t*)(lds + lay.memb);
-    double* lbuf = (double*)(lds + lay.lbuf);
     uint64_t* sbuf = (uint64_t*)(lds + lay.sbuf);
     uint32_t* dbuf = (uint32_t*)(lds + lay.dbuf);
-    int* pbuf = (int*)(lds + lay.pbuf);
     uint32_t* vbuf = (uint32_t*)(lds + lay.vbuf);
     uint16_t* stack = stack_lds + lane;
-
-    int64_t x0, y0, x1, y1, px0, py0, px1, py1;
-    tile_bounds(rp, tile, x0, y0, x1, y1);
-    film_tile_bounds(film, x0, y0, x1, y1, px0, py0, px1, py1);
-    const int64_t npx = (px1 - px0) * (py1 - py0);
-    for (int64_t i = lane; i < npx * 3; i += kWave) film_l[i] = 0.0;
-
-    const int n = rp.spp, ndims = rp.ndims, nl = sc.n_lights;
+    const int n = rp.spp, ndims = rp.ndims;
     const double inv_n = 1.0 / (double)n;
     const int s1 = rp.jitter ? 2 * n : n, s2 = rp.jitter ? 3 * n : n;   // StartPixel draws per 1D / 2D dim
-    Pcg seed;
-    pcg_seed(seed, (uint64_t)tile);   // Sampler.Clone(seed = tile index), integrator.go:318,328
-    const uint64_t inc = seed.inc;
-    uint64_t S = seed.state;
-    const SpecSampler ss{s1d, n, ndims};
     const pbrt_camera_desc& cam = *sc.camera;
-    unsigned long long paths = 0, windows = 0;
+    unsigned long long windows = 0;
     unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     long long tprev = clock64();
     auto mark = [&](int i) {
@@ -343,243 +333,396 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8
         ph[i] += (unsigned long long)(now - tprev);
         tprev = now;
     };
+    if (lane < G) {
+        const int64_t bs = (int64_t)blockIdx.x * G + lane;
+        GroupState& s = gs[lane];
+        s.pi = 0;
+        s.kh = 1;
+        s.stop = 0;
+        if (bs < nslots_batch) {
+            int64_t x0, y0, x1, y1;
+            tile_bounds(rp, tile_of_slot(rp, slot_base + bs), x0, y0, x1, y1);
+            Pcg seed;
+            pcg_seed(seed, (uint64_t)tile_of_slot(rp, slot_base + bs));   // Sampler.Clone(tile), integrator.go:318,328
+            s.S = seed.state;
+            s.npx = (x1 - x0) * (y1 - y0);
+            s.phase = s.npx > 0 ? 0 : 2;
+        } else {
+            s.S = 0;
+            s.npx = 0;
+            s.phase = 2;
+        }
+        if (bs < nslots_batch) wb.tile_npx[bs] = 0;
+    }
     __syncthreads();
 
-    for (int64_t py = y0; py < y1; py++) {
-        for (int64_t px = x0; px < x1; px++) {
-            // ---- 1. StartPixel (stratified.go:21-48)
-            // The pixel's draws form a fixed list of E events (jitter floats and
-            // pcg_bounded shuffle picks, sampling.go:101-145). A bounded pick
-            // retries on v < 2^32 mod b, which the reference's (rot+1)&31 output
-            // rotation makes common (v < 4 has probability ~1/64), so event e
-            // lands on draw e + R(e), R(e) = rejections before it. Lanes fill
-            // the raw stream by jump-ahead, then resolve R chunk by chunk: one
-            // ballot per rejection shifts every later event by one draw.
-            bool serial_sp = rp.sp_serial != 0;
-            if (!serial_sp) {
-                const int E = rp.sp_events, V = rp.sp_draws;
-                uint64_t st = pcg_advance(J, S, inc, (uint64_t)lane);
-                for (int t = lane; t < V; t += kWave) {
-                    vbuf[t] = pcg_output(st);
-                    st = J.a[6] * st + inc * J.b[6];   // +64 draws
-                }
-                __syncthreads();
-                mark(5);
-                int R = 0;
-                bool overflow = false;
-                for (int cb = 0; cb < E; cb += kWave) {
-                    const int e = cb + lane;
-                    int kind = 0, slot = 0, i = 0;   // kind 0 none, 1 1D float, 2 1D pick, 3 2D pick
-                    if (e < E) {
-                        if (e < ndims * s1) {
-                            const int d = e / s1, q = e - d * s1;
-                            if (rp.jitter && q < n) { kind = 1; slot = d * n + q; }
-                            else { kind = 2; i = q - (rp.jitter ? n : 0); slot = d * n + i; }
-                        } else {
-                            const int e2 = e - ndims * s1, d = e2 / s2, q = e2 - d * s2;
-                            if (!(rp.jitter && q < 2 * n)) { kind = 3; i = q - (rp.jitter ? 2 * n : 0); }
-                        }
-                    }
-                    const uint32_t b = (uint32_t)(n - i);
-                    const uint32_t thr = kind >= 2 ? (~b + 1u) % b : 0u;
-                    int local = 0;
-                    for (;;) {
-                        const int t = e + R + local;
-                        const bool out = kind != 0 && t >= V;
-                        const bool bad = !out && kind >= 2 && vbuf[t] < thr;
-                        if (__any(out)) { overflow = true; break; }
-                        const unsigned long long m = __ballot(bad);
-                        if (m == 0) break;
-                        const int first = __ffsll((long long)m) - 1;
-                        if (lane >= first) local++;
-                    }
-                    if (overflow) break;
-                    const uint32_t v = kind != 0 ? vbuf[e + R + local] : 0u;
-                    if (kind == 1)
-                        s1d[slot] = gomath::min(((double)(slot % n) + pcg_float_of(v)) * inv_n, gomath::kOneMinusEpsilon);
-                    else if (kind == 2)
-                        other[slot] = (uint16_t)(i + (int)(v % b));
-                    R += __shfl(local, kWave - 1);
-                }
-                serial_sp = overflow;
+    for (;;) {
+        // ---- (1) groups that need a pixel: StartPixel + bounce 1, one group at a time
+        for (int q = 0; q < G; q++) {
+            while (gs[q].phase == 0) {
+                const int64_t bs = (int64_t)blockIdx.x * G + q;
+                const int64_t tile = tile_of_slot(rp, slot_base + bs);
+                Pcg seed;
+                pcg_seed(seed, (uint64_t)tile);
+                const uint64_t inc = seed.inc;
+                const uint64_t S = gs[q].S;
+                const int64_t pi = gs[q].pi;
+                const int64_t rec = bs * wb.ppt + pi;
+                int64_t x0, y0, x1, y1;
+                tile_bounds(rp, tile, x0, y0, x1, y1);
+                const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
+                // StartPixel (stratified.go:21-48). The pixel's draws form a fixed
+                // list of E events (jitter floats and pcg_bounded picks,
+                // sampling.go:101-145). A pick retries on v < 2^32 mod b, which
+                // the reference's (rot+1)&31 output rotation makes common (v < 4
+                // has probability ~1/64), so event e lands on draw e + R(e),
+                // R(e) = rejections before it. Lanes fill the raw stream by
+                // jump-ahead, then resolve R chunk by chunk: one ballot per
+                // rejection shifts every later event by one draw.
+                bool serial_sp = rp.sp_serial != 0;
                 if (!serial_sp) {
-                    if (!rp.jitter)
-                        for (int idx = lane; idx < ndims * n; idx += kWave)
-                            s1d[idx] = gomath::min(((double)(idx % n) + 0.5) * inv_n, gomath::kOneMinusEpsilon);
-                    __syncthreads();
-                    if (lane < ndims) {
-                        double* samp = s1d + lane * n;
-                        const uint16_t* oth = other + lane * n;
-                        for (int k = 0; k < n; k++) {
-                            const int o = oth[k];
-                            double a = samp[k];
-                            samp[k] = samp[o];
-                            samp[o] = a;
-                        }
-                    }
-                    if (lane == 0) sh_state = pcg_advance(J, S, inc, (uint64_t)(E + R));
-                }
-            }
-            if (serial_sp || (rp.flags & PBRT_FLAG_SERIAL_START_PIXEL)) {
-                ph[7]++;
-                if (lane == 0) {   // serial replay (huge sample counts, or forced)
-                    Thread t;
-                    t.rng.state = S;
-                    t.rng.inc = inc;
-                    t.spp = n; t.ndims = ndims; t.xs = rp.xs; t.ys = rp.ys; t.jitter = rp.jitter;
-                    t.s1d = s1d;
-                    start_pixel(t);
-                    sh_state = t.rng.state;
-                }
-            }
-            __syncthreads();
-            S = sh_state;
-            mark(0);
-            if (n <= 1) continue;   // sample 0 is never traced (#2)
-
-            // ---- 2. bounce 1, shared by every sample of the pixel
-            const int hit0 = pixel_setup(sc, rp, cam, px, py, s1d[1 < n ? 1 : 0], &pc, stack, lane);
-            if (hit0 < 0) {   // the first traced sample panics at bounce 1
-                if (lane == 0) {
-                    PanicRec pr{hit0 + 1000, 1, 1, 0, px, py};
-                    panics[slot] = pr;
-                    atomicExch(&ctr->any_panic, 1);
-                }
-                return;
-            }
-            if (lane == 0) {
-                sh_trunc = 0;
-                sh_stop = 0;
-            }
-            __syncthreads();
-            mark(1);
-            // ---- 3. offsets of samples 1..n-1 (chain through speculative trajectories)
-            int kend = n;
-            if (hit0) {
-                uint64_t Sh = S;
-                int kh = 1;
-                while (kh < n) {
-                    const uint64_t st = pcg_advance(J, Sh, inc, 2 * (uint64_t)lane);
-                    Cursor c;
-                    c.rng.state = st;
-                    c.rng.inc = inc;
-                    c.draws = 0;
-                    c.cur1d = 1;   // camera: Get2D pFilm, Get2D pLens, Get1D time (stratified)
-                    c.cur2d = 2;
-                    c.k = lane == 0 ? kh : -1;
-                    c.kdep = 0;
-                    int pnc = 0, bnc = 0;
-                    (void)spec_path(sc, pc, ss, c, rp.max_depth, rp.rr_threshold, stack, pnc, bnc, false);
-                    windows++;
-                    sbuf[lane] = st;
-                    dbuf[lane] = (pnc || c.kdep) ? kBadD : c.draws;
-                    __syncthreads();
-                    mark(2);
-                    if (lane == 0) {
-                        uint64_t x = 0;
-                        int k = kh;
-                        while (k < n) {
-                            if ((x & 1) || (x >> 1) >= (uint64_t)kWave) break;
-                            const uint32_t d = dbuf[x >> 1];
-                            if (d == kBadD) break;
-                            memb[k++] = sbuf[x >> 1];
-                            x += d;
-                        }
-                        if (k == kh) {   // the exact head itself panicked
-                            memb[kh] = Sh;
-                            sh_trunc = kh;
-                            sh_tkind = pnc;
-                            sh_tbounce = bnc;
-                        }
-                        sh_k = k;
-                        sh_state = pcg_advance(J, Sh, inc, x);
+                    const int E = rp.sp_events, V = rp.sp_draws;
+                    uint64_t st = pcg_advance(J, S, inc, (uint64_t)lane);
+                    for (int t = lane; t < V; t += kWave) {
+                        vbuf[t] = pcg_output(st);
+                        st = J.a[6] * st + inc * J.b[6];   // +64 draws
                     }
                     __syncthreads();
-                    kh = sh_k;
-                    Sh = sh_state;
-                    mark(6);
-                    if (sh_trunc) break;
-                }
-                S = Sh;
-                if (sh_trunc) kend = sh_trunc + 1;
-            }
-
-            mark(2);
-            // ---- 4. full paths, one sample per lane, added in sample order
-            const double fx = (double)px + 0.0, fy = (double)py + 0.0;
-            Footprint fp;
-            int64_t p0x, p0y, p1x, p1y;
-            footprint(film, fx, fy, px0, py0, px1, py1, fp, p0x, p0y, p1x, p1y);
-            for (int kb = 1; kb < kend; kb += kWave) {
-                const int k = kb + lane;
-                Spec L = spec(0);
-                int pnc = 0, bnc = 0;
-                if (k < kend && hit0) {
-                    Cursor c;
-                    c.rng.state = memb[k];
-                    c.rng.inc = inc;
-                    c.draws = 0;
-                    c.cur1d = 1;
-                    c.cur2d = 2;
-                    c.k = k;
-                    c.kdep = 0;
-                    L = spec_path(sc, pc, ss, c, rp.max_depth, rp.rr_threshold, stack, pnc, bnc, true);
-                }
-                lbuf[lane * 3 + 0] = L.r;
-                lbuf[lane * 3 + 1] = L.g;
-                lbuf[lane * 3 + 2] = L.b;
-                pbuf[lane * 2 + 0] = (k < kend) ? pnc : 0;
-                pbuf[lane * 2 + 1] = bnc;
-                __syncthreads();
-                if (lane == 0) {
-                    for (int m = 0; m < kWave && kb + m < kend; m++) {
-                        if (pbuf[m * 2]) {
-                            PanicRec pr{pbuf[m * 2], kb + m, pbuf[m * 2 + 1], 0, px, py};
-                            panics[slot] = pr;
-                            atomicExch(&ctr->any_panic, 1);
-                            sh_stop = 1;
-                            break;
+                    int R = 0;
+                    bool overflow = false;
+                    for (int cb = 0; cb < E; cb += kWave) {
+                        const int e = cb + lane;
+                        int kind = 0, slt = 0, i = 0;   // 0 none, 1 1D float, 2 1D pick, 3 2D pick
+                        if (e < E) {
+                            if (e < ndims * s1) {
+                                const int d = e / s1, qq = e - d * s1;
+                                if (rp.jitter && qq < n) { kind = 1; slt = d * n + qq; }
+                                else { kind = 2; i = qq - (rp.jitter ? n : 0); slt = d * n + i; }
+                            } else {
+                                const int e2 = e - ndims * s1, d = e2 / s2, qq = e2 - d * s2;
+                                if (!(rp.jitter && qq < 2 * n)) { kind = 3; i = qq - (rp.jitter ? 2 * n : 0); }
+                            }
                         }
+                        const uint32_t b = (uint32_t)(n - i);
+                        const uint32_t thr = kind >= 2 ? (~b + 1u) % b : 0u;
+                        int local = 0;
+                        for (;;) {
+                            const int t = e + R + local;
+                            const bool out = kind != 0 && t >= V;
+                            const bool bad = !out && kind >= 2 && vbuf[t] < thr;
+                            if (__any(out)) { overflow = true; break; }
+                            const unsigned long long m = __ballot(bad);
+                            if (m == 0) break;
+                            const int first = __ffsll((long long)m) - 1;
+                            if (lane >= first) local++;
+                        }
+                        if (overflow) break;
+                        const uint32_t v = kind != 0 ? vbuf[e + R + local] : 0u;
+                        if (kind == 1)
+                            s1d[slt] = gomath::min(((double)(slt % n) + pcg_float_of(v)) * inv_n, gomath::kOneMinusEpsilon);
+                        else if (kind == 2)
+                            other[slt] = (uint16_t)(i + (int)(v % b));
+                        R += __shfl(local, kWave - 1);
+                    }
+                    serial_sp = overflow;
+                    if (!serial_sp) {
+                        if (!rp.jitter)
+                            for (int idx = lane; idx < ndims * n; idx += kWave)
+                                s1d[idx] = gomath::min(((double)(idx % n) + 0.5) * inv_n, gomath::kOneMinusEpsilon);
+                        __syncthreads();
+                        if (lane < ndims) {
+                            double* samp = s1d + lane * n;
+                            const uint16_t* oth = other + lane * n;
+                            for (int k = 0; k < n; k++) {
+                                const int o = oth[k];
+                                double a = samp[k];
+                                samp[k] = samp[o];
+                                samp[o] = a;
+                            }
+                        }
+                        if (lane == 0) sh_state = pcg_advance(J, S, inc, (uint64_t)(E + R));
+                    }
+                }
+                if (serial_sp || (rp.flags & PBRT_FLAG_SERIAL_START_PIXEL)) {
+                    if (lane == 0) {   // serial replay (huge sample counts, or forced)
+                        Thread t;
+                        t.rng.state = S;
+                        t.rng.inc = inc;
+                        t.spp = n; t.ndims = ndims; t.xs = rp.xs; t.ys = rp.ys; t.jitter = rp.jitter;
+                        t.s1d = s1d;
+                        start_pixel(t);
+                        sh_state = t.rng.state;
                     }
                 }
                 __syncthreads();
-                if (sh_stop) return;
-                mark(3);
-                const int kn = (kend - kb < kWave) ? kend - kb : kWave;
-                if (lane < fp.n * 3) {
-                    const int f = lane / 3, ch = lane - f * 3;
-                    const double w = fp.w[f];
-                    double acc = film_l[fp.off[f] * 3 + ch];
-                    for (int m = 0; m < kn; m++) {
-                        Spec Ls{lbuf[m * 3 + 0], lbuf[m * 3 + 1], lbuf[m * 3 + 2]};
-                        if (has_nans(Ls)) Ls = spec(0.1);   // integrator.go:256-262
-                        if (0.0 > film.max_sample_luminance) Ls = smuls(Ls, film.max_sample_luminance / 0.0);
-                        const double v = ch == 0 ? Ls.r : (ch == 1 ? Ls.g : Ls.b);
-                        acc += v * w;
+                const uint64_t S1 = sh_state;   // after StartPixel
+                double* gs1d = wb.s1d + rec * wb.s1d_stride;
+                for (int idx = lane; idx < ndims * n; idx += kWave) gs1d[idx] = s1d[idx];
+                mark(0);
+                PixelRec& pr = wb.prec[rec];
+                // bounce 1, shared by every sample of the pixel
+                int panic0 = 0, hit0 = 0;
+                SI si0;
+                BSDF b0;
+                b0.n_bxdfs = 0;
+                Ray ray = camera_ray(cam, (double)px + 0.0, (double)py + 0.0, s1d[1 < n ? 1 : 0], V2{0.0, 0.0});
+                if (n > 1 && 1 < rp.max_depth) {
+                    hit0 = bvh_traverse<false>(sc, ray, &si0, stack, panic0) ? 1 : 0;
+                    if (!panic0 && hit0 && compute_bsdf(sc, si0, b0) < 0) panic0 = -1;
+                }
+                if (lane == 0) {
+                    pcs[q].si = si0;
+                    pcs[q].b = b0;
+                    pcs[q].wo = ray.d;
+                    pcs[q].hit = hit0;
+                    pr.si = si0;
+                    pr.b = b0;
+                    pr.wo = ray.d;
+                    pr.hit = panic0 ? 0 : hit0;
+                    pr.panic0 = panic0;
+                    pr.nvalid = n;
+                    GroupState& s = gs[q];
+                    s.S = S1;
+                    wb.tile_npx[bs] = (int32_t)(pi + 1);
+                    if (panic0) {   // the first traced sample panics at bounce 1: the tile ends here
+                        s.stop = 1;
+                        s.phase = 2;
+                    } else if (hit0) {
+                        s.kh = 1;
+                        s.phase = 1;
+                    } else {   // no traced bounce: every sample is black and draws nothing
+                        s.pi = pi + 1;
+                        s.phase = s.pi < s.npx ? 0 : 2;
                     }
-                    film_l[fp.off[f] * 3 + ch] = acc;
                 }
                 __syncthreads();
-                mark(4);
+                mark(1);
             }
-            if (sh_trunc) {   // head panicked in the trajectory but no full path did: report it
-                if (lane == 0) {
-                    PanicRec pr{sh_tkind, sh_trunc, sh_tbounce, 0, px, py};
-                    panics[slot] = pr;
-                    atomicExch(&ctr->any_panic, 1);
-                }
-                return;
-            }
-            paths += (unsigned long long)(n - 1);
         }
+        bool any_chain = false;
+        for (int q = 0; q < G; q++) any_chain |= gs[q].phase == 1;
+        if (!any_chain) break;
+
+        // ---- (2) one window of speculative trajectories per resolving group
+        const GroupState sg = gs[g];
+        const int64_t bs = (int64_t)blockIdx.x * G + g;
+        const int64_t rec = bs * wb.ppt + sg.pi;
+        uint64_t st = 0;
+        uint32_t dres = kBadD;
+        if (sg.phase == 1) {
+            Pcg seed;
+            pcg_seed(seed, (uint64_t)tile_of_slot(rp, slot_base + bs));
+            st = pcg_advance(J, sg.S, seed.inc, 2 * (uint64_t)gl);
+            Cursor c;
+            c.rng.state = st;
+            c.rng.inc = seed.inc;
+            c.draws = 0;
+            c.cur1d = 1;   // camera: Get2D pFilm, Get2D pLens, Get1D time (stratified)
+            c.cur2d = 2;
+            c.k = gl == 0 ? sg.kh : -1;
+            c.kdep = 0;
+            const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, n, ndims};
+            int pnc = 0, bnc = 0;
+            (void)spec_path<false>(sc, pcs[g], ss, c, rp.max_depth, rp.rr_threshold, stack, pnc, bnc);
+            dres = (pnc || c.kdep) ? kBadD : c.draws;
+        }
+        sbuf[lane] = st;
+        dbuf[lane] = dres;
+        windows++;
+        __syncthreads();
+        mark(2);
+        // ---- (3) each group leader walks its chain through the window
+        if (gl == 0 && sg.phase == 1) {
+            Pcg seed;
+            pcg_seed(seed, (uint64_t)tile_of_slot(rp, slot_base + bs));
+            uint64_t x = 0;
+            int k = sg.kh;
+            while (k < n) {
+                if ((x & 1) || (x >> 1) >= (uint64_t)L) break;
+                const uint32_t d = dbuf[lane + (int)(x >> 1)];
+                if (d == kBadD) break;
+                wb.memb[rec * n + k] = sbuf[lane + (int)(x >> 1)];
+                k++;
+                x += d;
+            }
+            GroupState& s = gs[g];
+            if (k == sg.kh) {   // the exact head's trajectory panics: the tile ends at this sample
+                wb.memb[rec * n + k] = sg.S;
+                wb.prec[rec].nvalid = k + 1;
+                s.stop = 1;
+                s.phase = 2;
+            } else {
+                s.kh = k;
+                s.S = pcg_advance(J, sg.S, seed.inc, x);
+                if (k >= n) {   // every sample of the pixel has its offset
+                    s.pi = sg.pi + 1;
+                    s.phase = s.pi < s.npx ? 0 : 2;
+                }
+            }
+        }
+        __syncthreads();
+        mark(3);
     }
-    double* tf = films + slot * (rp.slot_w * rp.slot_h * 3);
-    for (int64_t i = lane; i < npx * 3; i += kWave) tf[i] = film_l[i];
     if (lane == 0) {
-        atomicAdd(&ctr->paths, paths);
-        atomicAdd(&ctr->camera_samples, paths);
         atomicAdd(&ctr->windows, windows);
         for (int i = 0; i < 8; i++) atomicAdd(&ctr->phase[i], ph[i]);
+    }
+}
+
+// One wave per pixel record: the pixel's samples as full paths.
+__global__ __launch_bounds__(kWave) void k_paths(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
+                                                 Counters* __restrict__ ctr) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ uint16_t stack_lds[64 * kStackStride];
+    __shared__ PixelCache pc;
+    __shared__ unsigned long long sh_pkey;   // (sample << 32) | (bounce << 8) | (kind + 1): min = first panic
+    const int lane = threadIdx.x;
+    const int64_t bslot = blockIdx.x / wb.ppt, pi = blockIdx.x % wb.ppt;
+    if (pi >= wb.tile_npx[bslot]) return;
+    const int64_t rec = blockIdx.x;
+    const int64_t tile = tile_of_slot(rp, slot_base + bslot);
+    int64_t x0, y0, x1, y1;
+    tile_bounds(rp, tile, x0, y0, x1, y1);
+    const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
+    const int n = rp.spp, ndims = rp.ndims;
+    double* s1d = (double*)lds;
+    uint16_t* stack = stack_lds + lane;
+    const PixelRec& pr = wb.prec[rec];
+    for (int idx = lane; idx < ndims * n; idx += kWave) s1d[idx] = wb.s1d[rec * wb.s1d_stride + idx];
+    const int hit = pr.hit, nvalid = pr.nvalid;
+    Pcg seed;
+    pcg_seed(seed, (uint64_t)tile);
+    const uint64_t inc = seed.inc;
+    if (lane == 0) {
+        pc.si = pr.si;
+        pc.b = pr.b;
+        pc.wo = pr.wo;
+        pc.hit = hit;
+        sh_pkey = ~0ULL;
+    }
+    const SI si0 = pr.si;
+    const BSDF b0 = pr.b;
+    if (hit && b0.n_bxdfs > 0 && lane < sc.n_lights) {   // bounce-1 light samples, uLight = (0,0)
+        int pl = 0;
+        Spec ld = estimate_direct(sc, stack, pl, si0, b0, lane, V2{0.0, 0.0});
+        if (!pl && max_component(ld) > 10) pl = PBRT_PANIC_LD_GT_10;
+        pc.ld[lane] = ld;
+        pc.ld_panic[lane] = pl;
+    }
+    __syncthreads();
+    const SpecSampler ss{s1d, n, ndims};
+    for (int kb = 1; kb < nvalid; kb += kWave) {
+        const int k = kb + lane;
+        Spec L = spec(0);
+        if (k < nvalid && hit) {
+            Cursor c;
+            c.rng.state = wb.memb[rec * n + k];
+            c.rng.inc = inc;
+            c.draws = 0;
+            c.cur1d = 1;   // camera: Get2D pFilm, Get2D pLens, Get1D time (stratified)
+            c.cur2d = 2;
+            c.k = k;
+            c.kdep = 0;
+            int pnc = 0, bnc = 0;
+            L = spec_path<true>(sc, pc, ss, c, rp.max_depth, rp.rr_threshold, stack, pnc, bnc);
+            if (pnc)
+                atomicMin(&sh_pkey, ((unsigned long long)k << 32) | ((unsigned long long)(bnc & 0xFFFFFF) << 8) |
+                                        (unsigned long long)((pnc + 1) & 0xFF));
+        }
+        if (k < n) {
+            double* o = wb.L + (rec * n + k) * 3;
+            o[0] = L.r;
+            o[1] = L.g;
+            o[2] = L.b;
+        }
+    }
+    __syncthreads();
+    if (lane == 0) {
+        PanicRec p{0, 0, 0, 0, px, py};
+        if (pr.panic0) {
+            p.kind = pr.panic0;
+            p.sample = 1;
+            p.bounce = 1;
+        } else if (sh_pkey != ~0ULL) {
+            p.kind = (int)(sh_pkey & 0xFF) - 1;
+            p.bounce = (int)((sh_pkey >> 8) & 0xFFFFFF);
+            p.sample = (int)(sh_pkey >> 32);
+        }
+        wb.ppanic[rec] = p;
+        if (!p.kind && nvalid > 1) {
+            atomicAdd(&ctr->paths, (unsigned long long)(nvalid - 1));
+            atomicAdd(&ctr->camera_samples, (unsigned long long)(nvalid - 1));
+        }
+    }
+}
+
+// One thread per tile-film pixel: the tile film of the serial replay.
+__global__ __launch_bounds__(256) void k_film(const pbrt_film_desc* __restrict__ film_desc, RenderParams rp,
+                                              WaveBufs wb, int64_t slot_base, int64_t nslots_batch,
+                                              double* __restrict__ films) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per = rp.slot_w * rp.slot_h;
+    if (gid >= nslots_batch * per) return;
+    const int64_t bslot = gid / per, fi = gid % per;
+    const int64_t slot = slot_base + bslot;
+    const pbrt_film_desc& film = *film_desc;
+    int64_t x0, y0, x1, y1, px0, py0, px1, py1;
+    tile_bounds(rp, tile_of_slot(rp, slot), x0, y0, x1, y1);
+    film_tile_bounds(film, x0, y0, x1, y1, px0, py0, px1, py1);
+    const int64_t tw = px1 - px0;
+    if (fi >= tw * (py1 - py0)) return;
+    const int64_t fx = px0 + fi % tw, fy = py0 + fi / tw;
+    const int n = rp.spp;
+    const int64_t npx = wb.tile_npx[bslot];
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+    // pixels whose footprint can reach (fx, fy): |p - f| < radius + 1, in row-major order
+    for (int64_t py = fy - 2; py <= fy + 2; py++) {
+        if (py < y0 || py >= y1) continue;
+        for (int64_t px = fx - 2; px <= fx + 2; px++) {
+            if (px < x0 || px >= x1) continue;
+            const int64_t pi = (py - y0) * (x1 - x0) + (px - x0);
+            if (pi >= npx) continue;
+            Footprint fp;
+            int64_t p0x, p0y, p1x, p1y;
+            footprint(film, (double)px + 0.0, (double)py + 0.0, px0, py0, px1, py1, fp, p0x, p0y, p1x, p1y);
+            const int64_t want = fi;
+            int f = -1;
+            for (int q = 0; q < fp.n; q++)
+                if (fp.off[q] == want) f = q;
+            if (f < 0) continue;
+            const double w = fp.w[f];
+            const int64_t rec = bslot * wb.ppt + pi;
+            const int nv = wb.prec[rec].nvalid;
+            const double* Lp = wb.L + rec * n * 3;
+            for (int k = 1; k < nv; k++) {
+                Spec Ls{Lp[k * 3 + 0], Lp[k * 3 + 1], Lp[k * 3 + 2]};
+                if (has_nans(Ls)) Ls = spec(0.1);   // integrator.go:256-262
+                if (0.0 > film.max_sample_luminance) Ls = smuls(Ls, film.max_sample_luminance / 0.0);
+                a0 += Ls.r * w;
+                a1 += Ls.g * w;
+                a2 += Ls.b * w;
+            }
+        }
+    }
+    double* tf = films + slot * per * 3 + fi * 3;
+    tf[0] = a0;
+    tf[1] = a1;
+    tf[2] = a2;
+}
+
+// First panic of each tile slot in pixel order -> panics[slot].
+__global__ void k_panic_reduce(WaveBufs wb, int64_t slot_base, int64_t nslots_batch, PanicRec* __restrict__ panics,
+                               Counters* __restrict__ ctr) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nslots_batch) return;
+    const int npx = wb.tile_npx[b];
+    for (int p = 0; p < npx; p++) {
+        const PanicRec& r = wb.ppanic[b * wb.ppt + p];
+        if (r.kind) {
+            panics[slot_base + b] = r;
+            atomicExch(&ctr->any_panic, 1);
+            return;
+        }
     }
 }
 
@@ -657,18 +800,26 @@ struct pbrt_gpu_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     double* film_target = nullptr;   // caller buffer of the last render_async_into
     int lanes_per_wave = 64;
+    bool lanes_per_wave_set = false;
     int min_waves = 1;      // amdgpu_waves_per_eu variant of k_render_exact
     int kernel_req = PBRT_KERNEL_AUTO;
     int last_kernel = 0;    // PBRT_KERNEL_SERIAL / PBRT_KERNEL_WAVE
     PcgJump* d_jump = nullptr;
     pbrt_distribution_desc host_dist;
-    SpecLayout lay{};
+    // wave-parallel EXACT path (k_chain / k_paths / k_film)
+    ChainLayout lay{};
     bool use_spec = false;
+    unsigned char* d_wave = nullptr;   // per-batch pixel records, stratified values, RNG states, L
+    size_t wave_cap = 0;
+    int64_t wave_batch = 0;            // tile slots per batch
+    int tiles_per_wave = 1;            // k_chain lane groups per wave (64 / lanes per tile)
+    int n_simd = 1024;                 // SIMDs of the device (4 per CU)
+    WaveBufs wb{};
     // device scene
     pbrt_shape_desc* d_shapes = nullptr;
     pbrt_material_desc* d_materials = nullptr;
     pbrt_primitive_desc* d_prims = nullptr;
-    pbrt_bvh_node* d_nodes = nullptr;
+    DevNode* d_nodes = nullptr;
     pbrt_light_desc* d_lights = nullptr;
     pbrt_camera_desc* d_camera = nullptr;
     pbrt_film_desc* d_film = nullptr;
@@ -740,6 +891,21 @@ DevScene dev_scene(const pbrt_gpu_ctx* c, bool with_dist) {
     return s;
 }
 
+std::vector<DevNode> dev_nodes(const pbrt_scene_desc* s) {
+    std::vector<DevNode> v((size_t)(s->n_nodes > 0 ? s->n_nodes : 1));
+    std::memset(v.data(), 0, v.size() * sizeof(DevNode));
+    for (int i = 0; i < s->n_nodes; i++) {
+        const pbrt_bvh_node& n = s->nodes[i];
+        for (int k = 0; k < 3; k++) {
+            v[i].bmin[k] = n.bmin[k];
+            v[i].bmax[k] = n.bmax[k];
+        }
+        v[i].offset = n.offset;
+        v[i].nprims_axis = (uint32_t)n.n_prims | ((uint32_t)n.axis << 16);
+    }
+    return v;
+}
+
 int validate_scene(const pbrt_scene_desc* s) {
     if (!s) return PBRT_E_INVALID;
     if (s->n_prims < 0 || s->n_nodes < 0 || s->n_lights < 0 || s->n_shapes < 0 || s->n_materials < 0)
@@ -785,9 +951,9 @@ const PcgJump& pcg_jump_table() {
     return J;
 }
 
-// Can k_render_spec replay this render exactly? (see pbrt_spec.h for the conditions)
-bool spec_layout(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const RenderParams& rp, SpecLayout& L) {
-    if (rd->integrator != PBRT_INTEGRATOR_PATH || rd->n_dims < 3) return false;
+// Can the wave-parallel kernels replay this render exactly? (conditions: pbrt_spec.h)
+bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const RenderParams& rp, ChainLayout& L) {
+    if (rd->integrator != PBRT_INTEGRATOR_PATH || rd->n_dims < 3 || rd->max_depth > 2048) return false;   // D < 2^32
     const int nl = c->host_scene.n_lights;
     if (nl > kMaxCachedLights) return false;
     if (nl > 0) {
@@ -806,20 +972,52 @@ bool spec_layout(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Render
         off += (bytes + 15) & ~int64_t(15);
         return (int)o;
     };
-    L.film = put(rp.slot_w * rp.slot_h * 3 * 8);
     L.s1d = put(nd * n * 8);
     L.other = put(nd * n * 2);
-    L.memb = put(n * 8);
-    L.lbuf = put(kWave * 3 * 8);
     L.sbuf = put(kWave * 8);
     L.dbuf = put(kWave * 4);
-    L.pbuf = put(kWave * 2 * 4);
-    const int64_t s1 = rd->jitter ? 2 * n : n, s2 = rd->jitter ? 3 * n : n;
-    const int64_t E = nd * (s1 + s2), V = E + 64 + E / 8;
-    const bool buffered = V * 4 <= 16 * 1024;
-    L.vbuf = put(buffered ? V * 4 : 4);
+    L.vbuf = put(rp.sp_serial ? 4 : (int64_t)rp.sp_draws * 4);
     L.total = (int)off;
     return off <= 48 * 1024;
+}
+
+// Carve the per-batch buffers of the wave path (budget: PBRT_WAVE_BUFFER_GB, default 12).
+int wave_buffers(pbrt_gpu_ctx* c) {
+    const RenderParams& rp = c->rp;
+    const int64_t ppt = rp.tile_size * rp.tile_size, n = rp.spp, nd = rp.ndims > 0 ? rp.ndims : 1;
+    auto al = [](int64_t b) { return (b + 255) & ~int64_t(255); };
+    const int64_t per_tile = al(ppt * (int64_t)sizeof(PixelRec)) + al(ppt * nd * n * 8) + al(ppt * n * 8) +
+                             al(ppt * n * 24) + al(ppt * (int64_t)sizeof(PanicRec)) + al(4);
+    double gb = 12.0;
+    if (const char* e = getenv("PBRT_WAVE_BUFFER_GB")) gb = atof(e) > 0 ? atof(e) : gb;
+    int64_t batch = (int64_t)(gb * 1073741824.0) / per_tile;
+    if (batch < 1) batch = 1;
+    if (batch > rp.n_slots) batch = rp.n_slots > 0 ? rp.n_slots : 1;
+    const size_t need = (size_t)(batch * per_tile);
+    if (c->wave_cap < need || !c->d_wave) {
+        if (c->d_wave) (void)hipFree(c->d_wave);
+        c->d_wave = nullptr;
+        c->wave_cap = 0;
+        HIPCHK(c, hipMalloc((void**)&c->d_wave, need));
+        c->wave_cap = need;
+    }
+    WaveBufs& wb = c->wb;
+    unsigned char* p = c->d_wave;
+    auto take = [&](int64_t bytes_per_tile) {
+        unsigned char* q = p;
+        p += batch * al(bytes_per_tile);
+        return q;
+    };
+    wb.prec = (PixelRec*)take(ppt * (int64_t)sizeof(PixelRec));
+    wb.s1d = (double*)take(ppt * nd * n * 8);
+    wb.memb = (uint64_t*)take(ppt * n * 8);
+    wb.L = (double*)take(ppt * n * 24);
+    wb.ppanic = (PanicRec*)take(ppt * (int64_t)sizeof(PanicRec));
+    wb.tile_npx = (int32_t*)take(4);
+    wb.ppt = ppt;
+    wb.s1d_stride = nd * n;
+    c->wave_batch = batch;
+    return PBRT_OK;
 }
 
 int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
@@ -873,7 +1071,6 @@ int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
         if (rc != PBRT_OK) return set_err(c, rc, "unsupported light sample strategy");
         HIPCHK(c, hipMemcpyAsync(c->d_dist, &dist, sizeof(dist), hipMemcpyHostToDevice, c->stream));
     }
-    c->use_spec = c->kernel_req != PBRT_KERNEL_SERIAL && spec_layout(c, rd, rp, c->lay);
     {
         const int64_t n = rp.spp, s1 = rp.jitter ? 2 * n : n, s2 = rp.jitter ? 3 * n : n;
         const int64_t E = (int64_t)rp.ndims * (s1 + s2), V = E + 64 + E / 8;
@@ -881,8 +1078,23 @@ int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
         rp.sp_draws = (int32_t)V;
         rp.sp_serial = V * 4 <= 16 * 1024 ? 0 : 1;
     }
+    c->use_spec = c->kernel_req != PBRT_KERNEL_SERIAL && wave_eligible(c, rd, rp, c->lay);
     if (c->kernel_req == PBRT_KERNEL_WAVE && !c->use_spec)
         return set_err(c, PBRT_E_UNSUPPORTED, "render not eligible for the wave-parallel kernel");
+    if (c->use_spec && rp.n_slots > 0) {
+        int rcw = wave_buffers(c);
+        if (rcw != PBRT_OK) return rcw;
+        // tiles per k_chain wave (opts.lanes_per_wave = 1, 2, 4, 8 or 16; default 1).
+        // One tile per wave is fastest on MI355X: its 64 trajectories leave the
+        // same bounce-1 point, so their traversals stay coherent; packing tiles
+        // cuts speculation but a window lasts as long as its slowest lane, and
+        // mixed-tile windows measured 2.5x slower per window.
+        int G = 1;
+        if (c->lanes_per_wave_set && c->lanes_per_wave >= 1 && c->lanes_per_wave <= kMaxGroups &&
+            (c->lanes_per_wave & (c->lanes_per_wave - 1)) == 0)
+            G = c->lanes_per_wave;
+        c->tiles_per_wave = G;
+    }
     size_t nslot = (size_t)(rp.n_slots > 0 ? rp.n_slots : 1);
     int rc;
     if ((rc = ensure(c, &c->d_films, &c->films_cap, nslot * (size_t)(rp.slot_w * rp.slot_h * 3)))) return rc;
@@ -904,7 +1116,10 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
     if (rc != PBRT_OK) return rc;
     auto* c = new pbrt_gpu_ctx();
     c->device = (opts && opts->device >= 0) ? opts->device : -1;
-    if (opts && opts->lanes_per_wave > 0 && opts->lanes_per_wave <= 64) c->lanes_per_wave = opts->lanes_per_wave;
+    if (opts && opts->lanes_per_wave > 0 && opts->lanes_per_wave <= 64) {
+        c->lanes_per_wave = opts->lanes_per_wave;
+        c->lanes_per_wave_set = true;
+    }
     if (opts && (opts->occupancy == 2 || opts->occupancy == 4 || opts->occupancy == 8)) c->min_waves = opts->occupancy;
     if (opts && (opts->kernel < PBRT_KERNEL_AUTO || opts->kernel > PBRT_KERNEL_WAVE)) {
         delete c;
@@ -920,6 +1135,11 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
         if (hipSetDevice(c->device) != hipSuccess) { delete c; return PBRT_E_HIP; }
     } else {
         (void)hipGetDevice(&c->device);
+    }
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)
+            c->n_simd = 4 * prop.multiProcessorCount;
     }
     c->host_scene = *scene;
     c->host_scene.shapes = nullptr;
@@ -937,7 +1157,7 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
     if ((rc = upload(c, &c->d_shapes, scene->shapes, scene->n_shapes)) ||
         (rc = upload(c, &c->d_materials, scene->materials, scene->n_materials)) ||
         (rc = upload(c, &c->d_prims, scene->prims, scene->n_prims)) ||
-        (rc = upload(c, &c->d_nodes, scene->nodes, scene->n_nodes)) ||
+        (rc = upload(c, &c->d_nodes, dev_nodes(scene).data(), scene->n_nodes)) ||
         (rc = upload(c, &c->d_lights, scene->lights, scene->n_lights)) ||
         (rc = upload(c, &c->d_camera, &scene->camera, 1)) || (rc = upload(c, &c->d_film, &scene->film, 1)) ||
         (rc = upload<pbrt_distribution_desc>(c, &c->d_dist, nullptr, 1)) ||
@@ -967,9 +1187,20 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
         DevScene sc = dev_scene(c, rd->integrator == PBRT_INTEGRATOR_PATH);
         if (c->use_spec) {
             c->last_kernel = PBRT_KERNEL_WAVE;
-            auto kern = c->min_waves >= 2 ? k_render_spec<2> : k_render_spec<1>;
-            hipLaunchKernelGGL(kern, dim3((unsigned)rp.n_slots), dim3(kWave), (unsigned)c->lay.total,
-                               c->stream, sc, rp, c->lay, c->d_jump, c->d_films, c->d_panics, c->d_ctr);
+            auto chain = c->min_waves >= 2 ? k_chain<2> : k_chain<1>;
+            const int64_t per = rp.slot_w * rp.slot_h;
+            for (int64_t sb = 0; sb < rp.n_slots; sb += c->wave_batch) {
+                const int64_t nb = std::min<int64_t>(c->wave_batch, rp.n_slots - sb);
+                const int G = c->tiles_per_wave;
+                hipLaunchKernelGGL(chain, dim3((unsigned)((nb + G - 1) / G)), dim3(kWave), (unsigned)c->lay.total,
+                                   c->stream, sc, rp, c->lay, c->d_jump, c->wb, sb, nb, kWave / G, c->d_ctr);
+                hipLaunchKernelGGL(k_paths, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
+                                   (unsigned)(rp.ndims * rp.spp * 8), c->stream, sc, rp, c->wb, sb, c->d_ctr);
+                hipLaunchKernelGGL(k_film, dim3((unsigned)((nb * per + 255) / 256)), dim3(256), 0, c->stream,
+                                   c->d_film, rp, c->wb, sb, nb, c->d_films);
+                hipLaunchKernelGGL(k_panic_reduce, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, c->stream, c->wb,
+                                   sb, nb, c->d_panics, c->d_ctr);
+            }
         } else {
             c->last_kernel = PBRT_KERNEL_SERIAL;
             int64_t blocks = (rp.n_slots + rp.lanes_per_wave - 1) / rp.lanes_per_wave;
@@ -1133,7 +1364,8 @@ void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_shapes, c->d_materials, c->d_prims, c->d_nodes, c->d_lights, c->d_camera, c->d_film,
-                    c->d_dist,   c->d_films,     c->d_s1d,   c->d_panics, c->d_ctr,   c->d_out,    c->d_jump};
+                    c->d_dist,   c->d_films,     c->d_s1d,   c->d_panics, c->d_ctr,   c->d_out,    c->d_jump,
+                    c->d_wave};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->ev0) (void)hipEventDestroy(c->ev0);

@@ -20,7 +20,7 @@ from . import abi
 from .abi import *  # noqa: F401,F403  (re-export the ABI constants/structs)
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libpbrt_gpu.so")
+LIB_PATH = os.environ.get("PBRT_GPU_LIB") or os.path.join(PKG_DIR, "lib", "libpbrt_gpu.so")
 
 _lib = None
 

@@ -265,6 +265,12 @@ def test_wave_kernel_variants(kw):
     check(G.Scene.readme(48, 40), abi.render_desc(**kw), kernel="wave")
 
 
+@pytest.mark.parametrize("tiles_per_wave", [1, 2, 8, 16])
+def test_wave_kernel_tiles_per_wave(tiles_per_wave):
+    """k_chain packs 64 / L lanes per tile; 37 tiles leave partial last waves."""
+    check(G.Scene.readme(112, 80), abi.render_desc(4, 4), kernel="wave", lanes_per_wave=tiles_per_wave)
+
+
 def test_wave_kernel_cornell_64spp():
     check(G.Scene.cornell(32, 32), abi.render_desc(8, 8, max_depth=10), kernel="wave")
 

@@ -23,8 +23,8 @@ a = ap.parse_args()
 
 scene = G.Scene.readme(a.width, a.height)
 names = ["paths", "camera_samples", "closest_rays", "shadow_rays", "any_panic", "windows",
-         "cyc_sp_swaps", "cyc_bounce1", "cyc_trajectories", "cyc_full_paths", "cyc_film_add",
-         "cyc_sp_draws", "cyc_chain_walk", "n_serial_start_pixel"]
+         "cyc_start_pixel", "cyc_bounce1", "cyc_trajectories", "cyc_chain_walk", "cyc_4",
+         "cyc_5", "cyc_6", "cyc_7"]
 with G.Renderer(scene, kernel=a.kernel, occupancy=a.occupancy) as r:
     rd = abi.render_desc(a.spp, a.spp)
     for i in range(a.reps):
@@ -40,6 +40,5 @@ with G.Renderer(scene, kernel=a.kernel, occupancy=a.occupancy) as r:
               f"Mpaths/s={st.paths_traced / dt / 1e6:.2f}")
         px = a.width * a.height
         print("  windows/pixel %.2f" % (vals["windows"] / px))
-        print("  serial StartPixel fallbacks", vals["n_serial_start_pixel"])
         for k in names[6:13]:
             print(f"  {k:16s} {vals[k] / tot * 100:5.1f}%  {vals[k] / px:10.0f} cyc/pixel")
