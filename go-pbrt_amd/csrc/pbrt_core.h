@@ -190,10 +190,15 @@ GO_HD EF ef_sub(EF a, EF b, int& panic) {
     ef_check(r, panic);
     return r;
 }
+// efloat.go Mul. Operands that passed Check are finite, so the four bound
+// products are never NaN and Go's Min/Max reduce to IEEE min/max (-0 < +0).
+// An operand that failed Check has already set the sticky panic: the caller
+// discards everything computed after it.
 GO_HD EF ef_mul(EF a, EF b, int& panic) {
     double p0 = a.lo * b.lo, p1 = a.hi * b.lo, p2 = a.lo * b.hi, p3 = a.hi * b.hi;
-    EF r{a.v * b.v, gomath::next_down(gomath::min(gomath::min(p0, p1), gomath::min(p2, p3))),
-         gomath::next_up(gomath::max(gomath::max(p0, p1), gomath::max(p2, p3)))};
+    EF r{a.v * b.v,
+         gomath::next_down(gomath::min_nonan(gomath::min_nonan(p0, p1), gomath::min_nonan(p2, p3))),
+         gomath::next_up(gomath::max_nonan(gomath::max_nonan(p0, p1), gomath::max_nonan(p2, p3)))};
     ef_check(r, panic);
     return r;
 }

@@ -1445,6 +1445,16 @@ __global__ void k_probe(int op, const double* __restrict__ in, int64_t n, int in
             for (int k = 0; k < out_stride; k++) o[k] = pcg_float(r);
             break;
         }
+        case PBRT_PROBE_MIN_NONAN: o[0] = gomath::min_nonan(a[0], a[1]); break;
+        case PBRT_PROBE_MAX_NONAN: o[0] = gomath::max_nonan(a[0], a[1]); break;
+        case PBRT_PROBE_EFLOAT_MUL:
+        case PBRT_PROBE_EFLOAT_DIV: {
+            int panic = 0;
+            EF x = ef_new(a[0], a[1], panic), y = ef_new(a[2], a[3], panic);
+            EF r = op == PBRT_PROBE_EFLOAT_MUL ? ef_mul(x, y, panic) : ef_div(x, y, panic);
+            o[0] = r.v; o[1] = r.lo; o[2] = r.hi; o[3] = panic;
+            break;
+        }
         case PBRT_PROBE_NEXT_FLOAT_UP: o[0] = gomath::next_up(a[0]); break;
         case PBRT_PROBE_NEXT_FLOAT_DOWN: o[0] = gomath::next_down(a[0]); break;
         default: o[0] = gomath::nan();

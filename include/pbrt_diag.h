@@ -35,7 +35,11 @@ enum {
     PBRT_PROBE_SPAWN_RAY_TO = 16,      /* in p0 perr0 n0 p1 perr1 n1 -> o d tmax */
     PBRT_PROBE_PCG = 17,               /* in seed -> out[out_stride] first floats */
     PBRT_PROBE_NEXT_FLOAT_UP = 18,     /* in v -> NextFloatUp(v)   (math.go:122-124) */
-    PBRT_PROBE_NEXT_FLOAT_DOWN = 19    /* in v -> NextFloatDown(v) (math.go:126-128) */
+    PBRT_PROBE_NEXT_FLOAT_DOWN = 19,   /* in v -> NextFloatDown(v) (math.go:126-128) */
+    PBRT_PROBE_MIN_NONAN = 20,         /* in x, y (not NaN) -> device min used by EFloat */
+    PBRT_PROBE_MAX_NONAN = 21,         /* in x, y (not NaN) -> device max used by EFloat */
+    PBRT_PROBE_EFLOAT_MUL = 22,        /* in v1 e1 v2 e2 -> value low high panic */
+    PBRT_PROBE_EFLOAT_DIV = 23         /* in v1 e1 v2 e2 -> value low high panic */
 };
 
 /* Inputs: n records of in_stride doubles; outputs: n records of out_stride. */

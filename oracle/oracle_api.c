@@ -40,6 +40,23 @@ int oracle_efloat_add(double v1, double e1, double v2, double e2, double out[3])
     out[0] = r.v; out[1] = r.lo; out[2] = r.hi;
     return 0;
 }
+/* efloat.go Mul / Div with the same contract as oracle_efloat_add */
+int oracle_efloat_mul(double v1, double e1, double v2, double e2, double out[3]) {
+    panic_ctx pc;
+    if (setjmp(pc.jb)) return 1;
+    ef_t a = ef_new(&pc, v1, e1), b = ef_new(&pc, v2, e2);
+    ef_t r = ef_mul(&pc, a, b);
+    out[0] = r.v; out[1] = r.lo; out[2] = r.hi;
+    return 0;
+}
+int oracle_efloat_div(double v1, double e1, double v2, double e2, double out[3]) {
+    panic_ctx pc;
+    if (setjmp(pc.jb)) return 1;
+    ef_t a = ef_new(&pc, v1, e1), b = ef_new(&pc, v2, e2);
+    ef_t r = ef_div(&pc, a, b);
+    out[0] = r.v; out[1] = r.lo; out[2] = r.hi;
+    return 0;
+}
 /* transform.go */
 void oracle_translate(double x, double y, double z, pbrt_transform* out) { *out = orc_translate(x, y, z); }
 void oracle_scale(double x, double y, double z, pbrt_transform* out) { *out = orc_scale(x, y, z); }

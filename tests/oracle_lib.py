@@ -60,7 +60,7 @@ def lib(flops=False):
 
 
 def _bind(L):
-    if True:
+    if True:  # noqa: SIM108 (one indented block of bindings)
         d = C.c_double
         P = C.POINTER
         for name in ("sin", "cos", "tan", "atan", "asin", "acos", "radians"):
@@ -70,8 +70,9 @@ def _bind(L):
             f = getattr(L, "oracle_go_" + name)
             f.argtypes, f.restype = [d, d], d
         L.oracle_go_f2i.argtypes, L.oracle_go_f2i.restype = [d], C.c_int64
-        L.oracle_efloat_add.argtypes = [d, d, d, d, P(d)]
-        L.oracle_efloat_add.restype = C.c_int
+        for name in ("oracle_efloat_add", "oracle_efloat_mul", "oracle_efloat_div"):
+            getattr(L, name).argtypes = [d, d, d, d, P(d)]
+            getattr(L, name).restype = C.c_int
         L.oracle_translate.argtypes = [d, d, d, P(abi.Transform)]
         L.oracle_scale.argtypes = [d, d, d, P(abi.Transform)]
         L.oracle_rotate.argtypes = [C.c_int, d, P(abi.Transform)]

@@ -137,6 +137,47 @@ def test_device_next_float_up_down_and_go_max_min_special_values():
     assert same_bits(mn, np.array([L.oracle_go_min(x, y) for x, y in pairs]))
 
 
+def test_device_nonan_min_max_order_signed_zeros_like_go():
+    """The device min/max used inside EFloat.Mul (v_min_f64 / v_max_f64) equal
+    Go's Min/Max on every non-NaN pair, incl. -0 vs +0 and infinities."""
+    L = O.lib()
+    v = special_values(3000, 12)
+    v = v[~np.isnan(v)]
+    a = np.concatenate([np.repeat(v[:40], 40), v, [0.0, -0.0, 0.0, -0.0]])
+    b = np.concatenate([np.tile(v[:40], 40), v[::-1], [-0.0, 0.0, 0.0, -0.0]])
+    pairs = np.stack([a, b], axis=1)
+    assert same_bits(probe(20, pairs)[:, 0], np.array([L.oracle_go_min(x, y) for x, y in pairs]))
+    assert same_bits(probe(21, pairs)[:, 0], np.array([L.oracle_go_max(x, y) for x, y in pairs]))
+
+
+@pytest.mark.parametrize("op,name", [(22, "oracle_efloat_mul"), (23, "oracle_efloat_div")])
+def test_device_efloat_mul_div_match_oracle(op, name):
+    """EFloat Mul / Div (efloat.go) incl. Check() panics, on random, signed-zero,
+    straddling-zero and overflowing intervals."""
+    rng = np.random.default_rng(op)
+    n = 20000
+    v1 = rng.standard_normal(n) * 10.0 ** rng.integers(-200, 200, n)
+    v2 = rng.standard_normal(n) * 10.0 ** rng.integers(-200, 200, n)
+    e1 = np.abs(v1) * 10.0 ** rng.integers(-17, 1, n) * (rng.uniform(size=n) < 0.8)
+    e2 = np.abs(v2) * 10.0 ** rng.integers(-17, 1, n) * (rng.uniform(size=n) < 0.8)
+    sp = np.array([0.0, -0.0, 1.0, -1.0, 5e-324, 1e308, -1e308])
+    k = len(sp)
+    with np.errstate(over="ignore"):
+        extra = np.array([[x, 0.0, y, 0.0] for x in sp for y in sp] +
+                         [[x, abs(x) * 2, y, 0.0] for x in sp for y in sp])
+    inp = np.concatenate([np.stack([v1, e1, v2, e2], axis=1), extra])
+    got = probe(op, inp, 4)
+    fn = getattr(O.lib(), name)
+    for i, (a, ea, b, eb) in enumerate(inp):
+        out = (C.c_double * 3)()
+        pan = fn(a, ea, b, eb, out)
+        if pan:
+            assert got[i, 3] != 0, (i, inp[i])
+        else:
+            assert got[i, 3] == 0, (i, inp[i])
+            assert same_bits(got[i, :3], np.array(list(out))), (i, inp[i], got[i], list(out))
+
+
 def test_device_div_sqrt_correctly_rounded():
     """gfx950 fp64 '/' and sqrt must be correctly rounded (SURVEY §9 'verify on
     gfx950'): 2e6 random operands incl. denormals vs the host (IEEE)."""
