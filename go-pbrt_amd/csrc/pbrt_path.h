@@ -186,8 +186,14 @@ __device__ __forceinline__ bool phi_beyond(double y, double x, double phi_max) {
 
 // Sphere.Intersect / IntersectP (sphere.go:64-268). world->object = the swap of
 // object_to_world (Transform.Inverse, transform.go:175-177).
-template <bool kFull>
-__device__ inline bool sphere_intersect(const pbrt_shape_desc& s, const Ray& r, SI* si, double& t_hit, int& panic) {
+// Shapes are split into the hit test (t and the object-space hit point) and
+// the SurfaceInteraction built from that point, so a closest-hit traversal
+// runs the EFloat test once per candidate and builds one interaction at the
+// end (see bvh_traverse).
+
+// Sphere.Intersect / IntersectP, hit part (sphere.go:64-131). world->object
+// = the swap of object_to_world (Transform.Inverse, transform.go:175-177).
+__device__ inline bool sphere_hit(const pbrt_shape_desc& s, const Ray& r, double& t_hit, V3& ph, int& panic) {
     V3 oerr, derr;
     Ray ray = xf_ray(s.object_to_world.m_inv, r, &oerr, &derr);
     EF ox = ef_new(ray.o.x, oerr.x, panic), oy = ef_new(ray.o.y, oerr.y, panic), oz = ef_new(ray.o.z, oerr.z, panic);
@@ -207,7 +213,7 @@ __device__ inline bool sphere_intersect(const pbrt_shape_desc& s, const Ray& r, 
         used_t1 = true;
         if (ts.hi > ray.tmax) return false;
     }
-    V3 ph = ray.o + muls(ray.d, ts.v);
+    ph = ray.o + muls(ray.d, ts.v);
     ph = muls(ph, s.radius / dist(ph, V3{0, 0, 0}));
     if (ph.x == 0.0 && ph.y == 0.0) ph.x = 1e-5 * s.radius;
     if ((s.z_min > -s.radius && ph.z < s.z_min) || (s.z_max < s.radius && ph.z > s.z_max) ||
@@ -224,8 +230,11 @@ __device__ inline bool sphere_intersect(const pbrt_shape_desc& s, const Ray& r, 
             return false;
     }
     t_hit = ts.v;
-    if (!kFull) return true;
-    // parametric representation; only dpdu, dpdv feed the outputs
+    return true;
+}
+// Sphere.Intersect, interaction part (sphere.go:133-186); ray in object space.
+// Only dpdu, dpdv of the parametric representation feed the outputs.
+__device__ inline void sphere_si(const pbrt_shape_desc& s, const Ray& ray, V3 ph, SI& si) {
     double theta = gomath::acos(gomath::clamp(ph.z / s.radius, -1, 1));
     double zr = gomath::sqrt(ph.x * ph.x + ph.y * ph.y);
     double izr = 1.0 / zr;
@@ -234,65 +243,70 @@ __device__ inline bool sphere_intersect(const pbrt_shape_desc& s, const Ray& r, 
     double dth = s.theta_max - s.theta_min;
     V3 dpdv = muls(V3{ph.z * cos_phi, ph.z * sin_phi, -s.radius * gomath::sin(theta)}, dth);
     V3 perr = muls(vabs(ph), gomath::gamma(5));
-    make_si(*si, s.object_to_world.m, s.object_to_world.m_inv, ph, perr, muls(ray.d, -1), dpdu, dpdv, ray.time,
+    make_si(si, s.object_to_world.m, s.object_to_world.m_inv, ph, perr, muls(ray.d, -1), dpdu, dpdv, ray.time,
             s.reverse_orientation != s.transform_swaps_handedness);
-    return true;
 }
 
-// Disk.Intersect / IntersectP (disk.go:64-159)
-template <bool kFull>
-__device__ inline bool disk_intersect(const pbrt_shape_desc& s, const Ray& r, SI* si, double& t_hit) {
+// Disk.Intersect / IntersectP, hit part (disk.go:64-95)
+__device__ inline bool disk_hit(const pbrt_shape_desc& s, const Ray& r, double& t_hit, V3& ph) {
     Ray ray = xf_ray(s.object_to_world.m_inv, r, nullptr, nullptr);
     if (ray.d.z == 0) return false;
     double ts = (s.height - ray.o.z) / ray.d.z;
     if (ts <= 0 || ts >= ray.tmax) return false;
-    V3 ph = ray.o + muls(ray.d, ts);
+    ph = ray.o + muls(ray.d, ts);
     double d2 = ph.x * ph.x + ph.y * ph.y;
     if (d2 > s.radius * s.radius || d2 < s.inner_radius * s.inner_radius) return false;
     if (phi_beyond(ph.y, ph.x, s.phi_max)) return false;
     t_hit = ts;
-    if (!kFull) return true;
+    return true;
+}
+// Disk.Intersect, interaction part (disk.go:96-110); ray in object space
+__device__ inline void disk_si(const pbrt_shape_desc& s, const Ray& ray, V3 ph, SI& si) {
+    double d2 = ph.x * ph.x + ph.y * ph.y;
     double rhit = gomath::sqrt(d2);
     V3 dpdu{-s.phi_max * ph.y, s.phi_max * ph.x, 0};
     V3 dpdv = muls(V3{ph.x, ph.y, 0}, (s.radius - s.inner_radius) / rhit);
     ph.z = s.height;
-    make_si(*si, s.object_to_world.m, s.object_to_world.m_inv, ph, V3{0, 0, 0}, muls(ray.d, -1), dpdu, dpdv, ray.time,
+    make_si(si, s.object_to_world.m, s.object_to_world.m_inv, ph, V3{0, 0, 0}, muls(ray.d, -1), dpdu, dpdv, ray.time,
             s.reverse_orientation != s.transform_swaps_handedness);
-    return true;
 }
 
-template <bool kFull>
-__device__ inline bool shape_intersect(const pbrt_shape_desc& s, const Ray& r, SI* si, double& t_hit, int& panic) {
-    if (s.type == PBRT_SHAPE_SPHERE) return sphere_intersect<kFull>(s, r, si, t_hit, panic);
-    return disk_intersect<kFull>(s, r, si, t_hit);
+__device__ inline bool shape_hit(const pbrt_shape_desc& s, const Ray& r, double& t_hit, V3& ph, int& panic) {
+    if (s.type == PBRT_SHAPE_SPHERE) return sphere_hit(s, r, t_hit, ph, panic);
+    return disk_hit(s, r, t_hit, ph);
+}
+// the interaction at an accepted hit point ph; r in the shape's parent space
+__device__ inline void shape_si(const pbrt_shape_desc& s, const Ray& r, V3 ph, SI& si) {
+    Ray ray = xf_ray(s.object_to_world.m_inv, r, nullptr, nullptr);   // the same o, d as in the hit test
+    if (s.type == PBRT_SHAPE_SPHERE) sphere_si(s, ray, ph, si);
+    else disk_si(s, ray, ph, si);
 }
 
-// Shape test without the SurfaceInteraction: the hit parameter only.
-__device__ inline bool prim_hit_t(const DevScene& sc, int pi, const Ray& r, double& t_hit, int& panic) {
+// Shape test without the SurfaceInteraction: the hit parameter and point.
+__device__ inline bool prim_hit_t(const DevScene& sc, int pi, const Ray& r, double& t_hit, V3& ph, int& panic) {
     const pbrt_primitive_desc& p = sc.prims[pi];
     const pbrt_shape_desc& s = sc.shapes[p.shape];
     Ray ray = r;
     if (p.kind == PBRT_PRIM_TRANSFORMED) ray = xf_ray(p.prim_to_world.m_inv, r, nullptr, nullptr);
-    return shape_intersect<false>(s, ray, nullptr, t_hit, panic);
+    return shape_hit(s, ray, t_hit, ph, panic);
 }
 
-// GeometricPrimitive / TransformedPrimitive (primitive.go:42-115)
-__device__ inline bool prim_intersect(const DevScene& sc, int pi, Ray& r, SI& si, int& panic) {
+// GeometricPrimitive / TransformedPrimitive (primitive.go:42-115): the
+// interaction of primitive pi at its accepted hit point ph (shape space).
+__device__ inline void prim_si(const DevScene& sc, int pi, const Ray& r, V3 ph, SI& si) {
     const pbrt_primitive_desc& p = sc.prims[pi];
     const pbrt_shape_desc& s = sc.shapes[p.shape];
     const bool xformed = p.kind == PBRT_PRIM_TRANSFORMED;
     Ray ray = r;
     if (xformed) ray = xf_ray(p.prim_to_world.m_inv, r, nullptr, nullptr);
-    double t_hit;
-    if (!shape_intersect<true>(s, ray, &si, t_hit, panic)) return false;
+    shape_si(s, ray, ph, si);
     si.prim = pi;
-    r.tmax = t_hit;
     if (xformed && !is_identity(p.prim_to_world.m)) transform_si_shared(si, p.prim_to_world.m, p.prim_to_world.m_inv);
-    return true;
 }
 __device__ inline bool prim_intersect_p(const DevScene& sc, int pi, const Ray& r, int& panic) {
     double t_hit;
-    return prim_hit_t(sc, pi, r, t_hit, panic);
+    V3 ph;
+    return prim_hit_t(sc, pi, r, t_hit, ph, panic);
 }
 
 // ------------------------------------------------------------------------ BVH
@@ -360,10 +374,10 @@ __device__ __forceinline__ bool node_hit(const NodeView& nd, const Ray& r, V3 in
 // box tests and TMax updates are exactly the reference's.
 //
 // Closest hit: each accepted primitive only shrinks TMax; the interaction of
-// the LAST accepted one is computed once after the walk. This equals the
-// reference's per-hit SurfaceInteraction: a shape's chosen root (t0 or t1)
-// never depends on TMax (TMax only rejects), so re-running the accepted
-// primitive with the unchanged ray gives the same hit and the same fields.
+// the LAST accepted one is built once after the walk from its hit point. This
+// equals the reference's per-hit SurfaceInteraction: every field is a function
+// of that hit point and of the (unchanged) ray, and the shared-interaction
+// aliasing of TransformedPrimitive (#20) only ever touches the last one.
 template <bool kAny>
 __device__ inline bool bvh_traverse(const DevScene& sc, Ray& ray, SI* si, uint16_t* stack, int& panic) {
     if (sc.n_nodes == 0) return false;
@@ -373,6 +387,7 @@ __device__ inline bool bvh_traverse(const DevScene& sc, Ray& ray, SI* si, uint16
     const uint32_t negmask = (uint32_t)nx | ((uint32_t)ny << 1) | ((uint32_t)nz << 2);
     uint32_t to_visit = 0, cur = 0;
     int best = -1;
+    V3 best_ph{0, 0, 0};
     for (;;) {
         // A: interior nodes
         bool leaf = false, done = false;
@@ -407,22 +422,21 @@ __device__ inline bool bvh_traverse(const DevScene& sc, Ray& ray, SI* si, uint16
         const uint32_t first = nd.offset, np = nd.n_prims;
         for (uint32_t i = 0; i < np; i++) {
             double t_hit;
-            const bool h = prim_hit_t(sc, (int)(first + i), ray, t_hit, panic);
+            V3 ph;
+            const bool h = prim_hit_t(sc, (int)(first + i), ray, t_hit, ph, panic);
             if (panic) return kAny ? false : best >= 0;
             if (h) {
                 if (kAny) return true;
                 ray.tmax = t_hit;
                 best = (int)(first + i);
+                best_ph = ph;
             }
         }
         if (to_visit == 0) break;
         cur = stack[(--to_visit) * kStackStride];
     }
-    if (!kAny && best >= 0) {
-        Ray r = ray;
-        r.tmax = ray_tmax0;
-        prim_intersect(sc, best, r, *si, panic);
-    }
+    if (!kAny && best >= 0) prim_si(sc, best, ray, best_ph, *si);
+    (void)ray_tmax0;
     return best >= 0;
 }
 
