@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=8, help="Stratified(spp, spp)")
-    ap.add_argument("--lanes-per-wave", type=int, default=0)
+    ap.add_argument("--kernel", default="auto", choices=["auto", "serial", "wave"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, nproc)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -89,6 +89,35 @@ def cpu_baseline(args, rd_kwargs):
     }
 
 
+def roofline(W, H, S, paths_per_launch, kernel_kind, kern_ms, chain_ms, paths_ms, merge_ms):
+    """Roofline of the dominant kernel, priced in ALGORITHMIC fp64 FLOPs: the
+    reference's own arithmetic per path, counted by the FLOP-accounting oracle
+    (profiles/flops_*.json, tools/count_flops.py) x the paths of one launch,
+    over the kernel's duration measured here with HIP events on its stream.
+
+    WAVE pipeline: k_chain is dominant; what it must reproduce per path is
+    the trajectory (everything but light sampling: flops_trajectory_per_path).
+    Its speculative, discarded trajectories are not algorithmic work, so they
+    lower `frac` -- that is the point of the measure."""
+    fl = load_json(os.path.join(REPO, "profiles", f"flops_readme_{W}x{H}_s{S}x{S}.json"))
+    if not fl:
+        return None
+    pmc = load_json(os.path.join(REPO, "profiles", f"pmc_readme_{W}x{H}_s{S}x{S}.json")) or {}
+    total = fl["flops_per_path"] * paths_per_launch
+    if kernel_kind == 2 and chain_ms > 0:   # PBRT_KERNEL_WAVE
+        algo = fl.get("flops_trajectory_per_path", fl["flops_per_path"]) * paths_per_launch
+        name, ms = "k_chain", chain_ms
+    else:
+        algo, name, ms = total, "k_render_exact", kern_ms
+    achieved = algo / (ms / 1e3) / 1e12
+    return {"bound": "fp64-valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved / FP64_PEAK_TFLOPS, "traffic": (pmc.get(name) or {}).get("hbm_bytes_per_launch"),
+            "kernel": name, "kernel_ms": ms, "flops_per_launch": algo,
+            "pipeline": {"kernels_ms": kern_ms, "k_paths_ms": paths_ms, "merge_ms": merge_ms,
+                         "achieved_tflops": total / (kern_ms / 1e3) / 1e12,
+                         "flops_per_path": fl["flops_per_path"]}}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -110,7 +139,7 @@ def main():
     W, H, S = args.width, args.height, args.spp
     rd_kwargs = dict(spp_x=S, spp_y=S)
     scene = G.Scene.readme(W, H)
-    renderer = G.Renderer(scene, device=local, lanes_per_wave=args.lanes_per_wave)
+    renderer = G.Renderer(scene, device=local, kernel=args.kernel)
     rd = G.render_desc(**rd_kwargs, tile_begin=rank, tile_stride=world)
     film = torch.zeros((H, W, 3), dtype=torch.float64, device=dev)
 
@@ -138,30 +167,22 @@ def main():
     paths_local = sum(int(s.paths_traced) for s in stats)
     kern_ms = sum(s.kernel_ms for s in stats) / len(stats)
     merge_ms = sum(s.merge_ms for s in stats) / len(stats)
+    chain_ms = sum(s.chain_ms for s in stats) / len(stats)
+    paths_ms = sum(s.paths_ms for s in stats) / len(stats)
+    kernel_kind = int(stats[0].kernel)
     agg = torch.tensor([elapsed, float(paths_local), kern_ms], dtype=torch.float64, device=dev)
     if world > 1:
         mx = agg.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = agg.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed, paths_total, kern_ms_max = float(mx[0]), float(sm[1]), float(mx[2])
+        elapsed, paths_total = float(mx[0]), float(sm[1])
     else:
-        paths_total, kern_ms_max = float(paths_local), kern_ms
+        paths_total = float(paths_local)
 
     if rank == 0:
         value = paths_total / elapsed / 1e6
-        # roofline of the dominant kernel (k_render_exact): fp64 VALU bound.
-        fl = load_json(os.path.join(REPO, "profiles", f"flops_readme_{W}x{H}_s{S}x{S}.json"))
-        roof = None
-        if fl:
-            flops_per_launch = fl["flops_per_path"] * (paths_local / len(stats))
-            achieved = flops_per_launch / (kern_ms / 1e3) / 1e12
-            pmc = load_json(os.path.join(REPO, "profiles", f"pmc_readme_{W}x{H}_s{S}x{S}.json"))
-            roof = {"bound": "fp64-valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": achieved / FP64_PEAK_TFLOPS,
-                    "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
-                    "kernel": "k_render_exact", "kernel_ms": kern_ms, "merge_ms": merge_ms,
-                    "flops_per_path": fl["flops_per_path"]}
+        roof = roofline(W, H, S, paths_local / len(stats), kernel_kind, kern_ms, chain_ms, paths_ms, merge_ms)
         out = {
             "metric": METRIC,
             "value": value,
@@ -181,7 +202,7 @@ def main():
                 "width": W, "height": H, "spp": S * S, "traced_spp": S * S - 1,
                 "paths_per_frame": int(paths_total / args.steps), "mode": "exact",
                 "parallelism": f"tiles mod {world}" + (" + RCCL film reduce" if world > 1 else ""),
-                "lanes_per_wave": args.lanes_per_wave or 64,
+                "kernel": {1: "serial", 2: "wave"}.get(kernel_kind, "?"),
             },
             "roofline": roof,
         }

@@ -813,6 +813,8 @@ struct pbrt_gpu_ctx {
     size_t wave_cap = 0;
     int64_t wave_batch = 0;            // tile slots per batch
     int tiles_per_wave = 1;            // k_chain lane groups per wave (64 / lanes per tile)
+    std::vector<hipEvent_t> bev;       // per batch: before k_chain, after k_chain, after k_paths
+    int n_batches = 0;
     int n_simd = 1024;                 // SIMDs of the device (4 per CU)
     WaveBufs wb{};
     // device scene
@@ -1189,13 +1191,22 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
             c->last_kernel = PBRT_KERNEL_WAVE;
             auto chain = c->min_waves >= 2 ? k_chain<2> : k_chain<1>;
             const int64_t per = rp.slot_w * rp.slot_h;
-            for (int64_t sb = 0; sb < rp.n_slots; sb += c->wave_batch) {
+            c->n_batches = (int)((rp.n_slots + c->wave_batch - 1) / c->wave_batch);
+            while ((int)c->bev.size() < 3 * c->n_batches) {
+                hipEvent_t e;
+                HIPCHK(c, hipEventCreate(&e));
+                c->bev.push_back(e);
+            }
+            for (int64_t sb = 0, bi = 0; sb < rp.n_slots; sb += c->wave_batch, bi++) {
                 const int64_t nb = std::min<int64_t>(c->wave_batch, rp.n_slots - sb);
+                HIPCHK(c, hipEventRecord(c->bev[3 * bi + 0], c->stream));
                 const int G = c->tiles_per_wave;
                 hipLaunchKernelGGL(chain, dim3((unsigned)((nb + G - 1) / G)), dim3(kWave), (unsigned)c->lay.total,
                                    c->stream, sc, rp, c->lay, c->d_jump, c->wb, sb, nb, kWave / G, c->d_ctr);
+                HIPCHK(c, hipEventRecord(c->bev[3 * bi + 1], c->stream));
                 hipLaunchKernelGGL(k_paths, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
                                    (unsigned)(rp.ndims * rp.spp * 8), c->stream, sc, rp, c->wb, sb, c->d_ctr);
+                HIPCHK(c, hipEventRecord(c->bev[3 * bi + 2], c->stream));
                 hipLaunchKernelGGL(k_film, dim3((unsigned)((nb * per + 255) / 256)), dim3(256), 0, c->stream,
                                    c->d_film, rp, c->wb, sb, nb, c->d_films);
                 hipLaunchKernelGGL(k_panic_reduce, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, c->stream, c->wb,
@@ -1203,6 +1214,7 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
             }
         } else {
             c->last_kernel = PBRT_KERNEL_SERIAL;
+            c->n_batches = 0;
             int64_t blocks = (rp.n_slots + rp.lanes_per_wave - 1) / rp.lanes_per_wave;
             auto kern = k_render_exact<1>;
             if (c->min_waves == 2) kern = k_render_exact<2>;
@@ -1245,6 +1257,14 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
     st.kernel_ms = ms;
     st.merge_ms = ms_merge;
     st.kernel = c->last_kernel;
+    st.batches = c->n_batches;
+    for (int b = 0; b < c->n_batches; b++) {
+        float a = 0, p = 0;
+        (void)hipEventElapsedTime(&a, c->bev[3 * b + 0], c->bev[3 * b + 1]);
+        (void)hipEventElapsedTime(&p, c->bev[3 * b + 1], c->bev[3 * b + 2]);
+        st.chain_ms += a;
+        st.paths_ms += p;
+    }
     if (ctr.any_panic) {
         std::vector<PanicRec> pr((size_t)c->rp.n_slots);
         HIPCHK(c, hipMemcpy(pr.data(), c->d_panics, sizeof(PanicRec) * pr.size(), hipMemcpyDeviceToHost));
@@ -1368,6 +1388,7 @@ void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
                     c->d_wave};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
+    for (hipEvent_t e : c->bev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev2) (void)hipEventDestroy(c->ev2);

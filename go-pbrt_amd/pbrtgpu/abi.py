@@ -210,7 +210,9 @@ class GpuStats(C.Structure):
         ("panic_sample", C.c_int32),
         ("panic_bounce", C.c_int32),
         ("kernel", C.c_int32),
-        ("pad0", C.c_int32),
+        ("batches", C.c_int32),
+        ("chain_ms", C.c_double),
+        ("paths_ms", C.c_double),
     ]
 
 

@@ -214,7 +214,9 @@ typedef struct pbrt_gpu_stats {
     int64_t panic_pixel_x, panic_pixel_y;
     int32_t panic_sample, panic_bounce;
     int32_t kernel;          /* PBRT_KERNEL_SERIAL or PBRT_KERNEL_WAVE (last render) */
-    int32_t pad0;
+    int32_t batches;         /* WAVE: tile batches the frame was split into       */
+    double chain_ms;         /* WAVE: k_chain time (speculative offsets), summed  */
+    double paths_ms;         /* WAVE: k_paths time (full paths), summed           */
 } pbrt_gpu_stats;
 
 /* ----------------------------------------------------------- ray batches */

@@ -22,6 +22,7 @@
 #ifdef ORACLE_COUNT_FLOPS
 __thread uint64_t orc_flops;
 static __thread uint64_t orc_flops_saved;
+static __thread uint64_t orc_flops_light;
 /* bracket reference computations whose results never reach an output (the
  * device path does not execute them) */
 #define FL_OFF_BEGIN (orc_flops_saved = orc_flops)
@@ -789,8 +790,14 @@ static spec path_li(orc_ctx* oc, sampler_t* smp, ray_t ray) {
         bsdf_t b;
         if (material_bsdf(sc, &isect, &b) < 0) { oc->unsupported = 1; break; }
         if (b.n_bxdfs > 0) {   /* NumComponents(BSDFAll &^ BSDFSpecular) > 0 */
+#ifdef ORACLE_COUNT_FLOPS
+            const uint64_t f0 = orc_flops;
+#endif
             spec ld = uniform_sample_one_light(oc, smp, &isect, &b, &oc->dist);
             L = s_add(L, s_mul(beta, ld));
+#ifdef ORACLE_COUNT_FLOPS
+            orc_flops_light += orc_flops - f0;
+#endif
         }
         v3 wo = ray.d;                           /* path.go:91 (#8)           */
         v2 u = sampler_get2d(smp);
@@ -1010,7 +1017,7 @@ typedef struct {
     int* panic_kind;
     int64_t* panic_info;    /* 4 per tile: px, py, sample, bounce */
     int flags;
-    atomic_ullong paths, samples, closest, shadow, flops;
+    atomic_ullong paths, samples, closest, shadow, flops, flops_light;
 } job_t;
 
 static void* worker(void* arg) {
@@ -1020,6 +1027,7 @@ static void* worker(void* arg) {
     oc.scene = j->sc; oc.rd = j->rd; oc.flags = j->flags;
 #ifdef ORACLE_COUNT_FLOPS
     orc_flops = 0;
+    orc_flops_light = 0;
 #endif
     orc_light_distribution(j->sc, j->rd, &oc.dist);
     int spp = j->rd->sampler_x * j->rd->sampler_y;
@@ -1044,6 +1052,7 @@ static void* worker(void* arg) {
     atomic_fetch_add(&j->shadow, oc.shadow_rays);
 #ifdef ORACLE_COUNT_FLOPS
     atomic_fetch_add(&j->flops, orc_flops);
+    atomic_fetch_add(&j->flops_light, orc_flops_light);
 #endif
     free(s1d);
     return NULL;
@@ -1146,6 +1155,7 @@ int orc_render(const pbrt_scene_desc* sc, const pbrt_render_desc* rd, int n_thre
         stats->closest_rays = atomic_load(&j.closest);
         stats->shadow_rays = atomic_load(&j.shadow);
         stats->flops = atomic_load(&j.flops);
+        stats->flops_light = atomic_load(&j.flops_light);
     }
     free(pool); free(j.films); free(j.status); free(j.panic_kind); free(j.panic_info); free(tiles);
     return rc;

@@ -32,6 +32,7 @@ typedef struct {
     uint64_t flops;   /* fp64 add/sub/mul/div/sqrt executed (liboracle_flops.so only) */
     int32_t panic_kind;
     int64_t panic_tile, panic_px, panic_py, panic_sample, panic_bounce;
+    uint64_t flops_light;   /* the part of flops spent in UniformSampleOneLight + L += beta*Ld */
 } orc_stats;
 
 void orc_light_distribution(const pbrt_scene_desc* sc, const pbrt_render_desc* rd,

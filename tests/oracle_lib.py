@@ -36,6 +36,7 @@ class OracleStats(C.Structure):
         ("panic_py", C.c_int64),
         ("panic_sample", C.c_int64),
         ("panic_bounce", C.c_int64),
+        ("flops_light", C.c_uint64),
     ]
 
 

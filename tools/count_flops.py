@@ -36,6 +36,8 @@ def main():
         "scene": "readme", "width": a.width, "height": a.height, "sampler": f"Stratified({a.spp},{a.spp})",
         "integrator": "Path(10, rr=1, Uniform)", "tiles": int(st.tiles), "paths": int(st.paths),
         "flops": int(st.flops), "flops_per_path": st.flops / st.paths,
+        "flops_light_per_path": st.flops_light / st.paths,
+        "flops_trajectory_per_path": (st.flops - st.flops_light) / st.paths,
         "closest_rays_per_path": st.closest_rays / st.paths, "shadow_rays_per_path": st.shadow_rays / st.paths,
         "count_build_wall_s": dt, "threads": a.threads,
         "definition": "fp64 add/sub/mul/div/sqrt executed by the reference algorithm on values that reach "
