@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=8, help="Stratified(spp, spp)")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "serial", "wave"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "serial", "wave", "wavefront"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, nproc)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -104,9 +104,9 @@ def roofline(W, H, S, paths_per_launch, kernel_kind, kern_ms, chain_ms, paths_ms
         return None
     pmc = load_json(os.path.join(REPO, "profiles", f"pmc_readme_{W}x{H}_s{S}x{S}.json")) or {}
     total = fl["flops_per_path"] * paths_per_launch
-    if kernel_kind == 2 and chain_ms > 0:   # PBRT_KERNEL_WAVE
+    if kernel_kind in (2, 3) and chain_ms > 0:   # PBRT_KERNEL_WAVE / _WAVEFRONT
         algo = fl.get("flops_trajectory_per_path", fl["flops_per_path"]) * paths_per_launch
-        name, ms = "k_chain", chain_ms
+        name, ms = ("k_chain" if kernel_kind == 2 else "wf_chain"), chain_ms
     else:
         algo, name, ms = total, "k_render_exact", kern_ms
     achieved = algo / (ms / 1e3) / 1e12
@@ -202,7 +202,7 @@ def main():
                 "width": W, "height": H, "spp": S * S, "traced_spp": S * S - 1,
                 "paths_per_frame": int(paths_total / args.steps), "mode": "exact",
                 "parallelism": f"tiles mod {world}" + (" + RCCL film reduce" if world > 1 else ""),
-                "kernel": {1: "serial", 2: "wave"}.get(kernel_kind, "?"),
+                "kernel": {1: "serial", 2: "wave", 3: "wavefront"}.get(kernel_kind, "?"),
             },
             "roofline": roof,
         }

@@ -20,17 +20,39 @@
 
 namespace pbrt {
 
+// Optional region timing of a trajectory step (built with -DPBRT_STEP_TIMING):
+// the first active lane adds each region's wall time to g_step_cycles.
+#ifdef PBRT_STEP_TIMING
+__device__ unsigned long long g_step_cycles[8];
+struct StepTimer {
+    long long t;
+    __device__ void start() { t = clock64(); }
+    __device__ void mark(int i) {
+        long long now = clock64();
+        if ((int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1)
+            atomicAdd(&g_step_cycles[i], (unsigned long long)(now - t));
+        t = now;
+    }
+};
+#define STEP_T(x) x
+#else
+#define STEP_T(x)
+#endif
+
 // ----------------------------------------------------------------- scene view
 struct DevScene {
     const pbrt_shape_desc* shapes;
     const pbrt_material_desc* materials;
     const pbrt_primitive_desc* prims;
     const struct DevNode* nodes;   // device copy of pbrt_bvh_node[], 64-byte records
+    const struct DevNode* lnodes_unused;   // (layout slot kept; see g_nodes_lds / use_lds_nodes)
+    const struct DevPrim* fprims;  // primitive + its shape in one record (leaf tests)
     const pbrt_light_desc* lights;
     const pbrt_camera_desc* camera;
     const pbrt_film_desc* film;
     const pbrt_distribution_desc* dist;   // Path light distribution (may be null)
-    int n_prims, n_nodes, n_lights, pad;
+    int n_prims, n_nodes, n_lights;
+    int use_lds_nodes;   // the kernel staged nodes[] in g_nodes_lds (uniform)
 };
 
 // ---------------------------------------------------------------- PCG32 (rng.go)
@@ -282,26 +304,32 @@ __device__ inline void shape_si(const pbrt_shape_desc& s, const Ray& r, V3 ph, S
     else disk_si(s, ray, ph, si);
 }
 
+// A primitive with a copy of its shape: a leaf test reads one record (one
+// dependent memory level) instead of primitive -> shape.
+struct alignas(16) DevPrim {
+    pbrt_shape_desc shape;
+    pbrt_transform prim_to_world;   // TransformedPrimitive only
+    int32_t kind, material, prim_identity, pad;
+};
+
 // Shape test without the SurfaceInteraction: the hit parameter and point.
 __device__ inline bool prim_hit_t(const DevScene& sc, int pi, const Ray& r, double& t_hit, V3& ph, int& panic) {
-    const pbrt_primitive_desc& p = sc.prims[pi];
-    const pbrt_shape_desc& s = sc.shapes[p.shape];
+    const DevPrim& p = sc.fprims[pi];
     Ray ray = r;
     if (p.kind == PBRT_PRIM_TRANSFORMED) ray = xf_ray(p.prim_to_world.m_inv, r, nullptr, nullptr);
-    return shape_hit(s, ray, t_hit, ph, panic);
+    return shape_hit(p.shape, ray, t_hit, ph, panic);
 }
 
 // GeometricPrimitive / TransformedPrimitive (primitive.go:42-115): the
 // interaction of primitive pi at its accepted hit point ph (shape space).
 __device__ inline void prim_si(const DevScene& sc, int pi, const Ray& r, V3 ph, SI& si) {
-    const pbrt_primitive_desc& p = sc.prims[pi];
-    const pbrt_shape_desc& s = sc.shapes[p.shape];
+    const DevPrim& p = sc.fprims[pi];
     const bool xformed = p.kind == PBRT_PRIM_TRANSFORMED;
     Ray ray = r;
     if (xformed) ray = xf_ray(p.prim_to_world.m_inv, r, nullptr, nullptr);
-    shape_si(s, ray, ph, si);
+    shape_si(p.shape, ray, ph, si);
     si.prim = pi;
-    if (xformed && !is_identity(p.prim_to_world.m)) transform_si_shared(si, p.prim_to_world.m, p.prim_to_world.m_inv);
+    if (xformed && !p.prim_identity) transform_si_shared(si, p.prim_to_world.m, p.prim_to_world.m_inv);
 }
 __device__ inline bool prim_intersect_p(const DevScene& sc, int pi, const Ray& r, int& panic) {
     double t_hit;
@@ -326,19 +354,32 @@ struct NodeView {
     double b[6];
     uint32_t offset, n_prims, axis;
 };
-__device__ __forceinline__ NodeView load_node(const DevNode* nodes, uint32_t i) {
-    const ulonglong2* q = reinterpret_cast<const ulonglong2*>(nodes + i);
-    const ulonglong2 a = q[0], b = q[1], c = q[2], d = q[3];
+// BVH nodes staged in LDS by kernels whose scene fits (README / Cornell:
+// <= 45 nodes). A file-scope __shared__ array, so every access is a ds_read.
+constexpr int kLdsNodes = 128;
+__shared__ DevNode g_nodes_lds[kLdsNodes];
+
+__device__ __forceinline__ NodeView load_node(const DevScene& sc, uint32_t i) {
+    uint64_t w[7];
+    if (sc.use_lds_nodes) {   // uniform
+        const DevNode& n = g_nodes_lds[i];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            w[k] = __builtin_bit_cast(uint64_t, n.bmin[k]);
+            w[3 + k] = __builtin_bit_cast(uint64_t, n.bmax[k]);
+        }
+        w[6] = (uint64_t)n.offset | ((uint64_t)n.nprims_axis << 32);
+    } else {
+        const ulonglong2* q = reinterpret_cast<const ulonglong2*>(sc.nodes + i);
+        const ulonglong2 a = q[0], b = q[1], c = q[2], d = q[3];
+        w[0] = a.x; w[1] = a.y; w[2] = b.x; w[3] = b.y; w[4] = c.x; w[5] = c.y; w[6] = d.x;
+    }
     NodeView v;
-    v.b[0] = __builtin_bit_cast(double, a.x);
-    v.b[1] = __builtin_bit_cast(double, a.y);
-    v.b[2] = __builtin_bit_cast(double, b.x);
-    v.b[3] = __builtin_bit_cast(double, b.y);
-    v.b[4] = __builtin_bit_cast(double, c.x);
-    v.b[5] = __builtin_bit_cast(double, c.y);
-    v.offset = (uint32_t)d.x;
-    v.n_prims = (uint32_t)(d.x >> 32) & 0xFFFFu;
-    v.axis = (uint32_t)(d.x >> 48) & 0xFFu;
+#pragma unroll
+    for (int k = 0; k < 6; k++) v.b[k] = __builtin_bit_cast(double, w[k]);
+    v.offset = (uint32_t)w[6];
+    v.n_prims = (uint32_t)(w[6] >> 32) & 0xFFFFu;
+    v.axis = (uint32_t)(w[6] >> 48) & 0xFFu;
     return v;
 }
 // Bounds3.IntersectP (bounds.go:149-185); (1 + 2*Gamma(3)) == 1 exactly.
@@ -378,21 +419,24 @@ __device__ __forceinline__ bool node_hit(const NodeView& nd, const Ray& r, V3 in
 // equals the reference's per-hit SurfaceInteraction: every field is a function
 // of that hit point and of the (unchanged) ray, and the shared-interaction
 // aliasing of TransformedPrimitive (#20) only ever touches the last one.
-template <bool kAny>
-__device__ inline bool bvh_traverse(const DevScene& sc, Ray& ray, SI* si, uint16_t* stack, int& panic) {
+//
+// bvh_walk leaves the closest primitive in `best` (-1: none) and its hit point
+// in `best_ph`; kStride is the distance between a lane's stack entries (the
+// block size: one uint16 column per thread).
+template <bool kAny, int kStride = kStackStride>
+__device__ inline bool bvh_walk(const DevScene& sc, Ray& ray, uint16_t* stack, int& panic, int& best, V3& best_ph) {
+    best = -1;
     if (sc.n_nodes == 0) return false;
-    const double ray_tmax0 = ray.tmax;
     V3 inv{1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z};
     const int nx = inv.x < 0, ny = inv.y < 0, nz = inv.z < 0;
     const uint32_t negmask = (uint32_t)nx | ((uint32_t)ny << 1) | ((uint32_t)nz << 2);
     uint32_t to_visit = 0, cur = 0;
-    int best = -1;
-    V3 best_ph{0, 0, 0};
+    STEP_T(StepTimer tt; tt.start();)
     for (;;) {
         // A: interior nodes
         bool leaf = false, done = false;
         for (;;) {
-            const NodeView nd = load_node(sc.nodes, cur);
+            const NodeView nd = load_node(sc, cur);
             if (node_hit(nd, ray, inv, nx, ny, nz)) {
                 if (nd.n_prims > 0) {
                     leaf = true;
@@ -405,20 +449,21 @@ __device__ inline bool bvh_traverse(const DevScene& sc, Ray& ray, SI* si, uint16
                 uint32_t far_node, near_node;
                 if ((negmask >> nd.axis) & 1u) { far_node = cur + 1; near_node = nd.offset; }
                 else { far_node = nd.offset; near_node = cur + 1; }
-                stack[(to_visit++) * kStackStride] = (uint16_t)far_node;
+                stack[(to_visit++) * kStride] = (uint16_t)far_node;
                 cur = near_node;
             } else {
                 if (to_visit == 0) {
                     done = true;
                     break;
                 }
-                cur = stack[(--to_visit) * kStackStride];
+                cur = stack[(--to_visit) * kStride];
             }
         }
+        STEP_T(if (!kAny) tt.mark(5);)
         if (done) break;
         (void)leaf;
         // B: the leaf's primitives
-        const NodeView nd = load_node(sc.nodes, cur);
+        const NodeView nd = load_node(sc, cur);
         const uint32_t first = nd.offset, np = nd.n_prims;
         for (uint32_t i = 0; i < np; i++) {
             double t_hit;
@@ -432,12 +477,22 @@ __device__ inline bool bvh_traverse(const DevScene& sc, Ray& ray, SI* si, uint16
                 best_ph = ph;
             }
         }
+        STEP_T(if (!kAny) tt.mark(6);)
         if (to_visit == 0) break;
-        cur = stack[(--to_visit) * kStackStride];
+        cur = stack[(--to_visit) * kStride];
     }
-    if (!kAny && best >= 0) prim_si(sc, best, ray, best_ph, *si);
-    (void)ray_tmax0;
+    STEP_T(if (!kAny) tt.mark(6);)
     return best >= 0;
+}
+template <bool kAny>
+__device__ inline bool bvh_traverse(const DevScene& sc, Ray& ray, SI* si, uint16_t* stack, int& panic) {
+    int best;
+    V3 best_ph{0, 0, 0};
+    const bool hit = bvh_walk<kAny>(sc, ray, stack, panic, best, best_ph);
+    STEP_T(StepTimer tt; tt.start();)
+    if (!kAny && best >= 0) prim_si(sc, best, ray, best_ph, *si);
+    STEP_T(if (!kAny) tt.mark(7);)
+    return hit;
 }
 
 // ----------------------------------------------------------------- material
@@ -698,8 +753,10 @@ __device__ inline Spec uniform_sample_one_light(const DevScene& sc, Thread& t, c
 }
 
 // -------------------------------------------------------------- integrators
-// Path.Li (path.go:32-157)
-__device__ inline Spec path_li(const DevScene& sc, Thread& t, Ray ray, int max_depth, double rr_threshold) {
+// Path.Li (path.go:32-157). Out of line in the serial kernel: fully inlined
+// into k_render_exact the compiler produced a kernel that faulted only after
+// other kernels had run on the device (an uninitialized-register read).
+__device__ __noinline__ Spec path_li(const DevScene& sc, Thread& t, Ray ray, int max_depth, double rr_threshold) {
     Spec L = spec(0), beta = spec(1);
     int32_t bounces = 0;
     const double eta_scale = 1.0;
@@ -742,7 +799,7 @@ __device__ inline Spec path_li(const DevScene& sc, Thread& t, Ray ray, int max_d
 }
 
 // DirectLighting.Li at depth 0 (directlighting.go:62-104)
-__device__ inline Spec direct_li(const DevScene& sc, Thread& t, Ray ray, int max_depth, int strategy) {
+__device__ __noinline__ Spec direct_li(const DevScene& sc, Thread& t, Ray ray, int max_depth, int strategy) {
     Spec L = spec(0);
     SI si;
     t.bounce = 1;

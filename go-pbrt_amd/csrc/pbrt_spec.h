@@ -120,6 +120,7 @@ struct ChainCache {
 template <bool kNEE, class Cache>
 __device__ inline Spec spec_path(const DevScene& sc, const Cache& pc, const SpecSampler& ss, Cursor& c,
                                  int max_depth, double rr_threshold, uint16_t* stack, int& panic, int& bounce) {
+    STEP_T(StepTimer tm; tm.start();)
     Spec L = spec(0), beta = spec(1);
     int32_t bounces = 1;
     bounce = 1;
@@ -134,12 +135,16 @@ __device__ inline Spec spec_path(const DevScene& sc, const Cache& pc, const Spec
             bounces++;
             bounce = bounces;
             if (bounces >= max_depth) break;
-            if (!bvh_traverse<false>(sc, ray, &isect, stack, panic)) break;
+            STEP_T(tm.mark(0);)
+            const bool hit = bvh_traverse<false>(sc, ray, &isect, stack, panic);
+            STEP_T(tm.mark(1);)
+            if (!hit) break;
             if (panic) break;
             if (compute_bsdf(sc, isect, b) < 0) {
                 panic = -1;
                 break;
             }
+            STEP_T(tm.mark(2);)
             wo = ray.d;
         }
         if (b.n_bxdfs > 0) {   // UniformSampleOneLight (integrator.go:48-77)
@@ -180,6 +185,7 @@ __device__ inline Spec spec_path(const DevScene& sc, const Cache& pc, const Spec
                 c_get2d(c, ss);
             }
         }
+        STEP_T(tm.mark(3);)
         first = false;
         V2 u = c_get2d(c, ss);
         V3 wi;
@@ -200,8 +206,46 @@ __device__ inline Spec spec_path(const DevScene& sc, const Cache& pc, const Spec
             if (u1 < q) break;
             beta = sdivs(beta, 1 - q);
         }
+        STEP_T(tm.mark(4);)
     }
     return L;
+}
+
+// The rest of one spec_path<false> iteration once the interaction at bounce
+// `bounces` and its BSDF are known (light draws consumed, BSDF sample,
+// throughput, Russian roulette), then the next iteration's depth test; the
+// wavefront chain kernels (k_wf_*) run a trajectory one such step per launch.
+// Returns 0: trace `ray` next; 1: the trajectory ended (D = c.draws);
+// 2: its draw count depends on the sample index (kBadD).
+__device__ inline int traj_scatter(const DevScene& sc, const SI& isect, const BSDF& b, V3 wo, Cursor& c,
+                                   const SpecSampler& ss, Spec& beta, int& bounces, Ray& ray, int max_depth,
+                                   double rr_threshold) {
+    if (b.n_bxdfs > 0 && sc.n_lights > 0) {   // UniformSampleOneLight's draws
+        c_skip1d(c, ss);
+        c_get2d(c, ss);
+        c_get2d(c, ss);
+    }
+    V2 u = c_get2d(c, ss);
+    V3 wi;
+    double pdf;
+    Spec f = bsdf_sample_f(b, wo, u, wi, pdf);
+    if (is_black(f) || pdf == 0.0) return 1;
+    double wp = absdot(wi, isect.sn) / pdf;
+    beta = smul(beta, smuls(f, wp));
+    ray.o = offset_ray_origin(isect.p, isect.perr, isect.n, wi);
+    ray.d = wi;
+    ray.tmax = kInf;
+    ray.time = isect.time;
+    Spec rr = smuls(beta, 1.0);
+    if (max_component(rr) < rr_threshold && bounces > 3) {
+        double q = gomath::max(0.05, 1 - max_component(rr));
+        double u1 = c_get1d(c, ss);
+        if (c.kdep) return 2;
+        if (u1 < q) return 1;
+        beta = sdivs(beta, 1 - q);
+    }
+    bounces++;
+    return bounces >= max_depth ? 1 : 0;
 }
 
 }  // namespace pbrt

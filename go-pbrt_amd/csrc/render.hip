@@ -254,6 +254,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kMinWaves
 //   k_film   one thread per tile-film pixel: FilmTile.AddSample contributions
 //            summed in the reference's order (pixels row-major, samples in
 //            order), i.e. the same floating-point sums as the serial replay.
+__device__ __forceinline__ void stage_nodes(DevScene& sc) {
+    if (sc.n_nodes > kLdsNodes) return;
+    for (int i = threadIdx.x; i < sc.n_nodes; i += blockDim.x) g_nodes_lds[i] = sc.nodes[i];
+    __syncthreads();
+    sc.use_lds_nodes = 1;
+}
+
 struct PixelRec {
     SI si;
     BSDF b;
@@ -302,6 +309,102 @@ struct GroupState {
 };
 constexpr int kMaxGroups = 16;
 
+// Stratified.StartPixel (stratified.go:21-48) for one pixel, by the whole
+// 64-lane workgroup (all lanes call it). The shuffled 1D values are left in
+// s1d (LDS); returns the PCG32 state after the pixel's draws.
+__device__ uint64_t start_pixel_wave(const RenderParams& rp, const PcgJump& J, uint64_t S, uint64_t inc, double* s1d,
+                                     uint16_t* other, uint32_t* vbuf, uint64_t* sh_state) {
+    const int lane = threadIdx.x;
+    const int n = rp.spp, ndims = rp.ndims;
+    const double inv_n = 1.0 / (double)n;
+    const int s1 = rp.jitter ? 2 * n : n, s2 = rp.jitter ? 3 * n : n;   // StartPixel draws per 1D / 2D dim
+    // StartPixel (stratified.go:21-48). The pixel's draws form a fixed
+    // list of E events (jitter floats and pcg_bounded picks,
+    // sampling.go:101-145). A pick retries on v < 2^32 mod b, which
+    // the reference's (rot+1)&31 output rotation makes common (v < 4
+    // has probability ~1/64), so event e lands on draw e + R(e),
+    // R(e) = rejections before it. Lanes fill the raw stream by
+    // jump-ahead, then resolve R chunk by chunk: one ballot per
+    // rejection shifts every later event by one draw.
+    bool serial_sp = rp.sp_serial != 0;
+    if (!serial_sp) {
+        const int E = rp.sp_events, V = rp.sp_draws;
+        uint64_t st = pcg_advance(J, S, inc, (uint64_t)lane);
+        for (int t = lane; t < V; t += kWave) {
+            vbuf[t] = pcg_output(st);
+            st = J.a[6] * st + inc * J.b[6];   // +64 draws
+        }
+        __syncthreads();
+        int R = 0;
+        bool overflow = false;
+        for (int cb = 0; cb < E; cb += kWave) {
+            const int e = cb + lane;
+            int kind = 0, slt = 0, i = 0;   // 0 none, 1 1D float, 2 1D pick, 3 2D pick
+            if (e < E) {
+                if (e < ndims * s1) {
+                    const int d = e / s1, qq = e - d * s1;
+                    if (rp.jitter && qq < n) { kind = 1; slt = d * n + qq; }
+                    else { kind = 2; i = qq - (rp.jitter ? n : 0); slt = d * n + i; }
+                } else {
+                    const int e2 = e - ndims * s1, d = e2 / s2, qq = e2 - d * s2;
+                    if (!(rp.jitter && qq < 2 * n)) { kind = 3; i = qq - (rp.jitter ? 2 * n : 0); }
+                }
+            }
+            const uint32_t b = (uint32_t)(n - i);
+            const uint32_t thr = kind >= 2 ? (~b + 1u) % b : 0u;
+            int local = 0;
+            for (;;) {
+                const int t = e + R + local;
+                const bool out = kind != 0 && t >= V;
+                const bool bad = !out && kind >= 2 && vbuf[t] < thr;
+                if (__any(out)) { overflow = true; break; }
+                const unsigned long long m = __ballot(bad);
+                if (m == 0) break;
+                const int first = __ffsll((long long)m) - 1;
+                if (lane >= first) local++;
+            }
+            if (overflow) break;
+            const uint32_t v = kind != 0 ? vbuf[e + R + local] : 0u;
+            if (kind == 1)
+                s1d[slt] = gomath::min(((double)(slt % n) + pcg_float_of(v)) * inv_n, gomath::kOneMinusEpsilon);
+            else if (kind == 2)
+                other[slt] = (uint16_t)(i + (int)(v % b));
+            R += __shfl(local, kWave - 1);
+        }
+        serial_sp = overflow;
+        if (!serial_sp) {
+            if (!rp.jitter)
+                for (int idx = lane; idx < ndims * n; idx += kWave)
+                    s1d[idx] = gomath::min(((double)(idx % n) + 0.5) * inv_n, gomath::kOneMinusEpsilon);
+            __syncthreads();
+            if (lane < ndims) {
+                double* samp = s1d + lane * n;
+                const uint16_t* oth = other + lane * n;
+                for (int k = 0; k < n; k++) {
+                    const int o = oth[k];
+                    double a = samp[k];
+                    samp[k] = samp[o];
+                    samp[o] = a;
+                }
+            }
+            if (lane == 0) *sh_state = pcg_advance(J, S, inc, (uint64_t)(E + R));
+        }
+    }
+    if (serial_sp || (rp.flags & PBRT_FLAG_SERIAL_START_PIXEL)) {
+        if (lane == 0) {   // serial replay (huge sample counts, or forced)
+            Thread t;
+            t.rng.state = S;
+            t.rng.inc = inc;
+            t.spp = n; t.ndims = ndims; t.xs = rp.xs; t.ys = rp.ys; t.jitter = rp.jitter;
+            t.s1d = s1d;
+            start_pixel(t);
+            *sh_state = t.rng.state;
+        }
+    }
+    __syncthreads();
+    return *sh_state;
+}
+
 template <int kWaves>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8))) void k_chain(
     DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
@@ -312,6 +415,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8
     __shared__ GroupState gs[kMaxGroups];
     __shared__ uint64_t sh_state;
     const int lane = threadIdx.x;
+    stage_nodes(sc);
     const int L = lanes_per_tile, G = kWave / L;
     const int g = lane / L, gl = lane - g * L;
     const PcgJump& J = *jump;
@@ -322,8 +426,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8
     uint32_t* vbuf = (uint32_t*)(lds + lay.vbuf);
     uint16_t* stack = stack_lds + lane;
     const int n = rp.spp, ndims = rp.ndims;
-    const double inv_n = 1.0 / (double)n;
-    const int s1 = rp.jitter ? 2 * n : n, s2 = rp.jitter ? 3 * n : n;   // StartPixel draws per 1D / 2D dim
     const pbrt_camera_desc& cam = *sc.camera;
     unsigned long long windows = 0;
     unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -371,91 +473,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8
                 int64_t x0, y0, x1, y1;
                 tile_bounds(rp, tile, x0, y0, x1, y1);
                 const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
-                // StartPixel (stratified.go:21-48). The pixel's draws form a fixed
-                // list of E events (jitter floats and pcg_bounded picks,
-                // sampling.go:101-145). A pick retries on v < 2^32 mod b, which
-                // the reference's (rot+1)&31 output rotation makes common (v < 4
-                // has probability ~1/64), so event e lands on draw e + R(e),
-                // R(e) = rejections before it. Lanes fill the raw stream by
-                // jump-ahead, then resolve R chunk by chunk: one ballot per
-                // rejection shifts every later event by one draw.
-                bool serial_sp = rp.sp_serial != 0;
-                if (!serial_sp) {
-                    const int E = rp.sp_events, V = rp.sp_draws;
-                    uint64_t st = pcg_advance(J, S, inc, (uint64_t)lane);
-                    for (int t = lane; t < V; t += kWave) {
-                        vbuf[t] = pcg_output(st);
-                        st = J.a[6] * st + inc * J.b[6];   // +64 draws
-                    }
-                    __syncthreads();
-                    int R = 0;
-                    bool overflow = false;
-                    for (int cb = 0; cb < E; cb += kWave) {
-                        const int e = cb + lane;
-                        int kind = 0, slt = 0, i = 0;   // 0 none, 1 1D float, 2 1D pick, 3 2D pick
-                        if (e < E) {
-                            if (e < ndims * s1) {
-                                const int d = e / s1, qq = e - d * s1;
-                                if (rp.jitter && qq < n) { kind = 1; slt = d * n + qq; }
-                                else { kind = 2; i = qq - (rp.jitter ? n : 0); slt = d * n + i; }
-                            } else {
-                                const int e2 = e - ndims * s1, d = e2 / s2, qq = e2 - d * s2;
-                                if (!(rp.jitter && qq < 2 * n)) { kind = 3; i = qq - (rp.jitter ? 2 * n : 0); }
-                            }
-                        }
-                        const uint32_t b = (uint32_t)(n - i);
-                        const uint32_t thr = kind >= 2 ? (~b + 1u) % b : 0u;
-                        int local = 0;
-                        for (;;) {
-                            const int t = e + R + local;
-                            const bool out = kind != 0 && t >= V;
-                            const bool bad = !out && kind >= 2 && vbuf[t] < thr;
-                            if (__any(out)) { overflow = true; break; }
-                            const unsigned long long m = __ballot(bad);
-                            if (m == 0) break;
-                            const int first = __ffsll((long long)m) - 1;
-                            if (lane >= first) local++;
-                        }
-                        if (overflow) break;
-                        const uint32_t v = kind != 0 ? vbuf[e + R + local] : 0u;
-                        if (kind == 1)
-                            s1d[slt] = gomath::min(((double)(slt % n) + pcg_float_of(v)) * inv_n, gomath::kOneMinusEpsilon);
-                        else if (kind == 2)
-                            other[slt] = (uint16_t)(i + (int)(v % b));
-                        R += __shfl(local, kWave - 1);
-                    }
-                    serial_sp = overflow;
-                    if (!serial_sp) {
-                        if (!rp.jitter)
-                            for (int idx = lane; idx < ndims * n; idx += kWave)
-                                s1d[idx] = gomath::min(((double)(idx % n) + 0.5) * inv_n, gomath::kOneMinusEpsilon);
-                        __syncthreads();
-                        if (lane < ndims) {
-                            double* samp = s1d + lane * n;
-                            const uint16_t* oth = other + lane * n;
-                            for (int k = 0; k < n; k++) {
-                                const int o = oth[k];
-                                double a = samp[k];
-                                samp[k] = samp[o];
-                                samp[o] = a;
-                            }
-                        }
-                        if (lane == 0) sh_state = pcg_advance(J, S, inc, (uint64_t)(E + R));
-                    }
-                }
-                if (serial_sp || (rp.flags & PBRT_FLAG_SERIAL_START_PIXEL)) {
-                    if (lane == 0) {   // serial replay (huge sample counts, or forced)
-                        Thread t;
-                        t.rng.state = S;
-                        t.rng.inc = inc;
-                        t.spp = n; t.ndims = ndims; t.xs = rp.xs; t.ys = rp.ys; t.jitter = rp.jitter;
-                        t.s1d = s1d;
-                        start_pixel(t);
-                        sh_state = t.rng.state;
-                    }
-                }
-                __syncthreads();
-                const uint64_t S1 = sh_state;   // after StartPixel
+                const uint64_t S1 = start_pixel_wave(rp, J, S, inc, s1d, other, vbuf, &sh_state);
                 double* gs1d = wb.s1d + rec * wb.s1d_stride;
                 for (int idx = lane; idx < ndims * n; idx += kWave) gs1d[idx] = s1d[idx];
                 mark(0);
@@ -577,6 +595,7 @@ __global__ __launch_bounds__(kWave) void k_paths(DevScene sc, RenderParams rp, W
     __shared__ PixelCache pc;
     __shared__ unsigned long long sh_pkey;   // (sample << 32) | (bounce << 8) | (kind + 1): min = first panic
     const int lane = threadIdx.x;
+    stage_nodes(sc);
     const int64_t bslot = blockIdx.x / wb.ppt, pi = blockIdx.x % wb.ppt;
     if (pi >= wb.tile_npx[bslot]) return;
     const int64_t rec = blockIdx.x;
@@ -726,6 +745,392 @@ __global__ void k_panic_reduce(WaveBufs wb, int64_t slot_base, int64_t nslots_ba
     }
 }
 
+// ------------------------------------------- EXACT, wavefront chain (k_wf_*)
+// The same speculative-offset chain as k_chain, reorganised so that the
+// trajectory bounces run as wide, register-light kernels instead of inside
+// one 350-register wave per tile:
+//   k_wf_primary  once per batch, one thread per pixel record: the camera
+//                 ray's first hit and BSDF (bounce 1 is the same for every
+//                 sample of a pixel, pbrt_spec.h) -> PixelRec.
+//   per window iteration (host loop, all tiles of the batch together):
+//   k_wf_tile     one wave per tile: walk the chain through the previous
+//                 window's draw counts, StartPixel + the PixelRec of the next
+//                 pixel when the current one is resolved, then the window's
+//                 64 candidates (RNG offsets head + 2j) take their bounce-1
+//                 scattering step; live ones are queued for bounce 2.
+//   k_wf_trace    closest hit of every queued ray (a thread per ray).
+//   k_wf_shade    interaction + BSDF + scattering step; queue for the next
+//                 bounce or record the candidate's draw count D.
+//   k_wf_tail     bounces past the split levels, one thread per trajectory.
+// Trajectories are compacted into dense queues between bounces, so a wave's
+// lanes stay busy however long the other trajectories of its window are.
+constexpr int kWfCand = 64;        // candidates per tile and window
+constexpr int kWfBlock = 256;      // threads per block of the bounce kernels
+constexpr int kWfMaxLevels = 16;   // split bounce levels (trace + shade launches)
+
+struct TileState {
+    uint64_t S;       // PCG32 state at the chain head
+    int32_t pi, npx;  // current pixel, pixels of the tile
+    int32_t kh;       // next sample without an offset
+    int32_t phase;    // 0 needs a pixel (first iteration), 1 window in flight, 2 finished
+    int32_t windows;
+    int32_t pad;
+};
+struct WfBufs {
+    TileState* ts;      // [nb]
+    uint64_t* start;    // [nb * C] PCG state at each candidate's offset
+    uint32_t* D;        // [nb * C] draws of the candidate's trajectory, or kBadD
+    uint64_t* rng;      // [cap] trajectory cursor: PCG state
+    uint32_t* draws;    // [cap]
+    uint32_t* meta;     // [cap] cur1d | cur2d << 8 | bounces << 16
+    double* beta;       // [3][cap]
+    double* ray;        // [6][cap] origin, direction
+    int32_t* hprim;     // [cap] closest primitive, -1 miss, -2 reference panic
+    double* hph;        // [3][cap] its hit point (shape space)
+    uint32_t* q[3];     // ids of rays to trace: split levels by parity, tail
+    uint32_t* cnt;      // [2][kWfMaxLevels + 1] queue lengths by iteration parity (last: tail)
+    uint32_t* finished; // tiles done
+    int64_t cap;        // nb * C
+};
+
+__device__ __forceinline__ uint64_t pcg_inc_of(uint64_t seed) { return (seed << 1) | 1; }   // rng.go:28-34
+
+// Append the ids of the lanes with push set to q (one atomic per wave). All
+// lanes of the wave call it.
+__device__ __forceinline__ void wf_push(uint32_t* q, uint32_t* cnt, bool push, uint32_t id) {
+    const unsigned long long m = __ballot(push);
+    if (m == 0) return;
+    const int lane = (int)(threadIdx.x & 63);
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(cnt, (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    if (push) q[base + (uint32_t)__popcll(m & ((1ULL << lane) - 1ULL))] = id;
+}
+__device__ __forceinline__ void wf_store(const WfBufs& wf, uint32_t id, const Cursor& c, int bounces, Spec beta,
+                                         const Ray& r) {
+    const int64_t cap = wf.cap;
+    wf.rng[id] = c.rng.state;
+    wf.draws[id] = c.draws;
+    wf.meta[id] = (uint32_t)c.cur1d | ((uint32_t)c.cur2d << 8) | ((uint32_t)bounces << 16);
+    wf.beta[id] = beta.r;
+    wf.beta[cap + id] = beta.g;
+    wf.beta[2 * cap + id] = beta.b;
+    wf.ray[id] = r.o.x;
+    wf.ray[cap + id] = r.o.y;
+    wf.ray[2 * cap + id] = r.o.z;
+    wf.ray[3 * cap + id] = r.d.x;
+    wf.ray[4 * cap + id] = r.d.y;
+    wf.ray[5 * cap + id] = r.d.z;
+}
+__device__ __forceinline__ Ray wf_ray(const WfBufs& wf, uint32_t id) {
+    const int64_t cap = wf.cap;
+    Ray r;
+    r.o = V3{wf.ray[id], wf.ray[cap + id], wf.ray[2 * cap + id]};
+    r.d = V3{wf.ray[3 * cap + id], wf.ray[4 * cap + id], wf.ray[5 * cap + id]};
+    r.tmax = kInf;
+    r.time = 0;
+    return r;
+}
+// queue of split level `level` (or the tail queue) and its length slot
+__device__ __forceinline__ uint32_t* wf_queue(const WfBufs& wf, int level, int n_levels) {
+    return level >= n_levels ? wf.q[2] : wf.q[level & 1];
+}
+__device__ __forceinline__ uint32_t* wf_count(const WfBufs& wf, int par, int level, int n_levels) {
+    return wf.cnt + par * (kWfMaxLevels + 1) + (level >= n_levels ? kWfMaxLevels : level);
+}
+
+__global__ void k_wf_init(RenderParams rp, WaveBufs wb, WfBufs wf, int64_t slot_base, int64_t nb) {
+    const int64_t bs = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (bs >= nb) return;
+    int64_t x0, y0, x1, y1;
+    const int64_t tile = tile_of_slot(rp, slot_base + bs);
+    tile_bounds(rp, tile, x0, y0, x1, y1);
+    Pcg seed;
+    pcg_seed(seed, (uint64_t)tile);   // Sampler.Clone(tile), integrator.go:318,328
+    TileState t;
+    t.S = seed.state;
+    t.pi = 0;
+    t.npx = (int32_t)((x1 - x0) * (y1 - y0));
+    t.kh = 1;
+    t.phase = t.npx > 0 ? 0 : 2;
+    t.windows = 0;
+    t.pad = 0;
+    wf.ts[bs] = t;
+    wb.tile_npx[bs] = 0;
+    if (t.phase == 2) atomicAdd(wf.finished, 1u);
+}
+
+// Bounce 1 of every pixel record of the batch: the camera ray through the
+// pixel corner (pFilm and pLens are (0,0) for every sample), its closest hit
+// and BSDF. The ray time is patched by k_wf_tile once StartPixel gives it.
+__global__ __launch_bounds__(kWave) void k_wf_primary(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
+                                                      int64_t nb) {
+    __shared__ uint16_t stack_lds[64 * kStackStride];
+    stage_nodes(sc);
+    const int64_t rec = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (rec >= nb * wb.ppt) return;
+    const int64_t bs = rec / wb.ppt, pi = rec % wb.ppt;
+    int64_t x0, y0, x1, y1;
+    tile_bounds(rp, tile_of_slot(rp, slot_base + bs), x0, y0, x1, y1);
+    if (pi >= (x1 - x0) * (y1 - y0)) return;
+    const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
+    int panic0 = 0, hit0 = 0;
+    SI si0;
+    BSDF b0;
+    b0.n_bxdfs = 0;
+    Ray ray = camera_ray(*sc.camera, (double)px + 0.0, (double)py + 0.0, 0.0, V2{0.0, 0.0});
+    if (rp.spp > 1 && 1 < rp.max_depth) {
+        hit0 = bvh_traverse<false>(sc, ray, &si0, stack_lds + threadIdx.x, panic0) ? 1 : 0;
+        if (!panic0 && hit0 && compute_bsdf(sc, si0, b0) < 0) panic0 = -1;
+    }
+    PixelRec& pr = wb.prec[rec];
+    pr.si = si0;
+    pr.b = b0;
+    pr.wo = ray.d;
+    pr.hit = panic0 ? 0 : hit0;
+    pr.panic0 = panic0;
+    pr.nvalid = rp.spp;
+}
+
+__global__ __launch_bounds__(kWave) void k_wf_tile(DevScene sc, RenderParams rp, ChainLayout lay,
+                                                   const PcgJump* __restrict__ jump, WaveBufs wb, WfBufs wf,
+                                                   int64_t slot_base, int par, int n_levels) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ uint64_t sh_state;
+    const int lane = threadIdx.x;
+    const int64_t bs = blockIdx.x;
+    if (bs == 0 && lane <= kWfMaxLevels) wf.cnt[(par ^ 1) * (kWfMaxLevels + 1) + lane] = 0;
+    TileState st = wf.ts[bs];
+    if (st.phase == 2) return;
+    const PcgJump& J = *jump;
+    const int64_t tile = tile_of_slot(rp, slot_base + bs);
+    const uint64_t inc = pcg_inc_of((uint64_t)tile);
+    const int n = rp.spp, ndims = rp.ndims;
+    if (st.phase == 1) {   // walk the chain through the last window
+        const uint32_t dj = wf.D[bs * kWfCand + lane];
+        const uint64_t sj = wf.start[bs * kWfCand + lane];
+        const int64_t rec = bs * wb.ppt + st.pi;
+        uint64_t x = 0;
+        int k = st.kh;
+        while (k < n) {
+            if ((x & 1) || (x >> 1) >= (uint64_t)kWfCand) break;
+            const int jj = (int)(x >> 1);
+            const uint32_t d = __shfl(dj, jj);
+            if (d == kBadD) break;
+            const uint64_t s = __shfl(sj, jj);
+            if (lane == 0) wb.memb[rec * n + k] = s;
+            k++;
+            x += d;
+        }
+        if (k == st.kh) {   // the exact head's trajectory panics: the tile ends at this sample
+            if (lane == 0) {
+                wb.memb[rec * n + k] = st.S;
+                wb.prec[rec].nvalid = k + 1;
+            }
+            st.phase = 2;
+        } else {
+            st.kh = k;
+            st.S = pcg_advance(J, st.S, inc, x);
+            if (k >= n) {   // every sample of the pixel has its offset
+                st.pi++;
+                st.phase = st.pi < st.npx ? 0 : 2;
+            }
+        }
+    }
+    while (st.phase == 0) {   // StartPixel, then the pixel's bounce-1 record
+        double* s1d = (double*)(lds + lay.s1d);
+        uint16_t* other = (uint16_t*)(lds + lay.other);
+        uint32_t* vbuf = (uint32_t*)(lds + lay.vbuf);
+        const int64_t rec = bs * wb.ppt + st.pi;
+        const uint64_t S1 = start_pixel_wave(rp, J, st.S, inc, s1d, other, vbuf, &sh_state);
+        double* gs1d = wb.s1d + rec * wb.s1d_stride;
+        for (int idx = lane; idx < ndims * n; idx += kWave) gs1d[idx] = s1d[idx];
+        PixelRec& pr = wb.prec[rec];
+        const int hit0 = pr.hit, panic0 = pr.panic0;
+        if (lane == 0) {
+            if (hit0) {   // the camera ray's time (Get1D after pFilm, pLens) of the pixel's first traced sample
+                int64_t x0, y0, x1, y1;
+                tile_bounds(rp, tile, x0, y0, x1, y1);
+                const int64_t px = x0 + st.pi % (x1 - x0), py = y0 + st.pi / (x1 - x0);
+                pr.si.time = camera_ray(*sc.camera, (double)px, (double)py, s1d[1 < n ? 1 : 0], V2{0.0, 0.0}).time;
+            }
+            wb.tile_npx[bs] = st.pi + 1;
+        }
+        st.S = S1;
+        if (panic0) {   // the first traced sample panics at bounce 1: the tile ends here
+            st.phase = 2;
+        } else if (hit0) {
+            st.kh = 1;
+            st.phase = 1;
+        } else {   // no traced bounce: every sample is black and draws nothing
+            st.pi++;
+            st.phase = st.pi < st.npx ? 0 : 2;
+        }
+        __syncthreads();
+    }
+    if (st.phase == 1) {   // the window: candidate lane at offset head + 2 * lane, bounce-1 step
+        const int64_t rec = bs * wb.ppt + st.pi;
+        const uint32_t id = (uint32_t)(bs * kWfCand + lane);
+        const uint64_t s0 = pcg_advance(J, st.S, inc, 2 * (uint64_t)lane);
+        wf.start[id] = s0;
+        Cursor c;
+        c.rng.state = s0;
+        c.rng.inc = inc;
+        c.draws = 0;
+        c.cur1d = 1;   // camera: Get2D pFilm, Get2D pLens, Get1D time (stratified)
+        c.cur2d = 2;
+        c.k = lane == 0 ? st.kh : -1;
+        c.kdep = 0;
+        const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, n, ndims};
+        const PixelRec& pr = wb.prec[rec];
+        Spec beta = spec(1);
+        int bounces = 1;
+        Ray ray;
+        const int r = traj_scatter(sc, pr.si, pr.b, pr.wo, c, ss, beta, bounces, ray, rp.max_depth, rp.rr_threshold);
+        if (r == 0) wf_store(wf, id, c, bounces, beta, ray);
+        else wf.D[id] = r == 1 ? c.draws : kBadD;
+        wf_push(wf_queue(wf, 0, n_levels), wf_count(wf, par, 0, n_levels), r == 0, id);
+        st.windows++;
+    }
+    if (lane == 0) {
+        wf.ts[bs] = st;
+        if (st.phase == 2) atomicAdd(wf.finished, 1u);
+    }
+}
+
+// Closest hit of every ray queued for split level `level`.
+__global__ __launch_bounds__(kWfBlock) void k_wf_trace(DevScene sc, WfBufs wf, int par, int level, int n_levels) {
+    __shared__ uint16_t stack_lds[kWfBlock * 64];
+    stage_nodes(sc);
+    const uint32_t n = *wf_count(wf, par, level, n_levels);
+    const uint32_t* q = wf_queue(wf, level, n_levels);
+    for (uint32_t i = blockIdx.x * kWfBlock + threadIdx.x; i < n; i += gridDim.x * kWfBlock) {
+        const uint32_t id = q[i];
+        Ray r = wf_ray(wf, id);
+        int panic = 0, best;
+        V3 ph;
+        bvh_walk<false, kWfBlock>(sc, r, stack_lds + threadIdx.x, panic, best, ph);
+        wf.hprim[id] = panic ? -2 : best;
+        const int64_t cap = wf.cap;
+        wf.hph[id] = ph.x;
+        wf.hph[cap + id] = ph.y;
+        wf.hph[2 * cap + id] = ph.z;
+    }
+}
+
+// Interaction, BSDF and scattering step of every ray traced at `level`.
+__global__ __launch_bounds__(kWfBlock) void k_wf_shade(DevScene sc, RenderParams rp, WaveBufs wb, WfBufs wf,
+                                                       int64_t slot_base, int par, int level, int n_levels) {
+    const uint32_t n = *wf_count(wf, par, level, n_levels);
+    const uint32_t* q = wf_queue(wf, level, n_levels);
+    uint32_t* qn = wf_queue(wf, level + 1, n_levels);
+    uint32_t* cn = wf_count(wf, par, level + 1, n_levels);
+    const int lane = (int)(threadIdx.x & 63);
+    const uint32_t stride = gridDim.x * kWfBlock;
+    for (uint32_t i0 = blockIdx.x * kWfBlock + (threadIdx.x & ~63u); i0 < n; i0 += stride) {
+        const uint32_t i = i0 + (uint32_t)lane;
+        bool push = false;
+        uint32_t id = 0;
+        if (i < n) {
+            id = q[i];
+            const int hp = wf.hprim[id];
+            uint32_t D = kBadD;
+            if (hp == -1) {
+                D = wf.draws[id];
+            } else if (hp >= 0) {
+                const int64_t cap = wf.cap;
+                Ray ray = wf_ray(wf, id);
+                const V3 ph{wf.hph[id], wf.hph[cap + id], wf.hph[2 * cap + id]};
+                SI si;
+                prim_si(sc, hp, ray, ph, si);
+                BSDF b;
+                if (compute_bsdf(sc, si, b) >= 0) {
+                    const int64_t bs = id / kWfCand;
+                    const TileState& ts = wf.ts[bs];
+                    const int64_t rec = bs * wb.ppt + ts.pi;
+                    const uint32_t meta = wf.meta[id];
+                    Cursor c;
+                    c.rng.state = wf.rng[id];
+                    c.rng.inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + bs));
+                    c.draws = wf.draws[id];
+                    c.cur1d = (int)(meta & 0xFF);
+                    c.cur2d = (int)((meta >> 8) & 0xFF);
+                    c.k = (id % kWfCand) == 0 ? ts.kh : -1;
+                    c.kdep = 0;
+                    int bounces = (int)(meta >> 16);
+                    Spec beta{wf.beta[id], wf.beta[cap + id], wf.beta[2 * cap + id]};
+                    const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, rp.spp, rp.ndims};
+                    const int r = traj_scatter(sc, si, b, ray.d, c, ss, beta, bounces, ray, rp.max_depth,
+                                               rp.rr_threshold);
+                    if (r == 0) {
+                        wf_store(wf, id, c, bounces, beta, ray);
+                        push = true;
+                    } else {
+                        D = r == 1 ? c.draws : kBadD;
+                    }
+                }
+            }
+            if (!push) wf.D[id] = D;
+        }
+        wf_push(qn, cn, push, id);
+    }
+}
+
+// Trajectories still alive past the split levels, each to its end.
+__global__ __launch_bounds__(kWfBlock) void k_wf_tail(DevScene sc, RenderParams rp, WaveBufs wb, WfBufs wf,
+                                                      int64_t slot_base, int par, int n_levels) {
+    __shared__ uint16_t stack_lds[kWfBlock * 64];
+    stage_nodes(sc);
+    const uint32_t n = *wf_count(wf, par, n_levels, n_levels);
+    const uint32_t* q = wf.q[2];
+    const int64_t cap = wf.cap;
+    for (uint32_t i = blockIdx.x * kWfBlock + threadIdx.x; i < n; i += gridDim.x * kWfBlock) {
+        const uint32_t id = q[i];
+        const int64_t bs = id / kWfCand;
+        const TileState& ts = wf.ts[bs];
+        const int64_t rec = bs * wb.ppt + ts.pi;
+        const uint32_t meta = wf.meta[id];
+        Cursor c;
+        c.rng.state = wf.rng[id];
+        c.rng.inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + bs));
+        c.draws = wf.draws[id];
+        c.cur1d = (int)(meta & 0xFF);
+        c.cur2d = (int)((meta >> 8) & 0xFF);
+        c.k = (id % kWfCand) == 0 ? ts.kh : -1;
+        c.kdep = 0;
+        int bounces = (int)(meta >> 16);
+        Spec beta{wf.beta[id], wf.beta[cap + id], wf.beta[2 * cap + id]};
+        const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, rp.spp, rp.ndims};
+        Ray ray = wf_ray(wf, id);
+        uint32_t D = kBadD;
+        for (;;) {
+            int panic = 0, best;
+            V3 ph;
+            bvh_walk<false, kWfBlock>(sc, ray, stack_lds + threadIdx.x, panic, best, ph);
+            if (panic) break;
+            if (best < 0) {
+                D = c.draws;
+                break;
+            }
+            SI si;
+            prim_si(sc, best, ray, ph, si);
+            BSDF b;
+            if (compute_bsdf(sc, si, b) < 0) break;
+            const int r = traj_scatter(sc, si, b, ray.d, c, ss, beta, bounces, ray, rp.max_depth, rp.rr_threshold);
+            if (r == 1) D = c.draws;
+            if (r != 0) break;
+        }
+        wf.D[id] = D;
+    }
+}
+
+// Per-tile window counts -> Counters.windows.
+__global__ void k_wf_finish(WfBufs wf, int64_t nb, Counters* __restrict__ ctr) {
+    const int64_t bs = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (bs < nb) atomicAdd(&ctr->windows, (unsigned long long)wf.ts[bs].windows);
+}
+
 // ---------------------------------------------------------- merge kernel
 // Film.MergeFilmTile (film.go:115-132) in tile-index order. A film pixel is
 // covered by at most the 3x3 tiles around its own (filter radius < tile size).
@@ -817,11 +1222,21 @@ struct pbrt_gpu_ctx {
     int n_batches = 0;
     int n_simd = 1024;                 // SIMDs of the device (4 per CU)
     WaveBufs wb{};
+    // wavefront chain (k_wf_*)
+    bool use_wf = false;
+    WfBufs wf{};
+    unsigned char* d_wf = nullptr;
+    size_t wf_cap = 0;
+    uint32_t* h_poll = nullptr;        // pinned: finished-tile counts read back by the window loop
+    hipEvent_t pev[2] = {nullptr, nullptr};
+    int wf_levels = 0;                 // split bounce levels (trace + shade launch pairs per window)
+    int64_t wf_iters = 0;              // window iterations of the last render
     // device scene
     pbrt_shape_desc* d_shapes = nullptr;
     pbrt_material_desc* d_materials = nullptr;
     pbrt_primitive_desc* d_prims = nullptr;
     DevNode* d_nodes = nullptr;
+    DevPrim* d_fprims = nullptr;
     pbrt_light_desc* d_lights = nullptr;
     pbrt_camera_desc* d_camera = nullptr;
     pbrt_film_desc* d_film = nullptr;
@@ -882,6 +1297,8 @@ DevScene dev_scene(const pbrt_gpu_ctx* c, bool with_dist) {
     s.materials = c->d_materials;
     s.prims = c->d_prims;
     s.nodes = c->d_nodes;
+    s.lnodes_unused = nullptr;
+    s.fprims = c->d_fprims;
     s.lights = c->d_lights;
     s.camera = c->d_camera;
     s.film = c->d_film;
@@ -889,7 +1306,7 @@ DevScene dev_scene(const pbrt_gpu_ctx* c, bool with_dist) {
     s.n_prims = c->host_scene.n_prims;
     s.n_nodes = c->host_scene.n_nodes;
     s.n_lights = c->host_scene.n_lights;
-    s.pad = 0;
+    s.use_lds_nodes = 0;
     return s;
 }
 
@@ -904,6 +1321,20 @@ std::vector<DevNode> dev_nodes(const pbrt_scene_desc* s) {
         }
         v[i].offset = n.offset;
         v[i].nprims_axis = (uint32_t)n.n_prims | ((uint32_t)n.axis << 16);
+    }
+    return v;
+}
+
+std::vector<DevPrim> dev_prims(const pbrt_scene_desc* s) {
+    std::vector<DevPrim> v((size_t)(s->n_prims > 0 ? s->n_prims : 1));
+    std::memset(v.data(), 0, v.size() * sizeof(DevPrim));
+    for (int i = 0; i < s->n_prims; i++) {
+        const pbrt_primitive_desc& p = s->prims[i];
+        v[i].shape = s->shapes[p.shape];
+        v[i].prim_to_world = p.prim_to_world;
+        v[i].kind = p.kind;
+        v[i].material = p.material;
+        v[i].prim_identity = is_identity(p.prim_to_world.m) ? 1 : 0;
     }
     return v;
 }
@@ -1022,6 +1453,104 @@ int wave_buffers(pbrt_gpu_ctx* c) {
     return PBRT_OK;
 }
 
+// Trajectory state of the wavefront chain for one batch (wave_batch tiles x kWfCand candidates).
+int wf_buffers(pbrt_gpu_ctx* c) {
+    const int64_t nb = c->wave_batch, cap = nb * kWfCand;
+    auto al = [](int64_t b) { return (b + 255) & ~int64_t(255); };
+    const int64_t bytes = al(nb * (int64_t)sizeof(TileState)) + al(cap * 8) + al(cap * 4) + al(cap * 8) +
+                          al(cap * 4) + al(cap * 4) + al(cap * 24) + al(cap * 48) + al(cap * 4) + al(cap * 24) +
+                          3 * al(cap * 4) + al(2 * (kWfMaxLevels + 1) * 4) + al(4);
+    if (c->wf_cap < (size_t)bytes || !c->d_wf) {
+        if (c->d_wf) (void)hipFree(c->d_wf);
+        c->d_wf = nullptr;
+        c->wf_cap = 0;
+        HIPCHK(c, hipMalloc((void**)&c->d_wf, (size_t)bytes));
+        c->wf_cap = (size_t)bytes;
+    }
+    if (!c->h_poll) HIPCHK(c, hipHostMalloc((void**)&c->h_poll, 2 * sizeof(uint32_t), hipHostMallocDefault));
+    for (int i = 0; i < 2; i++)
+        if (!c->pev[i]) HIPCHK(c, hipEventCreateWithFlags(&c->pev[i], hipEventDisableTiming));
+    unsigned char* p = c->d_wf;
+    auto take = [&](int64_t b) {
+        unsigned char* q = p;
+        p += al(b);
+        return q;
+    };
+    WfBufs& w = c->wf;
+    w.ts = (TileState*)take(nb * (int64_t)sizeof(TileState));
+    w.start = (uint64_t*)take(cap * 8);
+    w.D = (uint32_t*)take(cap * 4);
+    w.rng = (uint64_t*)take(cap * 8);
+    w.draws = (uint32_t*)take(cap * 4);
+    w.meta = (uint32_t*)take(cap * 4);
+    w.beta = (double*)take(cap * 24);
+    w.ray = (double*)take(cap * 48);
+    w.hprim = (int32_t*)take(cap * 4);
+    w.hph = (double*)take(cap * 24);
+    for (int i = 0; i < 3; i++) w.q[i] = (uint32_t*)take(cap * 4);
+    w.cnt = (uint32_t*)take(2 * (kWfMaxLevels + 1) * 4);
+    w.finished = (uint32_t*)take(4);
+    w.cap = cap;
+    // bounces 2 .. maxDepth-1 are traced; the first wf_levels of them as split launches
+    const int need = c->rp.max_depth > 2 ? c->rp.max_depth - 2 : 0;
+    int lv = 8;
+    if (const char* e = getenv("PBRT_WF_LEVELS")) lv = atoi(e);
+    if (lv < 0) lv = 0;
+    if (lv > kWfMaxLevels) lv = kWfMaxLevels;
+    c->wf_levels = need < lv ? need : lv;
+    return PBRT_OK;
+}
+
+// The offset chain of one batch as window iterations (k_wf_tile + per-bounce
+// trace/shade + tail). The host polls the finished-tile count every kPoll
+// iterations without stalling the queue (it waits for the count of the poll
+// before last); the extra iterations it queues meanwhile are no-ops.
+int wf_chain(pbrt_gpu_ctx* c, const DevScene& sc, int64_t sb, int64_t nb) {
+    const RenderParams& rp = c->rp;
+    WfBufs& wf = c->wf;
+    HIPCHK(c, hipMemsetAsync(wf.cnt, 0, 2 * (kWfMaxLevels + 1) * 4, c->stream));
+    HIPCHK(c, hipMemsetAsync(wf.finished, 0, 4, c->stream));
+    hipLaunchKernelGGL(k_wf_init, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, c->stream, rp, c->wb, wf, sb, nb);
+    hipLaunchKernelGGL(k_wf_primary, dim3((unsigned)((nb * c->wb.ppt + kWave - 1) / kWave)), dim3(kWave), 0,
+                       c->stream, sc, rp, c->wb, sb, nb);
+    const int nlev = c->wf_levels;
+    const bool tail = (rp.max_depth > 2 ? rp.max_depth - 2 : 0) > nlev;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((wf.cap + kWfBlock - 1) / kWfBlock,
+                                                                           (int64_t)c->n_simd * 2));
+    constexpr int kPoll = 8;
+    const int64_t max_iters = c->wb.ppt * rp.spp + 2 * kPoll + 2;   // each window resolves >= 1 sample
+    int64_t it = 0;
+    for (;; it++) {
+        const int par = (int)(it & 1);
+        hipLaunchKernelGGL(k_wf_tile, dim3((unsigned)nb), dim3(kWave), (unsigned)c->lay.total, c->stream, sc, rp,
+                           c->lay, c->d_jump, c->wb, wf, sb, par, nlev);
+        for (int l = 0; l < nlev; l++) {
+            hipLaunchKernelGGL(k_wf_trace, dim3(grid), dim3(kWfBlock), 0, c->stream, sc, wf, par, l, nlev);
+            hipLaunchKernelGGL(k_wf_shade, dim3(grid), dim3(kWfBlock), 0, c->stream, sc, rp, c->wb, wf, sb, par, l,
+                               nlev);
+        }
+        if (tail)
+            hipLaunchKernelGGL(k_wf_tail, dim3(grid), dim3(kWfBlock), 0, c->stream, sc, rp, c->wb, wf, sb, par,
+                               nlev);
+        HIPCHK(c, hipGetLastError());
+        if (it % kPoll == kPoll - 1) {
+            const int slot = (int)((it / kPoll) & 1);
+            HIPCHK(c, hipMemcpyAsync(&c->h_poll[slot], wf.finished, 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipEventRecord(c->pev[slot], c->stream));
+            if (it >= 2 * kPoll - 1) {
+                HIPCHK(c, hipEventSynchronize(c->pev[slot ^ 1]));
+                if ((int64_t)c->h_poll[slot ^ 1] >= nb) break;
+            }
+            if (c->cancel.load()) return set_err(c, PBRT_E_CANCELLED, "cancelled");
+        }
+        if (it > max_iters) return set_err(c, PBRT_E_HIP, "wavefront chain did not converge");
+    }
+    c->wf_iters += it + 1;
+    hipLaunchKernelGGL(k_wf_finish, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, c->stream, wf, nb, c->d_ctr);
+    HIPCHK(c, hipGetLastError());
+    return PBRT_OK;
+}
+
 int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
     if (!rd) return set_err(c, PBRT_E_INVALID, "null render desc");
     if (rd->tile_size <= 0 || rd->sampler_x <= 0 || rd->sampler_y <= 0 || rd->n_dims < 0 || rd->n_dims > 64)
@@ -1081,8 +1610,9 @@ int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
         rp.sp_serial = V * 4 <= 16 * 1024 ? 0 : 1;
     }
     c->use_spec = c->kernel_req != PBRT_KERNEL_SERIAL && wave_eligible(c, rd, rp, c->lay);
-    if (c->kernel_req == PBRT_KERNEL_WAVE && !c->use_spec)
-        return set_err(c, PBRT_E_UNSUPPORTED, "render not eligible for the wave-parallel kernel");
+    if ((c->kernel_req == PBRT_KERNEL_WAVE || c->kernel_req == PBRT_KERNEL_WAVEFRONT) && !c->use_spec)
+        return set_err(c, PBRT_E_UNSUPPORTED, "render not eligible for the wave-parallel kernels");
+    c->use_wf = c->use_spec && c->kernel_req == PBRT_KERNEL_WAVEFRONT;
     if (c->use_spec && rp.n_slots > 0) {
         int rcw = wave_buffers(c);
         if (rcw != PBRT_OK) return rcw;
@@ -1096,6 +1626,10 @@ int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
             (c->lanes_per_wave & (c->lanes_per_wave - 1)) == 0)
             G = c->lanes_per_wave;
         c->tiles_per_wave = G;
+        if (c->use_wf) {
+            int rcf = wf_buffers(c);
+            if (rcf != PBRT_OK) return rcf;
+        }
     }
     size_t nslot = (size_t)(rp.n_slots > 0 ? rp.n_slots : 1);
     int rc;
@@ -1123,7 +1657,7 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
         c->lanes_per_wave_set = true;
     }
     if (opts && (opts->occupancy == 2 || opts->occupancy == 4 || opts->occupancy == 8)) c->min_waves = opts->occupancy;
-    if (opts && (opts->kernel < PBRT_KERNEL_AUTO || opts->kernel > PBRT_KERNEL_WAVE)) {
+    if (opts && (opts->kernel < PBRT_KERNEL_AUTO || opts->kernel > PBRT_KERNEL_WAVEFRONT)) {
         delete c;
         return PBRT_E_INVALID;
     }
@@ -1160,6 +1694,7 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
         (rc = upload(c, &c->d_materials, scene->materials, scene->n_materials)) ||
         (rc = upload(c, &c->d_prims, scene->prims, scene->n_prims)) ||
         (rc = upload(c, &c->d_nodes, dev_nodes(scene).data(), scene->n_nodes)) ||
+        (rc = upload(c, &c->d_fprims, dev_prims(scene).data(), scene->n_prims)) ||
         (rc = upload(c, &c->d_lights, scene->lights, scene->n_lights)) ||
         (rc = upload(c, &c->d_camera, &scene->camera, 1)) || (rc = upload(c, &c->d_film, &scene->film, 1)) ||
         (rc = upload<pbrt_distribution_desc>(c, &c->d_dist, nullptr, 1)) ||
@@ -1188,7 +1723,8 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
     if (rp.n_slots > 0) {
         DevScene sc = dev_scene(c, rd->integrator == PBRT_INTEGRATOR_PATH);
         if (c->use_spec) {
-            c->last_kernel = PBRT_KERNEL_WAVE;
+            c->last_kernel = c->use_wf ? PBRT_KERNEL_WAVEFRONT : PBRT_KERNEL_WAVE;
+            c->wf_iters = 0;
             auto chain = c->min_waves >= 2 ? k_chain<2> : k_chain<1>;
             const int64_t per = rp.slot_w * rp.slot_h;
             c->n_batches = (int)((rp.n_slots + c->wave_batch - 1) / c->wave_batch);
@@ -1201,8 +1737,14 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                 const int64_t nb = std::min<int64_t>(c->wave_batch, rp.n_slots - sb);
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 0], c->stream));
                 const int G = c->tiles_per_wave;
-                hipLaunchKernelGGL(chain, dim3((unsigned)((nb + G - 1) / G)), dim3(kWave), (unsigned)c->lay.total,
-                                   c->stream, sc, rp, c->lay, c->d_jump, c->wb, sb, nb, kWave / G, c->d_ctr);
+                if (c->use_wf) {
+                    int rcc = wf_chain(c, sc, sb, nb);
+                    if (rcc != PBRT_OK) return rcc;
+                } else {
+                    hipLaunchKernelGGL(chain, dim3((unsigned)((nb + G - 1) / G)), dim3(kWave),
+                                       (unsigned)c->lay.total, c->stream, sc, rp, c->lay, c->d_jump, c->wb, sb, nb,
+                                       kWave / G, c->d_ctr);
+                }
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 1], c->stream));
                 hipLaunchKernelGGL(k_paths, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
                                    (unsigned)(rp.ndims * rp.spp * 8), c->stream, sc, rp, c->wb, sb, c->d_ctr);
@@ -1385,10 +1927,13 @@ void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_shapes, c->d_materials, c->d_prims, c->d_nodes, c->d_lights, c->d_camera, c->d_film,
                     c->d_dist,   c->d_films,     c->d_s1d,   c->d_panics, c->d_ctr,   c->d_out,    c->d_jump,
-                    c->d_wave};
+                    c->d_wave,   c->d_fprims, c->d_wf};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : c->bev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->pev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->h_poll) (void)hipHostFree(c->h_poll);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev2) (void)hipEventDestroy(c->ev2);
@@ -1517,6 +2062,25 @@ extern "C" int pbrt_gpu_counters(pbrt_gpu_ctx* c, uint64_t* out, int n) {
                                       ctr.phase[6], ctr.phase[7]};
     for (int i = 0; i < n && i < kNumCounters; i++) out[i] = v[i];
     return kNumCounters;
+}
+
+// Region cycles of trajectory steps (PBRT_STEP_TIMING builds only; else zeros):
+// [0] loop top / light-sample draws, [1] closest-hit traversal + interaction,
+// [2] BSDF setup, [3] light sampling (full paths), [4] BSDF sample + spawn + RR.
+extern "C" int pbrt_gpu_step_cycles(uint64_t* out, int n, int reset) {
+#ifdef PBRT_STEP_TIMING
+    unsigned long long h[8];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_step_cycles), sizeof(h)) != hipSuccess) return PBRT_E_HIP;
+    for (int i = 0; i < n && i < 8; i++) out[i] = h[i];
+    if (reset) {
+        std::memset(h, 0, sizeof(h));
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_step_cycles), h, sizeof(h)) != hipSuccess) return PBRT_E_HIP;
+    }
+#else
+    for (int i = 0; i < n && i < 8; i++) out[i] = 0;
+    (void)reset;
+#endif
+    return 8;
 }
 
 extern "C" int pbrt_abi_sizes(size_t* out, int n) {

@@ -54,6 +54,10 @@ int pbrt_gpu_probe(int device, int op, const double* in, size_t n, int in_stride
 struct pbrt_gpu_ctx;
 int pbrt_gpu_counters(struct pbrt_gpu_ctx* ctx, uint64_t* out, int n);
 
+/* Region cycles inside path steps, summed over waves (only in libraries built
+ * with -DPBRT_STEP_TIMING; zeros otherwise). Returns the count (8). */
+int pbrt_gpu_step_cycles(uint64_t* out, int n, int reset);
+
 /* sizeof() of every ABI struct, for binding checks (index order as in pbrt_gpu.h). */
 int pbrt_abi_sizes(size_t* out, int n);
 

@@ -213,10 +213,10 @@ typedef struct pbrt_gpu_stats {
     int32_t panic_tile;
     int64_t panic_pixel_x, panic_pixel_y;
     int32_t panic_sample, panic_bounce;
-    int32_t kernel;          /* PBRT_KERNEL_SERIAL or PBRT_KERNEL_WAVE (last render) */
-    int32_t batches;         /* WAVE: tile batches the frame was split into       */
-    double chain_ms;         /* WAVE: k_chain time (speculative offsets), summed  */
-    double paths_ms;         /* WAVE: k_paths time (full paths), summed           */
+    int32_t kernel;          /* PBRT_KERNEL_SERIAL / _WAVE / _WAVEFRONT (last render) */
+    int32_t batches;         /* WAVE/WAVEFRONT: tile batches of the frame         */
+    double chain_ms;         /* WAVE/WAVEFRONT: sample-offset chain time, summed  */
+    double paths_ms;         /* WAVE/WAVEFRONT: k_paths time (full paths), summed */
 } pbrt_gpu_stats;
 
 /* ----------------------------------------------------------- ray batches */
@@ -242,17 +242,21 @@ typedef struct pbrt_gpu_opts {
     int32_t reserved[4];
 } pbrt_gpu_opts;
 
-/* EXACT-mode kernels. Both replay the reference bit for bit:
- *  SERIAL  one lane per tile, the tile's PCG32 stream consumed in order;
- *  WAVE    one 64-lane wave per tile: per-pixel shared bounce 1, path
- *          offsets found by speculative trajectories + jump-ahead, the
- *          pixel's samples traced in parallel (Path integrator, n_dims >= 3,
- *          every light pdf > 0, filter radius < 1.5; else SERIAL is used). */
+/* EXACT-mode kernels. All replay the reference bit for bit:
+ *  SERIAL     one lane per tile, the tile's PCG32 stream consumed in order;
+ *  WAVE       one 64-lane wave per tile: per-pixel shared bounce 1, path
+ *             offsets found by speculative trajectories + jump-ahead, the
+ *             pixel's samples traced in parallel (Path integrator, n_dims >= 3,
+ *             every light pdf > 0, filter radius < 1.5; else SERIAL is used);
+ *  WAVEFRONT  the WAVE pipeline with the speculative trajectories run as
+ *             compacted per-bounce trace / shade kernels (same eligibility).
+ *             pbrt_gpu_render_async returns once the offset chain is done
+ *             (the host drives its window loop); the rest stays queued. */
 /* WAVE kernel: always replay StartPixel serially (the path normally taken
  * only after a pcg_bounded rejection); results are identical. */
 #define PBRT_FLAG_SERIAL_START_PIXEL 1
 
-enum { PBRT_KERNEL_AUTO = 0, PBRT_KERNEL_SERIAL = 1, PBRT_KERNEL_WAVE = 2 };
+enum { PBRT_KERNEL_AUTO = 0, PBRT_KERNEL_SERIAL = 1, PBRT_KERNEL_WAVE = 2, PBRT_KERNEL_WAVEFRONT = 3 };
 
 typedef struct pbrt_gpu_ctx pbrt_gpu_ctx;
 

@@ -38,6 +38,8 @@ def gpu_render(scene, rd, lanes_per_wave=0, kernel="auto"):
         assert st.kernel == abi.PBRT_KERNEL_SERIAL
     elif kernel == "wave":
         assert st.kernel == abi.PBRT_KERNEL_WAVE
+    elif kernel == "wavefront":
+        assert st.kernel == abi.PBRT_KERNEL_WAVEFRONT
     return film, st
 
 
@@ -233,13 +235,15 @@ def test_device_pcg_matches_golden():
 
 
 # ---------------------------------------------------------------- film parity
-@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("kernel", KERNELS + ["wavefront"])
 @pytest.mark.parametrize("name", sorted(GOLDEN["cases"]))
 def test_golden_fixtures(name, kernel):
     case = GOLDEN["cases"][name]
     w, h = case["w"], case["h"]
     scene = G.Scene.readme(w, h) if case["scene"] == "readme" else G.Scene.cornell(w, h)
     rd = abi.render_desc(**case["render"])
+    if kernel == "wavefront" and not wave_eligible(rd):
+        pytest.skip("not eligible for the wave-parallel kernels")
     film, st = gpu_render(scene, rd, kernel=kernel)
     gold = np.load(os.path.join(HERE, "golden", name + ".npz"))["film"]
     assert same_bits(film, gold)
@@ -293,7 +297,7 @@ def test_ragged_images(w, h, kernel):
     check(G.Scene.readme(w, h), abi.render_desc(3, 3), kernel=kernel)
 
 
-@pytest.mark.parametrize("kw", [
+WAVE_VARIANTS = [
     dict(spp_x=9, spp_y=9),                      # 80 traced samples: two 64-lane batches
     dict(spp_x=8, spp_y=8, n_dims=3),            # bounce-1 uScattering from the RNG
     dict(spp_x=5, spp_y=5, n_dims=5),            # bounce-1 BSDF sample stratified (0,0)
@@ -301,9 +305,42 @@ def test_ragged_images(w, h, kernel):
     dict(spp_x=6, spp_y=6, flags=abi.PBRT_FLAG_SERIAL_START_PIXEL),
     dict(spp_x=4, spp_y=4, max_depth=3),
     dict(spp_x=4, spp_y=4, max_depth=12, rr_threshold=0.0),
-])
+    dict(spp_x=4, spp_y=4, max_depth=2),
+]
+
+
+@pytest.mark.parametrize("kw", WAVE_VARIANTS)
 def test_wave_kernel_variants(kw):
     check(G.Scene.readme(48, 40), abi.render_desc(**kw), kernel="wave")
+
+
+@pytest.mark.parametrize("kw", WAVE_VARIANTS)
+@pytest.mark.parametrize("levels", ["8", "0", "2"])
+def test_wavefront_kernel_variants(kw, levels, monkeypatch):
+    """The wavefront chain: split per-bounce trace/shade levels, and the tail
+    kernel alone (0 levels) or after 2 split levels."""
+    monkeypatch.setenv("PBRT_WF_LEVELS", levels)
+    check(G.Scene.readme(48, 40), abi.render_desc(**kw), kernel="wavefront")
+
+
+def test_wavefront_cornell_64spp_and_readme_256():
+    check(G.Scene.cornell(32, 32), abi.render_desc(8, 8, max_depth=10), kernel="wavefront")
+    check(G.Scene.readme(256, 256), abi.render_desc(2, 2), kernel="wavefront")
+    check(G.Scene.readme(112, 80), abi.render_desc(4, 4), kernel="wavefront")
+
+
+def test_wavefront_panic_is_reported_like_the_oracle():
+    scene = panic_scene()
+    rd = abi.render_desc(2, 2)
+    rc, _, ost = O.render(scene.desc, rd, threads=1)
+    assert rc == abi.PBRT_E_REF_PANIC
+    with G.Renderer(scene, kernel="wavefront") as r:
+        with pytest.raises(G.PbrtError) as ei:
+            r.render(rd)
+    st = ei.value.stats
+    assert ei.value.code == abi.PBRT_E_REF_PANIC and st.kernel == abi.PBRT_KERNEL_WAVEFRONT
+    assert (st.panic_kind, st.panic_tile, st.panic_pixel_x, st.panic_pixel_y, st.panic_sample, st.panic_bounce) == (
+        ost.panic_kind, ost.panic_tile, ost.panic_px, ost.panic_py, ost.panic_sample, ost.panic_bounce)
 
 
 @pytest.mark.parametrize("tiles_per_wave", [1, 2, 8, 16])

@@ -40,5 +40,14 @@ with G.Renderer(scene, kernel=a.kernel, occupancy=a.occupancy) as r:
               f"Mpaths/s={st.paths_traced / dt / 1e6:.2f}")
         px = a.width * a.height
         print("  windows/pixel %.2f" % (vals["windows"] / px))
+        sc_ = (C.c_uint64 * 8)()
+        G.lib().pbrt_gpu_step_cycles(sc_, 8, 1)
+        tot_s = sum(sc_[:5])
+        if tot_s:
+            labels = ["loop top", "closest hit + SI", "BSDF setup", "light sampling", "BSDF sample+spawn+RR"]
+            print("  step regions: " + ", ".join(f"{l} {v / tot_s * 100:.1f}%" for l, v in zip(labels, sc_[:5])))
+            tt = sum(sc_[5:8]) or 1
+            print("  closest-hit traversal: node walk %.1f%%, leaf tests %.1f%%, interaction %.1f%%" % tuple(
+                v / tt * 100 for v in sc_[5:8]))
         for k in names[6:13]:
             print(f"  {k:16s} {vals[k] / tot * 100:5.1f}%  {vals[k] / px:10.0f} cyc/pixel")
