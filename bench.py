@@ -39,7 +39,9 @@ def parse():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=8, help="Stratified(spp, spp)")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "serial", "wave", "wavefront"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "serial", "wave", "wavefront", "wave_ci"])
+    ap.add_argument("--tiles-per-wave", type=int, default=0, help="k_chain lane groups per wave (0 = library default)")
+    ap.add_argument("--occupancy", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, nproc)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -104,9 +106,9 @@ def roofline(W, H, S, paths_per_launch, kernel_kind, kern_ms, chain_ms, paths_ms
         return None
     pmc = load_json(os.path.join(REPO, "profiles", f"pmc_readme_{W}x{H}_s{S}x{S}.json")) or {}
     total = fl["flops_per_path"] * paths_per_launch
-    if kernel_kind in (2, 3) and chain_ms > 0:   # PBRT_KERNEL_WAVE / _WAVEFRONT
+    if kernel_kind in (2, 3, 4) and chain_ms > 0:   # PBRT_KERNEL_WAVE / _WAVEFRONT / _WAVE_CI
         algo = fl.get("flops_trajectory_per_path", fl["flops_per_path"]) * paths_per_launch
-        name, ms = ("k_chain" if kernel_kind == 2 else "wf_chain"), chain_ms
+        name, ms = {2: "k_chain", 3: "wf_chain", 4: "k_chain_ci"}[kernel_kind], chain_ms
     else:
         algo, name, ms = total, "k_render_exact", kern_ms
     achieved = algo / (ms / 1e3) / 1e12
@@ -139,7 +141,8 @@ def main():
     W, H, S = args.width, args.height, args.spp
     rd_kwargs = dict(spp_x=S, spp_y=S)
     scene = G.Scene.readme(W, H)
-    renderer = G.Renderer(scene, device=local, kernel=args.kernel)
+    renderer = G.Renderer(scene, device=local, kernel=args.kernel, lanes_per_wave=args.tiles_per_wave,
+                          occupancy=args.occupancy)
     rd = G.render_desc(**rd_kwargs, tile_begin=rank, tile_stride=world)
     film = torch.zeros((H, W, 3), dtype=torch.float64, device=dev)
 
@@ -202,7 +205,7 @@ def main():
                 "width": W, "height": H, "spp": S * S, "traced_spp": S * S - 1,
                 "paths_per_frame": int(paths_total / args.steps), "mode": "exact",
                 "parallelism": f"tiles mod {world}" + (" + RCCL film reduce" if world > 1 else ""),
-                "kernel": {1: "serial", 2: "wave", 3: "wavefront"}.get(kernel_kind, "?"),
+                "kernel": {1: "serial", 2: "wave", 3: "wavefront", 4: "wave_ci"}.get(kernel_kind, "?"),
             },
             "roofline": roof,
         }

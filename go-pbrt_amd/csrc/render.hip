@@ -282,8 +282,11 @@ struct WaveBufs {
 };
 struct ChainLayout {   // byte offsets into k_chain's dynamic LDS block
     int s1d, other, sbuf, dbuf, vbuf, total;
+    int ring;   // k_chain_ci: offset ring after the StartPixel staging (no sbuf / dbuf)
 };
 constexpr uint32_t kBadD = 0xFFFFFFFFu;
+constexpr int kCiRingBytes = 4 * 1024;   // k_chain_ci offset ring (all lane groups of a wave)
+constexpr int kCiMaxGroups = 4;          // k_chain_ci lane groups (tiles) per wave
 
 __device__ __forceinline__ double pcg_float_of(uint32_t v) {
     return gomath::min(gomath::kOneMinusEpsilon, (double)v * 2.3283064365386963e-10);
@@ -1131,6 +1134,308 @@ __global__ void k_wf_finish(WfBufs wf, int64_t nb, Counters* __restrict__ ctr) {
     if (bs < nb) atomicAdd(&ctr->windows, (unsigned long long)wf.ts[bs].windows);
 }
 
+// ------------------------------------------- continuous-issue offset chain
+// k_chain_ci replaces k_chain's fixed windows. A window of 64 candidates
+// lasts as long as its longest trajectory (~6.5 bounces for a 2.25-bounce
+// mean), so most lanes idle through most of it. Here a lane that finishes a
+// trajectory, or whose candidate the chain has jumped over, takes the next
+// unissued offset at once: every bounce step keeps every lane busy, and
+// candidates left behind by the chain are dropped mid-trajectory.
+//
+// Per lane group (L = 64 / G lanes = one tile): a ring of resolved offsets
+// {offset, D, PCG state} in LDS; the group leader walks the exact chain
+// head -> head + D(head) through it after every step. Offsets are relative
+// to the pixel's first sample (the state after StartPixel). Candidates are
+// issued at head + even offsets; when D is odd the parity of the chain flips
+// and the group's in-flight candidates are dropped. A speculative result
+// that is not usable at the head (a panic or a draw count that depends on
+// the sample index) is re-run there with the sample index known; an exact
+// panic ends the tile at that sample, as in k_chain. Bit-identical to the
+// serial replay: only the schedule changes.
+constexpr uint32_t kNoOff = 0xFFFFFFFFu;
+constexpr uint32_t kBadSpecD = 0xFFFFFFFEu;   // speculative lane could not resolve D
+constexpr uint32_t kBadExactD = 0xFFFFFFFDu;  // the exact head's trajectory panics
+struct RingEnt {
+    uint32_t tag;   // offset this entry resolves (kNoOff: empty)
+    uint32_t d;     // its draw count D, or kBadSpecD / kBadExactD
+    uint64_t st;    // PCG32 state at the offset
+};
+struct CiGroup {
+    uint64_t S;     // PCG32 state at the current pixel's first sample (offset 0)
+    int64_t pi;     // current pixel (row-major index in the tile)
+    int64_t npx;    // pixels of the tile
+    uint32_t head;  // offset of sample kh
+    uint32_t nxt;   // next offset to issue (same parity as head)
+    int kh;         // next sample without an offset
+    int phase;      // 0 needs a pixel, 1 resolving offsets, 2 tile finished
+    int reissue;    // the head must be re-run with its sample index known
+    int pad;
+};
+
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2, 8))) void k_chain_ci(
+    DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
+    int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    // <= kLdsNodes (64) staged nodes: a binary tree that small is at most 31
+    // interior nodes deep, so 32 stack entries per lane cannot overflow
+    __shared__ uint16_t stack_lds[32 * kStackStride];
+    __shared__ ChainCache pcs[kCiMaxGroups];
+    __shared__ CiGroup gs[kCiMaxGroups];
+    __shared__ uint64_t sh_state;
+    const int lane = threadIdx.x;
+    stage_nodes(sc);
+    const int L = lanes_per_tile, G = kWave / L;
+    const int g = lane / L, gl = lane - g * L;
+    const uint32_t R = (uint32_t)ring_size;
+    const PcgJump& J = *jump;
+    double* s1d = (double*)(lds + lay.s1d);
+    uint16_t* other = (uint16_t*)(lds + lay.other);
+    uint32_t* vbuf = (uint32_t*)(lds + lay.vbuf);
+    RingEnt* ring = (RingEnt*)(lds + lay.ring) + (size_t)g * R;
+    uint16_t* stack = stack_lds + lane;
+    const int n = rp.spp, ndims = rp.ndims;
+    const pbrt_camera_desc& cam = *sc.camera;
+    const unsigned long long gmask = L >= 64 ? ~0ULL : (((1ULL << L) - 1ULL) << (g * L));
+    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
+    const int64_t bs = (int64_t)blockIdx.x * G + g;
+    const uint64_t inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + (bs < nslots_batch ? bs : 0)));
+    unsigned long long steps = 0;
+    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    long long tprev = clock64();
+    auto mark = [&](int k) {
+        long long now = clock64();
+        ph[k] += (unsigned long long)(now - tprev);
+        tprev = now;
+    };
+    if (lane < G) {
+        const int64_t b = (int64_t)blockIdx.x * G + lane;
+        CiGroup& s = gs[lane];
+        s.pi = 0;
+        s.kh = 1;
+        s.head = s.nxt = 0;
+        s.reissue = 0;
+        if (b < nslots_batch) {
+            int64_t x0, y0, x1, y1;
+            tile_bounds(rp, tile_of_slot(rp, slot_base + b), x0, y0, x1, y1);
+            Pcg seed;
+            pcg_seed(seed, (uint64_t)tile_of_slot(rp, slot_base + b));   // Sampler.Clone(tile), integrator.go:318,328
+            s.S = seed.state;
+            s.npx = (x1 - x0) * (y1 - y0);
+            s.phase = s.npx > 0 ? 0 : 2;
+            wb.tile_npx[b] = 0;
+        } else {
+            s.S = 0;
+            s.npx = 0;
+            s.phase = 2;
+        }
+    }
+    __syncthreads();
+
+    // lane trajectory state
+    uint32_t off = kNoOff;
+    uint64_t st0 = 0;
+    bool tracing = false;
+    Cursor c;
+    c.rng.state = 0;
+    c.rng.inc = inc;
+    c.draws = 0;
+    c.cur1d = c.cur2d = 0;
+    c.k = -1;
+    c.kdep = 0;
+    Spec beta = spec(1);
+    int bounces = 1;
+    Ray ray;
+    ray.o = ray.d = V3{0, 0, 0};
+    ray.tmax = kInf;
+    ray.time = 0;
+
+    for (;;) {
+        // ---- (1) groups that need a pixel: StartPixel + bounce 1, one group at a time
+        for (int q = 0; q < G; q++) {
+            while (gs[q].phase == 0) {
+                const int64_t bq = (int64_t)blockIdx.x * G + q;
+                const int64_t tile = tile_of_slot(rp, slot_base + bq);
+                const uint64_t incq = pcg_inc_of((uint64_t)tile);
+                const int64_t pi = gs[q].pi;
+                const int64_t rec = bq * wb.ppt + pi;
+                int64_t x0, y0, x1, y1;
+                tile_bounds(rp, tile, x0, y0, x1, y1);
+                const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
+                const uint64_t S1 = start_pixel_wave(rp, J, gs[q].S, incq, s1d, other, vbuf, &sh_state);
+                double* gs1d = wb.s1d + rec * wb.s1d_stride;
+                for (int idx = lane; idx < ndims * n; idx += kWave) gs1d[idx] = s1d[idx];
+                RingEnt* rq = (RingEnt*)(lds + lay.ring) + (size_t)q * R;
+                for (uint32_t i = (uint32_t)lane; i < R; i += kWave) rq[i].tag = kNoOff;
+                // bounce 1 (camera ray, first hit, BSDF) was computed for every
+                // pixel record by k_wf_primary; only the ray time needs StartPixel
+                PixelRec& pr = wb.prec[rec];
+                const int hit0 = pr.hit, panic0 = pr.panic0;
+                if (lane == 0) {
+                    if (hit0)   // the camera ray's time (Get1D after pFilm, pLens) of the pixel's first traced sample
+                        pr.si.time = camera_ray(cam, (double)px, (double)py, s1d[1 < n ? 1 : 0], V2{0.0, 0.0}).time;
+                    pcs[q].si = pr.si;
+                    pcs[q].b = pr.b;
+                    pcs[q].wo = pr.wo;
+                    pcs[q].hit = hit0;
+                    CiGroup& s = gs[q];
+                    s.S = S1;
+                    s.head = s.nxt = 0;
+                    s.kh = 1;
+                    s.reissue = 0;
+                    wb.tile_npx[bq] = (int32_t)(pi + 1);
+                    if (panic0) {   // the first traced sample panics at bounce 1: the tile ends here
+                        s.phase = 2;
+                    } else if (hit0) {
+                        s.phase = 1;
+                    } else {   // no traced bounce: every sample is black and draws nothing
+                        s.pi = pi + 1;
+                        s.phase = s.pi < s.npx ? 0 : 2;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        mark(0);
+        bool any_chain = false;
+        for (int q = 0; q < G; q++) any_chain |= gs[q].phase == 1;
+        if (!any_chain) break;
+        steps++;
+
+        // ---- (2) idle lanes take the next offsets of their group
+        const CiGroup sg = gs[g];
+        const int64_t rec = bs * wb.ppt + sg.pi;
+        const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, n, ndims};
+        {
+            const bool idle = sg.phase == 1 && off == kNoOff;
+            const unsigned long long m = __ballot(idle) & gmask;
+            const int nidle = __popcll(m);
+            int rank = __popcll(m & lt_mask);
+            const int re = (sg.reissue && nidle > 0) ? 1 : 0;
+            const uint32_t span = sg.head + R - sg.nxt;   // offsets < head + R keep the ring collision-free
+            const int avail = (int)((span + 1) / 2);
+            const int nspec = min(nidle - re, avail);
+            uint32_t o = kNoOff;
+            bool exact = false;
+            if (idle) {
+                if (re && rank == 0) {
+                    o = sg.head;
+                    exact = true;
+                } else {
+                    rank -= re;
+                    if (rank < nspec) o = sg.nxt + 2u * (uint32_t)rank;
+                }
+            }
+            if (gl == 0 && sg.phase == 1) {
+                gs[g].nxt = sg.nxt + 2u * (uint32_t)max(nspec, 0);
+                if (re) gs[g].reissue = 0;
+            }
+            if (o != kNoOff) {
+                off = o;
+                st0 = pcg_advance(J, sg.S, inc, (uint64_t)o);
+                c.rng.state = st0;
+                c.draws = 0;
+                c.cur1d = 1;   // camera: Get2D pFilm, Get2D pLens, Get1D time (stratified)
+                c.cur2d = 2;
+                c.k = exact ? sg.kh : -1;
+                c.kdep = 0;
+                beta = spec(1);
+                bounces = 1;
+                const ChainCache& pc = pcs[g];
+                const int r = traj_scatter(sc, pc.si, pc.b, pc.wo, c, ss, beta, bounces, ray, rp.max_depth,
+                                           rp.rr_threshold);
+                tracing = r == 0;
+                if (r != 0) {
+                    RingEnt& e = ring[off % R];
+                    e.st = st0;
+                    e.d = r == 1 ? c.draws : (c.k >= 0 ? kBadExactD : kBadSpecD);
+                    e.tag = off;
+                    off = kNoOff;
+                }
+            }
+        }
+        mark(1);
+        // ---- (3) one bounce of every live trajectory
+        if (tracing) {
+            int panic = 0, best;
+            V3 ph;
+            bvh_walk<false>(sc, ray, stack, panic, best, ph);
+            mark(2);
+            uint32_t d = kNoOff;
+            if (panic) {
+                d = c.k >= 0 ? kBadExactD : kBadSpecD;
+            } else if (best < 0) {
+                d = c.draws;
+            } else {
+                SI si;
+                prim_si(sc, best, ray, ph, si);
+                BSDF b;
+                if (compute_bsdf(sc, si, b) < 0) {
+                    d = c.k >= 0 ? kBadExactD : kBadSpecD;
+                } else {
+                    const int r = traj_scatter(sc, si, b, ray.d, c, ss, beta, bounces, ray, rp.max_depth,
+                                               rp.rr_threshold);
+                    if (r == 1) d = c.draws;
+                    else if (r == 2) d = c.k >= 0 ? kBadExactD : kBadSpecD;
+                }
+            }
+            if (d != kNoOff) {
+                RingEnt& e = ring[off % R];
+                e.st = st0;
+                e.d = d;
+                e.tag = off;
+                off = kNoOff;
+                tracing = false;
+            }
+        }
+        mark(3);
+        __syncthreads();
+        // ---- (4) each group leader walks its chain through the ring
+        if (gl == 0 && sg.phase == 1) {
+            CiGroup s = gs[g];
+            for (;;) {
+                RingEnt& e = ring[s.head % R];
+                if (e.tag != s.head) break;
+                const uint32_t d = e.d;
+                if (d == kBadSpecD) {   // re-run the head with its sample index known
+                    e.tag = kNoOff;
+                    s.reissue = 1;
+                    break;
+                }
+                wb.memb[rec * n + s.kh] = e.st;
+                if (d == kBadExactD) {   // the exact head's trajectory panics: the tile ends at this sample
+                    wb.prec[rec].nvalid = s.kh + 1;
+                    s.phase = 2;
+                    break;
+                }
+                s.kh++;
+                s.head += d;
+                if (s.kh >= n) {   // every sample of the pixel has its offset; the next StartPixel starts here
+                    s.S = pcg_advance(J, s.S, inc, (uint64_t)s.head);
+                    s.pi++;
+                    s.phase = s.pi < s.npx ? 0 : 2;
+                    break;
+                }
+            }
+            if (s.nxt < s.head || ((s.nxt ^ s.head) & 1u)) s.nxt = s.head;
+            gs[g] = s;
+        }
+        __syncthreads();
+        // ---- (5) drop candidates the chain has left behind
+        if (off != kNoOff) {
+            const CiGroup s2 = gs[g];
+            if (s2.phase != 1 || off < s2.head || ((off ^ s2.head) & 1u) || s2.pi != sg.pi) {
+                off = kNoOff;
+                tracing = false;
+            }
+        }
+        mark(4);
+    }
+    if (lane == 0) {
+        atomicAdd(&ctr->windows, steps);
+        for (int k = 0; k < 8; k++) atomicAdd(&ctr->phase[k], ph[k]);
+    }
+}
+
 // ---------------------------------------------------------- merge kernel
 // Film.MergeFilmTile (film.go:115-132) in tile-index order. A film pixel is
 // covered by at most the 3x3 tiles around its own (filter radius < tile size).
@@ -1224,6 +1529,8 @@ struct pbrt_gpu_ctx {
     WaveBufs wb{};
     // wavefront chain (k_wf_*)
     bool use_wf = false;
+    bool use_ci = false;   // k_chain_ci instead of k_chain
+    ChainLayout lay_ci{};
     WfBufs wf{};
     unsigned char* d_wf = nullptr;
     size_t wf_cap = 0;
@@ -1385,7 +1692,8 @@ const PcgJump& pcg_jump_table() {
 }
 
 // Can the wave-parallel kernels replay this render exactly? (conditions: pbrt_spec.h)
-bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const RenderParams& rp, ChainLayout& L) {
+bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const RenderParams& rp, ChainLayout& L,
+                   ChainLayout& Lci) {
     if (rd->integrator != PBRT_INTEGRATOR_PATH || rd->n_dims < 3 || rd->max_depth > 2048) return false;   // D < 2^32
     const int nl = c->host_scene.n_lights;
     if (nl > kMaxCachedLights) return false;
@@ -1411,7 +1719,16 @@ bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Rend
     L.dbuf = put(kWave * 4);
     L.vbuf = put(rp.sp_serial ? 4 : (int64_t)rp.sp_draws * 4);
     L.total = (int)off;
-    return off <= 48 * 1024;
+    L.ring = 0;
+    // k_chain_ci: the same staging without the window buffers, then the ring
+    off = 0;
+    Lci.s1d = put(nd * n * 8);
+    Lci.other = put(nd * n * 2);
+    Lci.sbuf = Lci.dbuf = 0;
+    Lci.vbuf = put(rp.sp_serial ? 4 : (int64_t)rp.sp_draws * 4);
+    Lci.ring = put(kCiRingBytes);
+    Lci.total = (int)off;
+    return L.total <= 48 * 1024;
 }
 
 // Carve the per-batch buffers of the wave path (budget: PBRT_WAVE_BUFFER_GB, default 12).
@@ -1609,10 +1926,14 @@ int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
         rp.sp_draws = (int32_t)V;
         rp.sp_serial = V * 4 <= 16 * 1024 ? 0 : 1;
     }
-    c->use_spec = c->kernel_req != PBRT_KERNEL_SERIAL && wave_eligible(c, rd, rp, c->lay);
-    if ((c->kernel_req == PBRT_KERNEL_WAVE || c->kernel_req == PBRT_KERNEL_WAVEFRONT) && !c->use_spec)
+    c->use_spec = c->kernel_req != PBRT_KERNEL_SERIAL && wave_eligible(c, rd, rp, c->lay, c->lay_ci);
+    if ((c->kernel_req == PBRT_KERNEL_WAVE || c->kernel_req == PBRT_KERNEL_WAVEFRONT ||
+         c->kernel_req == PBRT_KERNEL_WAVE_CI) && !c->use_spec)
         return set_err(c, PBRT_E_UNSUPPORTED, "render not eligible for the wave-parallel kernels");
     c->use_wf = c->use_spec && c->kernel_req == PBRT_KERNEL_WAVEFRONT;
+    c->use_ci = c->use_spec && c->kernel_req == PBRT_KERNEL_WAVE_CI;
+    if (c->use_ci && !(c->host_scene.n_nodes <= kLdsNodes && c->lay_ci.total <= 12 * 1024))
+        return set_err(c, PBRT_E_UNSUPPORTED, "render not eligible for the continuous-issue chain kernel");
     if (c->use_spec && rp.n_slots > 0) {
         int rcw = wave_buffers(c);
         if (rcw != PBRT_OK) return rcw;
@@ -1657,7 +1978,7 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
         c->lanes_per_wave_set = true;
     }
     if (opts && (opts->occupancy == 2 || opts->occupancy == 4 || opts->occupancy == 8)) c->min_waves = opts->occupancy;
-    if (opts && (opts->kernel < PBRT_KERNEL_AUTO || opts->kernel > PBRT_KERNEL_WAVEFRONT)) {
+    if (opts && (opts->kernel < PBRT_KERNEL_AUTO || opts->kernel > PBRT_KERNEL_WAVE_CI)) {
         delete c;
         return PBRT_E_INVALID;
     }
@@ -1723,7 +2044,7 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
     if (rp.n_slots > 0) {
         DevScene sc = dev_scene(c, rd->integrator == PBRT_INTEGRATOR_PATH);
         if (c->use_spec) {
-            c->last_kernel = c->use_wf ? PBRT_KERNEL_WAVEFRONT : PBRT_KERNEL_WAVE;
+            c->last_kernel = c->use_wf ? PBRT_KERNEL_WAVEFRONT : c->use_ci ? PBRT_KERNEL_WAVE_CI : PBRT_KERNEL_WAVE;
             c->wf_iters = 0;
             auto chain = c->min_waves >= 2 ? k_chain<2> : k_chain<1>;
             const int64_t per = rp.slot_w * rp.slot_h;
@@ -1740,6 +2061,14 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                 if (c->use_wf) {
                     int rcc = wf_chain(c, sc, sb, nb);
                     if (rcc != PBRT_OK) return rcc;
+                } else if (c->use_ci) {
+                    hipLaunchKernelGGL(k_wf_primary, dim3((unsigned)((nb * c->wb.ppt + kWave - 1) / kWave)),
+                                       dim3(kWave), 0, c->stream, sc, rp, c->wb, sb, nb);
+                    const int Gc = std::min(G, kCiMaxGroups);
+                    const int ring = kCiRingBytes / (int)sizeof(RingEnt) / Gc;
+                    hipLaunchKernelGGL(k_chain_ci, dim3((unsigned)((nb + Gc - 1) / Gc)), dim3(kWave),
+                                       (unsigned)c->lay_ci.total, c->stream, sc, rp, c->lay_ci, c->d_jump, c->wb, sb,
+                                       nb, kWave / Gc, ring, c->d_ctr);
                 } else {
                     hipLaunchKernelGGL(chain, dim3((unsigned)((nb + G - 1) / G)), dim3(kWave),
                                        (unsigned)c->lay.total, c->stream, sc, rp, c->lay, c->d_jump, c->wb, sb, nb,

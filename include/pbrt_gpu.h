@@ -251,12 +251,16 @@ typedef struct pbrt_gpu_opts {
  *  WAVEFRONT  the WAVE pipeline with the speculative trajectories run as
  *             compacted per-bounce trace / shade kernels (same eligibility).
  *             pbrt_gpu_render_async returns once the offset chain is done
- *             (the host drives its window loop); the rest stays queued. */
+ *             (the host drives its window loop); the rest stays queued.
+ *  WAVE_CI    the WAVE pipeline with a continuous-issue offset chain: a lane
+ *             that finishes a trajectory, or whose candidate offset the chain
+ *             has passed, takes the next offset at once (same eligibility). */
 /* WAVE kernel: always replay StartPixel serially (the path normally taken
  * only after a pcg_bounded rejection); results are identical. */
 #define PBRT_FLAG_SERIAL_START_PIXEL 1
 
-enum { PBRT_KERNEL_AUTO = 0, PBRT_KERNEL_SERIAL = 1, PBRT_KERNEL_WAVE = 2, PBRT_KERNEL_WAVEFRONT = 3 };
+enum { PBRT_KERNEL_AUTO = 0, PBRT_KERNEL_SERIAL = 1, PBRT_KERNEL_WAVE = 2, PBRT_KERNEL_WAVEFRONT = 3,
+       PBRT_KERNEL_WAVE_CI = 4 /* wave pipeline, continuous-issue offset chain */ };
 
 typedef struct pbrt_gpu_ctx pbrt_gpu_ctx;
 

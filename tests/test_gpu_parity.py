@@ -40,6 +40,8 @@ def gpu_render(scene, rd, lanes_per_wave=0, kernel="auto"):
         assert st.kernel == abi.PBRT_KERNEL_WAVE
     elif kernel == "wavefront":
         assert st.kernel == abi.PBRT_KERNEL_WAVEFRONT
+    elif kernel == "wave_ci":
+        assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
     return film, st
 
 
@@ -235,14 +237,14 @@ def test_device_pcg_matches_golden():
 
 
 # ---------------------------------------------------------------- film parity
-@pytest.mark.parametrize("kernel", KERNELS + ["wavefront"])
+@pytest.mark.parametrize("kernel", KERNELS + ["wavefront", "wave_ci"])
 @pytest.mark.parametrize("name", sorted(GOLDEN["cases"]))
 def test_golden_fixtures(name, kernel):
     case = GOLDEN["cases"][name]
     w, h = case["w"], case["h"]
     scene = G.Scene.readme(w, h) if case["scene"] == "readme" else G.Scene.cornell(w, h)
     rd = abi.render_desc(**case["render"])
-    if kernel == "wavefront" and not wave_eligible(rd):
+    if kernel in ("wavefront", "wave_ci") and not wave_eligible(rd):
         pytest.skip("not eligible for the wave-parallel kernels")
     film, st = gpu_render(scene, rd, kernel=kernel)
     gold = np.load(os.path.join(HERE, "golden", name + ".npz"))["film"]
@@ -310,8 +312,9 @@ WAVE_VARIANTS = [
 
 
 @pytest.mark.parametrize("kw", WAVE_VARIANTS)
-def test_wave_kernel_variants(kw):
-    check(G.Scene.readme(48, 40), abi.render_desc(**kw), kernel="wave")
+@pytest.mark.parametrize("kernel", ["wave", "wave_ci"])
+def test_wave_kernel_variants(kw, kernel):
+    check(G.Scene.readme(48, 40), abi.render_desc(**kw), kernel=kernel)
 
 
 @pytest.mark.parametrize("kw", WAVE_VARIANTS)
@@ -343,14 +346,40 @@ def test_wavefront_panic_is_reported_like_the_oracle():
         ost.panic_kind, ost.panic_tile, ost.panic_px, ost.panic_py, ost.panic_sample, ost.panic_bounce)
 
 
-@pytest.mark.parametrize("tiles_per_wave", [1, 2, 8, 16])
-def test_wave_kernel_tiles_per_wave(tiles_per_wave):
+@pytest.mark.parametrize("tiles_per_wave", [1, 2, 4, 8, 16])
+@pytest.mark.parametrize("kernel", ["wave", "wave_ci"])
+def test_wave_kernel_tiles_per_wave(tiles_per_wave, kernel):
     """k_chain packs 64 / L lanes per tile; 37 tiles leave partial last waves."""
-    check(G.Scene.readme(112, 80), abi.render_desc(4, 4), kernel="wave", lanes_per_wave=tiles_per_wave)
+    check(G.Scene.readme(112, 80), abi.render_desc(4, 4), kernel=kernel, lanes_per_wave=tiles_per_wave)
 
 
-def test_wave_kernel_cornell_64spp():
-    check(G.Scene.cornell(32, 32), abi.render_desc(8, 8, max_depth=10), kernel="wave")
+@pytest.mark.parametrize("kernel", ["wave", "wave_ci"])
+def test_wave_kernel_cornell_64spp(kernel):
+    check(G.Scene.cornell(32, 32), abi.render_desc(8, 8, max_depth=10), kernel=kernel)
+
+
+@pytest.mark.parametrize("tiles_per_wave", [1, 4])
+def test_wave_ci_readme_256_and_odd_draw_counts(tiles_per_wave):
+    """Continuous-issue chain on larger frames: D is odd for ~1% of paths
+    (no RR draw), which flips the chain's offset parity mid-pixel."""
+    check(G.Scene.readme(256, 256), abi.render_desc(2, 2), kernel="wave_ci", lanes_per_wave=tiles_per_wave)
+    check(G.Scene.readme(112, 80), abi.render_desc(8, 8), kernel="wave_ci", lanes_per_wave=tiles_per_wave)
+    check(G.Scene.cornell(48, 32), abi.render_desc(6, 6, max_depth=12, rr_threshold=0.5), kernel="wave_ci",
+          lanes_per_wave=tiles_per_wave)
+
+
+def test_wave_ci_panic_is_reported_like_the_oracle():
+    scene = panic_scene()
+    rd = abi.render_desc(2, 2)
+    rc, _, ost = O.render(scene.desc, rd, threads=1)
+    assert rc == abi.PBRT_E_REF_PANIC
+    with G.Renderer(scene, kernel="wave_ci") as r:
+        with pytest.raises(G.PbrtError) as ei:
+            r.render(rd)
+    st = ei.value.stats
+    assert ei.value.code == abi.PBRT_E_REF_PANIC and st.kernel == abi.PBRT_KERNEL_WAVE_CI
+    assert (st.panic_kind, st.panic_tile, st.panic_pixel_x, st.panic_pixel_y, st.panic_sample, st.panic_bounce) == (
+        ost.panic_kind, ost.panic_tile, ost.panic_px, ost.panic_py, ost.panic_sample, ost.panic_bounce)
 
 
 def test_wave_kernel_rejects_ineligible_render():

@@ -19,13 +19,14 @@ ap.add_argument("--spp", type=int, default=8)
 ap.add_argument("--kernel", default="auto")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--occupancy", type=int, default=0)
+ap.add_argument("--tiles-per-wave", type=int, default=0)
 a = ap.parse_args()
 
 scene = G.Scene.readme(a.width, a.height)
 names = ["paths", "camera_samples", "closest_rays", "shadow_rays", "any_panic", "windows",
          "cyc_start_pixel", "cyc_bounce1", "cyc_trajectories", "cyc_chain_walk", "cyc_4",
          "cyc_5", "cyc_6", "cyc_7"]
-with G.Renderer(scene, kernel=a.kernel, occupancy=a.occupancy) as r:
+with G.Renderer(scene, kernel=a.kernel, occupancy=a.occupancy, lanes_per_wave=a.tiles_per_wave) as r:
     rd = abi.render_desc(a.spp, a.spp)
     for i in range(a.reps):
         t0 = time.perf_counter()
