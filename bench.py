@@ -45,6 +45,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, nproc)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", default="exact", choices=["exact", "throughput"],
+                    help="mode of the headline line (exact = the reference's per-tile RNG, bit-exact)")
+    ap.add_argument("--no-side-mode", action="store_true",
+                    help="skip the extra frames in the other mode (reported under side_mode)")
     return ap.parse_args()
 
 
@@ -91,7 +95,7 @@ def cpu_baseline(args, rd_kwargs):
     }
 
 
-def roofline(W, H, S, paths_per_launch, kernel_kind, kern_ms, chain_ms, paths_ms, merge_ms):
+def roofline(W, H, S, paths_per_launch, kernel_kind, kern_ms, chain_ms, paths_ms, merge_ms, mode="exact"):
     """Roofline of the dominant kernel, priced in ALGORITHMIC fp64 FLOPs: the
     reference's own arithmetic per path, counted by the FLOP-accounting oracle
     (profiles/flops_*.json, tools/count_flops.py) x the paths of one launch,
@@ -106,7 +110,9 @@ def roofline(W, H, S, paths_per_launch, kernel_kind, kern_ms, chain_ms, paths_ms
         return None
     pmc = load_json(os.path.join(REPO, "profiles", f"pmc_readme_{W}x{H}_s{S}x{S}.json")) or {}
     total = fl["flops_per_path"] * paths_per_launch
-    if kernel_kind in (2, 3, 4) and chain_ms > 0:   # PBRT_KERNEL_WAVE / _WAVEFRONT / _WAVE_CI
+    if mode == "throughput" and kernel_kind == 2:   # no chain: k_paths<true> runs the whole path
+        algo, name, ms = total, "k_paths_mb", paths_ms
+    elif kernel_kind in (2, 3, 4) and chain_ms > 0:   # PBRT_KERNEL_WAVE / _WAVEFRONT / _WAVE_CI
         algo = fl.get("flops_trajectory_per_path", fl["flops_per_path"]) * paths_per_launch
         name, ms = {2: "k_chain", 3: "wf_chain", 4: "k_chain_ci"}[kernel_kind], chain_ms
     else:
@@ -143,49 +149,63 @@ def main():
     scene = G.Scene.readme(W, H)
     renderer = G.Renderer(scene, device=local, kernel=args.kernel, lanes_per_wave=args.tiles_per_wave,
                           occupancy=args.occupancy)
-    rd = G.render_desc(**rd_kwargs, tile_begin=rank, tile_stride=world)
+    modes = {"exact": G.abi.PBRT_MODE_EXACT, "throughput": G.abi.PBRT_MODE_THROUGHPUT}
     film = torch.zeros((H, W, 3), dtype=torch.float64, device=dev)
 
     def barrier():
         if world > 1:
             dist.barrier(device_ids=[local])
 
-    def step():
-        renderer.render_async(rd, film.data_ptr())
-        st = renderer.synchronize()
+    def timed(mode, steps, warmup):
+        rd = G.render_desc(**rd_kwargs, tile_begin=rank, tile_stride=world, mode=modes[mode])
+
+        def step():
+            renderer.render_async(rd, film.data_ptr())
+            st = renderer.synchronize()
+            if world > 1:
+                dist.reduce(film, dst=0, op=dist.ReduceOp.SUM)
+            return st
+
+        for _ in range(warmup):
+            step()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        stats = [step() for _ in range(steps)]
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        paths_local = sum(int(s.paths_traced) for s in stats)
+        agg = torch.tensor([elapsed, float(paths_local)], dtype=torch.float64, device=dev)
         if world > 1:
-            dist.reduce(film, dst=0, op=dist.ReduceOp.SUM)
-        return st
+            mx = agg.clone()
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            sm = agg.clone()
+            dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+            elapsed, paths_total = float(mx[0]), float(sm[1])
+        else:
+            paths_total = float(paths_local)
+        return elapsed, paths_local, paths_total, stats
 
-    for _ in range(args.warmup):
-        step()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    stats = [step() for _ in range(args.steps)]
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-
-    paths_local = sum(int(s.paths_traced) for s in stats)
+    elapsed, paths_local, paths_total, stats = timed(args.mode, args.steps, args.warmup)
     kern_ms = sum(s.kernel_ms for s in stats) / len(stats)
     merge_ms = sum(s.merge_ms for s in stats) / len(stats)
     chain_ms = sum(s.chain_ms for s in stats) / len(stats)
     paths_ms = sum(s.paths_ms for s in stats) / len(stats)
     kernel_kind = int(stats[0].kernel)
-    agg = torch.tensor([elapsed, float(paths_local), kern_ms], dtype=torch.float64, device=dev)
-    if world > 1:
-        mx = agg.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = agg.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed, paths_total = float(mx[0]), float(sm[1])
-    else:
-        paths_total = float(paths_local)
+    side = None
+    if not args.no_side_mode:
+        other = "throughput" if args.mode == "exact" else "exact"
+        e2, _, p2, st2 = timed(other, 2, 1)
+        side = {"mode": other, "value": p2 / e2 / 1e6, "unit": "Mpaths/s", "ms_per_step": e2 / 2 * 1e3,
+                "chain_ms": sum(s.chain_ms for s in st2) / 2, "k_paths_ms": sum(s.paths_ms for s in st2) / 2,
+                "note": "THROUGHPUT = one PCG32 stream per (pixel, sample): same arithmetic, statistically "
+                        "(not bitwise) the reference image; EXACT is the headline"}
 
     if rank == 0:
         value = paths_total / elapsed / 1e6
-        roof = roofline(W, H, S, paths_local / len(stats), kernel_kind, kern_ms, chain_ms, paths_ms, merge_ms)
+        roof = roofline(W, H, S, paths_local / len(stats), kernel_kind, kern_ms, chain_ms, paths_ms, merge_ms,
+                        args.mode)
         out = {
             "metric": METRIC,
             "value": value,
@@ -201,14 +221,17 @@ def main():
             "data": "synthetic (the reference's hard-coded README scene; no external data)",
             "config": {
                 "workload": f"README sphere scene {W}x{H}, Stratified({S},{S}) = {S * S - 1} traced paths/px, "
-                            "Path(maxDepth 10, rr 1, Uniform), tile 16, EXACT per-tile RNG",
+                            "Path(maxDepth 10, rr 1, Uniform), tile 16, "
+                            + ("EXACT per-tile RNG" if args.mode == "exact" else "THROUGHPUT per-path RNG"),
                 "width": W, "height": H, "spp": S * S, "traced_spp": S * S - 1,
-                "paths_per_frame": int(paths_total / args.steps), "mode": "exact",
+                "paths_per_frame": int(paths_total / args.steps), "mode": args.mode,
                 "parallelism": f"tiles mod {world}" + (" + RCCL film reduce" if world > 1 else ""),
                 "kernel": {1: "serial", 2: "wave", 3: "wavefront", 4: "wave_ci"}.get(kernel_kind, "?"),
             },
             "roofline": roof,
         }
+        if side:
+            out["side_mode"] = side
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args, rd_kwargs)
         print(json.dumps(out), flush=True)

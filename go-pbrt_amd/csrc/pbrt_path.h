@@ -73,6 +73,20 @@ __device__ __forceinline__ void pcg_seed(Pcg& r, uint64_t seed) {   // rng.go:28
     r.state += 0x853c49e6748fea9bULL;
     pcg_next(r);
 }
+// THROUGHPUT mode (SURVEY.md §8(a) "Mode B"; include/pbrt_gpu.h): the PCG32
+// state that starts stream `s` of pixel `pi` (row-major index in its tile) of
+// tile `tile`: s = 0 feeds Stratified.StartPixel, s = k >= 1 feeds sample k.
+// The increment stays the tile's ((tile << 1) | 1, rng.go:28-34). splitmix64
+// finalizer chain; the oracle states the same function (oracle_render.c).
+__host__ __device__ __forceinline__ uint64_t mb_mix(uint64_t x) {
+    uint64_t z = x + 0x9e3779b97f4a7c15ULL;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+__host__ __device__ __forceinline__ uint64_t mb_state(uint64_t tile, uint64_t pi, uint64_t s) {
+    return mb_mix(mb_mix(mb_mix(tile) ^ pi) ^ s);
+}
 __device__ __forceinline__ uint32_t pcg_bounded(Pcg& r, uint32_t b) {   // rng.go:44-53
     uint32_t threshold = (~b + 1u) % b;
     for (;;) {

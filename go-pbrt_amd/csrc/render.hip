@@ -46,7 +46,8 @@ struct RenderParams {
     double rr_threshold;
     int32_t lanes_per_wave;
     int32_t flags;   // pbrt_render_desc.flags
-    int32_t sp_events, sp_draws, sp_serial, pad1;   // wave kernel StartPixel: events, raw draws buffered
+    int32_t sp_events, sp_draws, sp_serial;   // wave kernel StartPixel: events, raw draws buffered
+    int32_t mode;                             // PBRT_MODE_EXACT / _THROUGHPUT
 };
 
 struct PanicRec {
@@ -161,8 +162,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kMinWaves
     unsigned long long paths = 0;
     const pbrt_camera_desc& cam = *sc.camera;
 
+    const bool mb = rp.mode == PBRT_MODE_THROUGHPUT;
     for (int64_t py = y0; py < y1; py++) {
         for (int64_t px = x0; px < x1; px++) {
+            const uint64_t pi = (uint64_t)((py - y0) * (x1 - x0) + (px - x0));
+            if (mb) t.rng.state = mb_state((uint64_t)tile, pi, 0);
             start_pixel(t);
             // camera sample: pFilm = pixel + Get2D() == pixel corner; pLens = Get2D() = (0,0)
             const double fx = (double)px + 0.0, fy = (double)py + 0.0;
@@ -178,6 +182,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kMinWaves
                 for (int k = 0; k < fp.n; k++)
                     for (int c = 0; c < 3; c++) acc[k][c] = tf[fp.off[k] * 3 + c];
             while (next_sample(t)) {
+                if (mb) t.rng.state = mb_state((uint64_t)tile, pi, (uint64_t)t.sample_index);
                 V2 u0 = get2d(t);
                 V2 plens = get2d(t);
                 double tu = get1d(t);
@@ -591,39 +596,80 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8
 }
 
 // One wave per pixel record: the pixel's samples as full paths.
-__global__ __launch_bounds__(kWave) void k_paths(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
-                                                 Counters* __restrict__ ctr) {
+//   kMB = false (EXACT): bounce 1, the stratified values and every sample's
+//                RNG state come from k_chain's records.
+//   kMB = true  (THROUGHPUT): the wave builds them itself, with no chain:
+//                StartPixel on the pixel's own stream (mb_state(tile, pi, 0)),
+//                bounce 1, and sample k's stream mb_state(tile, pi, k); it
+//                writes the PixelRec fields k_film and k_panic_reduce read.
+template <bool kMB>
+__global__ __launch_bounds__(kWave) void k_paths(DevScene sc, RenderParams rp, ChainLayout lay,
+                                                 const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
+                                                 int64_t nslots_batch, Counters* __restrict__ ctr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     __shared__ uint16_t stack_lds[64 * kStackStride];
     __shared__ PixelCache pc;
     __shared__ unsigned long long sh_pkey;   // (sample << 32) | (bounce << 8) | (kind + 1): min = first panic
+    __shared__ uint64_t sh_state;
     const int lane = threadIdx.x;
     stage_nodes(sc);
     const int64_t bslot = blockIdx.x / wb.ppt, pi = blockIdx.x % wb.ppt;
-    if (pi >= wb.tile_npx[bslot]) return;
     const int64_t rec = blockIdx.x;
     const int64_t tile = tile_of_slot(rp, slot_base + bslot);
     int64_t x0, y0, x1, y1;
     tile_bounds(rp, tile, x0, y0, x1, y1);
+    if (kMB) {
+        if (bslot >= nslots_batch) return;
+        if (pi == 0 && lane == 0) wb.tile_npx[bslot] = (int32_t)((x1 - x0) * (y1 - y0));
+        if (pi >= (x1 - x0) * (y1 - y0)) return;
+    } else if (pi >= wb.tile_npx[bslot]) {
+        return;
+    }
     const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
     const int n = rp.spp, ndims = rp.ndims;
-    double* s1d = (double*)lds;
+    double* s1d = (double*)(lds + lay.s1d);
     uint16_t* stack = stack_lds + lane;
-    const PixelRec& pr = wb.prec[rec];
-    for (int idx = lane; idx < ndims * n; idx += kWave) s1d[idx] = wb.s1d[rec * wb.s1d_stride + idx];
-    const int hit = pr.hit, nvalid = pr.nvalid;
+    PixelRec& pr = wb.prec[rec];
     Pcg seed;
     pcg_seed(seed, (uint64_t)tile);
     const uint64_t inc = seed.inc;
+    SI si0;
+    BSDF b0;
+    int hit, nvalid, panic0;
+    if constexpr (kMB) {
+        (void)start_pixel_wave(rp, *jump, mb_state((uint64_t)tile, (uint64_t)pi, 0), inc, s1d,
+                               (uint16_t*)(lds + lay.other), (uint32_t*)(lds + lay.vbuf), &sh_state);
+        // bounce 1, shared by every sample of the pixel (pbrt_spec.h)
+        panic0 = 0;
+        hit = 0;
+        b0.n_bxdfs = 0;
+        Ray ray = camera_ray(*sc.camera, (double)px + 0.0, (double)py + 0.0, s1d[1 < n ? 1 : 0], V2{0.0, 0.0});
+        if (n > 1 && 1 < rp.max_depth) {
+            hit = bvh_traverse<false>(sc, ray, &si0, stack, panic0) ? 1 : 0;
+            if (!panic0 && hit && compute_bsdf(sc, si0, b0) < 0) panic0 = -1;
+        }
+        if (panic0) hit = 0;
+        nvalid = n;
+        if (lane == 0) {
+            pc.wo = ray.d;
+            pr.nvalid = n;
+            pr.panic0 = panic0;
+        }
+    } else {
+        for (int idx = lane; idx < ndims * n; idx += kWave) s1d[idx] = wb.s1d[rec * wb.s1d_stride + idx];
+        si0 = pr.si;
+        b0 = pr.b;
+        hit = pr.hit;
+        nvalid = pr.nvalid;
+        panic0 = pr.panic0;
+        if (lane == 0) pc.wo = pr.wo;
+    }
     if (lane == 0) {
-        pc.si = pr.si;
-        pc.b = pr.b;
-        pc.wo = pr.wo;
+        pc.si = si0;
+        pc.b = b0;
         pc.hit = hit;
         sh_pkey = ~0ULL;
     }
-    const SI si0 = pr.si;
-    const BSDF b0 = pr.b;
     if (hit && b0.n_bxdfs > 0 && lane < sc.n_lights) {   // bounce-1 light samples, uLight = (0,0)
         int pl = 0;
         Spec ld = estimate_direct(sc, stack, pl, si0, b0, lane, V2{0.0, 0.0});
@@ -638,7 +684,7 @@ __global__ __launch_bounds__(kWave) void k_paths(DevScene sc, RenderParams rp, W
         Spec L = spec(0);
         if (k < nvalid && hit) {
             Cursor c;
-            c.rng.state = wb.memb[rec * n + k];
+            c.rng.state = kMB ? mb_state((uint64_t)tile, (uint64_t)pi, (uint64_t)k) : wb.memb[rec * n + k];
             c.rng.inc = inc;
             c.draws = 0;
             c.cur1d = 1;   // camera: Get2D pFilm, Get2D pLens, Get1D time (stratified)
@@ -661,8 +707,8 @@ __global__ __launch_bounds__(kWave) void k_paths(DevScene sc, RenderParams rp, W
     __syncthreads();
     if (lane == 0) {
         PanicRec p{0, 0, 0, 0, px, py};
-        if (pr.panic0) {
-            p.kind = pr.panic0;
+        if (panic0) {
+            p.kind = panic0;
             p.sample = 1;
             p.bounce = 1;
         } else if (sh_pkey != ~0ULL) {
@@ -1878,7 +1924,8 @@ int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
     if (rd->integrator == PBRT_INTEGRATOR_DIRECT_LIGHTING && rd->dl_strategy != PBRT_DL_UNIFORM_SAMPLE_ALL &&
         rd->dl_strategy != PBRT_DL_UNIFORM_SAMPLE_ONE)
         return set_err(c, PBRT_E_UNSUPPORTED, "unknown DirectLighting strategy");
-    if (rd->mode != PBRT_MODE_EXACT) return set_err(c, PBRT_E_UNSUPPORTED, "only EXACT mode is implemented");
+    if (rd->mode != PBRT_MODE_EXACT && rd->mode != PBRT_MODE_THROUGHPUT)
+        return set_err(c, PBRT_E_INVALID, "unknown mode");
     const pbrt_film_desc& f = c->host_scene.film;
     if (f.filter_radius_x <= 0 || f.filter_radius_y <= 0 || f.filter_radius_x >= (double)rd->tile_size ||
         f.filter_radius_y >= (double)rd->tile_size)
@@ -1912,6 +1959,7 @@ int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
     rp.rr_threshold = rd->rr_threshold;
     rp.lanes_per_wave = c->lanes_per_wave;
     rp.flags = rd->flags;
+    rp.mode = rd->mode;
     pbrt_distribution_desc& dist = c->host_dist;
     std::memset(&dist, 0, sizeof(dist));
     if (rd->integrator == PBRT_INTEGRATOR_PATH) {
@@ -2044,7 +2092,8 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
     if (rp.n_slots > 0) {
         DevScene sc = dev_scene(c, rd->integrator == PBRT_INTEGRATOR_PATH);
         if (c->use_spec) {
-            c->last_kernel = c->use_wf ? PBRT_KERNEL_WAVEFRONT : c->use_ci ? PBRT_KERNEL_WAVE_CI : PBRT_KERNEL_WAVE;
+            c->last_kernel = rp.mode == PBRT_MODE_THROUGHPUT ? PBRT_KERNEL_WAVE
+                             : c->use_wf ? PBRT_KERNEL_WAVEFRONT : c->use_ci ? PBRT_KERNEL_WAVE_CI : PBRT_KERNEL_WAVE;
             c->wf_iters = 0;
             auto chain = c->min_waves >= 2 ? k_chain<2> : k_chain<1>;
             const int64_t per = rp.slot_w * rp.slot_h;
@@ -2058,7 +2107,9 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                 const int64_t nb = std::min<int64_t>(c->wave_batch, rp.n_slots - sb);
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 0], c->stream));
                 const int G = c->tiles_per_wave;
-                if (c->use_wf) {
+                if (rp.mode == PBRT_MODE_THROUGHPUT) {
+                    // no offset chain: every sample's stream is known up front
+                } else if (c->use_wf) {
                     int rcc = wf_chain(c, sc, sb, nb);
                     if (rcc != PBRT_OK) return rcc;
                 } else if (c->use_ci) {
@@ -2075,8 +2126,14 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                                        kWave / G, c->d_ctr);
                 }
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 1], c->stream));
-                hipLaunchKernelGGL(k_paths, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
-                                   (unsigned)(rp.ndims * rp.spp * 8), c->stream, sc, rp, c->wb, sb, c->d_ctr);
+                if (rp.mode == PBRT_MODE_THROUGHPUT)
+                    hipLaunchKernelGGL(k_paths<true>, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
+                                       (unsigned)c->lay.total, c->stream, sc, rp, c->lay, c->d_jump, c->wb, sb, nb,
+                                       c->d_ctr);
+                else
+                    hipLaunchKernelGGL(k_paths<false>, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
+                                       (unsigned)(rp.ndims * rp.spp * 8), c->stream, sc, rp, c->lay, c->d_jump,
+                                       c->wb, sb, nb, c->d_ctr);
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 2], c->stream));
                 hipLaunchKernelGGL(k_film, dim3((unsigned)((nb * per + 255) / 256)), dim3(256), 0, c->stream,
                                    c->d_film, rp, c->wb, sb, nb, c->d_films);

@@ -960,6 +960,19 @@ static void film_tile_add(const pbrt_film_desc* fm, film_tile_t* ft, double pfx,
         }
 }
 
+/* THROUGHPUT mode ("Mode B"); NOT in the reference. The
+ * build's own definition, stated identically in csrc/pbrt_path.h mb_state:
+ * stream s of pixel pi (row-major in its tile) of tile t starts at PCG32
+ * state mb_state(t, pi, s) with the tile's increment; s = 0 feeds StartPixel,
+ * s = k >= 1 feeds sample k. Everything else is the EXACT arithmetic. */
+static uint64_t mb_mix(uint64_t x) {
+    uint64_t z = x + 0x9e3779b97f4a7c15ULL;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+static uint64_t mb_state(uint64_t tile, uint64_t pi, uint64_t s) { return mb_mix(mb_mix(mb_mix(tile) ^ pi) ^ s); }
+
 /* integrator.go:228-289 renderWorker body for one tile */
 static int render_tile(orc_ctx* oc, int64_t tile, film_tile_t* ft, double* s1d_buf) {
     const pbrt_scene_desc* sc = oc->scene;
@@ -976,15 +989,19 @@ static int render_tile(orc_ctx* oc, int64_t tile, film_tile_t* ft, double* s1d_b
     smp.ndims = rd->n_dims; smp.jitter = rd->jitter; smp.s1d = s1d_buf;
     orc_pcg_set_sequence(&smp.rng, (uint64_t)tile);   /* integrator.go:318,328 */
 
+    const int mb = rd->mode == PBRT_MODE_THROUGHPUT;
     oc->pc.kind = 0;
     oc->cur_tile = tile;
     if (setjmp(oc->pc.jb)) return -1;
     for (int64_t py = y0; py < y1; py++) {
         for (int64_t px = x0; px < x1; px++) {
             oc->cur_px = px; oc->cur_py = py;
+            const uint64_t pi = (uint64_t)((py - y0) * (x1 - x0) + (px - x0));
+            if (mb) smp.rng.state = mb_state((uint64_t)tile, pi, 0);
             sampler_start_pixel(&smp);
             while (sampler_next_sample(&smp)) {
                 oc->cur_sample = smp.sample_index;
+                if (mb) smp.rng.state = mb_state((uint64_t)tile, pi, (uint64_t)smp.sample_index);
                 /* sampler.go:75-80: pFilm = pixel + Get2D, pLens = Get2D, time = Get1D */
                 v2 u0 = sampler_get2d(&smp);
                 double fx = (double)px + u0.x, fy = (double)py + u0.y;

@@ -502,3 +502,63 @@ def test_1080p_64spp_properties_and_sampled_tiles():
             g, _ = r.render(one)
         o, _ = oracle_render(scene, one)
         assert same_bits(g, o), t
+
+
+# ------------------------------------------------- THROUGHPUT mode (Mode B)
+MB = abi.PBRT_MODE_THROUGHPUT
+MB_CASES = [
+    ("readme", 64, 48, dict(spp_x=2, spp_y=2)),
+    ("readme", 112, 80, dict(spp_x=8, spp_y=8)),
+    ("readme", 37, 23, dict(spp_x=3, spp_y=5, jitter=True)),
+    ("readme", 48, 40, dict(spp_x=4, spp_y=4, n_dims=7, max_depth=12)),
+    ("readme", 48, 40, dict(spp_x=4, spp_y=4, tile_size=13, rr_threshold=0.5)),
+    ("cornell", 48, 32, dict(spp_x=6, spp_y=6, max_depth=8)),
+]
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("case", MB_CASES, ids=lambda c: f"{c[0]}{c[1]}x{c[2]}-{c[3]}")
+def test_throughput_mode_bitexact_vs_oracle(case, kernel):
+    """Mode B on both device paths (serial lane-per-tile replay with reseeding,
+    and the chain-free wave-per-pixel k_paths<true>) equals the oracle's Mode B
+    restatement bit for bit."""
+    name, w, h, kw = case
+    scene = G.Scene.readme(w, h) if name == "readme" else G.Scene.cornell(w, h)
+    check(scene, abi.render_desc(**kw, mode=MB), kernel=kernel)
+
+
+@pytest.mark.parametrize("kw", [dict(n_dims=1), dict(integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING),
+                                dict(light_strategy=abi.PBRT_LIGHT_STRATEGY_POWER)])
+def test_throughput_mode_serial_fallback(kw):
+    """Renders the wave path cannot take run Mode B on the serial kernel."""
+    check(G.Scene.readme(40, 24), abi.render_desc(3, 3, mode=MB, **kw))
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_throughput_mode_panic_is_reported_like_the_oracle(kernel):
+    scene = panic_scene()
+    rd = abi.render_desc(2, 2, mode=MB)
+    rc, _, ost = O.render(scene.desc, rd, threads=1)
+    assert rc == abi.PBRT_E_REF_PANIC
+    with G.Renderer(scene, kernel=kernel) as r:
+        with pytest.raises(G.PbrtError) as ei:
+            r.render(rd)
+    st = ei.value.stats
+    assert ei.value.code == abi.PBRT_E_REF_PANIC
+    assert (st.panic_kind, st.panic_tile, st.panic_pixel_x, st.panic_pixel_y, st.panic_sample, st.panic_bounce) == (
+        ost.panic_kind, ost.panic_tile, ost.panic_px, ost.panic_py, ost.panic_sample, ost.panic_bounce)
+
+
+def test_throughput_mode_1080p_sampled_tiles_and_shards():
+    """Config B size in Mode B: every path traced, finite film, sampled tiles
+    bit-exact vs the oracle, and 3 interleaved shards sum to the frame's tiles."""
+    scene = G.Scene.readme(1920, 1080)
+    rd = abi.render_desc(8, 8, mode=MB)
+    with G.Renderer(scene) as r:
+        film, st = r.render(rd)
+        assert st.tiles_rendered == 8160 and st.paths_traced == 1920 * 1080 * 63
+        assert np.isfinite(film).all()
+        for t in (0, 4321, 8159):
+            g, _ = r.render(abi.render_desc(8, 8, tile_begin=t, tile_end=t + 1, mode=MB))
+            o, _ = oracle_render(scene, abi.render_desc(8, 8, tile_begin=t, tile_end=t + 1, mode=MB))
+            assert same_bits(g, o), t

@@ -97,3 +97,40 @@ def test_readme_bvh_shape():
     leaves = [d.nodes[i] for i in range(d.n_nodes) if d.nodes[i].n_prims > 0]
     assert len(leaves) == 23 and all(n.n_prims == 1 for n in leaves)
     assert sorted(n.offset for n in leaves) == list(range(23))
+
+
+# ------------------------------------------------ THROUGHPUT mode (Mode B)
+def test_throughput_mode_is_statistically_the_reference_image():
+    """Mode B swaps the per-tile PCG32 stream for one stream
+    per (pixel, sample); the image must be the same estimator. The reference's
+    estimator is heavy-tailed (BSDF.SampleF returns the local wi, parity
+    ledger #7, so beta = |wi.n|/pdf has fireflies), so the comparison is on
+    robust statistics. Noise scale: EXACT renders with tile 16 vs 8 (different
+    tile seeds for every pixel). Mode B vs EXACT must differ by about the same
+    clipped RMS, and its median / clipped mean must sit inside the spread of
+    the EXACT renders."""
+    sc = scene("readme", 128, 128)
+    inner = (slice(1, -1), slice(1, -1))   # film apron pixels collect fewer samples
+    a16 = O.render(sc.desc, abi.render_desc(4, 4, tile_size=16))[1][inner]
+    a8 = O.render(sc.desc, abi.render_desc(4, 4, tile_size=8))[1][inner]
+    rc, b16, st = O.render(sc.desc, abi.render_desc(4, 4, tile_size=16, mode=abi.PBRT_MODE_THROUGHPUT))
+    assert rc == 0 and st.paths == 128 * 128 * 15
+    b16 = b16[inner]
+    assert not np.array_equal(a16, b16)
+    cap = np.percentile(a16, 95)
+    clip = lambda x: np.clip(x, 0, cap)   # noqa: E731
+    noise = np.sqrt(np.mean((clip(a16) - clip(a8)) ** 2))
+    rms_b = np.sqrt(np.mean((clip(a16) - clip(b16)) ** 2))
+    assert 0.8 < rms_b / noise < 1.25, (rms_b, noise)
+    for stat in (np.median, lambda x: clip(x).mean()):
+        sa16, sa8, sb = stat(a16), stat(a8), stat(b16)
+        spread = abs(sa16 - sa8) + 0.01 * abs(sa16)
+        assert abs(sb - 0.5 * (sa16 + sa8)) < 3 * spread, (sa16, sa8, sb)
+
+
+def test_throughput_mode_is_deterministic_and_thread_invariant():
+    sc = scene("cornell", 40, 24)
+    rd = abi.render_desc(3, 3, mode=abi.PBRT_MODE_THROUGHPUT, max_depth=8)
+    _, a, _ = O.render(sc.desc, rd, threads=1)
+    _, b, _ = O.render(sc.desc, rd, threads=8)
+    assert a.tobytes() == b.tobytes() and a.any()
