@@ -370,7 +370,7 @@ struct NodeView {
 };
 // BVH nodes staged in LDS by kernels whose scene fits (README / Cornell:
 // <= 45 nodes). A file-scope __shared__ array, so every access is a ds_read.
-constexpr int kLdsNodes = 128;
+constexpr int kLdsNodes = 64;
 __shared__ DevNode g_nodes_lds[kLdsNodes];
 
 __device__ __forceinline__ NodeView load_node(const DevScene& sc, uint32_t i) {

@@ -413,13 +413,17 @@ __device__ uint64_t start_pixel_wave(const RenderParams& rp, const PcgJump& J, u
     return *sh_state;
 }
 
-template <int kWaves>
+// kDepth: LDS stack entries per lane. 32 when the nodes are staged in LDS
+// (<= kLdsNodes = 64 nodes: at most 31 interior nodes on any root-to-leaf
+// path, so the reference's [64] stack never holds more than 31 entries);
+// 64 otherwise. Bounce 1 (camera ray, first hit, BSDF) is read from the
+// PixelRec k_wf_primary wrote, so k_chain holds no second traversal.
+template <int kWaves, int kDepth>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8))) void k_chain(
     DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
     int64_t nslots_batch, int lanes_per_tile, Counters* __restrict__ ctr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    __shared__ uint16_t stack_lds[64 * kStackStride];
-    __shared__ ChainCache pcs[kMaxGroups];
+    __shared__ uint16_t stack_lds[kDepth * kStackStride];
     __shared__ GroupState gs[kMaxGroups];
     __shared__ uint64_t sh_state;
     const int lane = threadIdx.x;
@@ -432,9 +436,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8
     uint64_t* sbuf = (uint64_t*)(lds + lay.sbuf);
     uint32_t* dbuf = (uint32_t*)(lds + lay.dbuf);
     uint32_t* vbuf = (uint32_t*)(lds + lay.vbuf);
+    ChainCache* pcs = (ChainCache*)(lds + lay.total);   // G entries after the layout
     uint16_t* stack = stack_lds + lane;
     const int n = rp.spp, ndims = rp.ndims;
-    const pbrt_camera_desc& cam = *sc.camera;
     unsigned long long windows = 0;
     unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     long long tprev = clock64();
@@ -478,35 +482,17 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8
                 const uint64_t S = gs[q].S;
                 const int64_t pi = gs[q].pi;
                 const int64_t rec = bs * wb.ppt + pi;
-                int64_t x0, y0, x1, y1;
-                tile_bounds(rp, tile, x0, y0, x1, y1);
-                const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
                 const uint64_t S1 = start_pixel_wave(rp, J, S, inc, s1d, other, vbuf, &sh_state);
                 double* gs1d = wb.s1d + rec * wb.s1d_stride;
                 for (int idx = lane; idx < ndims * n; idx += kWave) gs1d[idx] = s1d[idx];
                 mark(0);
-                PixelRec& pr = wb.prec[rec];
-                // bounce 1, shared by every sample of the pixel
-                int panic0 = 0, hit0 = 0;
-                SI si0;
-                BSDF b0;
-                b0.n_bxdfs = 0;
-                Ray ray = camera_ray(cam, (double)px + 0.0, (double)py + 0.0, s1d[1 < n ? 1 : 0], V2{0.0, 0.0});
-                if (n > 1 && 1 < rp.max_depth) {
-                    hit0 = bvh_traverse<false>(sc, ray, &si0, stack, panic0) ? 1 : 0;
-                    if (!panic0 && hit0 && compute_bsdf(sc, si0, b0) < 0) panic0 = -1;
-                }
+                const PixelRec& pr = wb.prec[rec];   // bounce 1 (k_wf_primary)
+                const int panic0 = pr.panic0, hit0 = pr.hit;
                 if (lane == 0) {
-                    pcs[q].si = si0;
-                    pcs[q].b = b0;
-                    pcs[q].wo = ray.d;
+                    pcs[q].si = pr.si;
+                    pcs[q].b = pr.b;
+                    pcs[q].wo = pr.wo;
                     pcs[q].hit = hit0;
-                    pr.si = si0;
-                    pr.b = b0;
-                    pr.wo = ray.d;
-                    pr.hit = panic0 ? 0 : hit0;
-                    pr.panic0 = panic0;
-                    pr.nvalid = n;
                     GroupState& s = gs[q];
                     s.S = S1;
                     wb.tile_npx[bs] = (int32_t)(pi + 1);
@@ -1558,6 +1544,7 @@ struct pbrt_gpu_ctx {
     int lanes_per_wave = 64;
     bool lanes_per_wave_set = false;
     int min_waves = 1;      // amdgpu_waves_per_eu variant of k_render_exact
+    int occ_req = 0;        // opts.occupancy as given (0 = each kernel's default)
     int kernel_req = PBRT_KERNEL_AUTO;
     int last_kernel = 0;    // PBRT_KERNEL_SERIAL / PBRT_KERNEL_WAVE
     PcgJump* d_jump = nullptr;
@@ -2026,6 +2013,7 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
         c->lanes_per_wave_set = true;
     }
     if (opts && (opts->occupancy == 2 || opts->occupancy == 4 || opts->occupancy == 8)) c->min_waves = opts->occupancy;
+    if (opts) c->occ_req = opts->occupancy;
     if (opts && (opts->kernel < PBRT_KERNEL_AUTO || opts->kernel > PBRT_KERNEL_WAVE_CI)) {
         delete c;
         return PBRT_E_INVALID;
@@ -2095,7 +2083,11 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
             c->last_kernel = rp.mode == PBRT_MODE_THROUGHPUT ? PBRT_KERNEL_WAVE
                              : c->use_wf ? PBRT_KERNEL_WAVEFRONT : c->use_ci ? PBRT_KERNEL_WAVE_CI : PBRT_KERNEL_WAVE;
             c->wf_iters = 0;
-            auto chain = c->min_waves >= 2 ? k_chain<2> : k_chain<1>;
+            const bool lds_nodes = c->host_scene.n_nodes <= kLdsNodes;
+            // k_chain: 2 waves/SIMD by default (a few spilled registers; the
+            // trajectories are latency-bound), occupancy 1 on request
+            auto chain = c->occ_req == 1 ? (lds_nodes ? k_chain<1, 32> : k_chain<1, 64>)
+                                           : (lds_nodes ? k_chain<2, 32> : k_chain<2, 64>);
             const int64_t per = rp.slot_w * rp.slot_h;
             c->n_batches = (int)((rp.n_slots + c->wave_batch - 1) / c->wave_batch);
             while ((int)c->bev.size() < 3 * c->n_batches) {
@@ -2121,9 +2113,11 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                                        (unsigned)c->lay_ci.total, c->stream, sc, rp, c->lay_ci, c->d_jump, c->wb, sb,
                                        nb, kWave / Gc, ring, c->d_ctr);
                 } else {
+                    hipLaunchKernelGGL(k_wf_primary, dim3((unsigned)((nb * c->wb.ppt + kWave - 1) / kWave)),
+                                       dim3(kWave), 0, c->stream, sc, rp, c->wb, sb, nb);
                     hipLaunchKernelGGL(chain, dim3((unsigned)((nb + G - 1) / G)), dim3(kWave),
-                                       (unsigned)c->lay.total, c->stream, sc, rp, c->lay, c->d_jump, c->wb, sb, nb,
-                                       kWave / G, c->d_ctr);
+                                       (unsigned)(c->lay.total + G * (int)sizeof(ChainCache)), c->stream, sc, rp,
+                                       c->lay, c->d_jump, c->wb, sb, nb, kWave / G, c->d_ctr);
                 }
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 1], c->stream));
                 if (rp.mode == PBRT_MODE_THROUGHPUT)
