@@ -588,8 +588,16 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8
 //                StartPixel on the pixel's own stream (mb_state(tile, pi, 0)),
 //                bounce 1, and sample k's stream mb_state(tile, pi, k); it
 //                writes the PixelRec fields k_film and k_panic_reduce read.
-template <bool kMB>
-__global__ __launch_bounds__(kWave) void k_paths(DevScene sc, RenderParams rp, ChainLayout lay,
+#ifndef PBRT_CHAIN_WAVES
+#define PBRT_CHAIN_WAVES 2
+#endif
+constexpr int kChainWaves = PBRT_CHAIN_WAVES;   // k_chain waves/SIMD (build option)
+#ifndef PBRT_PATHS_WAVES
+#define PBRT_PATHS_WAVES 2
+#endif
+constexpr int kPathsWaves = PBRT_PATHS_WAVES;   // k_paths waves/SIMD (build option)
+template <bool kMB, int kWaves = 1>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8))) void k_paths(DevScene sc, RenderParams rp, ChainLayout lay,
                                                  const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
                                                  int64_t nslots_batch, Counters* __restrict__ ctr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -2087,7 +2095,7 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
             // k_chain: 2 waves/SIMD by default (a few spilled registers; the
             // trajectories are latency-bound), occupancy 1 on request
             auto chain = c->occ_req == 1 ? (lds_nodes ? k_chain<1, 32> : k_chain<1, 64>)
-                                           : (lds_nodes ? k_chain<2, 32> : k_chain<2, 64>);
+                                           : (lds_nodes ? k_chain<kChainWaves, 32> : k_chain<kChainWaves, 64>);
             const int64_t per = rp.slot_w * rp.slot_h;
             c->n_batches = (int)((rp.n_slots + c->wave_batch - 1) / c->wave_batch);
             while ((int)c->bev.size() < 3 * c->n_batches) {
@@ -2121,11 +2129,11 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                 }
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 1], c->stream));
                 if (rp.mode == PBRT_MODE_THROUGHPUT)
-                    hipLaunchKernelGGL(k_paths<true>, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
+                    hipLaunchKernelGGL((k_paths<true, kPathsWaves>), dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
                                        (unsigned)c->lay.total, c->stream, sc, rp, c->lay, c->d_jump, c->wb, sb, nb,
                                        c->d_ctr);
                 else
-                    hipLaunchKernelGGL(k_paths<false>, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
+                    hipLaunchKernelGGL((k_paths<false, kPathsWaves>), dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
                                        (unsigned)(rp.ndims * rp.spp * 8), c->stream, sc, rp, c->lay, c->d_jump,
                                        c->wb, sb, nb, c->d_ctr);
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 2], c->stream));
