@@ -1974,8 +1974,12 @@ int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
          c->kernel_req == PBRT_KERNEL_WAVE_CI) && !c->use_spec)
         return set_err(c, PBRT_E_UNSUPPORTED, "render not eligible for the wave-parallel kernels");
     c->use_wf = c->use_spec && c->kernel_req == PBRT_KERNEL_WAVEFRONT;
-    c->use_ci = c->use_spec && c->kernel_req == PBRT_KERNEL_WAVE_CI;
-    if (c->use_ci && !(c->host_scene.n_nodes <= kLdsNodes && c->lay_ci.total <= 12 * 1024))
+    const bool ci_fits = c->host_scene.n_nodes <= kLdsNodes && c->lay_ci.total <= 12 * 1024;
+    // AUTO: the continuous-issue chain wherever it fits (measured ~8% faster
+    // than the window chain on config B), else the window chain
+    c->use_ci = c->use_spec && (c->kernel_req == PBRT_KERNEL_WAVE_CI ||
+                                (c->kernel_req == PBRT_KERNEL_AUTO && ci_fits));
+    if (c->use_ci && !ci_fits)
         return set_err(c, PBRT_E_UNSUPPORTED, "render not eligible for the continuous-issue chain kernel");
     if (c->use_spec && rp.n_slots > 0) {
         int rcw = wave_buffers(c);

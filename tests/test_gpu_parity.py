@@ -59,8 +59,8 @@ def oracle_render(scene, rd):
 def check(scene, rd, **kw):
     film, st = gpu_render(scene, rd, **kw)
     if kw.get("kernel", "auto") == "auto":
-        want = abi.PBRT_KERNEL_WAVE if wave_eligible(rd) else abi.PBRT_KERNEL_SERIAL
-        assert st.kernel == want
+        want = (abi.PBRT_KERNEL_WAVE, abi.PBRT_KERNEL_WAVE_CI) if wave_eligible(rd) else (abi.PBRT_KERNEL_SERIAL,)
+        assert st.kernel in want
     ofilm, ost = oracle_render(scene, rd)
     assert st.paths_traced == ost.paths
     assert same_bits(film, ofilm), f"{int((film != ofilm).sum())} film values differ"
