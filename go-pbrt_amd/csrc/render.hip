@@ -19,6 +19,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -317,12 +318,15 @@ struct GroupState {
 };
 constexpr int kMaxGroups = 16;
 
-// Stratified.StartPixel (stratified.go:21-48) for one pixel, by the whole
-// 64-lane workgroup (all lanes call it). The shuffled 1D values are left in
-// s1d (LDS); returns the PCG32 state after the pixel's draws.
+// Stratified.StartPixel (stratified.go:21-48) for one pixel. Every thread of
+// the workgroup calls it (it holds the block's barriers); the first wave does
+// the work. The shuffled 1D values are left in s1d (LDS); returns the PCG32
+// state after the pixel's draws.
+__shared__ int g_sp_overflow;
 __device__ uint64_t start_pixel_wave(const RenderParams& rp, const PcgJump& J, uint64_t S, uint64_t inc, double* s1d,
                                      uint16_t* other, uint32_t* vbuf, uint64_t* sh_state) {
     const int lane = threadIdx.x;
+    const bool w0 = lane < kWave;
     const int n = rp.spp, ndims = rp.ndims;
     const double inv_n = 1.0 / (double)n;
     const int s1 = rp.jitter ? 2 * n : n, s2 = rp.jitter ? 3 * n : n;   // StartPixel draws per 1D / 2D dim
@@ -337,15 +341,17 @@ __device__ uint64_t start_pixel_wave(const RenderParams& rp, const PcgJump& J, u
     bool serial_sp = rp.sp_serial != 0;
     if (!serial_sp) {
         const int E = rp.sp_events, V = rp.sp_draws;
-        uint64_t st = pcg_advance(J, S, inc, (uint64_t)lane);
-        for (int t = lane; t < V; t += kWave) {
-            vbuf[t] = pcg_output(st);
-            st = J.a[6] * st + inc * J.b[6];   // +64 draws
+        if (w0) {
+            uint64_t st = pcg_advance(J, S, inc, (uint64_t)lane);
+            for (int t = lane; t < V; t += kWave) {
+                vbuf[t] = pcg_output(st);
+                st = J.a[6] * st + inc * J.b[6];   // +64 draws
+            }
         }
         __syncthreads();
         int R = 0;
         bool overflow = false;
-        for (int cb = 0; cb < E; cb += kWave) {
+        for (int cb = 0; w0 && cb < E; cb += kWave) {
             const int e = cb + lane;
             int kind = 0, slt = 0, i = 0;   // 0 none, 1 1D float, 2 1D pick, 3 2D pick
             if (e < E) {
@@ -379,9 +385,11 @@ __device__ uint64_t start_pixel_wave(const RenderParams& rp, const PcgJump& J, u
                 other[slt] = (uint16_t)(i + (int)(v % b));
             R += __shfl(local, kWave - 1);
         }
-        serial_sp = overflow;
+        if (lane == 0) g_sp_overflow = overflow;
+        __syncthreads();
+        serial_sp = g_sp_overflow != 0;
         if (!serial_sp) {
-            if (!rp.jitter)
+            if (!rp.jitter && w0)
                 for (int idx = lane; idx < ndims * n; idx += kWave)
                     s1d[idx] = gomath::min(((double)(idx % n) + 0.5) * inv_n, gomath::kOneMinusEpsilon);
             __syncthreads();
@@ -1212,32 +1220,46 @@ struct CiGroup {
     int pad;
 };
 
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2, 8))) void k_chain_ci(
+//
+// kW > 1: one tile per workgroup of kW waves (lanes_per_tile = 64 * kW). The
+// tile's chain then advances kW times as many candidates per step, which cuts
+// the slowest tile's latency, the frame's critical path when tiles are few
+// per GPU (a multi-GPU shard). Idle lanes are ranked across the waves through
+// LDS; StartPixel runs on the first wave.
+template <int kW>
+__global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(2, 8))) void k_chain_ci(
     DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
-    int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr) {
+    int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr,
+    const uint32_t* __restrict__ order, uint32_t* __restrict__ ticks) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const uint64_t t_begin = wall_clock64();
     // <= kLdsNodes (64) staged nodes: a binary tree that small is at most 31
     // interior nodes deep, so 32 stack entries per lane cannot overflow
-    __shared__ uint16_t stack_lds[32 * kStackStride];
+    constexpr int kT = kWave * kW;   // threads per workgroup (stack stride)
+    __shared__ uint16_t stack_lds[32 * kT];
     __shared__ ChainCache pcs[kCiMaxGroups];
     __shared__ CiGroup gs[kCiMaxGroups];
     __shared__ uint64_t sh_state;
-    const int lane = threadIdx.x;
+    __shared__ int wcnt[kW];
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
     stage_nodes(sc);
-    const int L = lanes_per_tile, G = kWave / L;
-    const int g = lane / L, gl = lane - g * L;
+    const int L = kW > 1 ? kT : lanes_per_tile, G = kW > 1 ? 1 : kWave / L;
+    const int g = kW > 1 ? 0 : lane / L, gl = kW > 1 ? tid : lane - g * L;
+    // workgroup -> tile slot: heaviest-first order from the previous frame
+    // (one tile per workgroup only), else the identity
+    const int64_t blk = order ? (int64_t)order[blockIdx.x] : (int64_t)blockIdx.x;
     const uint32_t R = (uint32_t)ring_size;
     const PcgJump& J = *jump;
     double* s1d = (double*)(lds + lay.s1d);
     uint16_t* other = (uint16_t*)(lds + lay.other);
     uint32_t* vbuf = (uint32_t*)(lds + lay.vbuf);
     RingEnt* ring = (RingEnt*)(lds + lay.ring) + (size_t)g * R;
-    uint16_t* stack = stack_lds + lane;
+    uint16_t* stack = stack_lds + tid;
     const int n = rp.spp, ndims = rp.ndims;
     const pbrt_camera_desc& cam = *sc.camera;
     const unsigned long long gmask = L >= 64 ? ~0ULL : (((1ULL << L) - 1ULL) << (g * L));
     const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
-    const int64_t bs = (int64_t)blockIdx.x * G + g;
+    const int64_t bs = blk * G + g;
     const uint64_t inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + (bs < nslots_batch ? bs : 0)));
     unsigned long long steps = 0;
     unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1247,9 +1269,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2, 8))) v
         ph[k] += (unsigned long long)(now - tprev);
         tprev = now;
     };
-    if (lane < G) {
-        const int64_t b = (int64_t)blockIdx.x * G + lane;
-        CiGroup& s = gs[lane];
+    if (tid < G) {
+        const int64_t b = blk * G + tid;
+        CiGroup& s = gs[tid];
         s.pi = 0;
         s.kh = 1;
         s.head = s.nxt = 0;
@@ -1293,7 +1315,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2, 8))) v
         // ---- (1) groups that need a pixel: StartPixel + bounce 1, one group at a time
         for (int q = 0; q < G; q++) {
             while (gs[q].phase == 0) {
-                const int64_t bq = (int64_t)blockIdx.x * G + q;
+                const int64_t bq = blk * G + q;
                 const int64_t tile = tile_of_slot(rp, slot_base + bq);
                 const uint64_t incq = pcg_inc_of((uint64_t)tile);
                 const int64_t pi = gs[q].pi;
@@ -1303,14 +1325,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2, 8))) v
                 const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
                 const uint64_t S1 = start_pixel_wave(rp, J, gs[q].S, incq, s1d, other, vbuf, &sh_state);
                 double* gs1d = wb.s1d + rec * wb.s1d_stride;
-                for (int idx = lane; idx < ndims * n; idx += kWave) gs1d[idx] = s1d[idx];
+                for (int idx = tid; idx < ndims * n; idx += kT) gs1d[idx] = s1d[idx];
                 RingEnt* rq = (RingEnt*)(lds + lay.ring) + (size_t)q * R;
-                for (uint32_t i = (uint32_t)lane; i < R; i += kWave) rq[i].tag = kNoOff;
+                for (uint32_t i = (uint32_t)tid; i < R; i += kT) rq[i].tag = kNoOff;
                 // bounce 1 (camera ray, first hit, BSDF) was computed for every
                 // pixel record by k_wf_primary; only the ray time needs StartPixel
                 PixelRec& pr = wb.prec[rec];
                 const int hit0 = pr.hit, panic0 = pr.panic0;
-                if (lane == 0) {
+                if (tid == 0) {
                     if (hit0)   // the camera ray's time (Get1D after pFilm, pLens) of the pixel's first traced sample
                         pr.si.time = camera_ray(cam, (double)px, (double)py, s1d[1 < n ? 1 : 0], V2{0.0, 0.0}).time;
                     pcs[q].si = pr.si;
@@ -1348,8 +1370,20 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2, 8))) v
         {
             const bool idle = sg.phase == 1 && off == kNoOff;
             const unsigned long long m = __ballot(idle) & gmask;
-            const int nidle = __popcll(m);
+            int nidle = __popcll(m);
             int rank = __popcll(m & lt_mask);
+            if (kW > 1) {   // rank the idle lanes across the tile's waves
+                if (lane == 0) wcnt[wv] = nidle;
+                __syncthreads();
+                int before = 0, tot = 0;
+                for (int w = 0; w < kW; w++) {
+                    const int cw = wcnt[w];
+                    before += w < wv ? cw : 0;
+                    tot += cw;
+                }
+                rank += before;
+                nidle = tot;
+            }
             const int re = (sg.reissue && nidle > 0) ? 1 : 0;
             const uint32_t span = sg.head + R - sg.nxt;   // offsets < head + R keep the ring collision-free
             const int avail = (int)((span + 1) / 2);
@@ -1398,7 +1432,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2, 8))) v
         if (tracing) {
             int panic = 0, best;
             V3 ph;
-            bvh_walk<false>(sc, ray, stack, panic, best, ph);
+            bvh_walk<false, kT>(sc, ray, stack, panic, best, ph);
             mark(2);
             uint32_t d = kNoOff;
             if (panic) {
@@ -1470,9 +1504,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2, 8))) v
         }
         mark(4);
     }
-    if (lane == 0) {
+    if (tid == 0) {
         atomicAdd(&ctr->windows, steps);
         for (int k = 0; k < 8; k++) atomicAdd(&ctr->phase[k], ph[k]);
+        if (ticks && G == 1 && bs < nslots_batch) ticks[bs] = (uint32_t)min(wall_clock64() - t_begin, (uint64_t)0xFFFFFFFFu);
     }
 }
 
@@ -1599,6 +1634,15 @@ struct pbrt_gpu_ctx {
     PanicRec* d_panics = nullptr;
     size_t panics_cap = 0;
     Counters* d_ctr = nullptr;
+    // k_chain_ci heaviest-first schedule: per-slot chain time of the last
+    // EXACT frame (wall_clock64 ticks) and the slot order derived from it
+    uint32_t* d_ticks = nullptr;
+    uint32_t* d_slot_order = nullptr;
+    int64_t ticks_cap = 0;
+    std::vector<uint32_t> h_slot_order;
+    uint64_t order_key = 0, ticks_key = 0;
+    int64_t ticks_n = 0;
+    bool ticks_pending = false;
     double* d_out = nullptr;
     size_t out_cap = 0;
     // last render
@@ -1770,6 +1814,43 @@ bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Rend
     Lci.ring = put(kCiRingBytes);
     Lci.total = (int)off;
     return L.total <= 48 * 1024;
+}
+
+// Waves per tile of k_chain_ci for a launch of nb tiles. The frame's EXACT
+// time is bounded below by its slowest tile's chain, so when the tiles of a
+// launch cannot keep every wave slot busy (2 waves/SIMD) a tile gets 2 or 4
+// waves. PBRT_CI_WAVES (1, 2, 4) overrides.
+int ci_waves(const pbrt_gpu_ctx* c, int64_t nb) {
+    if (const char* e = getenv("PBRT_CI_WAVES")) {
+        const int v = atoi(e);
+        if (v == 1 || v == 2 || v == 4) return v;
+    }
+    if (c->tiles_per_wave > 1) return 1;
+    // measured on config B shards (tools/shard_sim.py): 8160 tiles -> 1,
+    // 4080 -> 2, 2040 and 1020 -> 4
+    const int64_t slots = (int64_t)c->n_simd * 2;   // 2 waves/SIMD
+    if (nb <= slots) return 4;
+    if (nb <= 2 * slots) return 2;
+    return 1;
+}
+
+// k_chain_ci schedule. An EXACT frame lasts at least as long as its slowest
+// tile's chain, and workgroups start in launch order, so a heavy tile that
+// starts late stretches the frame. Each EXACT frame records every tile's
+// chain time; the next frame of the same configuration on this context
+// launches its tiles heaviest first (LPT). Only the schedule changes, never
+// a result. PBRT_CI_ORDER=0 disables it.
+bool ci_order_enabled() {
+    const char* e = getenv("PBRT_CI_ORDER");
+    return !(e && atoi(e) == 0);
+}
+uint64_t schedule_key(const RenderParams& rp, int kw) {
+    const int64_t v[] = {rp.film_min_x, rp.film_min_y, rp.film_w,   rp.film_h,    rp.tile_size, rp.tile_begin,
+                         rp.tile_stride, rp.n_slots,   rp.spp,      rp.ndims,     rp.jitter,    rp.max_depth,
+                         rp.flags,       kw,           (int64_t)(rp.rr_threshold * 1e9)};
+    uint64_t h = 1469598103934665603ull;
+    for (int64_t x : v) h = (h ^ (uint64_t)x) * 1099511628211ull;
+    return h;
 }
 
 // Carve the per-batch buffers of the wave path (budget: PBRT_WAVE_BUFFER_GB, default 12).
@@ -2119,11 +2200,45 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                 } else if (c->use_ci) {
                     hipLaunchKernelGGL(k_wf_primary, dim3((unsigned)((nb * c->wb.ppt + kWave - 1) / kWave)),
                                        dim3(kWave), 0, c->stream, sc, rp, c->wb, sb, nb);
-                    const int Gc = std::min(G, kCiMaxGroups);
-                    const int ring = kCiRingBytes / (int)sizeof(RingEnt) / Gc;
-                    hipLaunchKernelGGL(k_chain_ci, dim3((unsigned)((nb + Gc - 1) / Gc)), dim3(kWave),
-                                       (unsigned)c->lay_ci.total, c->stream, sc, rp, c->lay_ci, c->d_jump, c->wb, sb,
-                                       nb, kWave / Gc, ring, c->d_ctr);
+                    const int kw = ci_waves(c, nb);
+                    const uint32_t* order = nullptr;
+                    uint32_t* ticks = nullptr;
+                    if ((kw > 1 || G == 1) && c->n_batches == 1 && ci_order_enabled()) {
+                        if (c->ticks_cap < nb) {
+                            if (c->d_ticks) (void)hipFree(c->d_ticks);
+                            if (c->d_slot_order) (void)hipFree(c->d_slot_order);
+                            c->d_ticks = c->d_slot_order = nullptr;
+                            c->ticks_cap = 0;
+                            HIPCHK(c, hipMalloc((void**)&c->d_ticks, sizeof(uint32_t) * (size_t)nb));
+                            HIPCHK(c, hipMalloc((void**)&c->d_slot_order, sizeof(uint32_t) * (size_t)nb));
+                            c->ticks_cap = nb;
+                        }
+                        const uint64_t key = schedule_key(rp, kw);
+                        if (c->order_key == key && (int64_t)c->h_slot_order.size() == nb) {
+                            HIPCHK(c, hipMemcpyAsync(c->d_slot_order, c->h_slot_order.data(), sizeof(uint32_t) * (size_t)nb,
+                                                     hipMemcpyHostToDevice, c->stream));
+                            order = c->d_slot_order;
+                        }
+                        ticks = c->d_ticks;
+                        c->ticks_pending = true;
+                        c->ticks_key = key;
+                        c->ticks_n = nb;
+                    }
+                    if (kw > 1) {   // one tile per workgroup of kw waves; the ring grows with the lanes
+                        const int ring = kw * kCiRingBytes / (int)sizeof(RingEnt);
+                        const unsigned lds = (unsigned)(c->lay_ci.total + (kw - 1) * kCiRingBytes);
+                        auto kern = kw == 2 ? k_chain_ci<2> : k_chain_ci<4>;
+                        hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(kWave * kw), lds, c->stream, sc, rp,
+                                           c->lay_ci, c->d_jump, c->wb, sb, nb, kWave * kw, ring, c->d_ctr, order,
+                                           ticks);
+                    } else {
+                        const int Gc = std::min(G, kCiMaxGroups);
+                        const int ring = kCiRingBytes / (int)sizeof(RingEnt) / Gc;
+                        hipLaunchKernelGGL(k_chain_ci<1>, dim3((unsigned)((nb + Gc - 1) / Gc)), dim3(kWave),
+                                           (unsigned)c->lay_ci.total, c->stream, sc, rp, c->lay_ci, c->d_jump, c->wb,
+                                           sb, nb, kWave / Gc, ring, c->d_ctr, Gc == 1 ? order : nullptr,
+                                           Gc == 1 ? ticks : nullptr);
+                    }
                 } else {
                     hipLaunchKernelGGL(k_wf_primary, dim3((unsigned)((nb * c->wb.ppt + kWave - 1) / kWave)),
                                        dim3(kWave), 0, c->stream, sc, rp, c->wb, sb, nb);
@@ -2198,6 +2313,16 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
         (void)hipEventElapsedTime(&p, c->bev[3 * b + 1], c->bev[3 * b + 2]);
         st.chain_ms += a;
         st.paths_ms += p;
+    }
+    if (c->ticks_pending) {   // heaviest-first slot order for the next frame of this configuration
+        c->ticks_pending = false;
+        std::vector<uint32_t> t((size_t)c->ticks_n);
+        HIPCHK(c, hipMemcpy(t.data(), c->d_ticks, sizeof(uint32_t) * t.size(), hipMemcpyDeviceToHost));
+        c->h_slot_order.resize(t.size());
+        for (size_t i = 0; i < t.size(); i++) c->h_slot_order[i] = (uint32_t)i;
+        std::stable_sort(c->h_slot_order.begin(), c->h_slot_order.end(),
+                         [&](uint32_t a, uint32_t b) { return t[a] > t[b]; });
+        c->order_key = c->ticks_key;
     }
     if (ctr.any_panic) {
         std::vector<PanicRec> pr((size_t)c->rp.n_slots);
@@ -2319,7 +2444,7 @@ void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_shapes, c->d_materials, c->d_prims, c->d_nodes, c->d_lights, c->d_camera, c->d_film,
                     c->d_dist,   c->d_films,     c->d_s1d,   c->d_panics, c->d_ctr,   c->d_out,    c->d_jump,
-                    c->d_wave,   c->d_fprims, c->d_wf};
+                    c->d_wave,   c->d_fprims, c->d_wf,     c->d_ticks, c->d_slot_order};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : c->bev) (void)hipEventDestroy(e);

@@ -368,7 +368,41 @@ def test_wave_ci_readme_256_and_odd_draw_counts(tiles_per_wave):
           lanes_per_wave=tiles_per_wave)
 
 
-def test_wave_ci_panic_is_reported_like_the_oracle():
+@pytest.mark.parametrize("ci_waves", ["1", "2", "4"])
+@pytest.mark.parametrize("kw", WAVE_VARIANTS)
+def test_wave_ci_waves_per_tile(kw, ci_waves, monkeypatch):
+    """k_chain_ci with 1, 2 or 4 waves cooperating on one tile's chain
+    (idle lanes ranked across waves, StartPixel on the first wave)."""
+    monkeypatch.setenv("PBRT_CI_WAVES", ci_waves)
+    check(G.Scene.readme(48, 40), abi.render_desc(**kw), kernel="wave_ci")
+
+
+@pytest.mark.parametrize("ci_waves", ["1", "2", "4"])
+def test_wave_ci_waves_per_tile_larger_frames(ci_waves, monkeypatch):
+    monkeypatch.setenv("PBRT_CI_WAVES", ci_waves)
+    check(G.Scene.readme(112, 80), abi.render_desc(8, 8), kernel="wave_ci")
+    check(G.Scene.cornell(48, 32), abi.render_desc(6, 6, max_depth=12, rr_threshold=0.5), kernel="wave_ci")
+
+
+@pytest.mark.parametrize("ci_waves", ["1", "2", "4"])
+def test_wave_ci_heaviest_first_schedule_keeps_bits(ci_waves, monkeypatch):
+    """The second frame of a configuration launches its tiles in the
+    heaviest-first order measured on the first; only the schedule changes."""
+    monkeypatch.setenv("PBRT_CI_WAVES", ci_waves)
+    scene = G.Scene.readme(112, 80)
+    rds = [abi.render_desc(8, 8), abi.render_desc(4, 4, tile_begin=1, tile_stride=2)]
+    with G.Renderer(scene, kernel="wave_ci") as r:
+        for rd in rds:
+            ofilm, _ = oracle_render(scene, rd)
+            for _ in range(3):
+                film, st = r.render(rd)
+                assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
+                assert same_bits(film, ofilm)
+
+
+@pytest.mark.parametrize("ci_waves", ["1", "4"])
+def test_wave_ci_panic_is_reported_like_the_oracle(ci_waves, monkeypatch):
+    monkeypatch.setenv("PBRT_CI_WAVES", ci_waves)
     scene = panic_scene()
     rd = abi.render_desc(2, 2)
     rc, _, ost = O.render(scene.desc, rd, threads=1)
