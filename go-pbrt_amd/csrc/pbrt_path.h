@@ -45,7 +45,7 @@ struct DevScene {
     const pbrt_material_desc* materials;
     const pbrt_primitive_desc* prims;
     const struct DevNode* nodes;   // device copy of pbrt_bvh_node[], 64-byte records
-    const struct DevNode* lnodes_unused;   // (layout slot kept; see g_nodes_lds / use_lds_nodes)
+    const uint32_t* order;         // [8 octants][n_nodes] preorder visit table (see bvh_walk)
     const struct DevPrim* fprims;  // primitive + its shape in one record (leaf tests)
     const pbrt_light_desc* lights;
     const pbrt_camera_desc* camera;
@@ -53,6 +53,7 @@ struct DevScene {
     const pbrt_distribution_desc* dist;   // Path light distribution (may be null)
     int n_prims, n_nodes, n_lights;
     int use_lds_nodes;   // the kernel staged nodes[] in g_nodes_lds (uniform)
+    int n_leaves;        // leaves of the BVH (order[8 * n_nodes + oct * n_nodes + j]: leaf preorder)
 };
 
 // ---------------------------------------------------------------- PCG32 (rng.go)
@@ -419,43 +420,111 @@ __device__ __forceinline__ bool node_hit(const NodeView& nd, const Ray& r, V3 in
     return (hit & (int)(tmin < r.tmax) & (int)(tmax > 0)) != 0;
 }
 
-// BVH.Intersect (bvh.go:659-712) / IntersectP (:713-765). The [64] node stack
-// lives in LDS (one uint16 column per lane).
-//
-// Structured "while-while" for 64-lane waves: loop A walks interior nodes
-// until the lane reaches a leaf whose box it hits (or empties its stack),
-// loop B then tests that leaf's primitives, so the wave runs the expensive
-// shape code once per leaf round instead of once per node step. Node order,
-// box tests and TMax updates are exactly the reference's.
+// Preorder visit table of the BVH, one per ray-direction octant (built on the
+// host, dev_order in render.hip). The reference's traversal (bvh.go:659-765)
+// is a depth-first walk whose child order at an interior node depends only on
+// the sign of the ray direction along the node's split axis: for a given
+// octant it visits nodes in one fixed preorder, skipping the subtree of every
+// node whose box test fails. Entry i of an octant's table holds
+//   bits  0-14  the node index (pbrt_bvh_node order)
+//   bit   15    a hit at this interior node would push past the [64] stack
+//               (bvh.go:670: the reference panics there)
+//   bits 16-31  the table index that follows the node's subtree (its skip)
+constexpr uint32_t kOrdNode = 0x7FFFu, kOrdOverflow = 0x8000u;
+// Leaves only, per octant, in that preorder (LDS-staged trees).
+__shared__ uint16_t g_leaf_lds[8 * kLdsNodes];
+
+// Shared leaf-primitive loop of both walks: tests the leaf's primitives in
+// order; returns 1 when an any-hit query is answered, -1 on a panic.
+template <bool kAny>
+__device__ __forceinline__ int leaf_prims(const DevScene& sc, uint32_t first, uint32_t np, Ray& ray, int& panic,
+                                          int& best, V3& best_ph) {
+    for (uint32_t k = 0; k < np; k++) {
+        double t_hit;
+        V3 ph;
+        const bool h = prim_hit_t(sc, (int)(first + k), ray, t_hit, ph, panic);
+        if (panic) return -1;
+        if (h) {
+            if (kAny) return 1;
+            ray.tmax = t_hit;
+            best = (int)(first + k);
+            best_ph = ph;
+        }
+    }
+    return 0;
+}
+
+// BVH.Intersect (bvh.go:659-712) / IntersectP (:713-765).
 //
 // Closest hit: each accepted primitive only shrinks TMax; the interaction of
 // the LAST accepted one is built once after the walk from its hit point. This
 // equals the reference's per-hit SurfaceInteraction: every field is a function
 // of that hit point and of the (unchanged) ray, and the shared-interaction
 // aliasing of TransformedPrimitive (#20) only ever touches the last one.
-//
 // bvh_walk leaves the closest primitive in `best` (-1: none) and its hit point
-// in `best_ph`; kStride is the distance between a lane's stack entries (the
-// block size: one uint16 column per thread).
+// in `best_ph`.
+//
+// LDS-staged trees (<= 64 nodes: README, Cornell) walk only their leaves, in
+// the octant's preorder (g_leaf_lds), each box tested with the current TMax.
+// This tests exactly the primitives the reference tests, in its order, with
+// its TMax. A child's box lies inside its parent's (bounds are unions,
+// bvh.go:54-66) and the slab values are monotone in the bounds under
+// rounding, so: if the reference rejects an interior node (with the TMax of
+// its visit), every leaf below it fails its own test with the smaller or
+// equal TMax of its turn; and a leaf that passes implies that all its
+// ancestors passed when the reference visited them. Interior nodes therefore
+// decide nothing, and a 64-node tree cannot overflow the [64] stack.
+//
+// Larger trees walk with the reference's [64] stack in LDS (one uint16 column
+// per lane, kStride apart), structured "while-while" for 64-lane waves: loop
+// A walks interior nodes until the lane reaches a leaf whose box it hits,
+// loop B tests that leaf's primitives.
 template <bool kAny, int kStride = kStackStride>
 __device__ inline bool bvh_walk(const DevScene& sc, Ray& ray, uint16_t* stack, int& panic, int& best, V3& best_ph) {
     best = -1;
-    if (sc.n_nodes == 0) return false;
+    const int n = sc.n_nodes;
+    if (n == 0) return false;
     V3 inv{1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z};
     const int nx = inv.x < 0, ny = inv.y < 0, nz = inv.z < 0;
+    STEP_T(StepTimer tt; tt.start();)
+    if (sc.use_lds_nodes) {   // uniform: n <= kLdsNodes
+        (void)stack;
+        const int nl = sc.n_leaves;
+        const uint16_t* leaves = g_leaf_lds + (nx | (ny << 1) | (nz << 2)) * kLdsNodes;
+        int j = 0;
+        for (;;) {
+            // A: the next leaf in the octant's preorder whose box the ray enters
+            bool leaf = false;
+            uint32_t first = 0, np = 0;
+            while (j < nl) {
+                const NodeView nd = load_node(sc, leaves[j]);
+                j++;
+                if (node_hit(nd, ray, inv, nx, ny, nz)) {
+                    leaf = true;
+                    first = nd.offset;
+                    np = nd.n_prims;
+                    break;
+                }
+            }
+            STEP_T(if (!kAny) tt.mark(5);)
+            if (!leaf) break;
+            // B: its primitives
+            const int r = leaf_prims<kAny>(sc, first, np, ray, panic, best, best_ph);
+            if (r < 0) return kAny ? false : best >= 0;
+            if (kAny && r > 0) return true;
+            STEP_T(if (!kAny) tt.mark(6);)
+        }
+        return best >= 0;
+    }
     const uint32_t negmask = (uint32_t)nx | ((uint32_t)ny << 1) | ((uint32_t)nz << 2);
     uint32_t to_visit = 0, cur = 0;
-    STEP_T(StepTimer tt; tt.start();)
     for (;;) {
         // A: interior nodes
-        bool leaf = false, done = false;
+        bool done = false;
         for (;;) {
             const NodeView nd = load_node(sc, cur);
             if (node_hit(nd, ray, inv, nx, ny, nz)) {
-                if (nd.n_prims > 0) {
-                    leaf = true;
-                    break;
-                }
+                if (nd.n_prims > 0) break;
                 if (to_visit >= 64) {
                     panic = PBRT_PANIC_BVH_STACK;
                     return kAny ? false : best >= 0;
@@ -475,22 +544,11 @@ __device__ inline bool bvh_walk(const DevScene& sc, Ray& ray, uint16_t* stack, i
         }
         STEP_T(if (!kAny) tt.mark(5);)
         if (done) break;
-        (void)leaf;
         // B: the leaf's primitives
         const NodeView nd = load_node(sc, cur);
-        const uint32_t first = nd.offset, np = nd.n_prims;
-        for (uint32_t i = 0; i < np; i++) {
-            double t_hit;
-            V3 ph;
-            const bool h = prim_hit_t(sc, (int)(first + i), ray, t_hit, ph, panic);
-            if (panic) return kAny ? false : best >= 0;
-            if (h) {
-                if (kAny) return true;
-                ray.tmax = t_hit;
-                best = (int)(first + i);
-                best_ph = ph;
-            }
-        }
+        const int r = leaf_prims<kAny>(sc, nd.offset, nd.n_prims, ray, panic, best, best_ph);
+        if (r < 0) return kAny ? false : best >= 0;
+        if (kAny && r > 0) return true;
         STEP_T(if (!kAny) tt.mark(6);)
         if (to_visit == 0) break;
         cur = stack[(--to_visit) * kStride];
@@ -498,6 +556,7 @@ __device__ inline bool bvh_walk(const DevScene& sc, Ray& ray, uint16_t* stack, i
     STEP_T(if (!kAny) tt.mark(6);)
     return best >= 0;
 }
+
 template <bool kAny>
 __device__ inline bool bvh_traverse(const DevScene& sc, Ray& ray, SI* si, uint16_t* stack, int& panic) {
     int best;

@@ -263,6 +263,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kMinWaves
 __device__ __forceinline__ void stage_nodes(DevScene& sc) {
     if (sc.n_nodes > kLdsNodes) return;
     for (int i = threadIdx.x; i < sc.n_nodes; i += blockDim.x) g_nodes_lds[i] = sc.nodes[i];
+    for (int i = threadIdx.x; i < 8 * sc.n_nodes; i += blockDim.x) {
+        const int oct = i / sc.n_nodes, j = i - oct * sc.n_nodes;
+        if (j < sc.n_leaves) g_leaf_lds[oct * kLdsNodes + j] = (uint16_t)sc.order[8 * sc.n_nodes + i];
+    }
     __syncthreads();
     sc.use_lds_nodes = 1;
 }
@@ -1619,6 +1623,8 @@ struct pbrt_gpu_ctx {
     pbrt_material_desc* d_materials = nullptr;
     pbrt_primitive_desc* d_prims = nullptr;
     DevNode* d_nodes = nullptr;
+    uint32_t* d_order = nullptr;     // [8][n_nodes] preorder visit tables, then [8][n_nodes] leaf lists (dev_order)
+    std::vector<int> h_node_prims;   // nPrimitives per node (leaf count for DevScene)
     DevPrim* d_fprims = nullptr;
     pbrt_light_desc* d_lights = nullptr;
     pbrt_camera_desc* d_camera = nullptr;
@@ -1689,7 +1695,7 @@ DevScene dev_scene(const pbrt_gpu_ctx* c, bool with_dist) {
     s.materials = c->d_materials;
     s.prims = c->d_prims;
     s.nodes = c->d_nodes;
-    s.lnodes_unused = nullptr;
+    s.order = c->d_order;
     s.fprims = c->d_fprims;
     s.lights = c->d_lights;
     s.camera = c->d_camera;
@@ -1699,6 +1705,8 @@ DevScene dev_scene(const pbrt_gpu_ctx* c, bool with_dist) {
     s.n_nodes = c->host_scene.n_nodes;
     s.n_lights = c->host_scene.n_lights;
     s.use_lds_nodes = 0;
+    s.n_leaves = 0;
+    for (int i = 0; i < c->host_scene.n_nodes; i++) s.n_leaves += c->h_node_prims[i] > 0;
     return s;
 }
 
@@ -1715,6 +1723,54 @@ std::vector<DevNode> dev_nodes(const pbrt_scene_desc* s) {
         v[i].nprims_axis = (uint32_t)n.n_prims | ((uint32_t)n.axis << 16);
     }
     return v;
+}
+
+// Preorder visit tables of the BVH, one per ray-direction octant (bvh_walk,
+// pbrt_path.h). Node i's children: i + 1 and nodes[i].offset; the reference
+// visits offset first when the direction along nodes[i].axis is negative
+// (bvh.go:693-703). depth = far children pending on the reference's stack.
+// Returns false if the node array is not a tree in that depth-first layout.
+bool dev_order(const pbrt_scene_desc* s, std::vector<uint32_t>& out) {
+    const int n = s->n_nodes;
+    out.assign((size_t)16 * (n > 0 ? n : 1), 0u);   // [8][n] preorder, then [8][n] leaves in preorder
+    if (n == 0) return true;
+    struct Item { uint32_t node, depth; int64_t slot; };   // slot: table index whose skip this item sets (-1: none)
+    for (int oct = 0; oct < 8; oct++) {
+        uint32_t* t = out.data() + (size_t)oct * n;
+        std::vector<Item> st;
+        std::vector<int64_t> open;   // table indices of interior nodes whose skip is still unknown
+        int k = 0;
+        st.push_back({0u, 0u, -1});
+        while (!st.empty()) {
+            Item it = st.back();
+            st.pop_back();
+            if (it.slot >= 0) {   // marker: the subtree of table entry `slot` ends here
+                t[it.slot] |= (uint32_t)k << 16;
+                continue;
+            }
+            if (k >= n || it.node >= (uint32_t)n) return false;
+            const pbrt_bvh_node& nd = s->nodes[it.node];
+            const int idx = k++;
+            const bool interior = nd.n_prims == 0;
+            t[idx] = it.node | ((interior && it.depth >= 64) ? kOrdOverflow : 0u);
+            if (!interior) {
+                t[idx] |= (uint32_t)(idx + 1) << 16;
+                continue;
+            }
+            const bool neg = (oct >> nd.axis) & 1;
+            const uint32_t near_node = neg ? nd.offset : it.node + 1, far_node = neg ? it.node + 1 : nd.offset;
+            st.push_back({0u, 0u, (int64_t)idx});            // after both subtrees: set skip
+            st.push_back({far_node, it.depth, -1});           // visited after the near subtree
+            st.push_back({near_node, it.depth + 1, -1});      // far child pending on the stack
+        }
+        if (k != n) return false;
+        int nl = 0;
+        for (int i = 0; i < n; i++) {
+            const uint32_t node = t[i] & kOrdNode;
+            if (s->nodes[node].n_prims > 0) out[(size_t)8 * n + (size_t)oct * n + nl++] = node;
+        }
+    }
+    return true;
 }
 
 std::vector<DevPrim> dev_prims(const pbrt_scene_desc* s) {
@@ -1735,7 +1791,7 @@ int validate_scene(const pbrt_scene_desc* s) {
     if (!s) return PBRT_E_INVALID;
     if (s->n_prims < 0 || s->n_nodes < 0 || s->n_lights < 0 || s->n_shapes < 0 || s->n_materials < 0)
         return PBRT_E_INVALID;
-    if (s->n_nodes > 65535) return PBRT_E_UNSUPPORTED;   // uint16 LDS stack entries
+    if (s->n_nodes > 32767) return PBRT_E_UNSUPPORTED;   // 15-bit node index in the preorder tables
     for (int i = 0; i < s->n_prims; i++) {
         const pbrt_primitive_desc& p = s->prims[i];
         if (p.shape < 0 || p.shape >= s->n_shapes || p.material < 0 || p.material >= s->n_materials)
@@ -2127,7 +2183,14 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
         if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)
             c->n_simd = 4 * prop.multiProcessorCount;
     }
+    std::vector<uint32_t> order;
+    if (!dev_order(scene, order)) {
+        delete c;
+        return PBRT_E_INVALID;
+    }
     c->host_scene = *scene;
+    c->h_node_prims.resize((size_t)scene->n_nodes);
+    for (int i = 0; i < scene->n_nodes; i++) c->h_node_prims[i] = scene->nodes[i].n_prims;
     c->host_scene.shapes = nullptr;
     c->host_scene.materials = nullptr;
     c->host_scene.prims = nullptr;
@@ -2144,6 +2207,7 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
         (rc = upload(c, &c->d_materials, scene->materials, scene->n_materials)) ||
         (rc = upload(c, &c->d_prims, scene->prims, scene->n_prims)) ||
         (rc = upload(c, &c->d_nodes, dev_nodes(scene).data(), scene->n_nodes)) ||
+        (rc = upload(c, &c->d_order, order.data(), order.size())) ||
         (rc = upload(c, &c->d_fprims, dev_prims(scene).data(), scene->n_prims)) ||
         (rc = upload(c, &c->d_lights, scene->lights, scene->n_lights)) ||
         (rc = upload(c, &c->d_camera, &scene->camera, 1)) || (rc = upload(c, &c->d_film, &scene->film, 1)) ||
@@ -2442,7 +2506,7 @@ void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* bufs[] = {c->d_shapes, c->d_materials, c->d_prims, c->d_nodes, c->d_lights, c->d_camera, c->d_film,
+    void* bufs[] = {c->d_shapes, c->d_materials, c->d_prims, c->d_nodes, c->d_order, c->d_lights, c->d_camera, c->d_film,
                     c->d_dist,   c->d_films,     c->d_s1d,   c->d_panics, c->d_ctr,   c->d_out,    c->d_jump,
                     c->d_wave,   c->d_fprims, c->d_wf,     c->d_ticks, c->d_slot_order};
     for (void* b : bufs)
