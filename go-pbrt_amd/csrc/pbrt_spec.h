@@ -211,6 +211,96 @@ __device__ inline Spec spec_path(const DevScene& sc, const Cache& pc, const Spec
     return L;
 }
 
+// One iteration of spec_path<true>'s loop (path.go:32-157), for kernels that
+// refill a lane with a new path as soon as its path ends (k_paths_ci). The
+// loop-carried state is PathState + the Cursor; `bounce` reports the bounce
+// of a panic like spec_path. Returns true when the path has ended (radiance
+// in s.L). Arithmetic and draw order are spec_path<true>'s, step for step.
+struct PathState {
+    Spec L, beta;
+    Ray ray;
+    int bounces;
+    int first;
+};
+template <class Cache>
+__device__ inline bool path_step(const DevScene& sc, const Cache& pc, const SpecSampler& ss, Cursor& c,
+                                 PathState& s, int max_depth, double rr_threshold, uint16_t* stack, int& panic,
+                                 int& bounce) {
+    SI isect;
+    BSDF b;
+    V3 wo;
+    const int nl = sc.n_lights;
+    if (!s.first) {
+        s.bounces++;
+        bounce = s.bounces;
+        if (s.bounces >= max_depth) return true;
+        const bool hit = bvh_traverse<false>(sc, s.ray, &isect, stack, panic);
+        if (!hit) return true;
+        if (panic) return true;
+        if (compute_bsdf(sc, isect, b) < 0) {
+            panic = -1;
+            return true;
+        }
+        wo = s.ray.d;
+    } else {
+        isect = pc.si;
+        b = pc.b;
+        wo = pc.wo;
+    }
+    if (b.n_bxdfs > 0) {   // UniformSampleOneLight (integrator.go:48-77)
+        if (nl == 0) {
+            s.L = s.L + smul(s.beta, spec(0));
+        } else {
+            int ln;
+            if (sc.dist) {
+                double lpdf;   // > 0 for every light (launch precondition)
+                ln = sample_discrete(*sc.dist, c_get1d(c, ss), lpdf);
+            } else {
+                ln = (int)gomath::to_int(gomath::min(c_get1d(c, ss) * (double)nl, (double)(nl - 1)));
+            }
+            V2 ul = c_get2d(c, ss);
+            c_get2d(c, ss);
+            Spec ld;
+            if (s.first) {
+                ld = pc.ld[ln];
+                if (pc.ld_panic[ln]) {
+                    panic = pc.ld_panic[ln];
+                    return true;
+                }
+            } else {
+                ld = estimate_direct(sc, stack, panic, isect, b, ln, ul);
+                if (panic) return true;
+                if (max_component(ld) > 10) {
+                    panic = PBRT_PANIC_LD_GT_10;
+                    return true;
+                }
+            }
+            s.L = s.L + smul(s.beta, ld);
+        }
+    }
+    s.first = 0;
+    V2 u = c_get2d(c, ss);
+    V3 wi;
+    double pdf;
+    Spec f = bsdf_sample_f(b, wo, u, wi, pdf);
+    if (is_black(f) || pdf == 0.0) return true;
+    double wp = absdot(wi, isect.sn) / pdf;
+    s.beta = smul(s.beta, smuls(f, wp));
+    s.ray.o = offset_ray_origin(isect.p, isect.perr, isect.n, wi);
+    s.ray.d = wi;
+    s.ray.tmax = kInf;
+    s.ray.time = isect.time;
+    Spec rr = smuls(s.beta, 1.0);
+    if (max_component(rr) < rr_threshold && s.bounces > 3) {
+        double q = gomath::max(0.05, 1 - max_component(rr));
+        double u1 = c_get1d(c, ss);
+        if (c.kdep) return true;
+        if (u1 < q) return true;
+        s.beta = sdivs(s.beta, 1 - q);
+    }
+    return false;
+}
+
 // The rest of one spec_path<false> iteration once the interaction at bounce
 // `bounces` and its BSDF are known (light draws consumed, BSDF sample,
 // throughput, Russian roulette), then the next iteration's depth test; the

@@ -304,6 +304,7 @@ __device__ __forceinline__ double pcg_float_of(uint32_t v) {
 __device__ __forceinline__ int64_t tile_of_slot(const RenderParams& rp, int64_t slot) {
     return rp.tile_begin + slot * rp.tile_stride;
 }
+__device__ __forceinline__ uint64_t pcg_inc_of(uint64_t seed) { return (seed << 1) | 1; }   // rng.go:28-34
 
 // k_chain runs G = 64 / L tiles per wave: lane group g (L lanes) owns tile
 // slot blockIdx.x * G + g and speculates with L candidate offsets per window
@@ -730,6 +731,158 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8
     }
 }
 
+// k_paths_ci: EXACT full paths with lane refill. k_paths runs one pixel's
+// samples per wave, so a wave lasts as long as its longest path (~4x the
+// mean). Here a wave owns P pixel records and treats their samples as one
+// work list: a lane whose path ends writes its radiance and takes the next
+// (pixel, sample) at once, so the wave only waits for its longest path at
+// the end of the P pixels. Every path runs the same arithmetic as
+// spec_path<true> (path_step), from the offset the chain found, so L per
+// (pixel, sample) is bit-identical; k_film sums them in sample order as
+// before. Requires LDS-staged nodes (no traversal stack) and P * n_lights <= 64.
+template <int P>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kPathsWaves, 8))) void k_paths_ci(
+    DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];   // s1d of the P pixels
+    __shared__ PixelCache pcs[P];
+    __shared__ unsigned long long pkey[P];   // (sample << 32) | (bounce << 8) | (kind + 1): min = first panic
+    const int lane = threadIdx.x;
+    stage_nodes(sc);
+    const int n = rp.spp, ndims = rp.ndims, nl = sc.n_lights;
+    const int per = ndims * n;
+    double* s1d = (double*)lds;
+    const int64_t rec0 = (int64_t)blockIdx.x * P;
+    int nv[P], hit[P], cum[P + 1];
+    uint64_t inc[P];
+    cum[0] = 0;
+#pragma unroll
+    for (int j = 0; j < P; j++) {
+        const int64_t rec = rec0 + j;
+        nv[j] = 0;
+        hit[j] = 0;
+        inc[j] = 0;
+        if (rec < nrec) {
+            const int64_t bslot = rec / wb.ppt, pi = rec % wb.ppt;
+            if (pi < wb.tile_npx[bslot]) {
+                nv[j] = wb.prec[rec].nvalid;
+                hit[j] = wb.prec[rec].hit;
+                inc[j] = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + bslot));
+            }
+        }
+        cum[j + 1] = cum[j] + (nv[j] > 1 ? nv[j] - 1 : 0);
+    }
+    for (int idx = lane; idx < P * per; idx += kWave) {
+        const int j = idx / per;
+        if (nv[j] > 0) s1d[idx] = wb.s1d[(rec0 + j) * wb.s1d_stride + (idx - j * per)];
+    }
+    if (lane < P) {
+        pkey[lane] = ~0ULL;
+        if (nv[lane] > 0) {
+            const PixelRec& pr = wb.prec[rec0 + lane];
+            pcs[lane].si = pr.si;
+            pcs[lane].b = pr.b;
+            pcs[lane].wo = pr.wo;
+            pcs[lane].hit = pr.hit;
+        }
+    }
+    __syncthreads();
+    if (nl > 0 && lane < P * nl) {   // bounce-1 light samples, uLight = (0,0); lane = pixel * nl + light
+        const int j = lane / nl, l = lane - j * nl;
+        if (nv[j] > 0 && hit[j] && pcs[j].b.n_bxdfs > 0) {
+            int pl = 0;
+            Spec ld = estimate_direct(sc, nullptr, pl, pcs[j].si, pcs[j].b, l, V2{0.0, 0.0});
+            if (!pl && max_component(ld) > 10) pl = PBRT_PANIC_LD_GT_10;
+            pcs[j].ld[l] = ld;
+            pcs[j].ld_panic[l] = pl;
+        }
+    }
+    __syncthreads();
+    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
+    const int T = cum[P];
+    int base = 0;
+    int w = -1, j = 0, k = 0;
+    PathState ps;
+    Cursor c;
+    int pnc = 0, bnc = 1;
+    for (;;) {
+        const bool idle = w < 0;
+        const unsigned long long m = __ballot(idle);
+        if (idle) {
+            const int t = base + __popcll(m & lt_mask);
+            if (t < T) {
+                j = 0;
+#pragma unroll
+                for (int q = 1; q < P; q++) j += t >= cum[q] ? 1 : 0;
+                k = 1 + (t - cum[j]);
+                const int64_t rec = rec0 + j;
+                if (!hit[j]) {   // no traced bounce: the sample's radiance is 0
+                    double* o = wb.L + (rec * n + k) * 3;
+                    o[0] = 0.0;
+                    o[1] = 0.0;
+                    o[2] = 0.0;
+                } else {
+                    w = t;
+                    c.rng.state = wb.memb[rec * n + k];
+                    c.rng.inc = inc[j];
+                    c.draws = 0;
+                    c.cur1d = 1;   // camera: Get2D pFilm, Get2D pLens, Get1D time (stratified)
+                    c.cur2d = 2;
+                    c.k = k;
+                    c.kdep = 0;
+                    ps.L = spec(0);
+                    ps.beta = spec(1);
+                    ps.bounces = 1;
+                    ps.first = 1;
+                    pnc = 0;
+                    bnc = 1;
+                }
+            }
+        }
+        base += __popcll(m);
+        if (!__any(w >= 0)) {
+            if (base >= T) break;
+            continue;
+        }
+        if (w >= 0) {
+            const SpecSampler ss{s1d + j * per, n, ndims};
+            if (path_step(sc, pcs[j], ss, c, ps, rp.max_depth, rp.rr_threshold, nullptr, pnc, bnc)) {
+                const int64_t rec = rec0 + j;
+                double* o = wb.L + (rec * n + k) * 3;
+                o[0] = ps.L.r;
+                o[1] = ps.L.g;
+                o[2] = ps.L.b;
+                if (pnc)
+                    atomicMin(&pkey[j], ((unsigned long long)k << 32) | ((unsigned long long)(bnc & 0xFFFFFF) << 8) |
+                                            (unsigned long long)((pnc + 1) & 0xFF));
+                w = -1;
+            }
+        }
+    }
+    __syncthreads();
+    if (lane < P && nv[lane] > 0) {
+        const int64_t rec = rec0 + lane;
+        const int64_t bslot = rec / wb.ppt, pi = rec % wb.ppt;
+        int64_t x0, y0, x1, y1;
+        tile_bounds(rp, tile_of_slot(rp, slot_base + bslot), x0, y0, x1, y1);
+        PanicRec p{0, 0, 0, 0, x0 + pi % (x1 - x0), y0 + pi / (x1 - x0)};
+        const int panic0 = wb.prec[rec].panic0;
+        if (panic0) {
+            p.kind = panic0;
+            p.sample = 1;
+            p.bounce = 1;
+        } else if (pkey[lane] != ~0ULL) {
+            p.kind = (int)(pkey[lane] & 0xFF) - 1;
+            p.bounce = (int)((pkey[lane] >> 8) & 0xFFFFFF);
+            p.sample = (int)(pkey[lane] >> 32);
+        }
+        wb.ppanic[rec] = p;
+        if (!p.kind && nv[lane] > 1) {
+            atomicAdd(&ctr->paths, (unsigned long long)(nv[lane] - 1));
+            atomicAdd(&ctr->camera_samples, (unsigned long long)(nv[lane] - 1));
+        }
+    }
+}
+
 // One thread per tile-film pixel: the tile film of the serial replay.
 __global__ __launch_bounds__(256) void k_film(const pbrt_film_desc* __restrict__ film_desc, RenderParams rp,
                                               WaveBufs wb, int64_t slot_base, int64_t nslots_batch,
@@ -848,7 +1001,6 @@ struct WfBufs {
     int64_t cap;        // nb * C
 };
 
-__device__ __forceinline__ uint64_t pcg_inc_of(uint64_t seed) { return (seed << 1) | 1; }   // rng.go:28-34
 
 // Append the ids of the lanes with push set to q (one atomic per wave). All
 // lanes of the wave call it.
@@ -1261,7 +1413,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(2, 8
     uint16_t* stack = stack_lds + tid;
     const int n = rp.spp, ndims = rp.ndims;
     const pbrt_camera_desc& cam = *sc.camera;
-    const unsigned long long gmask = L >= 64 ? ~0ULL : (((1ULL << L) - 1ULL) << (g * L));
+    const unsigned long long gmask = L >= 64 ? ~0ULL : (((1ULL << (L & 63)) - 1ULL) << (g * L));
     const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
     const int64_t bs = blk * G + g;
     const uint64_t inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + (bs < nslots_batch ? bs : 0)));
@@ -1909,6 +2061,18 @@ uint64_t schedule_key(const RenderParams& rp, int kw) {
     return h;
 }
 
+// k_paths_ci (lane refill over kPathsPixels pixels per wave) where it fits:
+// LDS-staged nodes, the pixels' stratified values in 16 KB of LDS and one
+// lane per (pixel, light) for the bounce-1 estimates. PBRT_PATHS_CI=0 keeps
+// the one-pixel-per-wave k_paths.
+constexpr int kPathsPixels = 4;
+bool paths_ci_ok(const pbrt_gpu_ctx* c, const RenderParams& rp) {
+    if (const char* e = getenv("PBRT_PATHS_CI"))
+        if (atoi(e) == 0) return false;
+    return c->host_scene.n_nodes <= kLdsNodes && kPathsPixels * c->host_scene.n_lights <= kWave &&
+           (int64_t)kPathsPixels * rp.ndims * rp.spp * 8 <= 16 * 1024;
+}
+
 // Carve the per-batch buffers of the wave path (budget: PBRT_WAVE_BUFFER_GB, default 12).
 int wave_buffers(pbrt_gpu_ctx* c) {
     const RenderParams& rp = c->rp;
@@ -2315,6 +2479,11 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                     hipLaunchKernelGGL((k_paths<true, kPathsWaves>), dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
                                        (unsigned)c->lay.total, c->stream, sc, rp, c->lay, c->d_jump, c->wb, sb, nb,
                                        c->d_ctr);
+                else if (paths_ci_ok(c, rp))
+                    hipLaunchKernelGGL(k_paths_ci<kPathsPixels>,
+                                       dim3((unsigned)((nb * c->wb.ppt + kPathsPixels - 1) / kPathsPixels)),
+                                       dim3(kWave), (unsigned)(kPathsPixels * rp.ndims * rp.spp * 8), c->stream, sc,
+                                       rp, c->wb, sb, nb * c->wb.ppt, c->d_ctr);
                 else
                     hipLaunchKernelGGL((k_paths<false, kPathsWaves>), dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
                                        (unsigned)(rp.ndims * rp.spp * 8), c->stream, sc, rp, c->lay, c->d_jump,
