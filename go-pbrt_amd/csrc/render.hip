@@ -2065,12 +2065,17 @@ uint64_t schedule_key(const RenderParams& rp, int kw) {
 // LDS-staged nodes, the pixels' stratified values in 16 KB of LDS and one
 // lane per (pixel, light) for the bounce-1 estimates. PBRT_PATHS_CI=0 keeps
 // the one-pixel-per-wave k_paths.
-constexpr int kPathsPixels = 4;
-bool paths_ci_ok(const pbrt_gpu_ctx* c, const RenderParams& rp) {
-    if (const char* e = getenv("PBRT_PATHS_CI"))
-        if (atoi(e) == 0) return false;
-    return c->host_scene.n_nodes <= kLdsNodes && kPathsPixels * c->host_scene.n_lights <= kWave &&
-           (int64_t)kPathsPixels * rp.ndims * rp.spp * 8 <= 16 * 1024;
+// Returns the pixels per wave (2, 4 or 8; PBRT_PATHS_CI overrides, 0 = off).
+int paths_ci_pixels(const pbrt_gpu_ctx* c, const RenderParams& rp) {
+    int pp = 4;
+    if (const char* e = getenv("PBRT_PATHS_CI")) {
+        const int v = atoi(e);
+        if (v == 0) return 0;
+        if (v == 2 || v == 4 || v == 8) pp = v;
+    }
+    const bool fits = c->host_scene.n_nodes <= kLdsNodes && pp * c->host_scene.n_lights <= kWave &&
+                      (int64_t)pp * rp.ndims * rp.spp * 8 <= 16 * 1024;
+    return fits ? pp : 0;
 }
 
 // Carve the per-batch buffers of the wave path (budget: PBRT_WAVE_BUFFER_GB, default 12).
@@ -2479,11 +2484,12 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                     hipLaunchKernelGGL((k_paths<true, kPathsWaves>), dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
                                        (unsigned)c->lay.total, c->stream, sc, rp, c->lay, c->d_jump, c->wb, sb, nb,
                                        c->d_ctr);
-                else if (paths_ci_ok(c, rp))
-                    hipLaunchKernelGGL(k_paths_ci<kPathsPixels>,
-                                       dim3((unsigned)((nb * c->wb.ppt + kPathsPixels - 1) / kPathsPixels)),
-                                       dim3(kWave), (unsigned)(kPathsPixels * rp.ndims * rp.spp * 8), c->stream, sc,
-                                       rp, c->wb, sb, nb * c->wb.ppt, c->d_ctr);
+                else if (const int pp = paths_ci_pixels(c, rp)) {
+                    auto kern = pp == 8 ? k_paths_ci<8> : pp == 2 ? k_paths_ci<2> : k_paths_ci<4>;
+                    hipLaunchKernelGGL(kern, dim3((unsigned)((nb * c->wb.ppt + pp - 1) / pp)), dim3(kWave),
+                                       (unsigned)(pp * rp.ndims * rp.spp * 8), c->stream, sc, rp, c->wb, sb,
+                                       nb * c->wb.ppt, c->d_ctr);
+                }
                 else
                     hipLaunchKernelGGL((k_paths<false, kPathsWaves>), dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
                                        (unsigned)(rp.ndims * rp.spp * 8), c->stream, sc, rp, c->lay, c->d_jump,
