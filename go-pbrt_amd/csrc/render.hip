@@ -1404,7 +1404,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(2, 8
     // workgroup -> tile slot: heaviest-first order from the previous frame
     // (one tile per workgroup only), else the identity
     const int64_t blk = order ? (int64_t)order[blockIdx.x] : (int64_t)blockIdx.x;
-    const uint32_t R = (uint32_t)ring_size;
+    const uint32_t R = (uint32_t)ring_size;   // a power of two (host: 256 / G or 256 * kW entries)
     const PcgJump& J = *jump;
     double* s1d = (double*)(lds + lay.s1d);
     uint16_t* other = (uint16_t*)(lds + lay.other);
@@ -1541,8 +1541,9 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(2, 8
                 nidle = tot;
             }
             const int re = (sg.reissue && nidle > 0) ? 1 : 0;
-            const uint32_t span = sg.head + R - sg.nxt;   // offsets < head + R keep the ring collision-free
-            const int avail = (int)((span + 1) / 2);
+            const uint32_t nx0 = sg.nxt;
+            // offsets < head + R keep the ring collision-free
+            const int avail = nx0 < sg.head + R ? (int)((sg.head + R - nx0 + 1) / 2) : 0;
             const int nspec = min(nidle - re, avail);
             uint32_t o = kNoOff;
             bool exact = false;
@@ -1552,11 +1553,11 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(2, 8
                     exact = true;
                 } else {
                     rank -= re;
-                    if (rank < nspec) o = sg.nxt + 2u * (uint32_t)rank;
+                    if (rank < nspec) o = nx0 + 2u * (uint32_t)rank;
                 }
             }
             if (gl == 0 && sg.phase == 1) {
-                gs[g].nxt = sg.nxt + 2u * (uint32_t)max(nspec, 0);
+                gs[g].nxt = nx0 + 2u * (uint32_t)max(nspec, 0);
                 if (re) gs[g].reissue = 0;
             }
             if (o != kNoOff) {
@@ -1575,7 +1576,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(2, 8
                                            rp.rr_threshold);
                 tracing = r == 0;
                 if (r != 0) {
-                    RingEnt& e = ring[off % R];
+                    RingEnt& e = ring[off & (R - 1u)];
                     e.st = st0;
                     e.d = r == 1 ? c.draws : (c.k >= 0 ? kBadExactD : kBadSpecD);
                     e.tag = off;
@@ -1609,7 +1610,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(2, 8
                 }
             }
             if (d != kNoOff) {
-                RingEnt& e = ring[off % R];
+                RingEnt& e = ring[off & (R - 1u)];
                 e.st = st0;
                 e.d = d;
                 e.tag = off;
@@ -1623,7 +1624,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(2, 8
         if (gl == 0 && sg.phase == 1) {
             CiGroup s = gs[g];
             for (;;) {
-                RingEnt& e = ring[s.head % R];
+                RingEnt& e = ring[s.head & (R - 1u)];
                 if (e.tag != s.head) break;
                 const uint32_t d = e.d;
                 if (d == kBadSpecD) {   // re-run the head with its sample index known
