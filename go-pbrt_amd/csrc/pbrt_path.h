@@ -230,9 +230,9 @@ __device__ __forceinline__ bool phi_beyond(double y, double x, double phi_max) {
 
 // Sphere.Intersect / IntersectP, hit part (sphere.go:64-131). world->object
 // = the swap of object_to_world (Transform.Inverse, transform.go:175-177).
-__device__ inline bool sphere_hit(const pbrt_shape_desc& s, const Ray& r, double& t_hit, V3& ph, int& panic) {
-    V3 oerr, derr;
-    Ray ray = xf_ray(s.object_to_world.m_inv, r, &oerr, &derr);
+// `ray` is already in object space (shape_hit), oerr/derr its transform errors.
+__device__ inline bool sphere_hit(const pbrt_shape_desc& s, const Ray& ray, V3 oerr, V3 derr, double& t_hit, V3& ph,
+                                  int& panic) {
     EF ox = ef_new(ray.o.x, oerr.x, panic), oy = ef_new(ray.o.y, oerr.y, panic), oz = ef_new(ray.o.z, oerr.z, panic);
     EF dx = ef_new(ray.d.x, derr.x, panic), dy = ef_new(ray.d.y, derr.y, panic), dz = ef_new(ray.d.z, derr.z, panic);
     EF a = ef_add(ef_add(ef_mul(dx, dx, panic), ef_mul(dy, dy, panic), panic), ef_mul(dz, dz, panic), panic);
@@ -284,9 +284,8 @@ __device__ inline void sphere_si(const pbrt_shape_desc& s, const Ray& ray, V3 ph
             s.reverse_orientation != s.transform_swaps_handedness);
 }
 
-// Disk.Intersect / IntersectP, hit part (disk.go:64-95)
-__device__ inline bool disk_hit(const pbrt_shape_desc& s, const Ray& r, double& t_hit, V3& ph) {
-    Ray ray = xf_ray(s.object_to_world.m_inv, r, nullptr, nullptr);
+// Disk.Intersect / IntersectP, hit part (disk.go:64-95); `ray` in object space
+__device__ inline bool disk_hit(const pbrt_shape_desc& s, const Ray& ray, double& t_hit, V3& ph) {
     if (ray.d.z == 0) return false;
     double ts = (s.height - ray.o.z) / ray.d.z;
     if (ts <= 0 || ts >= ray.tmax) return false;
@@ -308,9 +307,14 @@ __device__ inline void disk_si(const pbrt_shape_desc& s, const Ray& ray, V3 ph, 
             s.reverse_orientation != s.transform_swaps_handedness);
 }
 
+// Both shapes start with the same world->object TransformRay (sphere.go:66,
+// disk.go:66), done once here so a wave whose lanes test different shape
+// kinds runs it once.
 __device__ inline bool shape_hit(const pbrt_shape_desc& s, const Ray& r, double& t_hit, V3& ph, int& panic) {
-    if (s.type == PBRT_SHAPE_SPHERE) return sphere_hit(s, r, t_hit, ph, panic);
-    return disk_hit(s, r, t_hit, ph);
+    V3 oerr, derr;
+    const Ray ray = xf_ray(s.object_to_world.m_inv, r, &oerr, &derr);
+    if (s.type == PBRT_SHAPE_SPHERE) return sphere_hit(s, ray, oerr, derr, t_hit, ph, panic);
+    return disk_hit(s, ray, t_hit, ph);
 }
 // the interaction at an accepted hit point ph; r in the shape's parent space
 __device__ inline void shape_si(const pbrt_shape_desc& s, const Ray& r, V3 ph, SI& si) {

@@ -44,6 +44,7 @@ with G.Renderer(scene, kernel=a.kernel, occupancy=a.occupancy, lanes_per_wave=a.
         sc_ = (C.c_uint64 * 8)()
         G.lib().pbrt_gpu_step_cycles(sc_, 8, 1)
         tot_s = sum(sc_[:5])
+        print("  step cycles (raw): " + " ".join(str(int(v)) for v in sc_))
         if tot_s:
             labels = ["loop top", "closest hit + SI", "BSDF setup", "light sampling", "BSDF sample+spawn+RR"]
             print("  step regions: " + ", ".join(f"{l} {v / tot_s * 100:.1f}%" for l, v in zip(labels, sc_[:5])))
