@@ -2558,6 +2558,12 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
         c->ticks_pending = false;
         std::vector<uint32_t> t((size_t)c->ticks_n);
         HIPCHK(c, hipMemcpy(t.data(), c->d_ticks, sizeof(uint32_t) * t.size(), hipMemcpyDeviceToHost));
+        if (const char* path = getenv("PBRT_TICKS_DUMP")) {   // diagnostics: per-slot chain ticks (100 MHz)
+            if (FILE* f = fopen(path, "wb")) {
+                fwrite(t.data(), sizeof(uint32_t), t.size(), f);
+                fclose(f);
+            }
+        }
         c->h_slot_order.resize(t.size());
         for (size_t i = 0; i < t.size(); i++) c->h_slot_order[i] = (uint32_t)i;
         std::stable_sort(c->h_slot_order.begin(), c->h_slot_order.end(),
