@@ -740,18 +740,28 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8
 // spec_path<true> (path_step), from the offset the chain found, so L per
 // (pixel, sample) is bit-identical; k_film sums them in sample order as
 // before. Requires LDS-staged nodes (no traversal stack) and P * n_lights <= 64.
+//
+// paths_group is the per-wave body, synchronised within the wave only (a
+// fused variant that ran it inside k_chain_ci after each tile's chain was
+// bit-exact but slower: 1000 vs 874 ms, the chain kernel spilled). Its LDS:
+// PixelCache[P], then P panic keys, then the P pixels' stratified values.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
 template <int P>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kPathsWaves, 8))) void k_paths_ci(
-    DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];   // s1d of the P pixels
-    __shared__ PixelCache pcs[P];
-    __shared__ unsigned long long pkey[P];   // (sample << 32) | (bounce << 8) | (kind + 1): min = first panic
-    const int lane = threadIdx.x;
-    stage_nodes(sc);
+__host__ __device__ constexpr int paths_group_lds(int per) {   // bytes, per wave
+    return (int)(((P * sizeof(PixelCache) + P * 8 + 15) & ~(size_t)15) + (size_t)P * per * 8);
+}
+template <int P>
+__device__ void paths_group(const DevScene& sc, const RenderParams& rp, const WaveBufs& wb, int64_t slot_base,
+                            int64_t rec0, int64_t rec_end, Counters* __restrict__ ctr, unsigned char* wlds) {
+    const int lane = threadIdx.x & (kWave - 1);
     const int n = rp.spp, ndims = rp.ndims, nl = sc.n_lights;
     const int per = ndims * n;
-    double* s1d = (double*)lds;
-    const int64_t rec0 = (int64_t)blockIdx.x * P;
+    PixelCache* pcs = (PixelCache*)wlds;
+    unsigned long long* pkey = (unsigned long long*)(wlds + P * sizeof(PixelCache));
+    double* s1d = (double*)(wlds + ((P * sizeof(PixelCache) + P * 8 + 15) & ~(size_t)15));
     int nv[P], hit[P], cum[P + 1];
     uint64_t inc[P];
     cum[0] = 0;
@@ -761,7 +771,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kPathsWav
         nv[j] = 0;
         hit[j] = 0;
         inc[j] = 0;
-        if (rec < nrec) {
+        if (rec < rec_end) {
             const int64_t bslot = rec / wb.ppt, pi = rec % wb.ppt;
             if (pi < wb.tile_npx[bslot]) {
                 nv[j] = wb.prec[rec].nvalid;
@@ -785,7 +795,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kPathsWav
             pcs[lane].hit = pr.hit;
         }
     }
-    __syncthreads();
+    wave_sync();
     if (nl > 0 && lane < P * nl) {   // bounce-1 light samples, uLight = (0,0); lane = pixel * nl + light
         const int j = lane / nl, l = lane - j * nl;
         if (nv[j] > 0 && hit[j] && pcs[j].b.n_bxdfs > 0) {
@@ -796,7 +806,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kPathsWav
             pcs[j].ld_panic[l] = pl;
         }
     }
-    __syncthreads();
+    wave_sync();
     const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
     const int T = cum[P];
     int base = 0;
@@ -858,7 +868,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kPathsWav
             }
         }
     }
-    __syncthreads();
+    wave_sync();
     if (lane < P && nv[lane] > 0) {
         const int64_t rec = rec0 + lane;
         const int64_t bslot = rec / wb.ppt, pi = rec % wb.ppt;
@@ -881,6 +891,15 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kPathsWav
             atomicAdd(&ctr->camera_samples, (unsigned long long)(nv[lane] - 1));
         }
     }
+    wave_sync();   // the LDS block is reused by the wave's next group
+}
+
+template <int P>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kPathsWaves, 8))) void k_paths_ci(
+    DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];   // paths_group_lds<P>
+    stage_nodes(sc);
+    paths_group<P>(sc, rp, wb, slot_base, (int64_t)blockIdx.x * P, nrec, ctr, lds);
 }
 
 // One thread per tile-film pixel: the tile film of the serial replay.
@@ -2486,10 +2505,12 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                                        (unsigned)c->lay.total, c->stream, sc, rp, c->lay, c->d_jump, c->wb, sb, nb,
                                        c->d_ctr);
                 else if (const int pp = paths_ci_pixels(c, rp)) {
+                    const int per = rp.ndims * rp.spp;
                     auto kern = pp == 8 ? k_paths_ci<8> : pp == 2 ? k_paths_ci<2> : k_paths_ci<4>;
+                    const int lds = pp == 8 ? paths_group_lds<8>(per) : pp == 2 ? paths_group_lds<2>(per)
+                                                                                : paths_group_lds<4>(per);
                     hipLaunchKernelGGL(kern, dim3((unsigned)((nb * c->wb.ppt + pp - 1) / pp)), dim3(kWave),
-                                       (unsigned)(pp * rp.ndims * rp.spp * 8), c->stream, sc, rp, c->wb, sb,
-                                       nb * c->wb.ppt, c->d_ctr);
+                                       (unsigned)lds, c->stream, sc, rp, c->wb, sb, nb * c->wb.ppt, c->d_ctr);
                 }
                 else
                     hipLaunchKernelGGL((k_paths<false, kPathsWaves>), dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
