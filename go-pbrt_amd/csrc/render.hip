@@ -66,6 +66,7 @@ struct Counters {
     // wave kernel diagnostics (pbrt_gpu_counters): speculation windows, and
     // lane-0 clock64 cycles in StartPixel / bounce 1 / chain / full paths / film add
     unsigned long long windows, phase[8];
+    unsigned long long dhist[64];   // k_chain_ci diagnostics: on-chain draw counts D (bin D/2, last bin >= 126)
 };
 constexpr int kNumCounters = 6 + 8;
 
@@ -1416,6 +1417,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(2, 8
     __shared__ CiGroup gs[kCiMaxGroups];
     __shared__ uint64_t sh_state;
     __shared__ int wcnt[kW];
+    __shared__ uint32_t dh[64];   // on-chain D histogram of the block (diagnostics)
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
     stage_nodes(sc);
     const int L = kW > 1 ? kT : lanes_per_tile, G = kW > 1 ? 1 : kWave / L;
@@ -1444,6 +1446,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(2, 8
         ph[k] += (unsigned long long)(now - tprev);
         tprev = now;
     };
+    if (tid < 64) dh[tid] = 0;
     if (tid < G) {
         const int64_t b = blk * G + tid;
         CiGroup& s = gs[tid];
@@ -1577,6 +1580,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(2, 8
             }
             if (gl == 0 && sg.phase == 1) {
                 gs[g].nxt = nx0 + 2u * (uint32_t)max(nspec, 0);
+                ph[5] += (unsigned long long)(max(nspec, 0) + re);   // candidate trajectories issued
                 if (re) gs[g].reissue = 0;
             }
             if (o != kNoOff) {
@@ -1657,6 +1661,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(2, 8
                     s.phase = 2;
                     break;
                 }
+                atomicAdd(&dh[min(d / 2u, 63u)], 1u);
                 s.kh++;
                 s.head += d;
                 if (s.kh >= n) {   // every sample of the pixel has its offset; the next StartPixel starts here
@@ -1680,6 +1685,8 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(2, 8
         }
         mark(4);
     }
+    __syncthreads();
+    if (tid < 64 && dh[tid]) atomicAdd(&ctr->dhist[tid], (unsigned long long)dh[tid]);
     if (tid == 0) {
         atomicAdd(&ctr->windows, steps);
         for (int k = 0; k < 8; k++) atomicAdd(&ctr->phase[k], ph[k]);
@@ -2579,6 +2586,12 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
         c->ticks_pending = false;
         std::vector<uint32_t> t((size_t)c->ticks_n);
         HIPCHK(c, hipMemcpy(t.data(), c->d_ticks, sizeof(uint32_t) * t.size(), hipMemcpyDeviceToHost));
+        if (const char* path = getenv("PBRT_DHIST_DUMP")) {   // diagnostics: on-chain D histogram + counters
+            if (FILE* f = fopen(path, "wb")) {
+                fwrite(&ctr, sizeof(ctr), 1, f);
+                fclose(f);
+            }
+        }
         if (const char* path = getenv("PBRT_TICKS_DUMP")) {   // diagnostics: per-slot chain ticks (100 MHz)
             if (FILE* f = fopen(path, "wb")) {
                 fwrite(t.data(), sizeof(uint32_t), t.size(), f);
