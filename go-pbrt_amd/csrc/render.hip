@@ -754,7 +754,9 @@ template <int P>
 __host__ __device__ constexpr int paths_group_lds(int per) {   // bytes, per wave
     return (int)(((P * sizeof(PixelCache) + P * 8 + 15) & ~(size_t)15) + (size_t)P * per * 8);
 }
-template <int P>
+// kMB: THROUGHPUT mode, sample k of pixel pi starts from its own stream
+// mb_state(tile, pi, k) instead of the chain's offset state.
+template <int P, bool kMB = false>
 __device__ void paths_group(const DevScene& sc, const RenderParams& rp, const WaveBufs& wb, int64_t slot_base,
                             int64_t rec0, int64_t rec_end, Counters* __restrict__ ctr, unsigned char* wlds) {
     const int lane = threadIdx.x & (kWave - 1);
@@ -764,7 +766,7 @@ __device__ void paths_group(const DevScene& sc, const RenderParams& rp, const Wa
     unsigned long long* pkey = (unsigned long long*)(wlds + P * sizeof(PixelCache));
     double* s1d = (double*)(wlds + ((P * sizeof(PixelCache) + P * 8 + 15) & ~(size_t)15));
     int nv[P], hit[P], cum[P + 1];
-    uint64_t inc[P];
+    uint64_t inc[P], tl[P];
     cum[0] = 0;
 #pragma unroll
     for (int j = 0; j < P; j++) {
@@ -772,12 +774,14 @@ __device__ void paths_group(const DevScene& sc, const RenderParams& rp, const Wa
         nv[j] = 0;
         hit[j] = 0;
         inc[j] = 0;
+        tl[j] = 0;
         if (rec < rec_end) {
             const int64_t bslot = rec / wb.ppt, pi = rec % wb.ppt;
             if (pi < wb.tile_npx[bslot]) {
                 nv[j] = wb.prec[rec].nvalid;
                 hit[j] = wb.prec[rec].hit;
-                inc[j] = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + bslot));
+                tl[j] = (uint64_t)tile_of_slot(rp, slot_base + bslot);
+                inc[j] = pcg_inc_of(tl[j]);
             }
         }
         cum[j + 1] = cum[j] + (nv[j] > 1 ? nv[j] - 1 : 0);
@@ -833,7 +837,7 @@ __device__ void paths_group(const DevScene& sc, const RenderParams& rp, const Wa
                     o[2] = 0.0;
                 } else {
                     w = t;
-                    c.rng.state = wb.memb[rec * n + k];
+                    c.rng.state = kMB ? mb_state(tl[j], (uint64_t)(rec % wb.ppt), (uint64_t)k) : wb.memb[rec * n + k];
                     c.rng.inc = inc[j];
                     c.draws = 0;
                     c.cur1d = 1;   // camera: Get2D pFilm, Get2D pLens, Get1D time (stratified)
@@ -895,12 +899,59 @@ __device__ void paths_group(const DevScene& sc, const RenderParams& rp, const Wa
     wave_sync();   // the LDS block is reused by the wave's next group
 }
 
-template <int P>
+template <int P, bool kMB = false>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kPathsWaves, 8))) void k_paths_ci(
     DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];   // paths_group_lds<P>
     stage_nodes(sc);
-    paths_group<P>(sc, rp, wb, slot_base, (int64_t)blockIdx.x * P, nrec, ctr, lds);
+    paths_group<P, kMB>(sc, rp, wb, slot_base, (int64_t)blockIdx.x * P, nrec, ctr, lds);
+}
+
+// THROUGHPUT mode setup for k_paths_ci<P, true>, one wave per pixel record:
+// StartPixel on the pixel's own stream mb_state(tile, pi, 0) and bounce 1
+// (camera ray, first hit, BSDF), written to the PixelRec / s1d buffers the
+// EXACT pipeline fills with k_wf_primary + k_chain_ci. The same arithmetic as
+// k_paths<true>'s prologue.
+__global__ __launch_bounds__(kWave) void k_mb_setup(DevScene sc, RenderParams rp, ChainLayout lay,
+                                                    const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
+                                                    int64_t nslots_batch) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ uint16_t stack_lds[64 * kStackStride];
+    __shared__ uint64_t sh_state;
+    const int lane = threadIdx.x;
+    stage_nodes(sc);
+    const int64_t bslot = blockIdx.x / wb.ppt, pi = blockIdx.x % wb.ppt, rec = blockIdx.x;
+    if (bslot >= nslots_batch) return;
+    const int64_t tile = tile_of_slot(rp, slot_base + bslot);
+    int64_t x0, y0, x1, y1;
+    tile_bounds(rp, tile, x0, y0, x1, y1);
+    if (pi == 0 && lane == 0) wb.tile_npx[bslot] = (int32_t)((x1 - x0) * (y1 - y0));
+    if (pi >= (x1 - x0) * (y1 - y0)) return;
+    const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
+    const int n = rp.spp;
+    double* s1d = (double*)(lds + lay.s1d);
+    (void)start_pixel_wave(rp, *jump, mb_state((uint64_t)tile, (uint64_t)pi, 0), pcg_inc_of((uint64_t)tile), s1d,
+                           (uint16_t*)(lds + lay.other), (uint32_t*)(lds + lay.vbuf), &sh_state);
+    for (int idx = lane; idx < rp.ndims * n; idx += kWave) wb.s1d[rec * wb.s1d_stride + idx] = s1d[idx];
+    int panic0 = 0, hit = 0;
+    SI si0;
+    BSDF b0;
+    b0.n_bxdfs = 0;
+    Ray ray = camera_ray(*sc.camera, (double)px + 0.0, (double)py + 0.0, s1d[1 < n ? 1 : 0], V2{0.0, 0.0});
+    if (n > 1 && 1 < rp.max_depth) {
+        hit = bvh_traverse<false>(sc, ray, &si0, stack_lds + lane, panic0) ? 1 : 0;
+        if (!panic0 && hit && compute_bsdf(sc, si0, b0) < 0) panic0 = -1;
+    }
+    if (panic0) hit = 0;
+    if (lane == 0) {
+        PixelRec& pr = wb.prec[rec];
+        pr.si = si0;
+        pr.b = b0;
+        pr.wo = ray.d;
+        pr.hit = hit;
+        pr.nvalid = n;
+        pr.panic0 = panic0;
+    }
 }
 
 // One thread per tile-film pixel: the tile film of the serial replay.
@@ -2507,7 +2558,14 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                                        c->lay, c->d_jump, c->wb, sb, nb, kWave / G, c->d_ctr);
                 }
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 1], c->stream));
-                if (rp.mode == PBRT_MODE_THROUGHPUT)
+                if (rp.mode == PBRT_MODE_THROUGHPUT && paths_ci_pixels(c, rp) > 0) {
+                    // setup (StartPixel + bounce 1 per pixel), then lane-refill paths
+                    hipLaunchKernelGGL(k_mb_setup, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
+                                       (unsigned)c->lay.total, c->stream, sc, rp, c->lay, c->d_jump, c->wb, sb, nb);
+                    hipLaunchKernelGGL((k_paths_ci<4, true>), dim3((unsigned)((nb * c->wb.ppt + 3) / 4)),
+                                       dim3(kWave), (unsigned)paths_group_lds<4>(rp.ndims * rp.spp), c->stream, sc,
+                                       rp, c->wb, sb, nb * c->wb.ppt, c->d_ctr);
+                } else if (rp.mode == PBRT_MODE_THROUGHPUT)
                     hipLaunchKernelGGL((k_paths<true, kPathsWaves>), dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
                                        (unsigned)c->lay.total, c->stream, sc, rp, c->lay, c->d_jump, c->wb, sb, nb,
                                        c->d_ctr);
