@@ -750,9 +750,17 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
 }
+struct PMeta {   // per pixel of a paths_group: PCG increment, tile, nvalid, hit, first work index
+    uint64_t inc, tile;
+    int32_t nv, hit, cum, pad;
+};
+template <int P>
+__host__ __device__ constexpr size_t paths_group_meta_off() {
+    return (P * sizeof(PixelCache) + P * 8 + 15) & ~(size_t)15;
+}
 template <int P>
 __host__ __device__ constexpr int paths_group_lds(int per) {   // bytes, per wave
-    return (int)(((P * sizeof(PixelCache) + P * 8 + 15) & ~(size_t)15) + (size_t)P * per * 8);
+    return (int)(paths_group_meta_off<P>() + (P + 1) * sizeof(PMeta) + (size_t)P * per * 8);
 }
 // kMB: THROUGHPUT mode, sample k of pixel pi starts from its own stream
 // mb_state(tile, pi, k) instead of the chain's offset state.
@@ -764,35 +772,36 @@ __device__ void paths_group(const DevScene& sc, const RenderParams& rp, const Wa
     const int per = ndims * n;
     PixelCache* pcs = (PixelCache*)wlds;
     unsigned long long* pkey = (unsigned long long*)(wlds + P * sizeof(PixelCache));
-    double* s1d = (double*)(wlds + ((P * sizeof(PixelCache) + P * 8 + 15) & ~(size_t)15));
-    int nv[P], hit[P], cum[P + 1];
-    uint64_t inc[P], tl[P];
-    cum[0] = 0;
-#pragma unroll
-    for (int j = 0; j < P; j++) {
-        const int64_t rec = rec0 + j;
-        nv[j] = 0;
-        hit[j] = 0;
-        inc[j] = 0;
-        tl[j] = 0;
-        if (rec < rec_end) {
-            const int64_t bslot = rec / wb.ppt, pi = rec % wb.ppt;
-            if (pi < wb.tile_npx[bslot]) {
-                nv[j] = wb.prec[rec].nvalid;
-                hit[j] = wb.prec[rec].hit;
-                tl[j] = (uint64_t)tile_of_slot(rp, slot_base + bslot);
-                inc[j] = pcg_inc_of(tl[j]);
+    // per-pixel metadata lives in LDS (not in per-lane register arrays)
+    PMeta* meta = (PMeta*)(wlds + paths_group_meta_off<P>());
+    double* s1d = (double*)(wlds + paths_group_meta_off<P>() + (P + 1) * sizeof(PMeta));
+    if (lane == 0) {
+        int cum = 0;
+        for (int j = 0; j < P; j++) {
+            const int64_t rec = rec0 + j;
+            PMeta m{0, 0, 0, 0, cum, 0};
+            if (rec < rec_end) {
+                const int64_t bslot = rec / wb.ppt, pi = rec % wb.ppt;
+                if (pi < wb.tile_npx[bslot]) {
+                    m.nv = wb.prec[rec].nvalid;
+                    m.hit = wb.prec[rec].hit;
+                    m.tile = (uint64_t)tile_of_slot(rp, slot_base + bslot);
+                    m.inc = pcg_inc_of(m.tile);
+                }
             }
+            meta[j] = m;
+            cum += m.nv > 1 ? m.nv - 1 : 0;
         }
-        cum[j + 1] = cum[j] + (nv[j] > 1 ? nv[j] - 1 : 0);
+        meta[P].cum = cum;
     }
+    wave_sync();
     for (int idx = lane; idx < P * per; idx += kWave) {
         const int j = idx / per;
-        if (nv[j] > 0) s1d[idx] = wb.s1d[(rec0 + j) * wb.s1d_stride + (idx - j * per)];
+        if (meta[j].nv > 0) s1d[idx] = wb.s1d[(rec0 + j) * wb.s1d_stride + (idx - j * per)];
     }
     if (lane < P) {
         pkey[lane] = ~0ULL;
-        if (nv[lane] > 0) {
+        if (meta[lane].nv > 0) {
             const PixelRec& pr = wb.prec[rec0 + lane];
             pcs[lane].si = pr.si;
             pcs[lane].b = pr.b;
@@ -803,7 +812,7 @@ __device__ void paths_group(const DevScene& sc, const RenderParams& rp, const Wa
     wave_sync();
     if (nl > 0 && lane < P * nl) {   // bounce-1 light samples, uLight = (0,0); lane = pixel * nl + light
         const int j = lane / nl, l = lane - j * nl;
-        if (nv[j] > 0 && hit[j] && pcs[j].b.n_bxdfs > 0) {
+        if (meta[j].nv > 0 && meta[j].hit && pcs[j].b.n_bxdfs > 0) {
             int pl = 0;
             Spec ld = estimate_direct(sc, nullptr, pl, pcs[j].si, pcs[j].b, l, V2{0.0, 0.0});
             if (!pl && max_component(ld) > 10) pl = PBRT_PANIC_LD_GT_10;
@@ -813,7 +822,7 @@ __device__ void paths_group(const DevScene& sc, const RenderParams& rp, const Wa
     }
     wave_sync();
     const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
-    const int T = cum[P];
+    const int T = meta[P].cum;
     int base = 0;
     int w = -1, j = 0, k = 0;
     PathState ps;
@@ -827,18 +836,19 @@ __device__ void paths_group(const DevScene& sc, const RenderParams& rp, const Wa
             if (t < T) {
                 j = 0;
 #pragma unroll
-                for (int q = 1; q < P; q++) j += t >= cum[q] ? 1 : 0;
-                k = 1 + (t - cum[j]);
+                for (int q = 1; q < P; q++) j += t >= meta[q].cum ? 1 : 0;
+                k = 1 + (t - meta[j].cum);
                 const int64_t rec = rec0 + j;
-                if (!hit[j]) {   // no traced bounce: the sample's radiance is 0
+                if (!meta[j].hit) {   // no traced bounce: the sample's radiance is 0
                     double* o = wb.L + (rec * n + k) * 3;
                     o[0] = 0.0;
                     o[1] = 0.0;
                     o[2] = 0.0;
                 } else {
                     w = t;
-                    c.rng.state = kMB ? mb_state(tl[j], (uint64_t)(rec % wb.ppt), (uint64_t)k) : wb.memb[rec * n + k];
-                    c.rng.inc = inc[j];
+                    c.rng.state = kMB ? mb_state(meta[j].tile, (uint64_t)(rec % wb.ppt), (uint64_t)k)
+                                      : wb.memb[rec * n + k];
+                    c.rng.inc = meta[j].inc;
                     c.draws = 0;
                     c.cur1d = 1;   // camera: Get2D pFilm, Get2D pLens, Get1D time (stratified)
                     c.cur2d = 2;
@@ -874,7 +884,7 @@ __device__ void paths_group(const DevScene& sc, const RenderParams& rp, const Wa
         }
     }
     wave_sync();
-    if (lane < P && nv[lane] > 0) {
+    if (lane < P && meta[lane].nv > 0) {
         const int64_t rec = rec0 + lane;
         const int64_t bslot = rec / wb.ppt, pi = rec % wb.ppt;
         int64_t x0, y0, x1, y1;
@@ -891,9 +901,9 @@ __device__ void paths_group(const DevScene& sc, const RenderParams& rp, const Wa
             p.sample = (int)(pkey[lane] >> 32);
         }
         wb.ppanic[rec] = p;
-        if (!p.kind && nv[lane] > 1) {
-            atomicAdd(&ctr->paths, (unsigned long long)(nv[lane] - 1));
-            atomicAdd(&ctr->camera_samples, (unsigned long long)(nv[lane] - 1));
+        if (!p.kind && meta[lane].nv > 1) {
+            atomicAdd(&ctr->paths, (unsigned long long)(meta[lane].nv - 1));
+            atomicAdd(&ctr->camera_samples, (unsigned long long)(meta[lane].nv - 1));
         }
     }
     wave_sync();   // the LDS block is reused by the wave's next group
