@@ -1437,6 +1437,9 @@ __global__ void k_wf_finish(WfBufs wf, int64_t nb, Counters* __restrict__ ctr) {
 // the sample index) is re-run there with the sample index known; an exact
 // panic ends the tile at that sample, as in k_chain. Bit-identical to the
 // serial replay: only the schedule changes.
+#ifndef PBRT_CI_EU_WAVES
+#define PBRT_CI_EU_WAVES 2   // k_chain_ci waves/SIMD (build option)
+#endif
 constexpr uint32_t kNoOff = 0xFFFFFFFFu;
 constexpr uint32_t kBadSpecD = 0xFFFFFFFEu;   // speculative lane could not resolve D
 constexpr uint32_t kBadExactD = 0xFFFFFFFDu;  // the exact head's trajectory panics
@@ -1464,7 +1467,7 @@ struct CiGroup {
 // per GPU (a multi-GPU shard). Idle lanes are ranked across the waves through
 // LDS; StartPixel runs on the first wave.
 template <int kW>
-__global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(2, 8))) void k_chain_ci(
+__global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT_CI_EU_WAVES, 8))) void k_chain_ci(
     DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
     int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr,
     const uint32_t* __restrict__ order, uint32_t* __restrict__ ticks) {
