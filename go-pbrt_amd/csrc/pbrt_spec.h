@@ -223,7 +223,7 @@ struct PathState {
     int first;
 };
 template <class Cache>
-__device__ inline bool path_step(const DevScene& sc, const Cache& pc, const SpecSampler& ss, Cursor& c,
+__device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, const SpecSampler& ss, Cursor& c,
                                  PathState& s, int max_depth, double rr_threshold, uint16_t* stack, int& panic,
                                  int& bounce) {
     SI isect;

@@ -765,7 +765,7 @@ __host__ __device__ constexpr int paths_group_lds(int per) {   // bytes, per wav
 // kMB: THROUGHPUT mode, sample k of pixel pi starts from its own stream
 // mb_state(tile, pi, k) instead of the chain's offset state.
 template <int P, bool kMB = false>
-__device__ void paths_group(const DevScene& sc, const RenderParams& rp, const WaveBufs& wb, int64_t slot_base,
+__device__ __forceinline__ void paths_group(const DevScene& sc, const RenderParams& rp, const WaveBufs& wb, int64_t slot_base,
                             int64_t rec0, int64_t rec_end, Counters* __restrict__ ctr, unsigned char* wlds) {
     const int lane = threadIdx.x & (kWave - 1);
     const int n = rp.spp, ndims = rp.ndims, nl = sc.n_lights;
