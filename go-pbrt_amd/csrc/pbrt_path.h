@@ -500,15 +500,22 @@ __device__ inline bool bvh_walk(const DevScene& sc, Ray& ray, uint16_t* stack, i
             // A: the next leaf in the octant's preorder whose box the ray enters
             bool leaf = false;
             uint32_t first = 0, np = 0;
+            // two leaves per iteration: independent loads and slab tests overlap;
+            // the second result is used only if the first leaf misses (same TMax)
             while (j < nl) {
-                const NodeView nd = load_node(sc, leaves[j]);
-                j++;
-                if (node_hit(nd, ray, inv, nx, ny, nz)) {
+                const NodeView n0 = load_node(sc, leaves[j]);
+                const bool two = j + 1 < nl;
+                const NodeView n1 = load_node(sc, leaves[two ? j + 1 : j]);
+                const bool h0 = node_hit(n0, ray, inv, nx, ny, nz);
+                const bool h1 = two && node_hit(n1, ray, inv, nx, ny, nz);
+                if (h0 || h1) {
                     leaf = true;
-                    first = nd.offset;
-                    np = nd.n_prims;
+                    first = h0 ? n0.offset : n1.offset;
+                    np = h0 ? n0.n_prims : n1.n_prims;
+                    j += h0 ? 1 : 2;
                     break;
                 }
+                j += 2;
             }
             STEP_T(if (!kAny) tt.mark(5);)
             if (!leaf) break;
