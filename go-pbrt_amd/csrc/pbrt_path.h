@@ -500,22 +500,27 @@ __device__ inline bool bvh_walk(const DevScene& sc, Ray& ray, uint16_t* stack, i
             // A: the next leaf in the octant's preorder whose box the ray enters
             bool leaf = false;
             uint32_t first = 0, np = 0;
-            // two leaves per iteration: independent loads and slab tests overlap;
-            // the second result is used only if the first leaf misses (same TMax)
+            // four leaves per iteration: independent loads and slab tests overlap;
+            // a later result is used only if the earlier leaves miss (same TMax)
             while (j < nl) {
+                const int j1 = j + 1 < nl ? j + 1 : j, j2 = j + 2 < nl ? j + 2 : j, j3 = j + 3 < nl ? j + 3 : j;
                 const NodeView n0 = load_node(sc, leaves[j]);
-                const bool two = j + 1 < nl;
-                const NodeView n1 = load_node(sc, leaves[two ? j + 1 : j]);
+                const NodeView n1 = load_node(sc, leaves[j1]);
+                const NodeView n2 = load_node(sc, leaves[j2]);
+                const NodeView n3 = load_node(sc, leaves[j3]);
                 const bool h0 = node_hit(n0, ray, inv, nx, ny, nz);
-                const bool h1 = two && node_hit(n1, ray, inv, nx, ny, nz);
-                if (h0 || h1) {
+                const bool h1 = j1 > j && node_hit(n1, ray, inv, nx, ny, nz);
+                const bool h2 = j2 > j && node_hit(n2, ray, inv, nx, ny, nz);
+                const bool h3 = j3 > j && node_hit(n3, ray, inv, nx, ny, nz);
+                if (h0 | h1 | h2 | h3) {
                     leaf = true;
-                    first = h0 ? n0.offset : n1.offset;
-                    np = h0 ? n0.n_prims : n1.n_prims;
-                    j += h0 ? 1 : 2;
+                    const int q = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
+                    first = q == 0 ? n0.offset : q == 1 ? n1.offset : q == 2 ? n2.offset : n3.offset;
+                    np = q == 0 ? n0.n_prims : q == 1 ? n1.n_prims : q == 2 ? n2.n_prims : n3.n_prims;
+                    j += q + 1;
                     break;
                 }
-                j += 2;
+                j += 4;
             }
             STEP_T(if (!kAny) tt.mark(5);)
             if (!leaf) break;
