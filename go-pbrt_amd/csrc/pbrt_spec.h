@@ -222,15 +222,18 @@ struct PathState {
     int bounces;
     int first;
 };
-template <class Cache>
+// kWhich: 0 any iteration, 1 only the first (s.first == 1: bounce 1 from the
+// pixel cache, no traversal), 2 only later ones (s.first == 0).
+template <int kWhich = 0, class Cache>
 __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, const SpecSampler& ss, Cursor& c,
                                  PathState& s, int max_depth, double rr_threshold, uint16_t* stack, int& panic,
                                  int& bounce) {
+    const bool first = kWhich == 1 ? true : kWhich == 2 ? false : (s.first != 0);
     SI isect;
     BSDF b;
     V3 wo;
     const int nl = sc.n_lights;
-    if (!s.first) {
+    if (!first) {
         s.bounces++;
         bounce = s.bounces;
         if (s.bounces >= max_depth) return true;
@@ -261,7 +264,7 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
             V2 ul = c_get2d(c, ss);
             c_get2d(c, ss);
             Spec ld;
-            if (s.first) {
+            if (first) {
                 ld = pc.ld[ln];
                 if (pc.ld_panic[ln]) {
                     panic = pc.ld_panic[ln];

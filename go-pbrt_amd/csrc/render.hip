@@ -869,8 +869,14 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
             continue;
         }
         if (w >= 0) {
+            // a path taken this iteration runs its bounce 1 from the pixel cache
+            // (no traversal) and then, with every other live path, one traced
+            // bounce: the cheap first step does not cost the wave an iteration
             const SpecSampler ss{s1d + j * per, n, ndims};
-            if (path_step(sc, pcs[j], ss, c, ps, rp.max_depth, rp.rr_threshold, nullptr, pnc, bnc)) {
+            bool done = false;
+            if (ps.first) done = path_step<1>(sc, pcs[j], ss, c, ps, rp.max_depth, rp.rr_threshold, nullptr, pnc, bnc);
+            if (!done) done = path_step<2>(sc, pcs[j], ss, c, ps, rp.max_depth, rp.rr_threshold, nullptr, pnc, bnc);
+            if (done) {
                 const int64_t rec = rec0 + j;
                 double* o = wb.L + (rec * n + k) * 3;
                 o[0] = ps.L.r;
