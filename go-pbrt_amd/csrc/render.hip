@@ -1836,6 +1836,12 @@ struct pbrt_gpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    // heavy/light split of k_chain_ci: the heaviest tiles with 4 waves each on
+    // the main stream, the rest on stream2, concurrently
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_split = nullptr, ev_join = nullptr;
+    int64_t heavy_k = 0;                 // slots at the front of h_slot_order that get 4 waves
+    std::vector<uint8_t> h_slot_kw;      // waves per tile each slot ran with in the last frame
     double* film_target = nullptr;   // caller buffer of the last render_async_into
     int lanes_per_wave = 64;
     bool lanes_per_wave_set = false;
@@ -2145,6 +2151,19 @@ int ci_waves(const pbrt_gpu_ctx* c, int64_t nb) {
 // chain time; the next frame of the same configuration on this context
 // launches its tiles heaviest first (LPT). Only the schedule changes, never
 // a result. PBRT_CI_ORDER=0 disables it.
+// Multi-GPU shards (launches that would run 2 or 4 waves per tile): the
+// heaviest tiles of the previous frame get 4 waves in a launch of their own
+// and the rest 1 wave each in a concurrent one (1/4- and 1/2-frame shards:
+// 387 -> 305 ms and 524 -> 472 ms per rank). PBRT_CI_SPLIT=0 disables it;
+// PBRT_CI_HEAVY=K forces the heavy count (tests).
+bool ci_split_enabled() {
+    const char* e = getenv("PBRT_CI_SPLIT");
+    return !(e && atoi(e) == 0);
+}
+int64_t ci_heavy_override() {
+    const char* e = getenv("PBRT_CI_HEAVY");
+    return e ? (int64_t)atoll(e) : -1;
+}
 bool ci_order_enabled() {
     const char* e = getenv("PBRT_CI_ORDER");
     return !(e && atoi(e) == 0);
@@ -2464,8 +2483,11 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
     c->host_lights.assign(scene->lights, scene->lights + scene->n_lights);
     c->host_scene.lights = c->host_lights.data();
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipEventCreate(&c->ev2) != hipSuccess) {
+        hipEventCreate(&c->ev2) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_split, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
         pbrt_gpu_destroy(c);
         return PBRT_E_HIP;
     }
@@ -2554,20 +2576,43 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                         c->ticks_key = key;
                         c->ticks_n = nb;
                     }
-                    if (kw > 1) {   // one tile per workgroup of kw waves; the ring grows with the lanes
-                        const int ring = kw * kCiRingBytes / (int)sizeof(RingEnt);
-                        const unsigned lds = (unsigned)(c->lay_ci.total + (kw - 1) * kCiRingBytes);
-                        auto kern = kw == 2 ? k_chain_ci<2> : k_chain_ci<4>;
-                        hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(kWave * kw), lds, c->stream, sc, rp,
-                                           c->lay_ci, c->d_jump, c->wb, sb, nb, kWave * kw, ring, c->d_ctr, order,
-                                           ticks);
+                    // one launch of n workgroups, workgroup b on slot ord[b] (identity if null)
+                    auto launch_ci = [&](int w, int64_t n, const uint32_t* ord, hipStream_t st) {
+                        if (w > 1) {   // one tile per workgroup of w waves; the ring grows with the lanes
+                            const int ring = w * kCiRingBytes / (int)sizeof(RingEnt);
+                            const unsigned lds = (unsigned)(c->lay_ci.total + (w - 1) * kCiRingBytes);
+                            auto kern = w == 2 ? k_chain_ci<2> : k_chain_ci<4>;
+                            hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3(kWave * w), lds, st, sc, rp, c->lay_ci,
+                                               c->d_jump, c->wb, sb, nb, kWave * w, ring, c->d_ctr, ord, ticks);
+                        } else {
+                            const int Gc = std::min(G, kCiMaxGroups);
+                            const int ring = kCiRingBytes / (int)sizeof(RingEnt) / Gc;
+                            hipLaunchKernelGGL(k_chain_ci<1>, dim3((unsigned)((n + Gc - 1) / Gc)), dim3(kWave),
+                                               (unsigned)c->lay_ci.total, st, sc, rp, c->lay_ci, c->d_jump, c->wb, sb,
+                                               nb, kWave / Gc, ring, c->d_ctr, Gc == 1 ? ord : nullptr,
+                                               Gc == 1 ? ticks : nullptr);
+                        }
+                    };
+                    // the heaviest tiles of the last frame get 4 waves each; they are
+                    // launched first, on the main stream, and the rest concurrently on
+                    // stream2 (same-stream launches would serialise)
+                    // (multi-GPU shards, where kw > 1: the rest then run at 1 wave per
+                    // tile, the most efficient per lane)
+                    const int64_t heavy = (order && kw > 1 && G == 1 && ci_split_enabled())
+                                              ? std::min<int64_t>(c->heavy_k, nb) : 0;
+                    if (ticks) {
+                        c->h_slot_kw.assign((size_t)nb, (uint8_t)(heavy > 0 ? 1 : kw));
+                        for (int64_t i = 0; i < heavy; i++) c->h_slot_kw[c->h_slot_order[(size_t)i]] = 4;
+                    }
+                    if (heavy > 0 && nb > heavy) {
+                        HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
+                        launch_ci(4, heavy, order, c->stream);
+                        HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
+                        launch_ci(1, nb - heavy, order + heavy, c->stream2);
+                        HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
+                        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
                     } else {
-                        const int Gc = std::min(G, kCiMaxGroups);
-                        const int ring = kCiRingBytes / (int)sizeof(RingEnt) / Gc;
-                        hipLaunchKernelGGL(k_chain_ci<1>, dim3((unsigned)((nb + Gc - 1) / Gc)), dim3(kWave),
-                                           (unsigned)c->lay_ci.total, c->stream, sc, rp, c->lay_ci, c->d_jump, c->wb,
-                                           sb, nb, kWave / Gc, ring, c->d_ctr, Gc == 1 ? order : nullptr,
-                                           Gc == 1 ? ticks : nullptr);
+                        launch_ci(kw, nb, order, c->stream);
                     }
                 } else {
                     hipLaunchKernelGGL(k_wf_primary, dim3((unsigned)((nb * c->wb.ppt + kWave - 1) / kWave)),
@@ -2675,10 +2720,25 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
                 fclose(f);
             }
         }
+        // cost at 1 wave per tile: 2 and 4 waves measured 1.3x / 1.8x faster per tile
+        std::vector<double> cost(t.size());
+        double sum = 0;
+        for (size_t i = 0; i < t.size(); i++) {
+            const int w = i < c->h_slot_kw.size() ? c->h_slot_kw[i] : 1;
+            cost[i] = (double)t[i] * (w == 4 ? 1.8 : w == 2 ? 1.3 : 1.0);
+            sum += cost[i];
+        }
         c->h_slot_order.resize(t.size());
         for (size_t i = 0; i < t.size(); i++) c->h_slot_order[i] = (uint32_t)i;
         std::stable_sort(c->h_slot_order.begin(), c->h_slot_order.end(),
-                         [&](uint32_t a, uint32_t b) { return t[a] > t[b]; });
+                         [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+        // heavy: tiles whose 1-wave chain alone would take over 0.7x the
+        // frame's throughput bound (summed cost over 2 waves/SIMD)
+        const double thr = 0.7 * sum / (2.0 * (double)c->n_simd);
+        int64_t k = 0;
+        while (k < (int64_t)t.size() && cost[c->h_slot_order[(size_t)k]] > thr) k++;
+        c->heavy_k = std::min<int64_t>(k, c->n_simd / 4);   // at most a quarter of the wave slots
+        if (ci_heavy_override() >= 0) c->heavy_k = ci_heavy_override();
         c->order_key = c->ticks_key;
     }
     if (ctr.any_panic) {
@@ -2811,6 +2871,12 @@ void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev2) (void)hipEventDestroy(c->ev2);
+    if (c->ev_split) (void)hipEventDestroy(c->ev_split);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->stream2) {
+        (void)hipStreamSynchronize(c->stream2);
+        (void)hipStreamDestroy(c->stream2);
+    }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }

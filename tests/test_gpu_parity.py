@@ -400,6 +400,26 @@ def test_wave_ci_heaviest_first_schedule_keeps_bits(ci_waves, monkeypatch):
                 assert same_bits(film, ofilm)
 
 
+@pytest.mark.parametrize("heavy", ["3", "12"])
+@pytest.mark.parametrize("ci_waves", ["2", "4"])
+def test_wave_ci_heavy_light_split_keeps_bits(ci_waves, heavy, monkeypatch):
+    """Shard mode: from the second frame the heaviest tiles run at 4 waves in
+    one launch and the rest at 1 wave in a concurrent launch on a second
+    stream; only the schedule changes."""
+    monkeypatch.setenv("PBRT_CI_WAVES", ci_waves)
+    monkeypatch.setenv("PBRT_CI_HEAVY", heavy)
+    scene = G.Scene.readme(112, 80)
+    rds = [abi.render_desc(8, 8), abi.render_desc(4, 4, tile_begin=1, tile_stride=2),
+           abi.render_desc(6, 6, max_depth=12, rr_threshold=0.5)]
+    with G.Renderer(scene, kernel="wave_ci") as r:
+        for rd in rds:
+            ofilm, _ = oracle_render(scene, rd)
+            for _ in range(3):
+                film, st = r.render(rd)
+                assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
+                assert same_bits(film, ofilm)
+
+
 @pytest.mark.parametrize("ci_waves", ["1", "4"])
 def test_wave_ci_panic_is_reported_like_the_oracle(ci_waves, monkeypatch):
     monkeypatch.setenv("PBRT_CI_WAVES", ci_waves)
