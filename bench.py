@@ -139,16 +139,18 @@ def main():
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)   # RCCL over xGMI
 
     import pbrtgpu as G
 
     W, H, S = args.width, args.height, args.spp
     rd_kwargs = dict(spp_x=S, spp_y=S)
     scene = G.Scene.readme(W, H)
+    # the renderer (and its two HIP streams) before RCCL's own streams, so the
+    # heavy/light chain launches get hardware queues of their own
     renderer = G.Renderer(scene, device=local, kernel=args.kernel, lanes_per_wave=args.tiles_per_wave,
                           occupancy=args.occupancy)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)   # RCCL over xGMI
     modes = {"exact": G.abi.PBRT_MODE_EXACT, "throughput": G.abi.PBRT_MODE_THROUGHPUT}
     film = torch.zeros((H, W, 3), dtype=torch.float64, device=dev)
 
