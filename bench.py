@@ -38,12 +38,17 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--spp", type=int, default=8, help="Stratified(spp, spp)")
+    ap.add_argument("--config", default="B", choices=["B", "C"],
+                    help="BASELINE config: B = README sphere scene, Stratified(8,8), Path(10); "
+                         "C = Cornell (SURVEY 8(d)), Stratified(16,16), Path(8)")
+    ap.add_argument("--spp", type=int, default=0, help="Stratified(spp, spp) (0 = the config's)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "serial", "wave", "wavefront", "wave_ci"])
     ap.add_argument("--tiles-per-wave", type=int, default=0, help="k_chain lane groups per wave (0 = library default)")
     ap.add_argument("--occupancy", type=int, default=0)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall budget of the CPU baseline sample")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, nproc)")
+    ap.add_argument("--cpu-seconds", type=float, default=30.0, help="wall budget of the CPU baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = this process's CPU share: OMP_NUM_THREADS if set (the GPU box allots 16 host "
+                         "cores per GPU), else the affinity mask")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="exact", choices=["exact", "throughput"],
                     help="mode of the headline line (exact = the reference's per-tile RNG, bit-exact)")
@@ -60,18 +65,43 @@ def load_json(path):
         return None
 
 
-def cpu_baseline(args, rd_kwargs):
-    """The oracle (C restatement of the Go path, oracle/) on a bounded, evenly
-    spread sample of the same frame's tiles, on this box's host cores."""
+def host_cpu():
+    """nproc, the affinity mask, the process's CPU share and the CPU model of this host."""
+    model = "?"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = nproc
+    share = affinity
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        share = min(share, int(omp))
+    return {"nproc": nproc, "affinity": affinity, "share": share, "cpu_model": model}
+
+
+def cpu_baseline(args, scene_name, rd_kwargs):
+    """The oracle (C restatement of the Go path, oracle/) on the same frame's
+    tiles, on this box's host cores: the whole frame when it fits the budget,
+    else an evenly spread tile sample (bit-reversed stride-64 batches, so every
+    prefix of batches is spread over the frame) -- stated in `sample`."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib as O
     from pbrtgpu import abi
 
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-    sc = O.OracleScene.readme(args.width, args.height)
+    cpu = host_cpu()
+    threads = args.cpu_threads or cpu["share"]
+    sc = (O.OracleScene.readme if scene_name == "readme" else O.OracleScene.cornell)(args.width, args.height)
     n_tiles = int(O.lib().oracle_num_tiles(sc.desc, abi.render_desc(**rd_kwargs)))
     stride = 64
-    # bit-reversed offsets: every prefix of batches is an evenly spread tile subset
     offsets = [int(format(i, "06b")[::-1], 2) for i in range(stride)]
     paths = tiles = 0
     t0 = time.perf_counter()
@@ -85,17 +115,25 @@ def cpu_baseline(args, rd_kwargs):
         if time.perf_counter() - t0 >= args.cpu_seconds:
             break
     dt = time.perf_counter() - t0
+    what = "the whole frame" if tiles == n_tiles else \
+        f"{tiles} of {n_tiles} tiles of the same frame (evenly spread, stride {stride})"
     return {
         "value": paths / dt / 1e6,
         "unit": "Mpaths/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{tiles} of {n_tiles} tiles of the same frame (evenly spread, stride {stride}), "
-                  f"{paths} paths in {dt:.2f} s on {threads} threads; oracle/ C restatement of the Go path",
+        "nproc": cpu["nproc"],
+        "affinity": cpu["affinity"],
+        "cpu_model": cpu["cpu_model"],
+        "per_core": paths / dt / 1e6 / threads,
+        "sample": f"{what}: {paths} paths in {dt:.2f} s on {threads} threads (this process's CPU share: "
+                  f"OMP_NUM_THREADS / affinity; nproc {cpu['nproc']}); oracle/ C restatement of the Go path, "
+                  "which has no Go per-op heap allocation, so it is expected to be faster than go-pbrt",
     }
 
 
-def roofline(W, H, S, paths_per_launch, kernel_kind, kern_ms, chain_ms, paths_ms, merge_ms, mode="exact"):
+def roofline(scene_name, W, H, S, paths_per_launch, kernel_kind, kern_ms, chain_ms, paths_ms, merge_ms,
+             mode="exact"):
     """Roofline of the dominant kernel, priced in ALGORITHMIC fp64 FLOPs: the
     reference's own arithmetic per path, counted by the FLOP-accounting oracle
     (profiles/flops_*.json, tools/count_flops.py) x the paths of one launch,
@@ -105,10 +143,10 @@ def roofline(W, H, S, paths_per_launch, kernel_kind, kern_ms, chain_ms, paths_ms
     the trajectory (everything but light sampling: flops_trajectory_per_path).
     Its speculative, discarded trajectories are not algorithmic work, so they
     lower `frac` -- that is the point of the measure."""
-    fl = load_json(os.path.join(REPO, "profiles", f"flops_readme_{W}x{H}_s{S}x{S}.json"))
+    fl = load_json(os.path.join(REPO, "profiles", f"flops_{scene_name}_{W}x{H}_s{S}x{S}.json"))
     if not fl:
         return None
-    pmc = load_json(os.path.join(REPO, "profiles", f"pmc_readme_{W}x{H}_s{S}x{S}.json")) or {}
+    pmc = load_json(os.path.join(REPO, "profiles", f"pmc_{scene_name}_{W}x{H}_s{S}x{S}.json")) or {}
     total = fl["flops_per_path"] * paths_per_launch
     if mode == "throughput" and kernel_kind == 2:   # no chain: k_paths<true> runs the whole path
         algo, name, ms = total, "k_paths_mb", paths_ms
@@ -118,12 +156,32 @@ def roofline(W, H, S, paths_per_launch, kernel_kind, kern_ms, chain_ms, paths_ms
     else:
         algo, name, ms = total, "k_render_exact", kern_ms
     achieved = algo / (ms / 1e3) / 1e12
+    traffic = (pmc.get(name) or {}).get("hbm_bytes_per_launch")
+    frame_bytes = sum(v.get("hbm_bytes_per_launch", 0) for v in pmc.values() if isinstance(v, dict))
     return {"bound": "fp64-valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": achieved / FP64_PEAK_TFLOPS, "traffic": (pmc.get(name) or {}).get("hbm_bytes_per_launch"),
+            "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
             "kernel": name, "kernel_ms": ms, "flops_per_launch": algo,
+            # the north_star's "HBM GB/s vs peak": PMC bytes (profiles/pmc_*.json, same command under
+            # rocprofv3) over this run's kernel time, for the dominant kernel and the whole frame
+            "hbm": {"kernel_gbs": traffic / (ms / 1e3) / 1e9 if traffic else None,
+                    "frame_gbs": frame_bytes / (kern_ms / 1e3) / 1e9 if frame_bytes else None,
+                    "peak_gbs": HBM_PEAK_GBS,
+                    "kernel_frac": traffic / (ms / 1e3) / 1e9 / HBM_PEAK_GBS if traffic else None},
             "pipeline": {"kernels_ms": kern_ms, "k_paths_ms": paths_ms, "merge_ms": merge_ms,
                          "achieved_tflops": total / (kern_ms / 1e3) / 1e12,
                          "flops_per_path": fl["flops_per_path"]}}
+
+
+CONFIGS = {
+    # BASELINE.json configs[1]: internal/render/server.go:29-164 verbatim
+    "B": dict(scene="readme", spp=8, max_depth=10,
+              text="README sphere scene {W}x{H}, Stratified({S},{S}) = {T} traced paths/px, "
+                   "Path(maxDepth 10, rr 1, Uniform), tile 16"),
+    # BASELINE.json configs[2]: SURVEY 8(d) Cornell fixture
+    "C": dict(scene="cornell", spp=16, max_depth=8,
+              text="Cornell 6 disks + 2 spheres {W}x{H}, Stratified({S},{S}) = {T} traced paths/px, "
+                   "Path(maxDepth 8, rr 1, Uniform), tile 16"),
+}
 
 
 def main():
@@ -142,9 +200,11 @@ def main():
 
     import pbrtgpu as G
 
-    W, H, S = args.width, args.height, args.spp
-    rd_kwargs = dict(spp_x=S, spp_y=S)
-    scene = G.Scene.readme(W, H)
+    cfg = CONFIGS[args.config]
+    W, H = args.width, args.height
+    S = args.spp or cfg["spp"]
+    rd_kwargs = dict(spp_x=S, spp_y=S, max_depth=cfg["max_depth"])
+    scene = (G.Scene.readme if cfg["scene"] == "readme" else G.Scene.cornell)(W, H)
     # the renderer (and its two HIP streams) before RCCL's own streams, so the
     # heavy/light chain launches get hardware queues of their own
     renderer = G.Renderer(scene, device=local, kernel=args.kernel, lanes_per_wave=args.tiles_per_wave,
@@ -153,21 +213,29 @@ def main():
         dist.init_process_group("nccl", device_id=dev)   # RCCL over xGMI
     modes = {"exact": G.abi.PBRT_MODE_EXACT, "throughput": G.abi.PBRT_MODE_THROUGHPUT}
     film = torch.zeros((H, W, 3), dtype=torch.float64, device=dev)
+    # the renderer launches on its own non-blocking HIP stream: order it after
+    # everything queued on torch's stream (the film's zero fill, the previous
+    # frame's RCCL reduce, which dist.reduce made torch's stream wait for)
+    rstream = torch.cuda.ExternalStream(renderer.stream(), device=dev)
 
     def barrier():
         if world > 1:
             dist.barrier(device_ids=[local])
 
-    def timed(mode, steps, warmup):
+    def make_step(mode):
         rd = G.render_desc(**rd_kwargs, tile_begin=rank, tile_stride=world, mode=modes[mode])
 
         def step():
+            rstream.wait_stream(torch.cuda.current_stream(dev))
             renderer.render_async(rd, film.data_ptr())
             st = renderer.synchronize()
             if world > 1:
                 dist.reduce(film, dst=0, op=dist.ReduceOp.SUM)
             return st
+        return step
 
+    def timed(mode, steps, warmup):
+        step = make_step(mode)
         for _ in range(warmup):
             step()
         barrier()
@@ -189,6 +257,19 @@ def main():
             paths_total = float(paths_local)
         return elapsed, paths_local, paths_total, stats
 
+    # cold frame: a fresh context's first frame (no schedule learned yet), as
+    # internal/render/server.go pays it when it builds a scene per RPC
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    first = make_step(args.mode)()
+    torch.cuda.synchronize()
+    first_ms = (time.perf_counter() - t0) * 1e3
+    if world > 1:
+        fm = torch.tensor([first_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(fm, op=dist.ReduceOp.MAX)
+        first_ms = float(fm[0])
+
     elapsed, paths_local, paths_total, stats = timed(args.mode, args.steps, args.warmup)
     kern_ms = sum(s.kernel_ms for s in stats) / len(stats)
     merge_ms = sum(s.merge_ms for s in stats) / len(stats)
@@ -206,8 +287,8 @@ def main():
 
     if rank == 0:
         value = paths_total / elapsed / 1e6
-        roof = roofline(W, H, S, paths_local / len(stats), kernel_kind, kern_ms, chain_ms, paths_ms, merge_ms,
-                        args.mode)
+        roof = roofline(cfg["scene"], W, H, S, paths_local / len(stats), kernel_kind, kern_ms, chain_ms, paths_ms,
+                        merge_ms, args.mode)
         out = {
             "metric": METRIC,
             "value": value,
@@ -220,22 +301,27 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (the reference's hard-coded README scene; no external data)",
+            "data": f"synthetic (the reference's hard-coded {'README' if cfg['scene'] == 'readme' else 'Cornell'} "
+                    "scene; no external data)",
             "config": {
-                "workload": f"README sphere scene {W}x{H}, Stratified({S},{S}) = {S * S - 1} traced paths/px, "
-                            "Path(maxDepth 10, rr 1, Uniform), tile 16, "
+                "workload": cfg["text"].format(W=W, H=H, S=S, T=S * S - 1) + ", "
                             + ("EXACT per-tile RNG" if args.mode == "exact" else "THROUGHPUT per-path RNG"),
-                "width": W, "height": H, "spp": S * S, "traced_spp": S * S - 1,
+                "baseline_config": args.config,
+                "width": W, "height": H, "spp": S * S, "traced_spp": S * S - 1, "max_depth": cfg["max_depth"],
                 "paths_per_frame": int(paths_total / args.steps), "mode": args.mode,
                 "parallelism": f"tiles mod {world}" + (" + RCCL film reduce" if world > 1 else ""),
                 "kernel": {1: "serial", 2: "wave", 3: "wavefront", 4: "wave_ci"}.get(kernel_kind, "?"),
             },
+            "first_frame_ms": first_ms,
+            "first_frame_chain_ms": first.chain_ms,
             "roofline": roof,
         }
         if side:
             out["side_mode"] = side
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args, rd_kwargs)
+            cb = cpu_baseline(args, cfg["scene"], rd_kwargs)
+            cb["gpu_over_cpu"] = value / cb["value"]
+            out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)
     renderer.close()
     if world > 1:

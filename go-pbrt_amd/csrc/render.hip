@@ -68,7 +68,7 @@ struct Counters {
     unsigned long long windows, phase[8];
     unsigned long long dhist[64];   // k_chain_ci diagnostics: on-chain draw counts D (bin D/2, last bin >= 126)
 };
-constexpr int kNumCounters = 6 + 8;
+constexpr int kNumCounters = 6 + 8 + 64;
 
 __device__ __forceinline__ void tile_bounds(const RenderParams& rp, int64_t tile, int64_t& x0, int64_t& y0,
                                             int64_t& x1, int64_t& y1) {
@@ -1841,6 +1841,8 @@ struct pbrt_gpu_ctx {
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_split = nullptr, ev_join = nullptr;
     int64_t heavy_k = 0;                 // slots at the front of h_slot_order that get 4 waves
+    int64_t last_heavy = 0;              // heavy slots of the last EXACT launch (0: no split)
+    std::vector<uint32_t> h_last_ticks;  // per-slot chain ticks of the last EXACT frame
     std::vector<uint8_t> h_slot_kw;      // waves per tile each slot ran with in the last frame
     double* film_target = nullptr;   // caller buffer of the last render_async_into
     int lanes_per_wave = 64;
@@ -2194,14 +2196,22 @@ int paths_ci_pixels(const pbrt_gpu_ctx* c, const RenderParams& rp) {
     return fits ? pp : 0;
 }
 
-// Carve the per-batch buffers of the wave path (budget: PBRT_WAVE_BUFFER_GB, default 12).
+// Carve the per-batch buffers of the wave path. Budget: PBRT_WAVE_BUFFER_GB,
+// default min(48 GB, half the free HBM) -- config C (1080p, 256 spp, ~34 GB)
+// is then one batch on a 288 GB MI355X, so its whole frame is one launch per
+// kernel and gets the heaviest-first schedule.
 int wave_buffers(pbrt_gpu_ctx* c) {
     const RenderParams& rp = c->rp;
     const int64_t ppt = rp.tile_size * rp.tile_size, n = rp.spp, nd = rp.ndims > 0 ? rp.ndims : 1;
     auto al = [](int64_t b) { return (b + 255) & ~int64_t(255); };
     const int64_t per_tile = al(ppt * (int64_t)sizeof(PixelRec)) + al(ppt * nd * n * 8) + al(ppt * n * 8) +
                              al(ppt * n * 24) + al(ppt * (int64_t)sizeof(PanicRec)) + al(4);
-    double gb = 12.0;
+    double gb = 48.0;
+    {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
+            gb = std::min(gb, 0.5 * (double)(free_b + c->wave_cap) / 1073741824.0);
+    }
     if (const char* e = getenv("PBRT_WAVE_BUFFER_GB")) gb = atof(e) > 0 ? atof(e) : gb;
     int64_t batch = (int64_t)(gb * 1073741824.0) / per_tile;
     if (batch < 1) batch = 1;
@@ -2519,6 +2529,7 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
     const RenderParams& rp = c->rp;
     double* out = film_device ? film_device : c->d_out;
     c->film_target = out;
+    c->last_heavy = 0;
     HIPCHK(c, hipMemsetAsync(c->d_ctr, 0, sizeof(Counters), c->stream));
     if (rp.n_slots > 0) HIPCHK(c, hipMemsetAsync(c->d_panics, 0, sizeof(PanicRec) * (size_t)rp.n_slots, c->stream));
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
@@ -2598,13 +2609,19 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                     // stream2 (same-stream launches would serialise)
                     // (multi-GPU shards, where kw > 1: the rest then run at 1 wave per
                     // tile, the most efficient per lane)
-                    const int64_t heavy = (order && kw > 1 && G == 1 && ci_split_enabled())
-                                              ? std::min<int64_t>(c->heavy_k, nb) : 0;
-                    if (ticks) {
+                    // measured wins at 1/2 and 1/4 shards (nb > n_simd); a loss at 1/8
+                    // (1020 tiles: 294 -> 307 ms), so smaller launches never split
+                    int64_t heavy = (order && kw > 1 && G == 1 && nb > c->n_simd && ci_split_enabled())
+                                        ? std::min<int64_t>(c->heavy_k, nb) : 0;
+                    if (ci_heavy_override() >= 0 && order && kw > 1 && G == 1)   // tests force the split
+                        heavy = std::min<int64_t>(ci_heavy_override(), nb);
+                    if (heavy >= nb) heavy = 0;   // nothing left for the light launch: one launch at kw
+                    c->last_heavy = heavy;
+                    if (ticks) {   // label every slot with the waves it actually runs at
                         c->h_slot_kw.assign((size_t)nb, (uint8_t)(heavy > 0 ? 1 : kw));
                         for (int64_t i = 0; i < heavy; i++) c->h_slot_kw[c->h_slot_order[(size_t)i]] = 4;
                     }
-                    if (heavy > 0 && nb > heavy) {
+                    if (heavy > 0) {
                         HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
                         launch_ci(4, heavy, order, c->stream);
                         HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
@@ -2708,18 +2725,7 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
         c->ticks_pending = false;
         std::vector<uint32_t> t((size_t)c->ticks_n);
         HIPCHK(c, hipMemcpy(t.data(), c->d_ticks, sizeof(uint32_t) * t.size(), hipMemcpyDeviceToHost));
-        if (const char* path = getenv("PBRT_DHIST_DUMP")) {   // diagnostics: on-chain D histogram + counters
-            if (FILE* f = fopen(path, "wb")) {
-                fwrite(&ctr, sizeof(ctr), 1, f);
-                fclose(f);
-            }
-        }
-        if (const char* path = getenv("PBRT_TICKS_DUMP")) {   // diagnostics: per-slot chain ticks (100 MHz)
-            if (FILE* f = fopen(path, "wb")) {
-                fwrite(t.data(), sizeof(uint32_t), t.size(), f);
-                fclose(f);
-            }
-        }
+        c->h_last_ticks = t;   // pbrt_gpu_tile_ticks
         // cost at 1 wave per tile: 2 and 4 waves measured 1.3x / 1.8x faster per tile
         std::vector<double> cost(t.size());
         double sum = 0;
@@ -3000,8 +3006,16 @@ extern "C" int pbrt_gpu_counters(pbrt_gpu_ctx* c, uint64_t* out, int n) {
                                       (uint64_t)ctr.any_panic, ctr.windows, ctr.phase[0], ctr.phase[1],
                                       ctr.phase[2], ctr.phase[3], ctr.phase[4], ctr.phase[5],
                                       ctr.phase[6], ctr.phase[7]};
-    for (int i = 0; i < n && i < kNumCounters; i++) out[i] = v[i];
+    for (int i = 0; i < n && i < kNumCounters; i++) out[i] = i < 14 ? v[i] : (uint64_t)ctr.dhist[i - 14];
     return kNumCounters;
+}
+
+extern "C" int64_t pbrt_gpu_tile_ticks(pbrt_gpu_ctx* c, uint32_t* out, int64_t n, int64_t* heavy) {
+    if (!c) return -PBRT_E_INVALID;
+    if (heavy) *heavy = c->last_heavy;
+    const int64_t m = (int64_t)c->h_last_ticks.size();
+    for (int64_t i = 0; out && i < n && i < m; i++) out[i] = c->h_last_ticks[(size_t)i];
+    return m;
 }
 
 // Region cycles of trajectory steps (PBRT_STEP_TIMING builds only; else zeros):

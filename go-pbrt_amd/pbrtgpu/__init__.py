@@ -61,6 +61,9 @@ def lib():
     L.pbrt_gpu_destroy.argtypes = [C.c_void_p]
     L.pbrt_gpu_destroy.restype = None
     L.pbrt_film_to_rgba8.argtypes = [P(d), i64, i64, P(C.c_uint8)]
+    L.pbrt_gpu_tile_ticks.argtypes = [C.c_void_p, P(C.c_uint32), i64, P(i64)]
+    L.pbrt_gpu_tile_ticks.restype = i64
+    L.pbrt_gpu_counters.argtypes = [C.c_void_p, P(C.c_uint64), C.c_int]
     for name in ("pbrt_translate", "pbrt_scale"):
         getattr(L, name).argtypes = [d, d, d, T]
         getattr(L, name).restype = None
@@ -324,6 +327,21 @@ class Renderer:
 
     def stream(self):
         return lib().pbrt_gpu_stream(self.h)
+
+    def tile_ticks(self):
+        """(per-slot chain ticks of the last EXACT frame at 100 MHz, heavy slots of its split)."""
+        heavy = C.c_int64(0)
+        n = lib().pbrt_gpu_tile_ticks(self.h, None, 0, C.byref(heavy))
+        out = np.zeros(max(n, 0), dtype=np.uint32)
+        if n > 0:
+            lib().pbrt_gpu_tile_ticks(self.h, out.ctypes.data_as(C.POINTER(C.c_uint32)), n, C.byref(heavy))
+        return out, int(heavy.value)
+
+    def counters(self):
+        """pbrt_gpu_counters of the last render (include/pbrt_diag.h order)."""
+        out = np.zeros(128, dtype=np.uint64)
+        n = lib().pbrt_gpu_counters(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), 128)
+        return out[:max(n, 0)]
 
     def intersect(self, rays):
         """rays: (n,7) [ox,oy,oz,dx,dy,dz,tmax] -> (n,9) like the oracle."""

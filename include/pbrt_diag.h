@@ -49,10 +49,18 @@ int pbrt_gpu_probe(int device, int op, const double* in, size_t n, int in_stride
  * paths, camera_samples, closest_rays, shadow_rays, any_panic, windows
  * (WAVE kernel speculation rounds), then lane-0 clock64 cycles summed over
  * tiles in: StartPixel swaps, bounce 1, speculative trajectories, full paths,
- * film add, StartPixel draws, chain walk, (spare).
+ * film add, StartPixel draws, chain walk, (spare); then 64 bins of the
+ * continuous-issue chain's on-chain draw counts D (bin D/2, last bin >= 126).
  * Returns the number of counters available. */
 struct pbrt_gpu_ctx;
 int pbrt_gpu_counters(struct pbrt_gpu_ctx* ctx, uint64_t* out, int n);
+
+/* Per-slot chain time of the last EXACT continuous-issue frame (wall_clock64
+ * ticks at 100 MHz, slot i = tile tile_begin + i * tile_stride), the input of
+ * the next frame's heaviest-first schedule. Copies min(n, slots) values and
+ * returns the slot count (0 if the last frame recorded none). *heavy = tiles of
+ * the last launch that ran at 4 waves in the heavy/light split (0: no split). */
+int64_t pbrt_gpu_tile_ticks(struct pbrt_gpu_ctx* ctx, uint32_t* out, int64_t n, int64_t* heavy);
 
 /* Region cycles inside path steps, summed over waves (only in libraries built
  * with -DPBRT_STEP_TIMING; zeros otherwise). Returns the count (8). */

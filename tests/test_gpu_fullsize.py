@@ -1,0 +1,79 @@
+"""BASELINE configs B and C at their full size, through the C ABI.
+
+Config B (README scene, 1920x1080, Stratified(8,8), Path(10)): the WHOLE frame
+against the oracle -- per-pixel RMS of the fp64 XYZ film and the fraction of
+bit-identical tiles (BASELINE.md:47-48), both at their exact-parity values.
+
+Config C (Cornell, 1920x1080, Stratified(16,16) = 255 traced paths/px,
+Path(maxDepth 8); SURVEY 8(d), internal/render/server.go:142 for the
+sampler): full-frame properties, and a bit-exact oracle check of the first,
+middle and last tiles plus the frame's heaviest tiles by measured chain time.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import pbrtgpu as G
+from pbrtgpu import abi
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+THREADS = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1))
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint64)
+
+
+def tile_parity(film, ofilm, tile=16):
+    """(per-pixel RMS over the XYZ film, fraction of tiles whose pixels are bit-identical)."""
+    rms = float(np.sqrt(np.mean((film - ofilm) ** 2)))
+    H, W, _ = film.shape
+    same = (bits(film) == bits(ofilm)).all(axis=2)
+    ok = n = 0
+    for y in range(0, H, tile):
+        for x in range(0, W, tile):
+            n += 1
+            ok += bool(same[y:y + tile, x:x + tile].all())
+    return rms, ok / n
+
+
+def test_config_B_whole_frame_vs_oracle():
+    scene = G.Scene.readme(1920, 1080)
+    rd = abi.render_desc(8, 8)
+    with G.Renderer(scene) as r:
+        film, st = r.render(rd)
+    assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
+    assert st.tiles_rendered == 8160 and st.paths_traced == 1920 * 1080 * 63
+    rc, ofilm, ost = O.render(scene.desc, rd, threads=THREADS)
+    assert rc == 0 and ost.paths == st.paths_traced
+    rms, frac = tile_parity(film, ofilm)
+    print(f"config B whole frame: rms {rms:.3e}, bit-identical tiles {frac:.6f}")
+    assert rms == 0.0 and frac == 1.0, (rms, frac)
+    assert np.array_equal(bits(film), bits(ofilm))
+
+
+def test_config_C_full_size_properties_and_heaviest_tiles():
+    W, H = 1920, 1080
+    scene = G.Scene.cornell(W, H)
+    rd = abi.render_desc(16, 16, max_depth=8)
+    with G.Renderer(scene) as r:
+        film, st = r.render(rd)
+        ticks, _ = r.tile_ticks()
+    assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
+    assert st.tiles_rendered == 8160 and st.paths_traced == W * H * 255
+    assert st.batches == 1
+    assert np.isfinite(film).all() and (film >= 0).all() and film.max() > 0
+    assert len(ticks) == 8160 and ticks.min() > 0
+    heaviest = [int(t) for t in np.argsort(ticks)[::-1][:3]]
+    tiles = sorted({0, 4080, 8159, *heaviest})
+    for t in tiles:
+        one = abi.render_desc(16, 16, max_depth=8, tile_begin=t, tile_end=t + 1)
+        with G.Renderer(scene) as r:
+            g, _ = r.render(one)
+        rc, o, _ = O.render(scene.desc, one, threads=1)
+        assert rc == 0
+        assert np.array_equal(bits(g), bits(o)), t
+    print(f"config C: bit-exact tiles {tiles} (heaviest by chain time: {heaviest})")

@@ -403,6 +403,7 @@ def test_wave_ci_heaviest_first_schedule_keeps_bits(ci_waves, monkeypatch):
 @pytest.mark.parametrize("heavy", ["3", "12"])
 @pytest.mark.parametrize("ci_waves", ["2", "4"])
 def test_wave_ci_heavy_light_split_keeps_bits(ci_waves, heavy, monkeypatch):
+    heavy_env = heavy
     """Shard mode: from the second frame the heaviest tiles run at 4 waves in
     one launch and the rest at 1 wave in a concurrent launch on a second
     stream; only the schedule changes."""
@@ -414,10 +415,30 @@ def test_wave_ci_heavy_light_split_keeps_bits(ci_waves, heavy, monkeypatch):
     with G.Renderer(scene, kernel="wave_ci") as r:
         for rd in rds:
             ofilm, _ = oracle_render(scene, rd)
-            for _ in range(3):
+            for frame in range(3):
                 film, st = r.render(rd)
                 assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
                 assert same_bits(film, ofilm)
+                ticks, heavy = r.tile_ticks()
+                assert len(ticks) == st.tiles_rendered and ticks.min() > 0
+                # the split runs from the second frame on (the first has no schedule yet)
+                assert (heavy > 0) == (frame > 0 and int(heavy_env) < st.tiles_rendered), (frame, heavy)
+
+
+def test_wave_ci_split_default_heuristic_on_a_quarter_shard():
+    """Without PBRT_CI_HEAVY: a 1/4 shard of the 1080p frame (2040 tiles, 4
+    waves per tile) gets the heavy/light split from its second frame; bits
+    stay the oracle's."""
+    scene = G.Scene.readme(1920, 1080)
+    rd = abi.render_desc(2, 2, tile_begin=1, tile_stride=4)
+    ofilm, _ = oracle_render(scene, rd)
+    with G.Renderer(scene) as r:
+        for frame in range(3):
+            film, st = r.render(rd)
+            assert st.kernel == abi.PBRT_KERNEL_WAVE_CI and st.tiles_rendered == 2040
+            assert same_bits(film, ofilm)
+            _, heavy = r.tile_ticks()
+            assert (heavy > 0) == (frame > 0), (frame, heavy)
 
 
 @pytest.mark.parametrize("ci_waves", ["1", "4"])
