@@ -38,9 +38,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--config", default="B", choices=["B", "C"],
+    ap.add_argument("--config", default="B", choices=["B", "C", "D"],
                     help="BASELINE config: B = README sphere scene, Stratified(8,8), Path(10); "
-                         "C = Cornell (SURVEY 8(d)), Stratified(16,16), Path(8)")
+                         "C = Cornell (SURVEY 8(d)), Stratified(16,16), Path(8); "
+                         "D = 999 698-triangle height field (extension), Stratified(8,8), Path(10)")
     ap.add_argument("--spp", type=int, default=0, help="Stratified(spp, spp) (0 = the config's)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "serial", "wave", "wavefront", "wave_ci"])
     ap.add_argument("--tiles-per-wave", type=int, default=0, help="k_chain lane groups per wave (0 = library default)")
@@ -88,7 +89,7 @@ def host_cpu():
     return {"nproc": nproc, "affinity": affinity, "share": share, "cpu_model": model}
 
 
-def cpu_baseline(args, scene_name, rd_kwargs):
+def cpu_baseline(args, scene_name, rd_kwargs, product_scene=None):
     """The oracle (C restatement of the Go path, oracle/) on the same frame's
     tiles, on this box's host cores: the whole frame when it fits the budget,
     else an evenly spread tile sample (bit-reversed stride-64 batches, so every
@@ -99,7 +100,10 @@ def cpu_baseline(args, scene_name, rd_kwargs):
 
     cpu = host_cpu()
     threads = args.cpu_threads or cpu["share"]
-    sc = (O.OracleScene.readme if scene_name == "readme" else O.OracleScene.cornell)(args.width, args.height)
+    if scene_name == "heightfield":   # the fixture is data: the oracle renders the product-built descriptor
+        sc = product_scene
+    else:
+        sc = (O.OracleScene.readme if scene_name == "readme" else O.OracleScene.cornell)(args.width, args.height)
     n_tiles = int(O.lib().oracle_num_tiles(sc.desc, abi.render_desc(**rd_kwargs)))
     stride = 64
     offsets = [int(format(i, "06b")[::-1], 2) for i in range(stride)]
@@ -181,7 +185,46 @@ CONFIGS = {
     "C": dict(scene="cornell", spp=16, max_depth=8,
               text="Cornell 6 disks + 2 spheres {W}x{H}, Stratified({S},{S}) = {T} traced paths/px, "
                    "Path(maxDepth 8, rr 1, Uniform), tile 16"),
+    # BASELINE.json configs[3] on one GPU: the triangle extension (include/pbrt_scene.h)
+    "D": dict(scene="heightfield", quads=707, spp=8, max_depth=10,
+              text="height field 999698 triangles (device LBVH) + README lights/camera {W}x{H}, "
+                   "Stratified({S},{S}) = {T} traced paths/px, Path(maxDepth 10, rr 1, Uniform), tile 16"),
 }
+
+
+def make_scene(G, cfg, W, H):
+    if cfg["scene"] == "readme":
+        return G.Scene.readme(W, H)
+    if cfg["scene"] == "cornell":
+        return G.Scene.cornell(W, H)
+    return G.Scene.heightfield(W, H, quads=cfg["quads"], seed=1)
+
+
+def mesh_roofline(cfg, W, H, S, mode, stats_ms):
+    """HBM roofline of the mesh traversal: the kernel's algorithmic bytes per
+    launch (nodes x 32 B + triangles x 36 B, counted once by
+    tools/count_mesh_bytes.py into profiles/meshbytes_*.json) over its
+    duration measured here with HIP events; the dominant of k_chain_ci /
+    k_paths_ci by time."""
+    mb = load_json(os.path.join(REPO, "profiles", f"meshbytes_heightfield{cfg['quads']}_{W}x{H}_s{S}x{S}_{mode}.json"))
+    if not mb:
+        return None
+    pmc = load_json(os.path.join(REPO, "profiles", f"pmc_heightfield{cfg['quads']}_{W}x{H}_s{S}x{S}.json")) or {}
+    cand = [("k_chain_ci", stats_ms["chain"]), ("k_paths_ci", stats_ms["paths"])] if mode == "exact" else \
+        [("k_paths_ci_mb", stats_ms["paths"])]
+    name, ms = max(cand, key=lambda x: x[1])
+    k = mb["kernels"].get(name)
+    if not k or ms <= 0:
+        return None
+    achieved = k["bytes_per_launch"] / (ms / 1e3) / 1e9
+    traffic = (pmc.get(name.replace("_mb", "")) or {}).get("hbm_bytes_per_launch")
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": name, "kernel_ms": ms,
+            "bytes_per_launch": k["bytes_per_launch"],
+            "per_walk": {q: {"nodes": k[q]["nodes_per_walk"], "triangles": k[q]["triangles_per_walk"]}
+                         for q in ("closest", "any") if q in k},
+            "pipeline": {"kernels_ms": stats_ms["kernels"], "k_chain_ms": stats_ms["chain"],
+                         "k_paths_ms": stats_ms["paths"]}}
 
 
 def main():
@@ -204,7 +247,7 @@ def main():
     W, H = args.width, args.height
     S = args.spp or cfg["spp"]
     rd_kwargs = dict(spp_x=S, spp_y=S, max_depth=cfg["max_depth"])
-    scene = (G.Scene.readme if cfg["scene"] == "readme" else G.Scene.cornell)(W, H)
+    scene = make_scene(G, cfg, W, H)
     # the renderer (and its two HIP streams) before RCCL's own streams, so the
     # heavy/light chain launches get hardware queues of their own
     renderer = G.Renderer(scene, device=local, kernel=args.kernel, lanes_per_wave=args.tiles_per_wave,
@@ -287,8 +330,11 @@ def main():
 
     if rank == 0:
         value = paths_total / elapsed / 1e6
-        roof = roofline(cfg["scene"], W, H, S, paths_local / len(stats), kernel_kind, kern_ms, chain_ms, paths_ms,
-                        merge_ms, args.mode)
+        if cfg["scene"] == "heightfield":
+            roof = mesh_roofline(cfg, W, H, S, args.mode, {"chain": chain_ms, "paths": paths_ms, "kernels": kern_ms})
+        else:
+            roof = roofline(cfg["scene"], W, H, S, paths_local / len(stats), kernel_kind, kern_ms, chain_ms,
+                            paths_ms, merge_ms, args.mode)
         out = {
             "metric": METRIC,
             "value": value,
@@ -301,8 +347,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": f"synthetic (the reference's hard-coded {'README' if cfg['scene'] == 'readme' else 'Cornell'} "
-                    "scene; no external data)",
+            "data": {"readme": "synthetic (the reference's hard-coded README scene; no external data)",
+                     "cornell": "synthetic (SURVEY 8(d) Cornell fixture built from reference types)",
+                     "heightfield": "synthetic (procedural height field, seed 1; triangle extension)"}[cfg["scene"]],
             "config": {
                 "workload": cfg["text"].format(W=W, H=H, S=S, T=S * S - 1) + ", "
                             + ("EXACT per-tile RNG" if args.mode == "exact" else "THROUGHPUT per-path RNG"),
@@ -319,7 +366,7 @@ def main():
         if side:
             out["side_mode"] = side
         if not args.no_cpu_baseline and world == 1:
-            cb = cpu_baseline(args, cfg["scene"], rd_kwargs)
+            cb = cpu_baseline(args, cfg["scene"], rd_kwargs, scene)
             cb["gpu_over_cpu"] = value / cb["value"]
             out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)

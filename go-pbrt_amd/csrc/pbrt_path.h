@@ -17,6 +17,7 @@
 #pragma clang fp contract(off)
 
 #include "pbrt_core.h"
+#include "pbrt_mesh.h"
 
 namespace pbrt {
 
@@ -54,6 +55,7 @@ struct DevScene {
     int n_prims, n_nodes, n_lights;
     int use_lds_nodes;   // the kernel staged nodes[] in g_nodes_lds (uniform)
     int n_leaves;        // leaves of the BVH (order[8 * n_nodes + oct * n_nodes + j]: leaf preorder)
+    DevMesh mesh;        // triangle meshes (extension, pbrt_mesh.h); mesh.n_nodes == 0: none
 };
 
 // ---------------------------------------------------------------- PCG32 (rng.go)
@@ -339,9 +341,55 @@ __device__ inline bool prim_hit_t(const DevScene& sc, int pi, const Ray& r, doub
     return shape_hit(p.shape, ray, t_hit, ph, panic);
 }
 
+// Mesh of global triangle index g (meshes are few: a linear scan)
+__device__ __forceinline__ int tri_mesh(const DevScene& sc, int32_t g) {
+    int m = 0;
+    while (m + 1 < sc.mesh.n_meshes && sc.mesh.mesh_first[m + 1] <= g) m++;
+    return m;
+}
+// The triangle of leaf slot `slot` hit by r (extension): pbrt-v3
+// Triangle::Intersect's interaction part with the default uv (0,0), (1,0),
+// (1,1) -- dpdu = dp12 - dp02, dpdv = -dp12 (uv determinant exactly 1) -- and
+// go-pbrt's normalized wo; oracle/oracle_render.c tri_si states the same.
+// The barycentrics come from re-running the (deterministic) hit test.
+__device__ inline void mesh_si(const DevScene& sc, int32_t slot, const Ray& r, SI& si) {
+    double v[9], t, b0 = 0, b1 = 0, b2 = 0;
+    load_tri(sc.mesh.tris, (uint32_t)slot, v);
+    (void)tri_hit(v, r, t, b0, b1, b2);
+    const int32_t g = sc.mesh.gid[slot];
+    const V3 p0{v[0], v[1], v[2]}, p1{v[3], v[4], v[5]}, p2{v[6], v[7], v[8]};
+    const V3 dp02 = p0 - p2, dp12 = p1 - p2;
+    V3 dpdu = dp12 - dp02;
+    V3 dpdv{-dp12.x, -dp12.y, -dp12.z};
+    if (len2(cross(dpdu, dpdv)) == 0) {
+        const V3 nn = normalized(cross(p2 - p0, p1 - p0));
+        coordinate_system(nn, dpdu, dpdv);
+    }
+    const V3 p{b0 * p0.x + b1 * p1.x + b2 * p2.x, b0 * p0.y + b1 * p1.y + b2 * p2.y,
+               b0 * p0.z + b1 * p1.z + b2 * p2.z};
+    const V3 err{gomath::abs(b0 * p0.x) + gomath::abs(b1 * p1.x) + gomath::abs(b2 * p2.x),
+                 gomath::abs(b0 * p0.y) + gomath::abs(b1 * p1.y) + gomath::abs(b2 * p2.y),
+                 gomath::abs(b0 * p0.z) + gomath::abs(b1 * p1.z) + gomath::abs(b2 * p2.z)};
+    V3 n = normalized(cross(dp02, dp12));
+    if (sc.mesh.mesh_rev[tri_mesh(sc, g)]) n = V3{-n.x, -n.y, -n.z};
+    si.p = p;
+    si.perr = muls(err, tri_gamma(7));
+    si.n = n;
+    si.wo = normalized(V3{-r.d.x, -r.d.y, -r.d.z});
+    si.time = r.time;
+    si.sn = n;
+    si.sdpdu = dpdu;
+    si.prim = sc.n_prims + g;
+}
+
 // GeometricPrimitive / TransformedPrimitive (primitive.go:42-115): the
 // interaction of primitive pi at its accepted hit point ph (shape space).
+// pi >= n_prims: leaf slot pi - n_prims of the meshes (mesh_si).
 __device__ inline void prim_si(const DevScene& sc, int pi, const Ray& r, V3 ph, SI& si) {
+    if (pi >= sc.n_prims) {
+        mesh_si(sc, pi - sc.n_prims, r, si);
+        return;
+    }
     const DevPrim& p = sc.fprims[pi];
     const bool xformed = p.kind == PBRT_PRIM_TRANSFORMED;
     Ray ray = r;
@@ -484,7 +532,8 @@ __device__ __forceinline__ int leaf_prims(const DevScene& sc, uint32_t first, ui
 // A walks interior nodes until the lane reaches a leaf whose box it hits,
 // loop B tests that leaf's primitives.
 template <bool kAny, int kStride = kStackStride>
-__device__ inline bool bvh_walk(const DevScene& sc, Ray& ray, uint16_t* stack, int& panic, int& best, V3& best_ph) {
+__device__ inline bool bvh_walk_analytic(const DevScene& sc, Ray& ray, uint16_t* stack, int& panic, int& best,
+                                         V3& best_ph) {
     best = -1;
     const int n = sc.n_nodes;
     if (n == 0) return false;
@@ -573,6 +622,23 @@ __device__ inline bool bvh_walk(const DevScene& sc, Ray& ray, uint16_t* stack, i
     return best >= 0;
 }
 
+// The scene's aggregate: the reference BVH over the analytic primitives, then
+// the triangle meshes (extension) with the TMax it left; a triangle wins only
+// with a strictly smaller t, so an analytic primitive keeps a tie. A mesh hit
+// is reported as best = n_prims + its leaf slot.
+template <bool kAny, int kStride = kStackStride>
+__device__ inline bool bvh_walk(const DevScene& sc, Ray& ray, uint16_t* stack, int& panic, int& best, V3& best_ph) {
+    const bool hit = bvh_walk_analytic<kAny, kStride>(sc, ray, stack, panic, best, best_ph);
+    if (sc.mesh.n_nodes == 0 || panic || (kAny && hit)) return hit;
+    double tm = ray.tmax;
+    int32_t slot = -1, gid = -1;
+    if (!mesh_walk<kAny>(sc.mesh, ray, tm, slot, gid)) return hit;
+    if (kAny) return true;
+    ray.tmax = tm;
+    best = sc.n_prims + slot;
+    return true;
+}
+
 template <bool kAny>
 __device__ inline bool bvh_traverse(const DevScene& sc, Ray& ray, SI* si, uint16_t* stack, int& panic) {
     int best;
@@ -598,7 +664,9 @@ __device__ __forceinline__ double inv_pi() { return 1.0 / gomath::kPi; }   // pk
 // MatteMaterial.ComputeScatteringFunctions (matte.go:21-37) + NewBSDF
 // (reflection.go:128-140) + Checkerboard2D/PlanarMapping2D (checkerboard.go:30-40)
 __device__ inline int compute_bsdf(const DevScene& sc, const SI& si, BSDF& b) {
-    const pbrt_material_desc& m = sc.materials[sc.prims[si.prim].material];
+    const pbrt_material_desc& m =
+        sc.materials[si.prim < sc.n_prims ? sc.prims[si.prim].material
+                                          : sc.mesh.mesh_mat[tri_mesh(sc, si.prim - sc.n_prims)]];
     b.ns = si.sn;
     b.ng = si.n;
     b.ss = normalized(si.sdpdu);

@@ -29,6 +29,7 @@
 
 #include "../../include/pbrt_gpu.h"
 #include "../../include/pbrt_scene.h"
+#include "mesh_bvh.h"
 #include "pbrt_spec.h"
 
 using namespace pbrt;
@@ -293,7 +294,8 @@ struct WaveBufs {
 };
 struct ChainLayout {   // byte offsets into k_chain's dynamic LDS block
     int s1d, other, sbuf, dbuf, vbuf, total;
-    int ring;   // k_chain_ci: offset ring after the StartPixel staging (no sbuf / dbuf)
+    int ring;      // k_chain_ci: offset ring after the StartPixel staging (no sbuf / dbuf)
+    int staging;   // k_chain_ci: bytes of the StartPixel staging (s1d, other, vbuf)
 };
 constexpr uint32_t kBadD = 0xFFFFFFFFu;
 constexpr int kCiRingBytes = 4 * 1024;   // k_chain_ci offset ring (all lane groups of a wave)
@@ -1574,6 +1576,10 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
                 const uint64_t S1 = start_pixel_wave(rp, J, gs[q].S, incq, s1d, other, vbuf, &sh_state);
                 double* gs1d = wb.s1d + rec * wb.s1d_stride;
                 for (int idx = tid; idx < ndims * n; idx += kT) gs1d[idx] = s1d[idx];
+                // the first traced sample's camera time value (read before the ring
+                // clear: with one tile per workgroup the StartPixel staging aliases the ring)
+                const double time_u = s1d[1 < n ? 1 : 0];
+                __syncthreads();
                 RingEnt* rq = (RingEnt*)(lds + lay.ring) + (size_t)q * R;
                 for (uint32_t i = (uint32_t)tid; i < R; i += kT) rq[i].tag = kNoOff;
                 // bounce 1 (camera ray, first hit, BSDF) was computed for every
@@ -1582,7 +1588,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
                 const int hit0 = pr.hit, panic0 = pr.panic0;
                 if (tid == 0) {
                     if (hit0)   // the camera ray's time (Get1D after pFilm, pLens) of the pixel's first traced sample
-                        pr.si.time = camera_ray(cam, (double)px, (double)py, s1d[1 < n ? 1 : 0], V2{0.0, 0.0}).time;
+                        pr.si.time = camera_ray(cam, (double)px, (double)py, time_u, V2{0.0, 0.0}).time;
                     pcs[q].si = pr.si;
                     pcs[q].b = pr.b;
                     pcs[q].wo = pr.wo;
@@ -1840,6 +1846,7 @@ struct pbrt_gpu_ctx {
     // the main stream, the rest on stream2, concurrently
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_split = nullptr, ev_join = nullptr;
+    MeshBuild mesh;                      // triangle meshes + their LBVH (extension)
     int64_t heavy_k = 0;                 // slots at the front of h_slot_order that get 4 waves
     int64_t last_heavy = 0;              // heavy slots of the last EXACT launch (0: no split)
     std::vector<uint32_t> h_last_ticks;  // per-slot chain ticks of the last EXACT frame
@@ -1964,6 +1971,16 @@ DevScene dev_scene(const pbrt_gpu_ctx* c, bool with_dist) {
     s.use_lds_nodes = 0;
     s.n_leaves = 0;
     for (int i = 0; i < c->host_scene.n_nodes; i++) s.n_leaves += c->h_node_prims[i] > 0;
+    s.mesh = c->mesh.view();
+    return s;
+}
+
+// The scene view a launch passes, tagged with its kernel's counter set for
+// the mesh-traversal counting build (PBRT_MESH_COUNT; ignored otherwise):
+// 1 k_wf_primary, 2 k_chain_ci / k_chain, 3 k_paths(_ci) EXACT, 4 k_mb_setup,
+// 5 k_paths(_ci) THROUGHPUT, 6 k_render_exact, 7 k_intersect.
+DevScene with_slot(DevScene s, int slot) {
+    s.mesh.count_slot = slot;
     return s;
 }
 
@@ -2062,6 +2079,15 @@ int validate_scene(const pbrt_scene_desc* s) {
         if (n.n_prims > 0 && (int64_t)n.offset + n.n_prims > s->n_prims) return PBRT_E_INVALID;
         if (n.n_prims == 0 && (n.offset >= (uint32_t)s->n_nodes || n.axis > 2)) return PBRT_E_INVALID;
     }
+    if (s->n_meshes < 0 || (s->n_meshes > 0 && !s->meshes)) return PBRT_E_INVALID;
+    for (int i = 0; i < s->n_meshes; i++) {
+        const pbrt_mesh_desc& m = s->meshes[i];
+        if (m.n_vertices < 0 || m.n_triangles < 0 || m.material < 0 || m.material >= s->n_materials ||
+            (m.n_triangles > 0 && (!m.p || !m.indices)))
+            return PBRT_E_INVALID;
+        for (int64_t k = 0; k < 3 * (int64_t)m.n_triangles; k++)
+            if (m.indices[k] < 0 || m.indices[k] >= m.n_vertices) return PBRT_E_INVALID;
+    }
     for (int i = 0; i < s->n_lights; i++) {
         const pbrt_light_desc& l = s->lights[i];
         if (l.type < PBRT_LIGHT_POINT || l.type > PBRT_LIGHT_DIFFUSE_AREA) return PBRT_E_UNSUPPORTED;
@@ -2124,9 +2150,26 @@ bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Rend
     Lci.other = put(nd * n * 2);
     Lci.sbuf = Lci.dbuf = 0;
     Lci.vbuf = put(rp.sp_serial ? 4 : (int64_t)rp.sp_draws * 4);
+    Lci.staging = (int)off;
     Lci.ring = put(kCiRingBytes);
     Lci.total = (int)off;
     return L.total <= 48 * 1024;
+}
+
+// k_chain_ci's LDS layout for w waves per tile and G tiles per wave. With one
+// tile per workgroup (G == 1) the StartPixel staging aliases the offset ring:
+// a group starts a pixel only after its chain has dropped every candidate,
+// so the two are never live together (config C, 256 spp: 19 KB of staging).
+ChainLayout ci_layout(const ChainLayout& base, int w, int G, unsigned& lds_bytes) {
+    ChainLayout l = base;
+    if (G == 1) {
+        l.ring = 0;
+        lds_bytes = (unsigned)std::max(base.staging, w * kCiRingBytes);
+    } else {
+        lds_bytes = (unsigned)(base.total + (w - 1) * kCiRingBytes);
+    }
+    l.total = (int)lds_bytes;
+    return l;
 }
 
 // Waves per tile of k_chain_ci for a launch of nb tiles. The frame's EXACT
@@ -2186,14 +2229,19 @@ uint64_t schedule_key(const RenderParams& rp, int kw) {
 // Returns the pixels per wave (2, 4 or 8; PBRT_PATHS_CI overrides, 0 = off).
 int paths_ci_pixels(const pbrt_gpu_ctx* c, const RenderParams& rp) {
     int pp = 4;
+    bool forced = false;
     if (const char* e = getenv("PBRT_PATHS_CI")) {
         const int v = atoi(e);
         if (v == 0) return 0;
-        if (v == 2 || v == 4 || v == 8) pp = v;
+        if (v == 2 || v == 4 || v == 8) pp = v, forced = true;
     }
-    const bool fits = c->host_scene.n_nodes <= kLdsNodes && pp * c->host_scene.n_lights <= kWave &&
-                      (int64_t)pp * rp.ndims * rp.spp * 8 <= 16 * 1024;
-    return fits ? pp : 0;
+    auto fits = [&](int p) {
+        return c->host_scene.n_nodes <= kLdsNodes && p * c->host_scene.n_lights <= kWave &&
+               (int64_t)p * rp.ndims * rp.spp * 8 <= 16 * 1024;
+    };
+    if (forced) return fits(pp) ? pp : 0;
+    // 4 pixels per wave where their stratified values fit, else 2 (config C, 256 spp)
+    return fits(4) ? 4 : fits(2) ? 2 : 0;
 }
 
 // Carve the per-batch buffers of the wave path. Budget: PBRT_WAVE_BUFFER_GB,
@@ -2406,7 +2454,10 @@ int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
          c->kernel_req == PBRT_KERNEL_WAVE_CI) && !c->use_spec)
         return set_err(c, PBRT_E_UNSUPPORTED, "render not eligible for the wave-parallel kernels");
     c->use_wf = c->use_spec && c->kernel_req == PBRT_KERNEL_WAVEFRONT;
-    const bool ci_fits = c->host_scene.n_nodes <= kLdsNodes && c->lay_ci.total <= 12 * 1024;
+    // (dynamic LDS of one 1-wave tile, staging aliased with the ring: <= 20 KB keeps
+    // 5+ workgroups per CU; config C at 256 spp needs 19.3 KB)
+    const bool ci_fits = c->host_scene.n_nodes <= kLdsNodes &&
+                         std::max(c->lay_ci.staging, kCiRingBytes) <= 20 * 1024;
     // AUTO: the continuous-issue chain wherever it fits (measured ~8% faster
     // than the window chain on config B), else the window chain
     c->use_ci = c->use_spec && (c->kernel_req == PBRT_KERNEL_WAVE_CI ||
@@ -2515,6 +2566,15 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
         pbrt_gpu_destroy(c);
         return rc;
     }
+    if (scene->n_meshes > 0) {   // triangle meshes: LBVH built on the device (mesh_bvh.hip)
+        std::string err;
+        rc = mesh_bvh_build(scene, c->stream, c->mesh, err);
+        if (rc != PBRT_OK) {
+            pbrt_gpu_destroy(c);
+            return rc;
+        }
+    }
+    c->host_scene.meshes = nullptr;
     *out = c;
     return PBRT_OK;
 }
@@ -2562,7 +2622,7 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                     if (rcc != PBRT_OK) return rcc;
                 } else if (c->use_ci) {
                     hipLaunchKernelGGL(k_wf_primary, dim3((unsigned)((nb * c->wb.ppt + kWave - 1) / kWave)),
-                                       dim3(kWave), 0, c->stream, sc, rp, c->wb, sb, nb);
+                                       dim3(kWave), 0, c->stream, with_slot(sc, 1), rp, c->wb, sb, nb);
                     const int kw = ci_waves(c, nb);
                     const uint32_t* order = nullptr;
                     uint32_t* ticks = nullptr;
@@ -2591,15 +2651,18 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                     auto launch_ci = [&](int w, int64_t n, const uint32_t* ord, hipStream_t st) {
                         if (w > 1) {   // one tile per workgroup of w waves; the ring grows with the lanes
                             const int ring = w * kCiRingBytes / (int)sizeof(RingEnt);
-                            const unsigned lds = (unsigned)(c->lay_ci.total + (w - 1) * kCiRingBytes);
+                            unsigned lds = 0;
+                            const ChainLayout lw = ci_layout(c->lay_ci, w, 1, lds);
                             auto kern = w == 2 ? k_chain_ci<2> : k_chain_ci<4>;
-                            hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3(kWave * w), lds, st, sc, rp, c->lay_ci,
+                            hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3(kWave * w), lds, st, with_slot(sc, 2), rp, lw,
                                                c->d_jump, c->wb, sb, nb, kWave * w, ring, c->d_ctr, ord, ticks);
                         } else {
                             const int Gc = std::min(G, kCiMaxGroups);
                             const int ring = kCiRingBytes / (int)sizeof(RingEnt) / Gc;
+                            unsigned lds = 0;
+                            const ChainLayout lw = ci_layout(c->lay_ci, 1, Gc, lds);
                             hipLaunchKernelGGL(k_chain_ci<1>, dim3((unsigned)((n + Gc - 1) / Gc)), dim3(kWave),
-                                               (unsigned)c->lay_ci.total, st, sc, rp, c->lay_ci, c->d_jump, c->wb, sb,
+                                               lds, st, with_slot(sc, 2), rp, lw, c->d_jump, c->wb, sb,
                                                nb, kWave / Gc, ring, c->d_ctr, Gc == 1 ? ord : nullptr,
                                                Gc == 1 ? ticks : nullptr);
                         }
@@ -2633,7 +2696,7 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                     }
                 } else {
                     hipLaunchKernelGGL(k_wf_primary, dim3((unsigned)((nb * c->wb.ppt + kWave - 1) / kWave)),
-                                       dim3(kWave), 0, c->stream, sc, rp, c->wb, sb, nb);
+                                       dim3(kWave), 0, c->stream, with_slot(sc, 1), rp, c->wb, sb, nb);
                     hipLaunchKernelGGL(chain, dim3((unsigned)((nb + G - 1) / G)), dim3(kWave),
                                        (unsigned)(c->lay.total + G * (int)sizeof(ChainCache)), c->stream, sc, rp,
                                        c->lay, c->d_jump, c->wb, sb, nb, kWave / G, c->d_ctr);
@@ -2642,25 +2705,30 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                 if (rp.mode == PBRT_MODE_THROUGHPUT && paths_ci_pixels(c, rp) > 0) {
                     // setup (StartPixel + bounce 1 per pixel), then lane-refill paths
                     hipLaunchKernelGGL(k_mb_setup, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
-                                       (unsigned)c->lay.total, c->stream, sc, rp, c->lay, c->d_jump, c->wb, sb, nb);
-                    hipLaunchKernelGGL((k_paths_ci<4, true>), dim3((unsigned)((nb * c->wb.ppt + 3) / 4)),
-                                       dim3(kWave), (unsigned)paths_group_lds<4>(rp.ndims * rp.spp), c->stream, sc,
-                                       rp, c->wb, sb, nb * c->wb.ppt, c->d_ctr);
+                                       (unsigned)c->lay.total, c->stream, with_slot(sc, 4), rp, c->lay, c->d_jump, c->wb, sb, nb);
+                    const int pp = paths_ci_pixels(c, rp) >= 4 ? 4 : 2;
+                    auto kern = pp == 4 ? k_paths_ci<4, true> : k_paths_ci<2, true>;
+                    const int lds = pp == 4 ? paths_group_lds<4>(rp.ndims * rp.spp)
+                                            : paths_group_lds<2>(rp.ndims * rp.spp);
+                    hipLaunchKernelGGL(kern, dim3((unsigned)((nb * c->wb.ppt + pp - 1) / pp)), dim3(kWave),
+                                       (unsigned)lds, c->stream, with_slot(sc, 5), rp, c->wb, sb, nb * c->wb.ppt,
+                                       c->d_ctr);
                 } else if (rp.mode == PBRT_MODE_THROUGHPUT)
                     hipLaunchKernelGGL((k_paths<true, kPathsWaves>), dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
-                                       (unsigned)c->lay.total, c->stream, sc, rp, c->lay, c->d_jump, c->wb, sb, nb,
-                                       c->d_ctr);
+                                       (unsigned)c->lay.total, c->stream, with_slot(sc, 5), rp, c->lay, c->d_jump, c->wb, sb,
+                                       nb, c->d_ctr);
                 else if (const int pp = paths_ci_pixels(c, rp)) {
                     const int per = rp.ndims * rp.spp;
                     auto kern = pp == 8 ? k_paths_ci<8> : pp == 2 ? k_paths_ci<2> : k_paths_ci<4>;
                     const int lds = pp == 8 ? paths_group_lds<8>(per) : pp == 2 ? paths_group_lds<2>(per)
                                                                                 : paths_group_lds<4>(per);
                     hipLaunchKernelGGL(kern, dim3((unsigned)((nb * c->wb.ppt + pp - 1) / pp)), dim3(kWave),
-                                       (unsigned)lds, c->stream, sc, rp, c->wb, sb, nb * c->wb.ppt, c->d_ctr);
+                                       (unsigned)lds, c->stream, with_slot(sc, 3), rp, c->wb, sb, nb * c->wb.ppt,
+                                       c->d_ctr);
                 }
                 else
                     hipLaunchKernelGGL((k_paths<false, kPathsWaves>), dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
-                                       (unsigned)(rp.ndims * rp.spp * 8), c->stream, sc, rp, c->lay, c->d_jump,
+                                       (unsigned)(rp.ndims * rp.spp * 8), c->stream, with_slot(sc, 3), rp, c->lay, c->d_jump,
                                        c->wb, sb, nb, c->d_ctr);
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 2], c->stream));
                 hipLaunchKernelGGL(k_film, dim3((unsigned)((nb * per + 255) / 256)), dim3(256), 0, c->stream,
@@ -2676,7 +2744,7 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
             if (c->min_waves == 2) kern = k_render_exact<2>;
             else if (c->min_waves == 4) kern = k_render_exact<4>;
             else if (c->min_waves == 8) kern = k_render_exact<8>;
-            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kWave), 0, c->stream, sc, rp, c->d_films,
+            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kWave), 0, c->stream, with_slot(sc, 6), rp, c->d_films,
                                c->d_s1d, c->d_panics, c->d_ctr);
         }
         HIPCHK(c, hipGetLastError());
@@ -2817,7 +2885,8 @@ static int intersect_batch(pbrt_gpu_ctx* c, const pbrt_ray_soa* rays, size_t n, 
     hipError_t e = hipMemcpyAsync(d_in, packed.data(), sizeof(double) * packed.size(), hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) {
         DevScene sc = dev_scene(c, false);
-        hipLaunchKernelGGL(k_intersect, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave), 0, c->stream, sc,
+        hipLaunchKernelGGL(k_intersect, dim3((unsigned)((n + kWave - 1) / kWave)), dim3(kWave), 0, c->stream,
+                           with_slot(sc, 7),
                            (int64_t)n, d_in, d_o, any);
         e = hipGetLastError();
     }
@@ -2870,6 +2939,7 @@ void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
                     c->d_wave,   c->d_fprims, c->d_wf,     c->d_ticks, c->d_slot_order};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
+    mesh_bvh_free(c->mesh);
     for (hipEvent_t e : c->bev) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->pev)
         if (e) (void)hipEventDestroy(e);
@@ -3010,6 +3080,43 @@ extern "C" int pbrt_gpu_counters(pbrt_gpu_ctx* c, uint64_t* out, int n) {
     return kNumCounters;
 }
 
+extern "C" int pbrt_gpu_mesh_info(pbrt_gpu_ctx* c, double* out, int n) {
+    if (!c || !out) return -PBRT_E_INVALID;
+    const double v[] = {(double)c->mesh.n_tris, (double)c->mesh.n_nodes, (double)c->mesh.depth, c->mesh.build_ms,
+                        (double)c->mesh.n_meshes};
+    const int m = (int)(sizeof(v) / sizeof(v[0]));
+    for (int i = 0; i < n && i < m; i++) out[i] = v[i];
+    return m;
+}
+extern "C" int pbrt_gpu_mesh_counters(uint64_t* out, int n, int reset) {
+#ifdef PBRT_MESH_COUNT
+    unsigned long long h[kMeshCountSlots * 6];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_mesh_count), sizeof(h)) != hipSuccess) return -PBRT_E_HIP;
+    for (int i = 0; i < n && i < kMeshCountSlots * 6; i++) out[i] = h[i];
+    if (reset) {
+        std::memset(h, 0, sizeof(h));
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_mesh_count), h, sizeof(h)) != hipSuccess) return -PBRT_E_HIP;
+    }
+    return kMeshCountSlots * 6;
+#else
+    (void)out; (void)n; (void)reset;
+    return 0;
+#endif
+}
+
+extern "C" int pbrt_gpu_mesh_download(pbrt_gpu_ctx* c, void* nodes, int32_t* gid, float* tris) {
+    if (!c) return PBRT_E_INVALID;
+    if (hipSetDevice(c->device) != hipSuccess) return PBRT_E_HIP;
+    const size_t nn = (size_t)c->mesh.n_nodes * 6, nt = (size_t)c->mesh.n_tris;
+    if (nodes && nn && hipMemcpy(nodes, c->mesh.nodes, nn * sizeof(MeshNode), hipMemcpyDeviceToHost) != hipSuccess)
+        return PBRT_E_HIP;
+    if (gid && nt && hipMemcpy(gid, c->mesh.gid, nt * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
+        return PBRT_E_HIP;
+    if (tris && nt && hipMemcpy(tris, c->mesh.tris, nt * 9 * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+        return PBRT_E_HIP;
+    return PBRT_OK;
+}
+
 extern "C" int64_t pbrt_gpu_tile_ticks(pbrt_gpu_ctx* c, uint32_t* out, int64_t n, int64_t* heavy) {
     if (!c) return -PBRT_E_INVALID;
     if (heavy) *heavy = c->last_heavy;
@@ -3043,7 +3150,7 @@ extern "C" int pbrt_abi_sizes(size_t* out, int n) {
                         sizeof(pbrt_light_desc),  sizeof(pbrt_camera_desc),  sizeof(pbrt_film_desc),
                         sizeof(pbrt_distribution_desc), sizeof(pbrt_scene_desc), sizeof(pbrt_render_desc),
                         sizeof(pbrt_gpu_stats),   sizeof(pbrt_ray_soa),      sizeof(pbrt_hit_soa),
-                        sizeof(pbrt_gpu_opts)};
+                        sizeof(pbrt_gpu_opts),    sizeof(pbrt_mesh_desc)};
     int m = (int)(sizeof(s) / sizeof(s[0]));
     for (int i = 0; i < n && i < m; i++) out[i] = s[i];
     return m;

@@ -220,6 +220,10 @@ struct pbrt_scene_builder {
     pbrt_camera_desc camera;
     pbrt_film_desc film;
     bool has_film = false, has_camera = false;
+    // triangle meshes (extension): owned copies of the vertex / index arrays
+    std::vector<std::vector<float>> mesh_p;
+    std::vector<std::vector<int32_t>> mesh_idx;
+    std::vector<pbrt_mesh_desc> meshes;
     pbrt_scene_desc desc;
 };
 
@@ -431,6 +435,22 @@ int pbrt_sb_add_light(pbrt_scene_builder* b, const pbrt_light_desc* l) {
     b->lights.push_back(*l);
     return (int)b->lights.size() - 1;
 }
+int pbrt_sb_add_mesh(pbrt_scene_builder* b, int32_t n_vertices, const float* p, int32_t n_triangles,
+                     const int32_t* indices, int32_t material, int32_t reverse_orientation) {
+    if (n_vertices <= 0 || n_triangles <= 0 || !p || !indices) return -PBRT_E_INVALID;
+    for (int64_t i = 0; i < 3 * (int64_t)n_triangles; i++)
+        if (indices[i] < 0 || indices[i] >= n_vertices) return -PBRT_E_INVALID;
+    b->mesh_p.emplace_back(p, p + 3 * (size_t)n_vertices);
+    b->mesh_idx.emplace_back(indices, indices + 3 * (size_t)n_triangles);
+    pbrt_mesh_desc m;
+    std::memset(&m, 0, sizeof(m));
+    m.n_vertices = n_vertices;
+    m.n_triangles = n_triangles;
+    m.material = material;
+    m.reverse_orientation = reverse_orientation;
+    b->meshes.push_back(m);
+    return (int)b->meshes.size() - 1;
+}
 int pbrt_sb_set_film(pbrt_scene_builder* b, int64_t res_x, int64_t res_y, const double crop[4], double frx,
                      double fry, double max_lum) {  // film.go:42-76 (BoxFilter)
     pbrt_film_desc& f = b->film;
@@ -506,11 +526,27 @@ int pbrt_sb_build(pbrt_scene_builder* b, int max_prims_in_node, const pbrt_scene
             b->order.push_back(bb.ordered[i]);
         }
     }
+    for (const auto& m : b->meshes)
+        if (m.material < 0 || m.material >= (int)b->materials.size()) return PBRT_E_INVALID;
     pbrt_scene_desc& d = b->desc;
     std::memset(&d, 0, sizeof(d));
     // scene.go:16-36: WorldBound = BVH root bounds; Distant.Preprocess (distant.go:36-38)
     if (!b->nodes.empty())
         for (int k = 0; k < 3; k++) { d.world_min[k] = b->nodes[0].bmin[k]; d.world_max[k] = b->nodes[0].bmax[k]; }
+    // extension: the aggregate also holds the meshes, so the world bound is the
+    // union with their vertex bounds (Bounds3.Union, bounds.go:54-66)
+    bool have = !b->nodes.empty();
+    for (size_t mi = 0; mi < b->meshes.size(); mi++) {
+        const std::vector<float>& P = b->mesh_p[mi];
+        for (int32_t v : b->mesh_idx[mi]) {
+            for (int k = 0; k < 3; k++) {
+                const double x = (double)P[3 * (size_t)v + k];
+                d.world_min[k] = have ? gm::min(d.world_min[k], x) : x;
+                d.world_max[k] = have ? gm::max(d.world_max[k], x) : x;
+            }
+            have = true;
+        }
+    }
     V3 mn = load3(d.world_min), mx = load3(d.world_max);
     V3 center = divs(mn + mx, 2.0);   // bounds.go:105-112 BoundingSphere
     double radius = 0;
@@ -531,6 +567,12 @@ int pbrt_sb_build(pbrt_scene_builder* b, int max_prims_in_node, const pbrt_scene
     d.lights = b->lights.data();
     d.camera = b->camera;
     d.film = b->film;
+    for (size_t mi = 0; mi < b->meshes.size(); mi++) {
+        b->meshes[mi].p = b->mesh_p[mi].data();
+        b->meshes[mi].indices = b->mesh_idx[mi].data();
+    }
+    d.n_meshes = (int)b->meshes.size();
+    d.meshes = b->meshes.empty() ? nullptr : b->meshes.data();
     if (out) *out = &d;
     return PBRT_OK;
 }
@@ -559,9 +601,8 @@ int pbrt_scene_light_distribution(const pbrt_scene_desc* s, int strategy, pbrt_d
     return PBRT_OK;
 }
 
-// internal/render/server.go:29-164
-int pbrt_scene_readme(int64_t w, int64_t h, pbrt_scene_builder** out) {
-    pbrt_scene_builder* b = pbrt_sb_create();
+// internal/render/server.go:44-69: the 21 reverse-oriented spheres
+static void readme_spheres(pbrt_scene_builder* b) {
     const int n = 8;
     for (int k = 1; k < n; k++) {
         for (int i = 0; i < 3; i++) {
@@ -587,27 +628,16 @@ int pbrt_scene_readme(int64_t w, int64_t h, pbrt_scene_builder** out) {
             pbrt_sb_add_primitive(b, &p);
         }
     }
+}
+// server.go:71-81: the floor's checkerboard Matte
+static int readme_checker(pbrt_scene_builder* b) {
     const double vs[3] = {.2, 0, 0}, vt[3] = {0, 0, .2}, one[3] = {1, 1, 1}, dark[3] = {0.18, 0.18, 0.18};
     pbrt_material_desc chk;
     pbrt_make_matte_checkerboard(vs, vt, 0, 0, one, dark, 0.0, &chk);
-    int mchk = pbrt_sb_add_material(b, &chk);
-    pbrt_transform t0, rx, dx;
-    pbrt_translate(0, 0, 0, &t0);
-    pbrt_rotate_x(90, &rx);
-    pbrt_transform_mul(&t0, &rx, &dx);
-    pbrt_shape_desc d1, d2;
-    pbrt_make_disk(&dx, 0.01, 10000, 0, 360, &d1);
-    pbrt_translate(-50, 0, -50, &dx);
-    pbrt_make_disk(&dx, 0.01, 10000, 0, 360, &d2);
-    pbrt_primitive_desc p;
-    std::memset(&p, 0, sizeof(p));
-    p.kind = PBRT_PRIM_GEOMETRIC;
-    p.material = mchk;
-    p.shape = pbrt_sb_add_shape(b, &d1);
-    pbrt_sb_add_primitive(b, &p);
-    p.shape = pbrt_sb_add_shape(b, &d2);
-    pbrt_sb_add_primitive(b, &p);
-
+    return pbrt_sb_add_material(b, &chk);
+}
+// server.go:112-164: the four lights, the film and the camera
+static void readme_lights_camera(pbrt_scene_builder* b, int64_t w, int64_t h) {
     pbrt_light_desc l;
     pbrt_transform l2w;
     const double Ld[3] = {0.05, 0.05, 0.05}, wd[3] = {-1, 1, 1};
@@ -638,6 +668,93 @@ int pbrt_scene_readme(int64_t w, int64_t h, pbrt_scene_builder** out) {
     pbrt_rotate_x(-30, &r);
     pbrt_transform_mul(&cam, &r, &cam);
     pbrt_sb_set_perspective_camera(b, &cam, crop, 0.0, 1.0, 0, 20, 100);
+}
+
+// internal/render/server.go:29-164
+int pbrt_scene_readme(int64_t w, int64_t h, pbrt_scene_builder** out) {
+    pbrt_scene_builder* b = pbrt_sb_create();
+    readme_spheres(b);
+    int mchk = readme_checker(b);
+    pbrt_transform t0, rx, dx;
+    pbrt_translate(0, 0, 0, &t0);
+    pbrt_rotate_x(90, &rx);
+    pbrt_transform_mul(&t0, &rx, &dx);
+    pbrt_shape_desc d1, d2;
+    pbrt_make_disk(&dx, 0.01, 10000, 0, 360, &d1);
+    pbrt_translate(-50, 0, -50, &dx);
+    pbrt_make_disk(&dx, 0.01, 10000, 0, 360, &d2);
+    pbrt_primitive_desc p;
+    std::memset(&p, 0, sizeof(p));
+    p.kind = PBRT_PRIM_GEOMETRIC;
+    p.material = mchk;
+    p.shape = pbrt_sb_add_shape(b, &d1);
+    pbrt_sb_add_primitive(b, &p);
+    p.shape = pbrt_sb_add_shape(b, &d2);
+    pbrt_sb_add_primitive(b, &p);
+    readme_lights_camera(b, w, h);
+    int rc = pbrt_sb_build(b, 2, nullptr);
+    if (rc != PBRT_OK) { pbrt_sb_destroy(b); return rc; }
+    *out = b;
+    return PBRT_OK;
+}
+
+// Value noise of the height field: lattice values in [-1, 1) at integer
+// points of (x, z) / 10, from a splitmix64 hash of (seed, i, j), blended with
+// the smoothstep weights.
+static double hf_lattice(uint64_t seed, int64_t i, int64_t j) {
+    uint64_t z = seed * 0x9e3779b97f4a7c15ULL ^ (uint64_t)i * 0xbf58476d1ce4e5b9ULL ^ (uint64_t)j * 0x94d049bb133111ebULL;
+    z += 0x9e3779b97f4a7c15ULL;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    z ^= z >> 31;
+    return (double)(z >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0;
+}
+static double hf_noise(uint64_t seed, double x, double z) {
+    const double gx = x / 10.0, gz = z / 10.0;
+    const double fx = gm::floor(gx), fz = gm::floor(gz);
+    const int64_t i = (int64_t)fx, j = (int64_t)fz;
+    const double tx = gx - fx, tz = gz - fz;
+    const double sx = tx * tx * (3.0 - 2.0 * tx), sz = tz * tz * (3.0 - 2.0 * tz);
+    const double a = hf_lattice(seed, i, j), bb = hf_lattice(seed, i + 1, j);
+    const double c = hf_lattice(seed, i, j + 1), d = hf_lattice(seed, i + 1, j + 1);
+    const double top = a + (bb - a) * sx, bot = c + (d - c) * sx;
+    return top + (bot - top) * sz;
+}
+
+int pbrt_scene_heightfield(int64_t w, int64_t h, int32_t quads, uint64_t seed, int32_t flags,
+                           pbrt_scene_builder** out) {
+    if (quads < 1 || quads > 46340) return PBRT_E_INVALID;
+    pbrt_scene_builder* b = pbrt_sb_create();
+    if (flags & PBRT_HF_README_SPHERES) readme_spheres(b);
+    const int mchk = readme_checker(b);
+    const int64_t nv = (int64_t)(quads + 1) * (quads + 1);
+    std::vector<float> P((size_t)(3 * nv));
+    const double lo = -100.0, span = 300.0;
+    for (int64_t j = 0; j <= quads; j++) {
+        for (int64_t i = 0; i <= quads; i++) {
+            const double x = lo + span * (double)i / (double)quads;
+            const double z = lo + span * (double)j / (double)quads;
+            const double y = 2.0 * gm::sin(0.3 * x) * gm::cos(0.2 * z) + 3.0 * hf_noise(seed, x, z);
+            const size_t v = (size_t)(j * (quads + 1) + i);
+            P[3 * v + 0] = (float)x;
+            P[3 * v + 1] = (float)y;
+            P[3 * v + 2] = (float)z;
+        }
+    }
+    std::vector<int32_t> I((size_t)6 * quads * quads);
+    size_t k = 0;
+    for (int64_t j = 0; j < quads; j++) {
+        for (int64_t i = 0; i < quads; i++) {
+            const int32_t v00 = (int32_t)(j * (quads + 1) + i), v10 = v00 + 1;
+            const int32_t v01 = v00 + (quads + 1), v11 = v01 + 1;
+            // counter-clockwise seen from +y: the geometric normal points up
+            I[k++] = v00; I[k++] = v01; I[k++] = v10;
+            I[k++] = v10; I[k++] = v01; I[k++] = v11;
+        }
+    }
+    int mi = pbrt_sb_add_mesh(b, (int32_t)nv, P.data(), (int32_t)(2 * (int64_t)quads * quads), I.data(), mchk, 0);
+    if (mi < 0) { pbrt_sb_destroy(b); return -mi; }
+    readme_lights_camera(b, w, h);
     int rc = pbrt_sb_build(b, 2, nullptr);
     if (rc != PBRT_OK) { pbrt_sb_destroy(b); return rc; }
     *out = b;

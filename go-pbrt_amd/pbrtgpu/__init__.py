@@ -111,6 +111,11 @@ def lib():
     L.pbrt_scene_light_distribution.argtypes = [P(abi.SceneDesc), C.c_int, P(abi.DistributionDesc)]
     L.pbrt_scene_readme.argtypes = [i64, i64, P(C.c_void_p)]
     L.pbrt_scene_cornell.argtypes = [i64, i64, P(C.c_void_p)]
+    L.pbrt_scene_heightfield.argtypes = [i64, i64, C.c_int32, C.c_uint64, C.c_int32, P(C.c_void_p)]
+    L.pbrt_sb_add_mesh.argtypes = [C.c_void_p, C.c_int32, P(C.c_float), C.c_int32, P(C.c_int32), C.c_int32,
+                                   C.c_int32]
+    L.pbrt_gpu_mesh_info.argtypes = [C.c_void_p, P(d), C.c_int]
+    L.pbrt_gpu_mesh_download.argtypes = [C.c_void_p, C.c_void_p, P(C.c_int32), P(C.c_float)]
     _lib = L
     return L
 
@@ -186,7 +191,29 @@ class Scene:
         s._fetch()
         return s
 
+    @classmethod
+    def heightfield(cls, w, h, quads=707, seed=1, spheres=False):
+        """BASELINE config D (quads 707: 999 698 triangles) / E (2236): the
+        height-field extension scene (include/pbrt_scene.h)."""
+        hb = C.c_void_p()
+        rc = lib().pbrt_scene_heightfield(w, h, quads, seed, 1 if spheres else 0, C.byref(hb))
+        if rc:
+            raise PbrtError(rc, "pbrt_scene_heightfield")
+        s = cls(hb.value)
+        s._fetch()
+        return s
+
     # builder API (pbrt_sb_*) -------------------------------------------------
+    def add_mesh(self, p, indices, material, reverse=False):
+        """p: (nv, 3) float32 world positions; indices: (nt, 3) int32."""
+        p = np.ascontiguousarray(p, dtype=np.float32)
+        idx = np.ascontiguousarray(indices, dtype=np.int32)
+        r = lib().pbrt_sb_add_mesh(self.h, p.shape[0], p.ctypes.data_as(C.POINTER(C.c_float)), idx.shape[0],
+                                   idx.ctypes.data_as(C.POINTER(C.c_int32)), material, int(reverse))
+        if r < 0:
+            raise PbrtError(-r, "pbrt_sb_add_mesh")
+        return r
+
     def add_sphere(self, o2w, radius, reverse=False, z_min=None, z_max=None, phi_max=360.0):
         sd = abi.ShapeDesc()
         lib().pbrt_make_sphere(C.byref(o2w), int(reverse), radius, -radius if z_min is None else z_min,
@@ -327,6 +354,27 @@ class Renderer:
 
     def stream(self):
         return lib().pbrt_gpu_stream(self.h)
+
+    def mesh_info(self):
+        """{tris, nodes, depth, build_ms, meshes} of the context's device LBVH."""
+        out = (C.c_double * 8)()
+        lib().pbrt_gpu_mesh_info(self.h, out, 8)
+        return {"tris": int(out[0]), "nodes": int(out[1]), "depth": int(out[2]), "build_ms": out[3],
+                "meshes": int(out[4])}
+
+    def mesh_download(self):
+        """(nodes [6, n] structured array, gid [tris], tris [tris, 9]) of the device LBVH."""
+        info = self.mesh_info()
+        dt = np.dtype([("bmin", np.float32, 3), ("escape", np.uint32), ("bmax", np.float32, 3),
+                       ("leaf", np.uint32)])
+        nodes = np.zeros(6 * info["nodes"], dtype=dt)
+        gid = np.zeros(info["tris"], dtype=np.int32)
+        tris = np.zeros((info["tris"], 9), dtype=np.float32)
+        rc = lib().pbrt_gpu_mesh_download(self.h, nodes.ctypes.data_as(C.c_void_p),
+                                          gid.ctypes.data_as(C.POINTER(C.c_int32)),
+                                          tris.ctypes.data_as(C.POINTER(C.c_float)))
+        self._check(rc)
+        return nodes.reshape(6, info["nodes"]), gid, tris
 
     def tile_ticks(self):
         """(per-slot chain ticks of the last EXACT frame at 100 MHz, heavy slots of its split)."""

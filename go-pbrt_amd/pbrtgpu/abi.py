@@ -157,6 +157,18 @@ class DistributionDesc(C.Structure):
     ]
 
 
+class MeshDesc(C.Structure):
+    """pbrt_mesh_desc: extension (configs D/E), include/pbrt_gpu.h."""
+    _fields_ = [
+        ("n_vertices", C.c_int32),
+        ("n_triangles", C.c_int32),
+        ("material", C.c_int32),
+        ("reverse_orientation", C.c_int32),
+        ("p", C.POINTER(C.c_float)),
+        ("indices", C.POINTER(C.c_int32)),
+    ]
+
+
 class SceneDesc(C.Structure):
     _fields_ = [
         ("n_shapes", C.c_int32),
@@ -174,6 +186,9 @@ class SceneDesc(C.Structure):
         ("film", FilmDesc),
         ("world_min", C.c_double * 3),
         ("world_max", C.c_double * 3),
+        ("n_meshes", C.c_int32),
+        ("pad1", C.c_int32),
+        ("meshes", C.POINTER(MeshDesc)),
     ]
 
 

@@ -62,6 +62,22 @@ int pbrt_gpu_counters(struct pbrt_gpu_ctx* ctx, uint64_t* out, int n);
  * the last launch that ran at 4 waves in the heavy/light split (0: no split). */
 int64_t pbrt_gpu_tile_ticks(struct pbrt_gpu_ctx* ctx, uint32_t* out, int64_t n, int64_t* heavy);
 
+/* Triangle meshes of the context (extension): out = {triangles in the tree
+ * (zero-area ones are left out), nodes per ordering, deepest leaf, device
+ * build ms, meshes}. Returns the number of values. */
+int pbrt_gpu_mesh_info(struct pbrt_gpu_ctx* ctx, double* out, int n);
+/* Copies the device LBVH: nodes = 6 * nodes-per-ordering records of 32 bytes
+ * (float bmin[3], uint32 escape, float bmax[3], uint32 leaf: 0xFFFFFFFF for an
+ * interior node, else first_slot << 3 | count), gid = the global triangle
+ * index of each leaf slot, tris = 9 floats per slot. Any pointer may be NULL. */
+int pbrt_gpu_mesh_download(struct pbrt_gpu_ctx* ctx, void* nodes, int32_t* gid, float* tris);
+
+/* Mesh-traversal counters of libraries built with -DPBRT_MESH_COUNT (make
+ * meshcount; 0 values otherwise): [8 kernel slots][closest, any][walks, nodes
+ * fetched, triangles tested], slots as render.hip's with_slot(). Returns the
+ * count (48), or 0 in a normal build. */
+int pbrt_gpu_mesh_counters(uint64_t* out, int n, int reset);
+
 /* Region cycles inside path steps, summed over waves (only in libraries built
  * with -DPBRT_STEP_TIMING; zeros otherwise). Returns the count (8). */
 int pbrt_gpu_step_cycles(uint64_t* out, int n, int reset);

@@ -113,6 +113,26 @@ typedef struct pbrt_bvh_node {
     uint8_t pad0;
 } pbrt_bvh_node;
 
+/* ----------------------------------------------------------- triangle meshes */
+/* EXTENSION (BASELINE configs D/E): go-pbrt has no triangle shape (pkg/shapes
+ * holds only disk.go) and its BVH builder is O(n^2) (bvh.go:272-411), so a
+ * triangle mesh is not part of the reference's semantics. Semantics here are
+ * pbrt-v3's Triangle::Intersect (watertight, Woop et al.; default uv), in
+ * float64 after exact widening of float32 world-space vertices, with error
+ * bounds from the real machine epsilon 2^-53 (go-pbrt's own Gamma() is
+ * denormal). Meshes are traversed through their own BVH, built
+ * on the device (LBVH); a closest hit is the smallest (t, triangle index)
+ * over all triangles, so results do not depend on that BVH. Triangles of
+ * mesh m carry the global index mesh_first(m) + i and report prim =
+ * n_prims + that index. */
+typedef struct pbrt_mesh_desc {
+    int32_t n_vertices, n_triangles;
+    int32_t material;              /* index into materials (Matte)              */
+    int32_t reverse_orientation;   /* flips the geometric normal                */
+    const float* p;                /* n_vertices * 3 world-space positions     */
+    const int32_t* indices;        /* n_triangles * 3 vertex indices            */
+} pbrt_mesh_desc;
+
 /* ------------------------------------------------------------------ lights */
 enum { PBRT_LIGHT_POINT = 1, PBRT_LIGHT_DISTANT = 2, PBRT_LIGHT_DIFFUSE_AREA = 3 };
 
@@ -171,6 +191,8 @@ typedef struct pbrt_scene_desc {
     pbrt_camera_desc camera;
     pbrt_film_desc film;
     double world_min[3], world_max[3];     /* Scene.WorldBound (BVH root)     */
+    int32_t n_meshes, pad1;                /* extension: triangle meshes      */
+    const pbrt_mesh_desc* meshes;
 } pbrt_scene_desc;
 
 /* ------------------------------------------------------------------ render */

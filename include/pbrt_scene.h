@@ -75,6 +75,10 @@ int pbrt_sb_add_shape(pbrt_scene_builder* b, const pbrt_shape_desc* s);        /
 int pbrt_sb_add_material(pbrt_scene_builder* b, const pbrt_material_desc* m);  /* -> index */
 int pbrt_sb_add_primitive(pbrt_scene_builder* b, const pbrt_primitive_desc* p);/* -> index */
 int pbrt_sb_add_light(pbrt_scene_builder* b, const pbrt_light_desc* l);        /* -> index */
+/* Extension (configs D/E): a triangle mesh, copied; p = n_vertices*3 float32
+ * world-space positions, indices = n_triangles*3. Returns the mesh index. */
+int pbrt_sb_add_mesh(pbrt_scene_builder* b, int32_t n_vertices, const float* p, int32_t n_triangles,
+                     const int32_t* indices, int32_t material, int32_t reverse_orientation);
 /* film.go:42-76 with a BoxFilter of the given radius */
 int pbrt_sb_set_film(pbrt_scene_builder* b, int64_t res_x, int64_t res_y, const double crop[4],
                      double filter_rx, double filter_ry, double max_sample_luminance);
@@ -98,6 +102,17 @@ int pbrt_scene_light_distribution(const pbrt_scene_desc* s, int strategy,
 int pbrt_scene_readme(int64_t w, int64_t h, pbrt_scene_builder** out);
 /* Cornell-style 6 disks + 2 spheres, built only from reference types */
 int pbrt_scene_cornell(int64_t w, int64_t h, pbrt_scene_builder** out);
+
+/* SURVEY §8(d) configs D/E (extension): a height field of quads x quads
+ * cells (2 triangles each) over x, z in [-100, 200], height
+ * y = 2 sin(.3x) cos(.2z) + 3 valuenoise(x, z; seed) (Go-math trig, vertices
+ * rounded to float32), checkerboard Matte as the README floor, with the README
+ * lights and camera (server.go:112-164). flags & PBRT_HF_README_SPHERES adds
+ * the README's 21 spheres (a mixed analytic + mesh scene).
+ * D: quads = 707 (999 698 triangles); E: quads = 2236 (9 999 392). */
+#define PBRT_HF_README_SPHERES 1
+int pbrt_scene_heightfield(int64_t w, int64_t h, int32_t quads, uint64_t seed, int32_t flags,
+                           pbrt_scene_builder** out);
 
 #ifdef __cplusplus
 }

@@ -152,3 +152,15 @@ void oracle_spawn_ray_to(const double in[18], double out[7]) {
     out[3] = d.x; out[4] = d.y; out[5] = d.z;
     out[6] = 1 - 0.0001;
 }
+
+/* ------------------------------------------------ triangle extension (mesh) */
+/* oracle_mesh.c orc_triangle_hit: ray = o[3] d[3] tmax; out = t, b0, b1, b2 */
+#include "oracle_mesh.h"
+int oracle_triangle_hit(const double v[9], const double ray[7], double out[4]) {
+    ray_t r;
+    r.o = V3(ray[0], ray[1], ray[2]);
+    r.d = V3(ray[3], ray[4], ray[5]);
+    r.tmax = ray[6];
+    r.time = 0;
+    return orc_triangle_hit(v, &r, &out[0], &out[1], &out[2], &out[3]);
+}

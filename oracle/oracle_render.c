@@ -18,6 +18,7 @@
  *    goroutine completion order under a mutex, film.go:115-132).
  */
 #include "oracle_render.h"
+#include "oracle_mesh.h"
 
 #ifdef ORACLE_COUNT_FLOPS
 __thread uint64_t orc_flops;
@@ -367,10 +368,14 @@ static int bounds_intersect_p(const pbrt_bvh_node* nd, const ray_t* r, v3 inv, c
     return tmin < r->tmax && tmax > 0;
 }
 
-/* bvh.go:659-712 */
-int orc_bvh_intersect(panic_ctx* pc, const pbrt_scene_desc* sc, ray_t* ray, si_t* si) {
-    if (sc->n_nodes == 0) return 0;
+static void tri_si(const orc_tri_hit* h, const ray_t* r, si_t* si);
+
+/* bvh.go:659-712, then the triangle meshes (extension, oracle_mesh.h) */
+static int orc_bvh_intersect(orc_ctx* oc, ray_t* ray, si_t* si) {
+    panic_ctx* pc = &oc->pc;
+    const pbrt_scene_desc* sc = oc->scene;
     int hit = 0;
+    if (sc->n_nodes == 0) goto meshes;
     v3 inv = V3(1 / ray->d.x, 1 / ray->d.y, 1 / ray->d.z);
     FL(3);
     int neg[3] = {inv.x < 0, inv.y < 0, inv.z < 0};
@@ -399,10 +404,22 @@ int orc_bvh_intersect(panic_ctx* pc, const pbrt_scene_desc* sc, ray_t* ray, si_t
             cur = stack[--to_visit];
         }
     }
+meshes:
+    if (oc->mesh) {
+        orc_tri_hit h;
+        /* a triangle at exactly TMax never wins: TMax is exclusive, and an
+           analytic primitive that set it is tested first */
+        if (orc_mesh_closest(oc->mesh, ray, ray->tmax, -1, &h)) {
+            ray->tmax = h.t;
+            tri_si(&h, ray, si);
+            si->prim = sc->n_prims + h.gid;
+            hit = 1;
+        }
+    }
     return hit;
 }
 /* bvh.go:713-765 */
-int orc_bvh_intersect_p(panic_ctx* pc, const pbrt_scene_desc* sc, const ray_t* ray) {
+static int orc_bvh_intersect_p_analytic(panic_ctx* pc, const pbrt_scene_desc* sc, const ray_t* ray) {
     if (sc->n_nodes == 0) return 0;
     v3 inv = V3(1 / ray->d.x, 1 / ray->d.y, 1 / ray->d.z);
     FL(3);
@@ -434,6 +451,61 @@ int orc_bvh_intersect_p(panic_ctx* pc, const pbrt_scene_desc* sc, const ray_t* r
     }
 }
 
+static int orc_bvh_intersect_p(orc_ctx* oc, const ray_t* ray) {
+    if (orc_bvh_intersect_p_analytic(&oc->pc, oc->scene, ray)) return 1;
+    return oc->mesh ? orc_mesh_any(oc->mesh, ray) : 0;
+}
+
+/* pbrt-v3 Triangle::Intersect, interaction part (default uv (0,0), (1,0),
+ * (1,1); no shading normals), float64: the extension's SurfaceInteraction.
+ * With those uv, dpdu = dp12 - dp02 and dpdv = -dp12 (the uv determinant is
+ * exactly 1). wo is normalized as every go-pbrt interaction's (the shapes'
+ * TransformSurfaceInteraction, transform.go:302-334). */
+static void tri_si(const orc_tri_hit* h, const ray_t* r, si_t* si) {
+    const double eps = 1.1102230246251565e-16;
+    const double g7 = (7 * eps) / (1 - 7 * eps);
+    FL(4);
+    v3 dp02 = v_sub(h->p0, h->p2), dp12 = v_sub(h->p1, h->p2);
+    v3 dpdu = v_sub(dp12, dp02);
+    v3 dpdv = V3(-dp12.x, -dp12.y, -dp12.z);
+    if (v_len2(v_cross(dpdu, dpdv)) == 0) {
+        v3 ng = v_cross(v_sub(h->p2, h->p0), v_sub(h->p1, h->p0));
+        v3 nn = v_normalized(ng), a, b;
+        coordinate_system(nn, &a, &b);
+        dpdu = a;
+        dpdv = b;
+    }
+    v3 p = V3(h->b0 * h->p0.x + h->b1 * h->p1.x + h->b2 * h->p2.x,
+              h->b0 * h->p0.y + h->b1 * h->p1.y + h->b2 * h->p2.y,
+              h->b0 * h->p0.z + h->b1 * h->p1.z + h->b2 * h->p2.z);
+    v3 err = V3(gm_abs(h->b0 * h->p0.x) + gm_abs(h->b1 * h->p1.x) + gm_abs(h->b2 * h->p2.x),
+                gm_abs(h->b0 * h->p0.y) + gm_abs(h->b1 * h->p1.y) + gm_abs(h->b2 * h->p2.y),
+                gm_abs(h->b0 * h->p0.z) + gm_abs(h->b1 * h->p1.z) + gm_abs(h->b2 * h->p2.z));
+    FL(15 + 15);
+    v3 n = v_normalized(v_cross(dp02, dp12));
+    if (h->reverse) n = V3(-n.x, -n.y, -n.z);
+    memset(si, 0, sizeof(*si));
+    si->p = p;
+    si->perr = v_muls(err, g7);
+    si->n = n;
+    si->wo = v_normalized(V3(-r->d.x, -r->d.y, -r->d.z));
+    si->time = r->time;
+    si->dpdu = dpdu; si->dpdv = dpdv;
+    si->sn = n; si->sdpdu = dpdu; si->sdpdv = dpdv;
+    si->prim = -1;
+}
+
+/* material of primitive index `prim`: scene prims, then the meshes' triangles */
+static int prim_material(const pbrt_scene_desc* sc, int prim) {
+    if (prim < sc->n_prims) return sc->prims[prim].material;
+    int64_t g = prim - sc->n_prims;
+    for (int mi = 0; mi < sc->n_meshes; mi++) {
+        if (g < sc->meshes[mi].n_triangles) return sc->meshes[mi].material;
+        g -= sc->meshes[mi].n_triangles;
+    }
+    return 0;
+}
+
 /* ============================================================ BSDF (Matte) */
 typedef struct {
     v3 ns, ng, ss, ts;
@@ -454,7 +526,7 @@ static int matches_flags(int t, int flags) { return (t & flags) == t; }
 
 /* matte.go:21-37 + reflection.go:128-140 + checkerboard.go:30-40 */
 static int material_bsdf(const pbrt_scene_desc* sc, const si_t* si, bsdf_t* b) {
-    const pbrt_material_desc* m = &sc->materials[sc->prims[si->prim].material];
+    const pbrt_material_desc* m = &sc->materials[prim_material(sc, si->prim)];
     b->ns = si->sn;
     b->ng = si->n;
     b->ss = v_normalized(si->sdpdu);
@@ -700,7 +772,7 @@ static spec estimate_direct(orc_ctx* oc, const si_t* si, const bsdf_t* b, v2 u_s
         if (!s_is_black(f)) {
             ray_t sr = spawn_ray_to(si, tp, tperr, tn);
             oc->shadow_rays++;
-            if (orc_bvh_intersect_p(&oc->pc, sc, &sr)) Li = S3(0, 0, 0);
+            if (orc_bvh_intersect_p(oc, &sr)) Li = S3(0, 0, 0);
             if (!s_is_black(Li)) {
                 if (is_delta) {
                     Ld = s_add(Ld, s_divs(s_mul(f, Li), light_pdf));
@@ -725,7 +797,7 @@ static spec estimate_direct(orc_ctx* oc, const si_t* si, const bsdf_t* b, v2 u_s
             r2.d = wi2; r2.tmax = INFINITY; r2.time = si->time;
             si_t tmp;
             oc->closest_rays++;
-            orc_bvh_intersect(&oc->pc, sc, &r2, &tmp);
+            orc_bvh_intersect(oc, &r2, &tmp);
         }
     }
     return Ld;
@@ -786,7 +858,7 @@ static spec path_li(orc_ctx* oc, sampler_t* smp, ray_t ray) {
         if (bounces >= rd->max_depth) break;     /* path.go:66 (hit or miss)  */
         si_t isect;
         oc->closest_rays++;
-        if (!orc_bvh_intersect(&oc->pc, sc, &ray, &isect)) break;
+        if (!orc_bvh_intersect(oc, &ray, &isect)) break;
         bsdf_t b;
         if (material_bsdf(sc, &isect, &b) < 0) { oc->unsupported = 1; break; }
         if (b.n_bxdfs > 0) {   /* NumComponents(BSDFAll &^ BSDFSpecular) > 0 */
@@ -834,7 +906,7 @@ static spec direct_li(orc_ctx* oc, sampler_t* smp, ray_t ray) {
     si_t si;
     oc->cur_bounce = 1;
     oc->closest_rays++;
-    if (!orc_bvh_intersect(&oc->pc, sc, &ray, &si)) {
+    if (!orc_bvh_intersect(oc, &ray, &si)) {
         for (int i = 0; i < sc->n_lights; i++) L = s_add(L, S3(0, 0, 0));
         return L;
     }
@@ -1042,6 +1114,7 @@ static void* worker(void* arg) {
     orc_ctx oc;
     memset(&oc, 0, sizeof(oc));
     oc.scene = j->sc; oc.rd = j->rd; oc.flags = j->flags;
+    oc.mesh = orc_mesh_get(j->sc);
 #ifdef ORACLE_COUNT_FLOPS
     orc_flops = 0;
     orc_flops_light = 0;
@@ -1191,12 +1264,12 @@ static void intersect_one(orc_ctx* oc, const double* q, int closest, double* o) 
         si_t si;
         memset(&si, 0, sizeof(si));
         si.prim = -1;
-        int h = orc_bvh_intersect(&oc->pc, oc->scene, &r, &si);
+        int h = orc_bvh_intersect(oc, &r, &si);
         o[0] = h; o[1] = r.tmax; o[2] = h ? si.prim : -1;
         o[3] = si.p.x; o[4] = si.p.y; o[5] = si.p.z;
         o[6] = si.n.x; o[7] = si.n.y; o[8] = si.n.z;
     } else {
-        o[0] = orc_bvh_intersect_p(&oc->pc, oc->scene, &r);
+        o[0] = orc_bvh_intersect_p(oc, &r);
     }
 }
 
@@ -1206,6 +1279,7 @@ int orc_intersect(const pbrt_scene_desc* sc, const double* rays, size_t n, int c
     orc_ctx oc;
     memset(&oc, 0, sizeof(oc));
     oc.scene = sc;
+    oc.mesh = orc_mesh_get(sc);
     for (size_t i = 0; i < n; i++)
         intersect_one(&oc, rays + 7 * i, closest, closest ? out + 9 * i : out + i);
     return 0;

@@ -25,6 +25,7 @@ typedef struct {
     int32_t cur_sample, cur_bounce;
     int unsupported;
     uint64_t paths, camera_samples, closest_rays, shadow_rays;
+    const struct orc_mesh* mesh;   /* triangle meshes of the scene (extension), or NULL */
 } orc_ctx;
 
 typedef struct {

@@ -109,6 +109,7 @@ def _bind(L):
         L.oracle_intersect.argtypes = [P(abi.SceneDesc), P(d), C.c_size_t, C.c_int, P(d)]
         L.oracle_light_distribution.argtypes = [P(abi.SceneDesc), P(abi.RenderDesc), P(abi.DistributionDesc)]
         L.oracle_spawn_ray_to.argtypes = [P(d), P(d)]
+        L.oracle_triangle_hit.argtypes = [P(d), P(d), P(d)]
     return L
 
 
@@ -160,3 +161,12 @@ def intersect(desc, rays, closest=True):
     out = np.zeros((n, 9) if closest else (n,), dtype=np.float64)
     lib().oracle_intersect(C.byref(desc), dptr(rays), n, 1 if closest else 0, dptr(out))
     return out
+
+
+def triangle_hit(v, ray):
+    """orc_triangle_hit (triangle extension): (hit, t, b0, b1, b2)."""
+    v = np.ascontiguousarray(v, dtype=np.float64)
+    ray = np.ascontiguousarray(ray, dtype=np.float64)
+    out = np.zeros(4)
+    h = lib().oracle_triangle_hit(dptr(v), dptr(ray), dptr(out))
+    return bool(h), out[0], out[1], out[2], out[3]

@@ -40,7 +40,7 @@ def test_symbol_exported(name):
 def test_struct_sizes_match_ctypes():
     mirrors = [abi.Matrix4x4, abi.Transform, abi.ShapeDesc, abi.MaterialDesc, abi.PrimitiveDesc, abi.BVHNode,
                abi.LightDesc, abi.CameraDesc, abi.FilmDesc, abi.DistributionDesc, abi.SceneDesc, abi.RenderDesc,
-               abi.GpuStats, abi.RaySoA, abi.HitSoA, abi.GpuOpts]
+               abi.GpuStats, abi.RaySoA, abi.HitSoA, abi.GpuOpts, abi.MeshDesc]
     sizes = (C.c_size_t * 32)()
     n = G.lib().pbrt_abi_sizes(sizes, 32)
     assert n == len(mirrors)

@@ -637,3 +637,22 @@ def test_throughput_mode_1080p_sampled_tiles_and_shards():
             g, _ = r.render(abi.render_desc(8, 8, tile_begin=t, tile_end=t + 1, mode=MB))
             o, _ = oracle_render(scene, abi.render_desc(8, 8, tile_begin=t, tile_end=t + 1, mode=MB))
             assert same_bits(g, o), t
+
+
+# ------------------------------------------- config C sampler (256 spp) at small size
+@pytest.mark.parametrize("ci_waves", ["1", "2", "4"])
+def test_cornell_256spp_wave_ci(ci_waves, monkeypatch):
+    """Stratified(16,16) as config C: the continuous-issue chain with its
+    StartPixel staging aliased on the offset ring (19 KB of LDS) and k_paths_ci
+    at 2 pixels per wave; 1, 2 and 4 waves per tile."""
+    monkeypatch.setenv("PBRT_CI_WAVES", ci_waves)
+    check(G.Scene.cornell(48, 32), abi.render_desc(16, 16, max_depth=8), kernel="wave_ci")
+
+
+def test_cornell_256spp_wave_ci_tiles_per_wave():
+    """Several tiles per wave (no staging/ring aliasing) at 256 spp."""
+    check(G.Scene.cornell(64, 32), abi.render_desc(16, 16, max_depth=8), kernel="wave_ci", lanes_per_wave=4)
+
+
+def test_cornell_256spp_throughput_mode():
+    check(G.Scene.cornell(48, 32), abi.render_desc(16, 16, max_depth=8, mode=MB))
