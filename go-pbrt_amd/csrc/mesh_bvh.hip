@@ -93,11 +93,16 @@ __global__ __launch_bounds__(kB) void k_morton(const float* __restrict__ cen, in
         keys[i] = ~0ull;   // padding sorts last
         return;
     }
+    // one scale for all axes (the largest extent): a flat scene (a height field
+    // is 300 x 10 x 300) then spends its top Morton bits on its long axes
+    // instead of splitting along the thin one first
+    float ext = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) ext = fmaxf(ext, ord2f(bounds[3 + k]) - ord2f(bounds[k]));
     uint32_t code = 0;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-        const float lo = ord2f(bounds[k]), hi = ord2f(bounds[3 + k]);
-        const float ext = hi - lo;
+        const float lo = ord2f(bounds[k]);
         float u = ext > 0 ? (cen[(size_t)i * 3 + k] - lo) / ext : 0.5f;
         u = fminf(fmaxf(u, 0.0f), 1.0f);
         const uint32_t q = min((uint32_t)(u * 1024.0f), 1023u);

@@ -838,40 +838,48 @@ __device__ inline void sample_li(const DevScene& sc, const pbrt_light_desc& L, c
     }
 }
 
-// EstimateDirect, light-sampling half (integrator.go:79-130). The BSDF-sampled
+// EstimateDirect, light-sampling half (integrator.go:79-130), up to its
+// visibility test: the shadow ray (SpawnRayToInteraction) and the Ld the
+// estimate returns if that ray is unoccluded. Returns false when no ray is
+// traced (zero pdf, black Li or black f): Ld is then spec(0). The BSDF-sampled
 // MIS half (:132-192) is not executed: no primitive carries an area light
 // (primitive.go:33, GetAreaLight() == nil) so it always contributes 0.
-__device__ inline Spec estimate_direct(const DevScene& sc, uint16_t* stack, int& panic, const SI& si, const BSDF& b,
-                                       int li, V2 u_light) {
+__device__ inline bool estimate_direct_begin(const DevScene& sc, const SI& si, const BSDF& b, int li, V2 u_light,
+                                             Ray& sr, Spec& ld_vis) {
     const pbrt_light_desc& L = sc.lights[li];
     const bool is_delta = L.type != PBRT_LIGHT_DIFFUSE_AREA;
-    Spec Ld = spec(0);
     LightSample ls;
     sample_li(sc, L, si, u_light, ls);
-    if (ls.pdf > 0 && !is_black(ls.Li)) {
-        Spec f = bsdf_f(b, si.wo, ls.wi);
-        double wdn = absdot(ls.wi, si.sn);
-        f = smuls(f, wdn);
-        double scat_pdf = bsdf_pdf(b, si.wo, ls.wi);
-        if (!is_black(f)) {
-            // VisibilityTester.Unoccluded -> SpawnRayToInteraction (interaction.go:91-102, #14)
-            V3 origin = offset_ray_origin(si.p, si.perr, si.n, ls.tp - si.p);
-            V3 target = offset_ray_origin(ls.tp, ls.tperr, ls.tn, origin - ls.tp);
-            Ray sr{si.p, target - origin, 1 - 0.0001, si.time};
-            Spec Li = ls.Li;
-            if (bvh_traverse<true>(sc, sr, nullptr, stack, panic)) Li = spec(0);
-            if (!is_black(Li)) {
-                if (is_delta) {
-                    Ld = Ld + sdivs(smul(f, Li), ls.pdf);
-                } else {
-                    double fp = 1.0 * ls.pdf, gp = 1.0 * scat_pdf;   // PowerHeuristic(1, lightPdf, 1, scatteringPdf)
-                    double w = (fp * fp) / (fp * fp + gp * gp);
-                    Ld = Ld + sdivs(smuls(smul(f, Li), w), ls.pdf);
-                }
-            }
-        }
+    if (!(ls.pdf > 0 && !is_black(ls.Li))) return false;
+    Spec f = bsdf_f(b, si.wo, ls.wi);
+    double wdn = absdot(ls.wi, si.sn);
+    f = smuls(f, wdn);
+    double scat_pdf = bsdf_pdf(b, si.wo, ls.wi);
+    if (is_black(f)) return false;
+    // VisibilityTester.Unoccluded -> SpawnRayToInteraction (interaction.go:91-102, #14)
+    V3 origin = offset_ray_origin(si.p, si.perr, si.n, ls.tp - si.p);
+    V3 target = offset_ray_origin(ls.tp, ls.tperr, ls.tn, origin - ls.tp);
+    sr = Ray{si.p, target - origin, 1 - 0.0001, si.time};
+    Spec Ld = spec(0);
+    if (is_delta) {
+        Ld = Ld + sdivs(smul(f, ls.Li), ls.pdf);
+    } else {
+        double fp = 1.0 * ls.pdf, gp = 1.0 * scat_pdf;   // PowerHeuristic(1, lightPdf, 1, scatteringPdf)
+        double w = (fp * fp) / (fp * fp + gp * gp);
+        Ld = Ld + sdivs(smuls(smul(f, ls.Li), w), ls.pdf);
     }
-    return Ld;
+    ld_vis = Ld;
+    return true;
+}
+// EstimateDirect (integrator.go:79-195): an occluded shadow ray zeroes Li, so
+// Ld stays spec(0).
+__device__ inline Spec estimate_direct(const DevScene& sc, uint16_t* stack, int& panic, const SI& si, const BSDF& b,
+                                       int li, V2 u_light) {
+    Ray sr;
+    Spec ld_vis;
+    if (!estimate_direct_begin(sc, si, b, li, u_light, sr, ld_vis)) return spec(0);
+    if (bvh_traverse<true>(sc, sr, nullptr, stack, panic)) return spec(0);
+    return ld_vis;
 }
 
 // Distribution1D.SampleDiscrete + FindInterval (sampling.go:42-55, math.go:64-80)

@@ -224,6 +224,15 @@ struct PathState {
 };
 // kWhich: 0 any iteration, 1 only the first (s.first == 1: bounce 1 from the
 // pixel cache, no traversal), 2 only later ones (s.first == 0).
+//
+// A traced iteration defers its light sample's shadow ray to the end of the
+// iteration: the light draws, the estimate up to its visibility test, the
+// BSDF sample, the throughput and Russian roulette run first (in the
+// reference's draw order), then the shadow ray is traced and L += beta * Ld
+// with the throughput of the interaction. The interaction and its BSDF are
+// dead by then, so the any-hit traversal runs with their registers free (no
+// scratch spills). Every value and every draw is the reference's; a panic of
+// the shadow ray or Ld > 10 ends the path at this bounce, as it would have.
 template <int kWhich = 0, class Cache>
 __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, const SpecSampler& ss, Cursor& c,
                                  PathState& s, int max_depth, double rr_threshold, uint16_t* stack, int& panic,
@@ -250,6 +259,10 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
         b = pc.b;
         wo = pc.wo;
     }
+    bool pending = false, shadow = false;   // a deferred L += beta0 * Ld (with a shadow ray)
+    Ray sr;
+    Spec ld_vis = spec(0);
+    const Spec beta0 = s.beta;
     if (b.n_bxdfs > 0) {   // UniformSampleOneLight (integrator.go:48-77)
         if (nl == 0) {
             s.L = s.L + smul(s.beta, spec(0));
@@ -263,45 +276,58 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
             }
             V2 ul = c_get2d(c, ss);
             c_get2d(c, ss);
-            Spec ld;
             if (first) {
-                ld = pc.ld[ln];
+                const Spec ld = pc.ld[ln];
                 if (pc.ld_panic[ln]) {
                     panic = pc.ld_panic[ln];
                     return true;
                 }
+                s.L = s.L + smul(s.beta, ld);
             } else {
-                ld = estimate_direct(sc, stack, panic, isect, b, ln, ul);
-                if (panic) return true;
-                if (max_component(ld) > 10) {
-                    panic = PBRT_PANIC_LD_GT_10;
-                    return true;
-                }
+                pending = true;
+                shadow = estimate_direct_begin(sc, isect, b, ln, ul, sr, ld_vis);
             }
-            s.L = s.L + smul(s.beta, ld);
         }
     }
     s.first = 0;
-    V2 u = c_get2d(c, ss);
-    V3 wi;
-    double pdf;
-    Spec f = bsdf_sample_f(b, wo, u, wi, pdf);
-    if (is_black(f) || pdf == 0.0) return true;
-    double wp = absdot(wi, isect.sn) / pdf;
-    s.beta = smul(s.beta, smuls(f, wp));
-    s.ray.o = offset_ray_origin(isect.p, isect.perr, isect.n, wi);
-    s.ray.d = wi;
-    s.ray.tmax = kInf;
-    s.ray.time = isect.time;
-    Spec rr = smuls(s.beta, 1.0);
-    if (max_component(rr) < rr_threshold && s.bounces > 3) {
-        double q = gomath::max(0.05, 1 - max_component(rr));
-        double u1 = c_get1d(c, ss);
-        if (c.kdep) return true;
-        if (u1 < q) return true;
-        s.beta = sdivs(s.beta, 1 - q);
+    bool done = false;
+    {
+        V2 u = c_get2d(c, ss);
+        V3 wi;
+        double pdf;
+        Spec f = bsdf_sample_f(b, wo, u, wi, pdf);
+        if (is_black(f) || pdf == 0.0) {
+            done = true;
+        } else {
+            double wp = absdot(wi, isect.sn) / pdf;
+            s.beta = smul(s.beta, smuls(f, wp));
+            s.ray.o = offset_ray_origin(isect.p, isect.perr, isect.n, wi);
+            s.ray.d = wi;
+            s.ray.tmax = kInf;
+            s.ray.time = isect.time;
+            Spec rr = smuls(s.beta, 1.0);
+            if (max_component(rr) < rr_threshold && s.bounces > 3) {
+                double q = gomath::max(0.05, 1 - max_component(rr));
+                double u1 = c_get1d(c, ss);
+                if (c.kdep || u1 < q) done = true;
+                else s.beta = sdivs(s.beta, 1 - q);
+            }
+        }
     }
-    return false;
+    if (pending) {
+        Spec ld = spec(0);
+        if (shadow) {
+            const bool occluded = bvh_traverse<true>(sc, sr, nullptr, stack, panic);
+            if (panic) return true;
+            if (!occluded) ld = ld_vis;
+        }
+        if (max_component(ld) > 10) {
+            panic = PBRT_PANIC_LD_GT_10;
+            return true;
+        }
+        s.L = s.L + smul(beta0, ld);
+    }
+    return done;
 }
 
 // The rest of one spec_path<false> iteration once the interaction at bounce
