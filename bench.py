@@ -359,6 +359,7 @@ def main():
                 "parallelism": f"tiles mod {world}" + (" + RCCL film reduce" if world > 1 else ""),
                 "kernel": {1: "serial", 2: "wave", 3: "wavefront", 4: "wave_ci"}.get(kernel_kind, "?"),
             },
+            "pipeline_ms": {"kernels": kern_ms, "chain": chain_ms, "paths": paths_ms, "merge": merge_ms},
             "first_frame_ms": first_ms,
             "first_frame_chain_ms": first.chain_ms,
             "roofline": roof,

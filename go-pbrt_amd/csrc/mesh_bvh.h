@@ -10,7 +10,7 @@
 namespace pbrt {
 
 struct MeshBuild {
-    MeshNode* nodes = nullptr;        // [6][n_nodes]
+    MeshNode* nodes = nullptr;        // [kMeshOrders][n_nodes]
     float* tris = nullptr;            // [n_tris][9], leaf order
     int32_t* gid = nullptr;           // [n_tris]
     int32_t* mesh_first = nullptr;    // [n_meshes + 1]

@@ -13,8 +13,8 @@
 //   5. radix-tree topology                 (k_karras: one thread per inner node)
 //   6. boxes, triangle counts and collapsed subtree sizes bottom-up
 //                                          (k_up: the second child to finish climbs)
-//   7. six threaded depth-first layouts    (k_flatten: each kept node finds its
-//      position by walking to the root)
+//   7. eight threaded depth-first layouts  (k_flatten: each kept node finds its
+//      position by walking to the root), one per ray-direction octant
 //
 // Subtrees of <= kMeshLeafMax triangles become one leaf (their triangles are a
 // contiguous key range). Boxes are float32, each triangle's rounded out by one
@@ -247,10 +247,12 @@ __global__ __launch_bounds__(kB) void k_up(const float* __restrict__ tris_s, int
 }
 
 // Each kept node (the root, or a child of an uncollapsed node) walks to the
-// root once and finds its depth-first position in all six orderings: at an
-// ancestor whose nearer child (box centre along the ordering's axis, in the
-// ordering's direction; ties: left) is not on its path it comes after that
-// child's whole subtree.
+// root once and finds its depth-first position in all eight orderings (one
+// per ray-direction octant): at each ancestor the child visited first is the
+// nearer one along that ancestor's split axis (the axis where the children's
+// box centres differ most) for the octant's sign on that axis -- pbrt's
+// front-to-back rule (bvh.go:683-693 uses dirIsNeg[node.axis] the same way).
+// A node whose nearer sibling is on the path comes after that sibling's subtree.
 __global__ __launch_bounds__(kB) void k_flatten(int n, const int32_t* __restrict__ cl, const int32_t* __restrict__ cr,
                                                 const int32_t* __restrict__ parent,
                                                 const int32_t* __restrict__ rfirst, const float* __restrict__ box,
@@ -260,18 +262,26 @@ __global__ __launch_bounds__(kB) void k_flatten(int n, const int32_t* __restrict
     if (v >= 2 * n - 1) return;
     const int pv = parent[v];
     if (pv >= 0 && tc[pv] <= kMeshLeafMax) return;   // inside a collapsed leaf
-    uint32_t pos[6] = {0, 0, 0, 0, 0, 0};
+    uint32_t pos[kMeshOrders];
+#pragma unroll
+    for (int o = 0; o < kMeshOrders; o++) pos[o] = 0;
     int c = v, p = pv, dep = 0;
     while (p >= 0) {
         const int l = cl[p], r = cr[p];
         const int sib = (c == l) ? r : l;
         const uint32_t ssz = (uint32_t)sz[sib];
+        float dl[3];
+        int a = 0;
 #pragma unroll
-        for (int o = 0; o < 6; o++) {
-            const int a = o >> 1;
-            const float cl2 = box[(size_t)l * 6 + a] + box[(size_t)l * 6 + 3 + a];
-            const float cr2 = box[(size_t)r * 6 + a] + box[(size_t)r * 6 + 3 + a];
-            const bool left_first = (o & 1) ? (cl2 >= cr2) : (cl2 <= cr2);
+        for (int k = 0; k < 3; k++)
+            dl[k] = (box[(size_t)l * 6 + k] + box[(size_t)l * 6 + 3 + k]) -
+                    (box[(size_t)r * 6 + k] + box[(size_t)r * 6 + 3 + k]);
+        if (fabsf(dl[1]) > fabsf(dl[a])) a = 1;
+        if (fabsf(dl[2]) > fabsf(dl[a])) a = 2;
+#pragma unroll
+        for (int o = 0; o < kMeshOrders; o++) {
+            const bool neg = (o >> a) & 1;
+            const bool left_first = neg ? (dl[a] >= 0) : (dl[a] <= 0);
             const int first = left_first ? l : r;
             pos[o] += 1u + (c == first ? 0u : ssz);
         }
@@ -292,7 +302,7 @@ __global__ __launch_bounds__(kB) void k_flatten(int n, const int32_t* __restrict
     } else {
         nd.leaf = kMeshInterior;
     }
-    for (int o = 0; o < 6; o++) {
+    for (int o = 0; o < kMeshOrders; o++) {
         nd.escape = pos[o] + (uint32_t)sz[v];
         out[(size_t)o * n_out + pos[o]] = nd;
     }
@@ -429,7 +439,7 @@ int mesh_bvh_build(const pbrt_scene_desc* s, hipStream_t st, MeshBuild& out, std
         MB_CHK(hipGetLastError());
         MB_CHK(hipMemcpyAsync(&n_out, sz, sizeof(int32_t), hipMemcpyDeviceToHost, st));   // root = node 0
         MB_CHK(hipStreamSynchronize(st));
-        MB_CHK(dmalloc(&out.nodes, (size_t)6 * n_out));
+        MB_CHK(dmalloc(&out.nodes, (size_t)kMeshOrders * n_out));
         hipLaunchKernelGGL(k_flatten, dim3((unsigned)((2 * n - 1 + kB - 1) / kB)), dim3(kB), 0, st, n, cl, cr, par,
                            rfirst, box, tc, sz, n_out, out.nodes, depth);
         MB_CHK(hipEventRecord(e1, st));

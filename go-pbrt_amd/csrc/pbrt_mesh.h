@@ -8,19 +8,20 @@
 //  * triangle test: pbrt-v3 Triangle::Intersect (watertight, Woop et al.), in
 //    float64 after exact widening of the float32 world-space vertices, error
 //    bounds with epsilon = 2^-53 (go-pbrt's own Gamma() is denormal, #16);
-//  * accelerator: an LBVH built on the device (mesh_bvh.hip), stored as six
-//    stackless "threaded" node arrays, one per dominant ray direction (+-x,
-//    +-y, +-z): nodes in depth-first order with the child nearer along that
-//    direction first, each node holding the index that follows its subtree
-//    (its escape). A lane walks i -> i + 1 on a box hit and i -> escape on a
-//    miss or after a leaf: no stack, no LDS, one 32-byte node per step;
+//  * accelerator: an LBVH built on the device (mesh_bvh.hip), stored as eight
+//    stackless "threaded" node arrays, one per ray-direction octant: nodes in
+//    depth-first order with, at every node, the child nearer along the node's
+//    split axis for that octant first (pbrt's front-to-back rule), each node
+//    holding the index that follows its subtree (its escape). A lane walks
+//    i -> i + 1 on a box hit and i -> escape on a miss or after a leaf: no
+//    stack, no LDS, one 32-byte node per step;
 //  * closest hit = the smallest (t, global triangle index) over every
 //    triangle hit with t < TMax. The traversal order and the tree shape then
 //    cannot change a result, so the oracle (oracle/oracle_mesh.c) checks this
 //    path with an accelerator of its own.
 //
 // HBM layout (per scene, built once in pbrt_gpu_create):
-//   nodes  [6][n_nodes] MeshNode (32 B: float32 box rounded out by one ulp,
+//   nodes  [8][n_nodes] MeshNode (32 B: float32 box rounded out by one ulp,
 //          escape index, leaf word)
 //   tris   [n_tris][9] float32 vertices in leaf order (36 B per triangle)
 //   gid    [n_tris] global triangle index of each leaf slot (read on a hit)
@@ -40,9 +41,10 @@ struct alignas(16) MeshNode {
 static_assert(sizeof(MeshNode) == 32, "MeshNode is two 16-byte loads");
 constexpr uint32_t kMeshInterior = 0xFFFFFFFFu;
 constexpr int kMeshLeafMax = 4;   // triangles per leaf (subtrees this small are collapsed)
+constexpr int kMeshOrders = 8;    // threaded orderings, one per ray-direction octant
 
 struct DevMesh {
-    const MeshNode* nodes;       // [6][n_nodes]
+    const MeshNode* nodes;       // [kMeshOrders][n_nodes]
     const float* tris;           // [n_tris][9]
     const int32_t* gid;          // [n_tris]
     const int32_t* mesh_first;   // [n_meshes + 1] first global index of each mesh
@@ -113,13 +115,8 @@ GO_HD bool tri_hit(const double* v, const Ray& r, double& t_out, double& b0o, do
     return true;
 }
 
-// Ordering of the threaded node arrays for a ray: 2 * (dominant axis) + (its sign < 0)
-GO_HD int mesh_ordering(V3 d) {
-    const double ax = gomath::abs(d.x), ay = gomath::abs(d.y), az = gomath::abs(d.z);
-    const int a = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
-    const double s = a == 0 ? d.x : a == 1 ? d.y : d.z;
-    return 2 * a + (s < 0 ? 1 : 0);
-}
+// Ordering of the threaded node arrays for a ray: its direction octant
+GO_HD int mesh_ordering(V3 d) { return (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0); }
 
 #ifdef __HIPCC__
 __device__ __forceinline__ void load_tri(const float* __restrict__ tris, uint32_t slot, double v[9]) {

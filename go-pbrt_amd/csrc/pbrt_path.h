@@ -56,6 +56,12 @@ struct DevScene {
     int use_lds_nodes;   // the kernel staged nodes[] in g_nodes_lds (uniform)
     int n_leaves;        // leaves of the BVH (order[8 * n_nodes + oct * n_nodes + j]: leaf preorder)
     DevMesh mesh;        // triangle meshes (extension, pbrt_mesh.h); mesh.n_nodes == 0: none
+    // leaf culling groups of LDS-staged trees (see bvh_walk_analytic): [n_groups][6]
+    // bounds, then per octant [n_groups + 1] leaf-position masks (the last: leaves
+    // that are always tested); n_groups == 0: test every leaf
+    const double* groups;
+    const unsigned long long* gmasks;
+    int n_groups;
 };
 
 // ---------------------------------------------------------------- PCG32 (rng.go)
@@ -235,6 +241,30 @@ __device__ __forceinline__ bool phi_beyond(double y, double x, double phi_max) {
 // `ray` is already in object space (shape_hit), oerr/derr its transform errors.
 __device__ inline bool sphere_hit(const pbrt_shape_desc& s, const Ray& ray, V3 oerr, V3 derr, double& t_hit, V3& ph,
                                   int& panic) {
+    // Early miss: the EFloat values are plain float64 arithmetic on the values
+    // (efloat.go Add/Mul), so the quadratic's discriminant below is computed
+    // here bit for bit without the interval bounds; when it is negative
+    // efloat/math.go:38-40 returns false. With every operand finite and below
+    // 1e100 no Check() (efloat.go:102-111) can panic on the way there, so the
+    // reference returns that same miss.
+    {
+        const double av = (ray.d.x * ray.d.x + ray.d.y * ray.d.y) + ray.d.z * ray.d.z;
+        const double bv = ((ray.d.x * ray.o.x + ray.d.y * ray.o.y) + ray.d.z * ray.o.z) * 2.0;
+        const double cv = ((ray.o.x * ray.o.x + ray.o.y * ray.o.y) + ray.o.z * ray.o.z) - s.radius * s.radius;
+        const double disc = bv * bv - 4. * av * cv;
+        const double big = 1e100;
+        const bool moderate =
+            gomath::abs(ray.o.x) < big && gomath::abs(ray.o.y) < big && gomath::abs(ray.o.z) < big &&
+            gomath::abs(ray.d.x) < big && gomath::abs(ray.d.y) < big && gomath::abs(ray.d.z) < big &&
+            gomath::abs(oerr.x) < big && gomath::abs(oerr.y) < big && gomath::abs(oerr.z) < big &&
+            gomath::abs(derr.x) < big && gomath::abs(derr.y) < big && gomath::abs(derr.z) < big &&
+            gomath::abs(s.radius) < big;
+#ifndef PBRT_NO_EARLY_MISS
+        if (disc < 0 && moderate) return false;
+#else
+        (void)disc; (void)moderate;
+#endif
+    }
     EF ox = ef_new(ray.o.x, oerr.x, panic), oy = ef_new(ray.o.y, oerr.y, panic), oz = ef_new(ray.o.z, oerr.z, panic);
     EF dx = ef_new(ray.d.x, derr.x, panic), dy = ef_new(ray.d.y, derr.y, panic), dz = ef_new(ray.d.z, derr.z, panic);
     EF a = ef_add(ef_add(ef_mul(dx, dx, panic), ef_mul(dy, dy, panic), panic), ef_mul(dz, dz, panic), panic);
@@ -485,6 +515,12 @@ __device__ __forceinline__ bool node_hit(const NodeView& nd, const Ray& r, V3 in
 constexpr uint32_t kOrdNode = 0x7FFFu, kOrdOverflow = 0x8000u;
 // Leaves only, per octant, in that preorder (LDS-staged trees).
 __shared__ uint16_t g_leaf_lds[8 * kLdsNodes];
+// Leaf culling groups (LDS-staged trees): boxes, and per octant the mask of
+// leaf positions (in that octant's leaf preorder) each group covers, plus the
+// mask of leaves tested unconditionally.
+constexpr int kMaxCullGroups = 16;
+__shared__ double g_grp_lds[kMaxCullGroups * 6];
+__shared__ unsigned long long g_gmask_lds[8 * (kMaxCullGroups + 1)];
 
 // Shared leaf-primitive loop of both walks: tests the leaf's primitives in
 // order; returns 1 when an any-hit query is answered, -1 on a panic.
@@ -518,6 +554,11 @@ __device__ __forceinline__ int leaf_prims(const DevScene& sc, uint32_t first, ui
 //
 // LDS-staged trees (<= 64 nodes: README, Cornell) walk only their leaves, in
 // the octant's preorder (g_leaf_lds), each box tested with the current TMax.
+// A leaf whose culling group's box (the union of its members' boxes, built on
+// the host) the ray misses with its initial TMax is skipped: by the same
+// monotonicity its own test would fail with any TMax <= the initial one. The
+// groups only prune tests that fail; the leaves tested, their order and TMax
+// at each test are the reference's.
 // This tests exactly the primitives the reference tests, in its order, with
 // its TMax. A child's box lies inside its parent's (bounds are unions,
 // bvh.go:54-66) and the slab values are monotone in the bounds under
@@ -543,33 +584,55 @@ __device__ inline bool bvh_walk_analytic(const DevScene& sc, Ray& ray, uint16_t*
     if (sc.use_lds_nodes) {   // uniform: n <= kLdsNodes
         (void)stack;
         const int nl = sc.n_leaves;
-        const uint16_t* leaves = g_leaf_lds + (nx | (ny << 1) | (nz << 2)) * kLdsNodes;
-        int j = 0;
+        const int oct = nx | (ny << 1) | (nz << 2);
+        const uint16_t* leaves = g_leaf_lds + oct * kLdsNodes;
+        // candidate leaves: the unconditional ones, plus the members of every
+        // group whose box the ray enters (initial TMax)
+        unsigned long long cand;
+        const int ng = sc.n_groups;
+        if (ng > 0) {
+            const unsigned long long* gm = g_gmask_lds + oct * (kMaxCullGroups + 1);
+            cand = gm[ng];
+            for (int g = 0; g < ng; g++) {
+                NodeView gv;
+#pragma unroll
+                for (int k = 0; k < 6; k++) gv.b[k] = g_grp_lds[g * 6 + k];
+                if (node_hit(gv, ray, inv, nx, ny, nz)) cand |= gm[g];
+            }
+        } else {
+            cand = nl >= 64 ? ~0ull : ((1ull << nl) - 1ull);
+        }
         for (;;) {
-            // A: the next leaf in the octant's preorder whose box the ray enters
+            // A: the next candidate leaf in the octant's preorder whose box the ray enters
             bool leaf = false;
             uint32_t first = 0, np = 0;
-            // four leaves per iteration: independent loads and slab tests overlap;
+            // four candidates per iteration: independent loads and slab tests overlap;
             // a later result is used only if the earlier leaves miss (same TMax)
-            while (j < nl) {
-                const int j1 = j + 1 < nl ? j + 1 : j, j2 = j + 2 < nl ? j + 2 : j, j3 = j + 3 < nl ? j + 3 : j;
-                const NodeView n0 = load_node(sc, leaves[j]);
+            while (cand) {
+                const int j0 = __builtin_ctzll(cand);
+                const unsigned long long r1 = cand & (cand - 1);
+                const int j1 = r1 ? __builtin_ctzll(r1) : j0;
+                const unsigned long long r2 = r1 & (r1 - 1);
+                const int j2 = r2 ? __builtin_ctzll(r2) : j0;
+                const unsigned long long r3 = r2 & (r2 - 1);
+                const int j3 = r3 ? __builtin_ctzll(r3) : j0;
+                const NodeView n0 = load_node(sc, leaves[j0]);
                 const NodeView n1 = load_node(sc, leaves[j1]);
                 const NodeView n2 = load_node(sc, leaves[j2]);
                 const NodeView n3 = load_node(sc, leaves[j3]);
                 const bool h0 = node_hit(n0, ray, inv, nx, ny, nz);
-                const bool h1 = j1 > j && node_hit(n1, ray, inv, nx, ny, nz);
-                const bool h2 = j2 > j && node_hit(n2, ray, inv, nx, ny, nz);
-                const bool h3 = j3 > j && node_hit(n3, ray, inv, nx, ny, nz);
+                const bool h1 = j1 != j0 && node_hit(n1, ray, inv, nx, ny, nz);
+                const bool h2 = j2 != j0 && node_hit(n2, ray, inv, nx, ny, nz);
+                const bool h3 = j3 != j0 && node_hit(n3, ray, inv, nx, ny, nz);
                 if (h0 | h1 | h2 | h3) {
                     leaf = true;
                     const int q = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
                     first = q == 0 ? n0.offset : q == 1 ? n1.offset : q == 2 ? n2.offset : n3.offset;
                     np = q == 0 ? n0.n_prims : q == 1 ? n1.n_prims : q == 2 ? n2.n_prims : n3.n_prims;
-                    j += q + 1;
+                    cand = q == 0 ? r1 : q == 1 ? r2 : q == 2 ? r3 : (r3 & (r3 - 1));
                     break;
                 }
-                j += 4;
+                cand = r3 & (r3 - 1);
             }
             STEP_T(if (!kAny) tt.mark(5);)
             if (!leaf) break;

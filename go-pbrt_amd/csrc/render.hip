@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "../../include/pbrt_gpu.h"
@@ -268,6 +269,11 @@ __device__ __forceinline__ void stage_nodes(DevScene& sc) {
     for (int i = threadIdx.x; i < 8 * sc.n_nodes; i += blockDim.x) {
         const int oct = i / sc.n_nodes, j = i - oct * sc.n_nodes;
         if (j < sc.n_leaves) g_leaf_lds[oct * kLdsNodes + j] = (uint16_t)sc.order[8 * sc.n_nodes + i];
+    }
+    for (int i = threadIdx.x; i < sc.n_groups * 6; i += blockDim.x) g_grp_lds[i] = sc.groups[i];
+    for (int i = threadIdx.x; i < 8 * (sc.n_groups + 1) && sc.n_groups > 0; i += blockDim.x) {
+        const int oct = i / (sc.n_groups + 1), g = i - oct * (sc.n_groups + 1);
+        g_gmask_lds[oct * (kMaxCullGroups + 1) + g] = sc.gmasks[i];
     }
     __syncthreads();
     sc.use_lds_nodes = 1;
@@ -1888,6 +1894,9 @@ struct pbrt_gpu_ctx {
     pbrt_primitive_desc* d_prims = nullptr;
     DevNode* d_nodes = nullptr;
     uint32_t* d_order = nullptr;     // [8][n_nodes] preorder visit tables, then [8][n_nodes] leaf lists (dev_order)
+    double* d_groups = nullptr;      // leaf culling groups (cull_groups)
+    unsigned long long* d_gmasks = nullptr;
+    int n_groups = 0;
     std::vector<int> h_node_prims;   // nPrimitives per node (leaf count for DevScene)
     DevPrim* d_fprims = nullptr;
     pbrt_light_desc* d_lights = nullptr;
@@ -1972,6 +1981,9 @@ DevScene dev_scene(const pbrt_gpu_ctx* c, bool with_dist) {
     s.n_leaves = 0;
     for (int i = 0; i < c->host_scene.n_nodes; i++) s.n_leaves += c->h_node_prims[i] > 0;
     s.mesh = c->mesh.view();
+    s.groups = c->d_groups;
+    s.gmasks = c->d_gmasks;
+    s.n_groups = c->n_groups;
     return s;
 }
 
@@ -2045,6 +2057,81 @@ bool dev_order(const pbrt_scene_desc* s, std::vector<uint32_t>& out) {
         }
     }
     return true;
+}
+
+// Leaf culling groups of an LDS-staged tree (bvh_walk_analytic): leaves whose
+// box diagonal exceeds half the root's (the README floor and wall disks) and
+// singletons are tested unconditionally; the others are split recursively at
+// the median of their box centres along the widest axis into groups of <= 8
+// (the README's three rows of seven spheres become row segments). A group's
+// box is the exact union of its members' boxes. Output: boxes [G][6], then per
+// octant [G + 1] masks over the octant's leaf preorder positions (last: the
+// unconditional leaves). G = 0 (no culling) when the tree is not LDS-staged
+// or the grouping needs more than kMaxCullGroups groups.
+int cull_groups(const pbrt_scene_desc* s, const std::vector<uint32_t>& order, std::vector<double>& boxes,
+                std::vector<unsigned long long>& masks) {
+    boxes.clear();
+    masks.clear();
+    const int n = s->n_nodes;
+    if (n == 0 || n > kLdsNodes) return 0;
+    std::vector<int> leaves;
+    for (int i = 0; i < n; i++)
+        if (s->nodes[i].n_prims > 0) leaves.push_back(i);
+    if (leaves.size() > 64) return 0;
+    auto diag2 = [&](int i) {
+        double d = 0;
+        for (int k = 0; k < 3; k++) d += (s->nodes[i].bmax[k] - s->nodes[i].bmin[k]) * (s->nodes[i].bmax[k] - s->nodes[i].bmin[k]);
+        return d;
+    };
+    const double root = diag2(0);
+    std::vector<int> rest;
+    std::vector<int> group_of((size_t)n, -1);   // -1: unconditional
+    for (int v : leaves)
+        if (!(diag2(v) > 0.25 * root)) rest.push_back(v);
+    std::vector<std::vector<int>> groups;
+    std::function<void(std::vector<int>)> split = [&](std::vector<int> g) {
+        if (g.size() <= 8) {
+            if (g.size() > 1) groups.push_back(g);
+            return;
+        }
+        double lo[3] = {kInf, kInf, kInf}, hi[3] = {-kInf, -kInf, -kInf};
+        auto cen = [&](int v, int k) { return 0.5 * (s->nodes[v].bmin[k] + s->nodes[v].bmax[k]); };
+        for (int v : g)
+            for (int k = 0; k < 3; k++) { lo[k] = std::min(lo[k], cen(v, k)); hi[k] = std::max(hi[k], cen(v, k)); }
+        int a = 0;
+        for (int k = 1; k < 3; k++)
+            if (hi[k] - lo[k] > hi[a] - lo[a]) a = k;
+        std::stable_sort(g.begin(), g.end(), [&](int x, int y) { return cen(x, a) < cen(y, a); });
+        const size_t h = g.size() / 2;
+        split(std::vector<int>(g.begin(), g.begin() + (long)h));
+        split(std::vector<int>(g.begin() + (long)h, g.end()));
+    };
+    if (!rest.empty()) split(rest);
+    const int G = (int)groups.size();
+    if (G == 0 || G > kMaxCullGroups) return 0;
+    boxes.assign((size_t)G * 6, 0.0);
+    for (int gi = 0; gi < G; gi++) {
+        for (int k = 0; k < 3; k++) {
+            boxes[(size_t)gi * 6 + k] = kInf;
+            boxes[(size_t)gi * 6 + 3 + k] = -kInf;
+        }
+        for (int v : groups[(size_t)gi]) {
+            group_of[(size_t)v] = gi;
+            for (int k = 0; k < 3; k++) {
+                boxes[(size_t)gi * 6 + k] = std::min(boxes[(size_t)gi * 6 + k], s->nodes[v].bmin[k]);
+                boxes[(size_t)gi * 6 + 3 + k] = std::max(boxes[(size_t)gi * 6 + 3 + k], s->nodes[v].bmax[k]);
+            }
+        }
+    }
+    masks.assign((size_t)8 * (G + 1), 0ull);
+    const int nl = (int)leaves.size();
+    for (int oct = 0; oct < 8; oct++)
+        for (int j = 0; j < nl; j++) {
+            const uint32_t node = order[(size_t)8 * n + (size_t)oct * n + (size_t)j];
+            const int gi = group_of[node];
+            masks[(size_t)oct * (G + 1) + (size_t)(gi < 0 ? G : gi)] |= 1ull << j;
+        }
+    return G;
 }
 
 std::vector<DevPrim> dev_prims(const pbrt_scene_desc* s) {
@@ -2566,6 +2653,18 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
         pbrt_gpu_destroy(c);
         return rc;
     }
+    {   // leaf culling groups of the LDS-staged walk
+        std::vector<double> gb;
+        std::vector<unsigned long long> gm;
+        c->n_groups = cull_groups(scene, order, gb, gm);
+        if (const char* e = getenv("PBRT_CULL_GROUPS"))   // 0: test every leaf (A/B)
+            if (atoi(e) == 0) c->n_groups = 0;
+        if (c->n_groups > 0 && ((rc = upload(c, &c->d_groups, gb.data(), gb.size())) ||
+                                (rc = upload(c, &c->d_gmasks, gm.data(), gm.size())))) {
+            pbrt_gpu_destroy(c);
+            return rc;
+        }
+    }
     if (scene->n_meshes > 0) {   // triangle meshes: LBVH built on the device (mesh_bvh.hip)
         std::string err;
         rc = mesh_bvh_build(scene, c->stream, c->mesh, err);
@@ -2936,7 +3035,8 @@ void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_shapes, c->d_materials, c->d_prims, c->d_nodes, c->d_order, c->d_lights, c->d_camera, c->d_film,
                     c->d_dist,   c->d_films,     c->d_s1d,   c->d_panics, c->d_ctr,   c->d_out,    c->d_jump,
-                    c->d_wave,   c->d_fprims, c->d_wf,     c->d_ticks, c->d_slot_order};
+                    c->d_wave,   c->d_fprims, c->d_wf,     c->d_ticks, c->d_slot_order, c->d_groups,
+                    c->d_gmasks};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     mesh_bvh_free(c->mesh);
@@ -3107,7 +3207,7 @@ extern "C" int pbrt_gpu_mesh_counters(uint64_t* out, int n, int reset) {
 extern "C" int pbrt_gpu_mesh_download(pbrt_gpu_ctx* c, void* nodes, int32_t* gid, float* tris) {
     if (!c) return PBRT_E_INVALID;
     if (hipSetDevice(c->device) != hipSuccess) return PBRT_E_HIP;
-    const size_t nn = (size_t)c->mesh.n_nodes * 6, nt = (size_t)c->mesh.n_tris;
+    const size_t nn = (size_t)c->mesh.n_nodes * kMeshOrders, nt = (size_t)c->mesh.n_tris;
     if (nodes && nn && hipMemcpy(nodes, c->mesh.nodes, nn * sizeof(MeshNode), hipMemcpyDeviceToHost) != hipSuccess)
         return PBRT_E_HIP;
     if (gid && nt && hipMemcpy(gid, c->mesh.gid, nt * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)

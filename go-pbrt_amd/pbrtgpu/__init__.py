@@ -363,18 +363,18 @@ class Renderer:
                 "meshes": int(out[4])}
 
     def mesh_download(self):
-        """(nodes [6, n] structured array, gid [tris], tris [tris, 9]) of the device LBVH."""
+        """(nodes [8, n] structured array, gid [tris], tris [tris, 9]) of the device LBVH."""
         info = self.mesh_info()
         dt = np.dtype([("bmin", np.float32, 3), ("escape", np.uint32), ("bmax", np.float32, 3),
                        ("leaf", np.uint32)])
-        nodes = np.zeros(6 * info["nodes"], dtype=dt)
+        nodes = np.zeros(8 * info["nodes"], dtype=dt)
         gid = np.zeros(info["tris"], dtype=np.int32)
         tris = np.zeros((info["tris"], 9), dtype=np.float32)
         rc = lib().pbrt_gpu_mesh_download(self.h, nodes.ctypes.data_as(C.c_void_p),
                                           gid.ctypes.data_as(C.POINTER(C.c_int32)),
                                           tris.ctypes.data_as(C.POINTER(C.c_float)))
         self._check(rc)
-        return nodes.reshape(6, info["nodes"]), gid, tris
+        return nodes.reshape(8, info["nodes"]), gid, tris
 
     def tile_ticks(self):
         """(per-slot chain ticks of the last EXACT frame at 100 MHz, heavy slots of its split)."""

@@ -66,7 +66,7 @@ int64_t pbrt_gpu_tile_ticks(struct pbrt_gpu_ctx* ctx, uint32_t* out, int64_t n, 
  * (zero-area ones are left out), nodes per ordering, deepest leaf, device
  * build ms, meshes}. Returns the number of values. */
 int pbrt_gpu_mesh_info(struct pbrt_gpu_ctx* ctx, double* out, int n);
-/* Copies the device LBVH: nodes = 6 * nodes-per-ordering records of 32 bytes
+/* Copies the device LBVH: nodes = 8 * nodes-per-ordering records of 32 bytes
  * (float bmin[3], uint32 escape, float bmax[3], uint32 leaf: 0xFFFFFFFF for an
  * interior node, else first_slot << 3 | count), gid = the global triangle
  * index of each leaf slot, tris = 9 floats per slot. Any pointer may be NULL. */

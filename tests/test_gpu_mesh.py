@@ -50,9 +50,9 @@ def test_lbvh_structure(quads):
     assert sorted(gid.tolist()) == list(range(nt))
     assert np.array_equal(tris, tris_in[gid])
     n = info["nodes"]
-    assert nodes.shape == (6, n) and n >= 1
+    assert nodes.shape == (8, n) and n >= 1
     recs = None
-    for o in range(6):
+    for o in range(8):
         N = nodes[o]
         covered = np.zeros(nt, dtype=np.int32)
 
@@ -77,7 +77,7 @@ def test_lbvh_structure(quads):
         assert (covered == 1).all()
         rec = sorted((tuple(N[i]["bmin"]), tuple(N[i]["bmax"]), int(N[i]["leaf"])) for i in range(n))
         recs = rec if recs is None else recs
-        assert rec == recs   # the six orderings hold the same nodes
+        assert rec == recs   # the eight orderings hold the same nodes
 
 
 def random_rays(n, seed):
