@@ -60,7 +60,7 @@ struct DevScene {
     // bounds, then per octant [n_groups + 1] leaf-position masks (the last: leaves
     // that are always tested); n_groups == 0: test every leaf
     const double* groups;
-    const unsigned long long* gmasks;
+    const uint32_t* gmasks;
     int n_groups;
 };
 
@@ -520,7 +520,7 @@ __shared__ uint16_t g_leaf_lds[8 * kLdsNodes];
 // mask of leaves tested unconditionally.
 constexpr int kMaxCullGroups = 16;
 __shared__ double g_grp_lds[kMaxCullGroups * 6];
-__shared__ unsigned long long g_gmask_lds[8 * (kMaxCullGroups + 1)];
+__shared__ uint32_t g_gmask_lds[8 * (kMaxCullGroups + 1)];
 
 // Shared leaf-primitive loop of both walks: tests the leaf's primitives in
 // order; returns 1 when an any-hit query is answered, -1 on a panic.
@@ -586,53 +586,86 @@ __device__ inline bool bvh_walk_analytic(const DevScene& sc, Ray& ray, uint16_t*
         const int nl = sc.n_leaves;
         const int oct = nx | (ny << 1) | (nz << 2);
         const uint16_t* leaves = g_leaf_lds + oct * kLdsNodes;
-        // candidate leaves: the unconditional ones, plus the members of every
-        // group whose box the ray enters (initial TMax)
-        unsigned long long cand;
         const int ng = sc.n_groups;
-        if (ng > 0) {
-            const unsigned long long* gm = g_gmask_lds + oct * (kMaxCullGroups + 1);
-            cand = gm[ng];
+        if (ng > 0) {   // uniform; the host groups trees of <= 32 leaves only
+            // candidate leaves: the unconditional ones, plus the members of
+            // every group whose box the ray enters (initial TMax)
+            const uint32_t* gm = g_gmask_lds + oct * (kMaxCullGroups + 1);
+            uint32_t cand = gm[ng];
             for (int g = 0; g < ng; g++) {
                 NodeView gv;
 #pragma unroll
                 for (int k = 0; k < 6; k++) gv.b[k] = g_grp_lds[g * 6 + k];
                 if (node_hit(gv, ray, inv, nx, ny, nz)) cand |= gm[g];
             }
-        } else {
-            cand = nl >= 64 ? ~0ull : ((1ull << nl) - 1ull);
+            for (;;) {
+                // A: the next candidate in the octant's leaf preorder whose box the
+                // ray enters; four per iteration (independent loads and slab tests;
+                // a later result is used only if the earlier ones miss, same TMax)
+                bool leaf = false;
+                uint32_t first = 0, np = 0;
+                while (cand) {
+                    const int j0 = __builtin_ctz(cand);
+                    const uint32_t r1 = cand & (cand - 1);
+                    const int j1 = r1 ? __builtin_ctz(r1) : j0;
+                    const uint32_t r2 = r1 & (r1 - 1);
+                    const int j2 = r2 ? __builtin_ctz(r2) : j0;
+                    const uint32_t r3 = r2 & (r2 - 1);
+                    const int j3 = r3 ? __builtin_ctz(r3) : j0;
+                    const NodeView n0 = load_node(sc, leaves[j0]);
+                    const NodeView n1 = load_node(sc, leaves[j1]);
+                    const NodeView n2 = load_node(sc, leaves[j2]);
+                    const NodeView n3 = load_node(sc, leaves[j3]);
+                    const bool h0 = node_hit(n0, ray, inv, nx, ny, nz);
+                    const bool h1 = j1 != j0 && node_hit(n1, ray, inv, nx, ny, nz);
+                    const bool h2 = j2 != j0 && node_hit(n2, ray, inv, nx, ny, nz);
+                    const bool h3 = j3 != j0 && node_hit(n3, ray, inv, nx, ny, nz);
+                    if (h0 | h1 | h2 | h3) {
+                        leaf = true;
+                        const int q = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
+                        first = q == 0 ? n0.offset : q == 1 ? n1.offset : q == 2 ? n2.offset : n3.offset;
+                        np = q == 0 ? n0.n_prims : q == 1 ? n1.n_prims : q == 2 ? n2.n_prims : n3.n_prims;
+                        cand = q == 0 ? r1 : q == 1 ? r2 : q == 2 ? r3 : (r3 & (r3 - 1));
+                        break;
+                    }
+                    cand = r3 & (r3 - 1);
+                }
+                STEP_T(if (!kAny) tt.mark(5);)
+                if (!leaf) break;
+                // B: its primitives
+                const int r = leaf_prims<kAny>(sc, first, np, ray, panic, best, best_ph);
+                if (r < 0) return kAny ? false : best >= 0;
+                if (kAny && r > 0) return true;
+                STEP_T(if (!kAny) tt.mark(6);)
+            }
+            return best >= 0;
         }
+        int j = 0;
         for (;;) {
-            // A: the next candidate leaf in the octant's preorder whose box the ray enters
+            // A: the next leaf in the octant's preorder whose box the ray enters
             bool leaf = false;
             uint32_t first = 0, np = 0;
-            // four candidates per iteration: independent loads and slab tests overlap;
+            // four leaves per iteration: independent loads and slab tests overlap;
             // a later result is used only if the earlier leaves miss (same TMax)
-            while (cand) {
-                const int j0 = __builtin_ctzll(cand);
-                const unsigned long long r1 = cand & (cand - 1);
-                const int j1 = r1 ? __builtin_ctzll(r1) : j0;
-                const unsigned long long r2 = r1 & (r1 - 1);
-                const int j2 = r2 ? __builtin_ctzll(r2) : j0;
-                const unsigned long long r3 = r2 & (r2 - 1);
-                const int j3 = r3 ? __builtin_ctzll(r3) : j0;
-                const NodeView n0 = load_node(sc, leaves[j0]);
+            while (j < nl) {
+                const int j1 = j + 1 < nl ? j + 1 : j, j2 = j + 2 < nl ? j + 2 : j, j3 = j + 3 < nl ? j + 3 : j;
+                const NodeView n0 = load_node(sc, leaves[j]);
                 const NodeView n1 = load_node(sc, leaves[j1]);
                 const NodeView n2 = load_node(sc, leaves[j2]);
                 const NodeView n3 = load_node(sc, leaves[j3]);
                 const bool h0 = node_hit(n0, ray, inv, nx, ny, nz);
-                const bool h1 = j1 != j0 && node_hit(n1, ray, inv, nx, ny, nz);
-                const bool h2 = j2 != j0 && node_hit(n2, ray, inv, nx, ny, nz);
-                const bool h3 = j3 != j0 && node_hit(n3, ray, inv, nx, ny, nz);
+                const bool h1 = j1 > j && node_hit(n1, ray, inv, nx, ny, nz);
+                const bool h2 = j2 > j && node_hit(n2, ray, inv, nx, ny, nz);
+                const bool h3 = j3 > j && node_hit(n3, ray, inv, nx, ny, nz);
                 if (h0 | h1 | h2 | h3) {
                     leaf = true;
                     const int q = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
                     first = q == 0 ? n0.offset : q == 1 ? n1.offset : q == 2 ? n2.offset : n3.offset;
                     np = q == 0 ? n0.n_prims : q == 1 ? n1.n_prims : q == 2 ? n2.n_prims : n3.n_prims;
-                    cand = q == 0 ? r1 : q == 1 ? r2 : q == 2 ? r3 : (r3 & (r3 - 1));
+                    j += q + 1;
                     break;
                 }
-                cand = r3 & (r3 - 1);
+                j += 4;
             }
             STEP_T(if (!kAny) tt.mark(5);)
             if (!leaf) break;

@@ -12,6 +12,7 @@
 #include <memory>
 #include <vector>
 
+#include "../../include/pbrt_diag.h"
 #include "../../include/pbrt_scene.h"
 #include "pbrt_core.h"
 
@@ -824,6 +825,55 @@ int pbrt_scene_cornell(int64_t w, int64_t h, pbrt_scene_builder** out) {
     if (rc != PBRT_OK) { pbrt_sb_destroy(b); return rc; }
     *out = b;
     return PBRT_OK;
+}
+
+
+// ------------------------------------------------------------- diagnostics
+int pbrt_diag_vec_op(int op, const double* a, const double* b, double s, double* out) {
+    const V3 x = load3(a), y = b ? load3(b) : V3{0, 0, 0};
+    const Spec p = spec3(a), q = b ? spec3(b) : spec(0);
+    V3 r{0, 0, 0};
+    Spec t = spec(0);
+    bool vec = true, sp = false;
+    double sc = 0;
+    switch (op) {
+        case PBRT_VOP_ABS: r = vabs(x); break;
+        case PBRT_VOP_ABSDOT: sc = absdot(x, y); vec = false; break;
+        case PBRT_VOP_ADD: r = x + y; break;
+        case PBRT_VOP_CROSS: r = cross(x, y); break;
+        case PBRT_VOP_DISTANCE: sc = dist(x, y); vec = false; break;
+        case PBRT_VOP_DISTANCE_SQUARED: sc = dist2(x, y); vec = false; break;
+        case PBRT_VOP_DIV: r = divv(x, y); break;
+        case PBRT_VOP_DIV_SCALAR: r = divs(x, s); break;
+        case PBRT_VOP_DOT: sc = dot(x, y); vec = false; break;
+        case PBRT_VOP_LENGTH: sc = length(x); vec = false; break;
+        case PBRT_VOP_LENGTH_SQUARED: sc = len2(x); vec = false; break;
+        case PBRT_VOP_MUL: r = mul(x, y); break;
+        case PBRT_VOP_MUL_SCALAR: r = muls(x, s); break;
+        case PBRT_VOP_NORMALIZED: r = normalized(x); break;
+        case PBRT_VOP_SUB: r = x - y; break;
+        case PBRT_SOP_ADD: t = p + q; sp = true; break;
+        case PBRT_SOP_MUL: t = smul(p, q); sp = true; break;
+        case PBRT_SOP_DIV_SCALAR: t = sdivs(p, s); sp = true; break;
+        case PBRT_SOP_MUL_SCALAR: t = smuls(p, s); sp = true; break;
+        case PBRT_SOP_IS_BLACK: sc = is_black(p) ? 1.0 : 0.0; vec = false; break;
+        default: return PBRT_E_INVALID;
+    }
+    if (sp) { out[0] = t.r; out[1] = t.g; out[2] = t.b; }
+    else if (vec) { out[0] = r.x; out[1] = r.y; out[2] = r.z; }
+    else { out[0] = sc; out[1] = out[2] = 0; }
+    return PBRT_OK;
+}
+
+int64_t pbrt_diag_partition_at(int32_t* prim, double* cx, int64_t n, int64_t start, int64_t end, int64_t pivot) {
+    if (!prim || !cx || n <= 0 || start < 0 || end >= n || pivot < start || pivot > end || start > end) return -1;
+    BVHBuilder bb;
+    for (int64_t i = 0; i < n; i++) bb.info.push_back(PrimInfo{prim[i], Bounds{}, V3{cx[i], 0, 0}});
+    const int64_t m = bb.partition_at(start, end, pivot, [](const PrimInfo& x, const PrimInfo& y) {
+        return x.centroid.x < y.centroid.x;
+    });
+    for (int64_t i = 0; i < n; i++) { prim[i] = bb.info[(size_t)i].prim; cx[i] = bb.info[(size_t)i].centroid.x; }
+    return m;
 }
 
 }  // extern "C"

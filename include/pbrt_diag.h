@@ -42,6 +42,26 @@ enum {
     PBRT_PROBE_EFLOAT_DIV = 23         /* in v1 e1 v2 e2 -> value low high panic */
 };
 
+/* Host instantiation of the float64 vector / spectrum operations the kernels
+ * use (csrc/pbrt_core.h, compiled for host and device from one source), for
+ * the reference's pkg/geometry/xyz_test.go and pkg/pbrt/spectrum_test.go
+ * known answers. a, b: 3 doubles; s: scalar; out: 3 doubles (scalars in out[0]). */
+enum {
+    PBRT_VOP_ABS = 1, PBRT_VOP_ABSDOT = 2, PBRT_VOP_ADD = 3, PBRT_VOP_CROSS = 4, PBRT_VOP_DISTANCE = 5,
+    PBRT_VOP_DISTANCE_SQUARED = 6, PBRT_VOP_DIV = 7, PBRT_VOP_DIV_SCALAR = 8, PBRT_VOP_DOT = 9,
+    PBRT_VOP_LENGTH = 10, PBRT_VOP_LENGTH_SQUARED = 11, PBRT_VOP_MUL = 12, PBRT_VOP_MUL_SCALAR = 13,
+    PBRT_VOP_NORMALIZED = 14, PBRT_VOP_SUB = 15,
+    PBRT_SOP_ADD = 16, PBRT_SOP_MUL = 17, PBRT_SOP_DIV_SCALAR = 18, PBRT_SOP_IS_BLACK = 19,
+    PBRT_SOP_MUL_SCALAR = 20
+};
+int pbrt_diag_vec_op(int op, const double* a, const double* b, double s, double* out);
+
+/* The BVH builder's PartitionPrimitiveInfoAt (bvh.go:163-175, Lomuto around
+ * in[pivot] moved to `end`) on records (prim[i], centroid x = cx[i]) with the
+ * less-than-on-centroid-x predicate of pkg/accelerator/bvh_test.go:143-264;
+ * permutes both arrays in place and returns the pivot's final index. */
+int64_t pbrt_diag_partition_at(int32_t* prim, double* cx, int64_t n, int64_t start, int64_t end, int64_t pivot);
+
 /* Inputs: n records of in_stride doubles; outputs: n records of out_stride. */
 int pbrt_gpu_probe(int device, int op, const double* in, size_t n, int in_stride, double* out, int out_stride);
 

@@ -164,3 +164,46 @@ int oracle_triangle_hit(const double v[9], const double ray[7], double out[4]) {
     r.time = 0;
     return orc_triangle_hit(v, &r, &out[0], &out[1], &out[2], &out[3]);
 }
+
+/* ---------------------------------- pkg/geometry/xyz_test.go, spectrum_test.go */
+#include "../include/pbrt_diag.h"
+/* the oracle's XYZFloat64 (xyz.go:424-614) and Spectrum (spectrum.go:35-233)
+ * operations, op codes of include/pbrt_diag.h */
+int oracle_vec_op(int op, const double* a, const double* b, double s, double* out) {
+    v3 x = V3(a[0], a[1], a[2]), y = b ? V3(b[0], b[1], b[2]) : V3(0, 0, 0), r = V3(0, 0, 0);
+    spec p = S3(a[0], a[1], a[2]), q = b ? S3(b[0], b[1], b[2]) : S3(0, 0, 0), t = S3(0, 0, 0);
+    int vec = 1, sp = 0;
+    double sc = 0;
+    switch (op) {
+        case PBRT_VOP_ABS: r = v_abs(x); break;
+        case PBRT_VOP_ABSDOT: sc = v_absdot(x, y); vec = 0; break;
+        case PBRT_VOP_ADD: r = v_add(x, y); break;
+        case PBRT_VOP_CROSS: r = v_cross(x, y); break;
+        case PBRT_VOP_DISTANCE: sc = v_dist(x, y); vec = 0; break;
+        case PBRT_VOP_DISTANCE_SQUARED: sc = v_dist2(x, y); vec = 0; break;
+        case PBRT_VOP_DIV: r = v_divv(x, y); break;
+        case PBRT_VOP_DIV_SCALAR: r = v_divs(x, s); break;
+        case PBRT_VOP_DOT: sc = v_dot(x, y); vec = 0; break;
+        case PBRT_VOP_LENGTH: sc = v_len(x); vec = 0; break;
+        case PBRT_VOP_LENGTH_SQUARED: sc = v_len2(x); vec = 0; break;
+        case PBRT_VOP_MUL: r = v_mul(x, y); break;
+        case PBRT_VOP_MUL_SCALAR: r = v_muls(x, s); break;
+        case PBRT_VOP_NORMALIZED: r = v_normalized(x); break;
+        case PBRT_VOP_SUB: r = v_sub(x, y); break;
+        case PBRT_SOP_ADD: t = s_add(p, q); sp = 1; break;
+        case PBRT_SOP_MUL: t = s_mul(p, q); sp = 1; break;
+        case PBRT_SOP_DIV_SCALAR: t = s_divs(p, s); sp = 1; break;
+        case PBRT_SOP_MUL_SCALAR: t = s_muls(p, s); sp = 1; break;
+        case PBRT_SOP_IS_BLACK: sc = s_is_black(p); vec = 0; break;
+        default: return 1;
+    }
+    if (sp) { out[0] = t.c[0]; out[1] = t.c[1]; out[2] = t.c[2]; }
+    else if (vec) { out[0] = r.x; out[1] = r.y; out[2] = r.z; }
+    else { out[0] = sc; out[1] = out[2] = 0; }
+    return 0;
+}
+
+int64_t orc_partition_at_x(int32_t* prim, double* cx, int64_t n, int64_t start, int64_t end, int64_t pivot);
+int64_t oracle_partition_at(int32_t* prim, double* cx, int64_t n, int64_t start, int64_t end, int64_t pivot) {
+    return orc_partition_at_x(prim, cx, n, start, end, pivot);
+}

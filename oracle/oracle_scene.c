@@ -600,3 +600,15 @@ void orc_scene_desc(orc_scene* sc, pbrt_scene_desc* d) {
     for (int k = 0; k < 3; k++) { d->world_min[k] = sc->world_min[k]; d->world_max[k] = sc->world_max[k]; }
 }
 void orc_scene_free(orc_scene* sc) { free(sc); }
+
+/* bvh.go:163-175 PartitionPrimitiveInfoAt with bvh_test.go's centroid-x
+ * predicate (mode 0, dim 0) on (prim, cx) records; for tests/ */
+int64_t orc_partition_at_x(int32_t* prim, double* cx, int64_t n, int64_t start, int64_t end, int64_t pivot) {
+    if (n <= 0 || start < 0 || end >= n || pivot < start || pivot > end || start > end) return -1;
+    prim_info* in = (prim_info*)calloc((size_t)n, sizeof(prim_info));
+    for (int64_t i = 0; i < n; i++) { in[i].prim = prim[i]; in[i].c = V3(cx[i], 0, 0); }
+    int64_t m = partition_at(in, start, end, pivot, 0, 0, NULL, 0);
+    for (int64_t i = 0; i < n; i++) { prim[i] = in[i].prim; cx[i] = in[i].c.x; }
+    free(in);
+    return m;
+}

@@ -110,6 +110,9 @@ def _bind(L):
         L.oracle_light_distribution.argtypes = [P(abi.SceneDesc), P(abi.RenderDesc), P(abi.DistributionDesc)]
         L.oracle_spawn_ray_to.argtypes = [P(d), P(d)]
         L.oracle_triangle_hit.argtypes = [P(d), P(d), P(d)]
+        L.oracle_vec_op.argtypes = [C.c_int, P(d), P(d), d, P(d)]
+        L.oracle_partition_at.argtypes = [P(C.c_int32), P(d), C.c_int64, C.c_int64, C.c_int64, C.c_int64]
+        L.oracle_partition_at.restype = C.c_int64
     return L
 
 

@@ -656,3 +656,14 @@ def test_cornell_256spp_wave_ci_tiles_per_wave():
 
 def test_cornell_256spp_throughput_mode():
     check(G.Scene.cornell(48, 32), abi.render_desc(16, 16, max_depth=8, mode=MB))
+
+
+@pytest.mark.parametrize("cull", ["0", "1"])
+def test_leaf_culling_groups_keep_bits(cull, monkeypatch):
+    """The README tree's leaf culling groups (cull_groups in render.hip) only
+    skip leaf tests that fail; with and without them the films are the
+    oracle's (EXACT and THROUGHPUT)."""
+    monkeypatch.setenv("PBRT_CULL_GROUPS", cull)
+    scene = G.Scene.readme(96, 64)
+    check(scene, abi.render_desc(4, 4))
+    check(scene, abi.render_desc(3, 3, mode=MB))
