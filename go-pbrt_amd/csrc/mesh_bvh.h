@@ -29,4 +29,8 @@ struct MeshBuild {
 int mesh_bvh_build(const pbrt_scene_desc* s, hipStream_t st, MeshBuild& out, std::string& err);
 void mesh_bvh_free(MeshBuild& b);
 
+// Ascending bitonic sort of npad 64-bit keys on stream `st` (npad a power of
+// two >= 2048; pad with ~0). Also orders k_chain_ci's cold-frame schedule.
+void bitonic_sort_u64(uint64_t* keys, uint32_t npad, hipStream_t st);
+
 }  // namespace pbrt

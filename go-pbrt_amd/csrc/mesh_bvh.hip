@@ -315,6 +315,17 @@ hipError_t dmalloc(T** p, size_t n) {
 
 }  // namespace
 
+// stages k <= 2048 sort each 2048-key block in LDS (one launch); later
+// stages: global passes for strides >= 2048, then the rest in LDS
+void bitonic_sort_u64(uint64_t* keys, uint32_t npad, hipStream_t st) {
+    hipLaunchKernelGGL(k_bitonic_local, dim3(npad / 2048), dim3(1024), 0, st, keys, 2u, 2048u, 1u);
+    for (uint32_t k = 4096; k <= npad; k <<= 1) {
+        for (uint32_t j = k >> 1; j >= 2048; j >>= 1)
+            hipLaunchKernelGGL(k_bitonic_global, dim3(npad / 1024), dim3(1024), 0, st, keys, k, j);
+        hipLaunchKernelGGL(k_bitonic_local, dim3(npad / 2048), dim3(1024), 0, st, keys, k, k, 1024u);
+    }
+}
+
 void mesh_bvh_free(MeshBuild& b) {
     (void)hipFree(b.nodes);
     (void)hipFree(b.tris);
@@ -425,12 +436,7 @@ int mesh_bvh_build(const pbrt_scene_desc* s, hipStream_t st, MeshBuild& out, std
         hipLaunchKernelGGL(k_morton, dim3(gpad), dim3(kB), 0, st, cen, n, npad, bounds, keys);
         // stages k <= 2048 sort each 2048-key block in LDS (one launch); later
         // stages: global passes for strides >= 2048, then the rest in LDS
-        hipLaunchKernelGGL(k_bitonic_local, dim3((unsigned)(npad / 2048)), dim3(1024), 0, st, keys, 2u, 2048u, 1u);
-        for (uint32_t k = 4096; k <= (uint32_t)npad; k <<= 1) {
-            for (uint32_t j = k >> 1; j >= 2048; j >>= 1)
-                hipLaunchKernelGGL(k_bitonic_global, dim3((unsigned)(npad / 1024)), dim3(1024), 0, st, keys, k, j);
-            hipLaunchKernelGGL(k_bitonic_local, dim3((unsigned)(npad / 2048)), dim3(1024), 0, st, keys, k, k, 1024u);
-        }
+        bitonic_sort_u64(keys, (uint32_t)npad, st);
         hipLaunchKernelGGL(k_gather, dim3(gb), dim3(kB), 0, st, keys, n, tris, gid, out.tris, out.gid);
         if (n > 1)
             hipLaunchKernelGGL(k_karras, dim3((unsigned)((n - 1 + kB - 1) / kB)), dim3(kB), 0, st, keys, n, cl, cr,

@@ -1195,6 +1195,83 @@ __global__ __launch_bounds__(kWave) void k_wf_primary(DevScene sc, RenderParams 
     pr.nvalid = rp.spp;
 }
 
+// Cold-frame schedule of k_chain_ci. Workgroups start in launch order, so a
+// heavy tile launched late stretches the frame; a context that has rendered
+// this configuration before orders its tiles by their measured chain times
+// (heaviest first). A fresh context (internal/render/server.go builds one per
+// RPC) estimates them instead: one wave per tile slot runs kProbes trajectories
+// per pixel from the pixel's bounce-1 record (k_wf_primary) at pseudo-random
+// PCG32 states, exactly the work a chain candidate does (traj_scatter), and
+// prices the slot as
+//   cost = traced_spp * mean(D * bounces) summed over the hit pixels   (chain lane-bounces)
+//        + kCostPixel * pixels                                         (StartPixel)
+// Only the launch order depends on it, never a result. Writes the features
+// (feat[4 * slot]: work, hit pixels, pixels, cost) and the sort key
+// (~cost bits << 32 | slot: ascending = heaviest first).
+constexpr int kProbes = 2;
+constexpr double kCostPixel = 150.0;   // one StartPixel ~ this many trajectory bounces of one lane
+__global__ __launch_bounds__(kWave) void k_tile_cost(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
+                                                     int64_t nb, float* __restrict__ feat,
+                                                     uint64_t* __restrict__ keys) {
+    __shared__ uint16_t stack_lds[64 * kStackStride];
+    stage_nodes(sc);
+    const int64_t bs = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (bs >= nb) return;
+    const int64_t tile = tile_of_slot(rp, slot_base + bs);
+    int64_t x0, y0, x1, y1;
+    tile_bounds(rp, tile, x0, y0, x1, y1);
+    const int64_t npx = (x1 - x0) * (y1 - y0);
+    const uint64_t inc = pcg_inc_of((uint64_t)tile);
+    const SpecSampler ss{nullptr, rp.spp, rp.ndims};   // k < 0: stratified values are never read
+    double work = 0;
+    int hits = 0;
+    for (int64_t it = lane; it < npx * kProbes; it += kWave) {
+        const int64_t pi = it / kProbes;
+        const PixelRec& pr = wb.prec[bs * wb.ppt + pi];
+        if (!pr.hit) continue;
+        hits += (it % kProbes) == 0;
+        Cursor c;
+        c.rng.state = mb_state((uint64_t)tile, (uint64_t)pi, 0x70726f6265ULL + (uint64_t)(it % kProbes));
+        c.rng.inc = inc;
+        c.draws = 0;
+        c.cur1d = 1;
+        c.cur2d = 2;
+        c.k = -1;
+        c.kdep = 0;
+        Spec beta = spec(1);
+        int bounces = 1;
+        Ray ray;
+        int r = traj_scatter(sc, pr.si, pr.b, pr.wo, c, ss, beta, bounces, ray, rp.max_depth, rp.rr_threshold);
+        while (r == 0) {
+            SI si;
+            int panic = 0;
+            if (!bvh_traverse<false>(sc, ray, &si, stack_lds + lane, panic) || panic) break;
+            BSDF b;
+            if (compute_bsdf(sc, si, b) < 0) break;
+            r = traj_scatter(sc, si, b, ray.d, c, ss, beta, bounces, ray, rp.max_depth, rp.rr_threshold);
+        }
+        work += (double)c.draws * (double)bounces;
+    }
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        work += __shfl_xor(work, o);
+        hits += __shfl_xor(hits, o);
+    }
+    if (lane == 0) {
+        const double w = work / kProbes * (double)(rp.spp - 1);
+        const float cost = (float)(w + kCostPixel * (double)npx);
+        feat[4 * bs + 0] = (float)w;
+        feat[4 * bs + 1] = (float)hits;
+        feat[4 * bs + 2] = (float)npx;
+        feat[4 * bs + 3] = cost;
+        keys[bs] = ((uint64_t)~__float_as_uint(cost) << 32) | (uint64_t)bs;
+    }
+}
+__global__ void k_order_of_keys(const uint64_t* __restrict__ keys, int64_t nb, uint32_t* __restrict__ order) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nb) order[i] = (uint32_t)keys[i];
+}
+
 __global__ __launch_bounds__(kWave) void k_wf_tile(DevScene sc, RenderParams rp, ChainLayout lay,
                                                    const PcgJump* __restrict__ jump, WaveBufs wb, WfBufs wf,
                                                    int64_t slot_base, int par, int n_levels) {
@@ -1919,6 +1996,11 @@ struct pbrt_gpu_ctx {
     uint32_t* d_slot_order = nullptr;
     int64_t ticks_cap = 0;
     std::vector<uint32_t> h_slot_order;
+    // cold-frame schedule (k_tile_cost): per-slot features and sort keys
+    float* d_cost = nullptr;
+    uint64_t* d_cost_keys = nullptr;
+    int64_t cost_cap = 0, cost_n = 0;
+    bool probed = false;               // the last EXACT frame ran the cost probe
     uint64_t order_key = 0, ticks_key = 0;
     int64_t ticks_n = 0;
     bool ticks_pending = false;
@@ -2300,6 +2382,11 @@ int64_t ci_heavy_override() {
 }
 bool ci_order_enabled() {
     const char* e = getenv("PBRT_CI_ORDER");
+    return !(e && atoi(e) == 0);
+}
+// PBRT_CI_PROBE=0: a fresh context's first frame runs in launch order (no k_tile_cost)
+bool ci_probe_enabled() {
+    const char* e = getenv("PBRT_CI_PROBE");
     return !(e && atoi(e) == 0);
 }
 uint64_t schedule_key(const RenderParams& rp, int kw) {
@@ -2726,6 +2813,7 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                                        dim3(kWave), 0, c->stream, with_slot(sc, 1), rp, c->wb, sb, nb);
                     const int kw = ci_waves(c, nb);
                     const uint32_t* order = nullptr;
+                    bool learned = false;   // order from the last frame's measured chain times
                     uint32_t* ticks = nullptr;
                     if ((kw > 1 || G == 1) && c->n_batches == 1 && ci_order_enabled()) {
                         if (c->ticks_cap < nb) {
@@ -2742,6 +2830,32 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                             HIPCHK(c, hipMemcpyAsync(c->d_slot_order, c->h_slot_order.data(), sizeof(uint32_t) * (size_t)nb,
                                                      hipMemcpyHostToDevice, c->stream));
                             order = c->d_slot_order;
+                            learned = true;
+                        }
+                        c->probed = false;
+                        if (!order && ci_probe_enabled() && nb <= (int64_t)1 << 24) {
+                            // no measured order for this configuration yet: estimate it
+                            int64_t npad = 2048;
+                            while (npad < nb) npad <<= 1;
+                            if (c->cost_cap < npad) {
+                                if (c->d_cost) (void)hipFree(c->d_cost);
+                                if (c->d_cost_keys) (void)hipFree(c->d_cost_keys);
+                                c->d_cost = nullptr;
+                                c->d_cost_keys = nullptr;
+                                c->cost_cap = 0;
+                                HIPCHK(c, hipMalloc((void**)&c->d_cost, sizeof(float) * 4 * (size_t)npad));
+                                HIPCHK(c, hipMalloc((void**)&c->d_cost_keys, sizeof(uint64_t) * (size_t)npad));
+                                c->cost_cap = npad;
+                            }
+                            HIPCHK(c, hipMemsetAsync(c->d_cost_keys, 0xFF, sizeof(uint64_t) * (size_t)npad, c->stream));
+                            hipLaunchKernelGGL(k_tile_cost, dim3((unsigned)nb), dim3(kWave), 0, c->stream, with_slot(sc, 7),
+                                               rp, c->wb, sb, nb, c->d_cost, c->d_cost_keys);
+                            bitonic_sort_u64(c->d_cost_keys, (uint32_t)npad, c->stream);
+                            hipLaunchKernelGGL(k_order_of_keys, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0,
+                                               c->stream, c->d_cost_keys, nb, c->d_slot_order);
+                            order = c->d_slot_order;
+                            c->probed = true;
+                            c->cost_n = nb;
                         }
                         ticks = c->d_ticks;
                         c->ticks_pending = true;
@@ -2775,9 +2889,9 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                     // tile, the most efficient per lane)
                     // measured wins at 1/2 and 1/4 shards (nb > n_simd); a loss at 1/8
                     // (1020 tiles: 294 -> 307 ms), so smaller launches never split
-                    int64_t heavy = (order && kw > 1 && G == 1 && nb > c->n_simd && ci_split_enabled())
+                    int64_t heavy = (learned && kw > 1 && G == 1 && nb > c->n_simd && ci_split_enabled())
                                         ? std::min<int64_t>(c->heavy_k, nb) : 0;
-                    if (ci_heavy_override() >= 0 && order && kw > 1 && G == 1)   // tests force the split
+                    if (ci_heavy_override() >= 0 && learned && kw > 1 && G == 1)   // tests force the split
                         heavy = std::min<int64_t>(ci_heavy_override(), nb);
                     if (heavy >= nb) heavy = 0;   // nothing left for the light launch: one launch at kw
                     c->last_heavy = heavy;
@@ -3038,7 +3152,7 @@ void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
     void* bufs[] = {c->d_shapes, c->d_materials, c->d_prims, c->d_nodes, c->d_order, c->d_lights, c->d_camera, c->d_film,
                     c->d_dist,   c->d_films,     c->d_s1d,   c->d_panics, c->d_ctr,   c->d_out,    c->d_jump,
                     c->d_wave,   c->d_fprims, c->d_wf,     c->d_ticks, c->d_slot_order, c->d_groups,
-                    c->d_gmasks};
+                    c->d_gmasks, c->d_cost,   c->d_cost_keys};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     mesh_bvh_free(c->mesh);
@@ -3225,6 +3339,18 @@ extern "C" int64_t pbrt_gpu_tile_ticks(pbrt_gpu_ctx* c, uint32_t* out, int64_t n
     const int64_t m = (int64_t)c->h_last_ticks.size();
     for (int64_t i = 0; out && i < n && i < m; i++) out[i] = c->h_last_ticks[(size_t)i];
     return m;
+}
+
+extern "C" int64_t pbrt_gpu_tile_costs(pbrt_gpu_ctx* c, float* out, int64_t n) {
+    if (!c) return -PBRT_E_INVALID;
+    if (!c->probed || !c->d_cost) return 0;
+    if (out && n > 0) {
+        const int64_t m = std::min<int64_t>(n, c->cost_n);
+        if (hipSetDevice(c->device) != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess ||
+            hipMemcpy(out, c->d_cost, sizeof(float) * 4 * (size_t)m, hipMemcpyDeviceToHost) != hipSuccess)
+            return -PBRT_E_HIP;
+    }
+    return c->cost_n;
 }
 
 // Region cycles of trajectory steps (PBRT_STEP_TIMING builds only; else zeros):

@@ -63,6 +63,8 @@ def lib():
     L.pbrt_film_to_rgba8.argtypes = [P(d), i64, i64, P(C.c_uint8)]
     L.pbrt_gpu_tile_ticks.argtypes = [C.c_void_p, P(C.c_uint32), i64, P(i64)]
     L.pbrt_gpu_tile_ticks.restype = i64
+    L.pbrt_gpu_tile_costs.argtypes = [C.c_void_p, P(C.c_float), i64]
+    L.pbrt_gpu_tile_costs.restype = i64
     L.pbrt_gpu_counters.argtypes = [C.c_void_p, P(C.c_uint64), C.c_int]
     for name in ("pbrt_translate", "pbrt_scale"):
         getattr(L, name).argtypes = [d, d, d, T]
@@ -384,6 +386,17 @@ class Renderer:
         if n > 0:
             lib().pbrt_gpu_tile_ticks(self.h, out.ctypes.data_as(C.POINTER(C.c_uint32)), n, C.byref(heavy))
         return out, int(heavy.value)
+
+    def tile_costs(self):
+        """(n_slots, 4) cold-frame cost features of the last EXACT frame's probe
+        (chain work, hit pixels, pixels, cost); empty if that frame had a learned order."""
+        n = lib().pbrt_gpu_tile_costs(self.h, None, 0)
+        out = np.zeros((max(n, 0), 4), dtype=np.float32)
+        if n > 0:
+            rc = lib().pbrt_gpu_tile_costs(self.h, out.ctypes.data_as(C.POINTER(C.c_float)), n)
+            if rc < 0:
+                self._check(-rc)
+        return out
 
     def counters(self):
         """pbrt_gpu_counters of the last render (include/pbrt_diag.h order)."""

@@ -82,6 +82,12 @@ int pbrt_gpu_counters(struct pbrt_gpu_ctx* ctx, uint64_t* out, int n);
  * the last launch that ran at 4 waves in the heavy/light split (0: no split). */
 int64_t pbrt_gpu_tile_ticks(struct pbrt_gpu_ctx* ctx, uint32_t* out, int64_t n, int64_t* heavy);
 
+/* Cold-frame schedule estimate of the last EXACT frame, if that frame ran
+ * render.hip's k_tile_cost probe (a fresh context or a new configuration):
+ * per slot {chain work (lane-bounces), hit pixels, pixels, cost}. Copies
+ * min(n, slots) records of 4 floats and returns the slot count (0: no probe). */
+int64_t pbrt_gpu_tile_costs(struct pbrt_gpu_ctx* ctx, float* out, int64_t n);
+
 /* Triangle meshes of the context (extension): out = {triangles in the tree
  * (zero-area ones are left out), nodes per ordering, deepest leaf, device
  * build ms, meshes}. Returns the number of values. */

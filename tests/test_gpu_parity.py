@@ -425,6 +425,28 @@ def test_wave_ci_heavy_light_split_keeps_bits(ci_waves, heavy, monkeypatch):
                 assert (heavy > 0) == (frame > 0 and int(heavy_env) < st.tiles_rendered), (frame, heavy)
 
 
+@pytest.mark.parametrize("probe", ["0", "1"])
+def test_wave_ci_cold_frame_probe_order_keeps_bits(probe, monkeypatch):
+    """A fresh context's first frame launches its tiles in the order of the
+    k_tile_cost estimate (no measured chain times yet); later frames use the
+    measured order. Only the schedule changes: every frame is the oracle's."""
+    monkeypatch.setenv("PBRT_CI_PROBE", probe)
+    scene = G.Scene.readme(160, 96)
+    rd = abi.render_desc(5, 5)
+    ofilm, _ = oracle_render(scene, rd)
+    with G.Renderer(scene, kernel="wave_ci") as r:
+        for frame in range(2):
+            film, st = r.render(rd)
+            assert same_bits(film, ofilm)
+            costs = r.tile_costs()
+            if frame == 0 and probe == "1":
+                assert costs.shape == (st.tiles_rendered, 4)
+                assert (costs[:, 3] > 0).all() and (costs[:, 2] == 256).all()
+                assert costs[:, 1].sum() > 0   # hit pixels were probed
+            else:
+                assert len(costs) == 0
+
+
 def test_wave_ci_split_default_heuristic_on_a_quarter_shard():
     """Without PBRT_CI_HEAVY: a 1/4 shard of the 1080p frame (2040 tiles, 4
     waves per tile) gets the heavy/light split from its second frame; bits
