@@ -1593,6 +1593,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
     const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
     const int64_t bs = blk * G + g;
     const uint64_t inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + (bs < nslots_batch ? bs : 0)));
+#ifdef PBRT_CI_DIAG   // diagnostics build (make diag): steps, lane-0 phase clocks, on-chain D histogram
     unsigned long long steps = 0;
     unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     long long tprev = clock64();
@@ -1602,6 +1603,11 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
         tprev = now;
     };
     if (tid < 64) dh[tid] = 0;
+#define CI_DIAG(x) x
+#else
+    auto mark = [](int) {};
+#define CI_DIAG(x)
+#endif
     if (tid < G) {
         const int64_t b = blk * G + tid;
         CiGroup& s = gs[tid];
@@ -1698,7 +1704,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
         bool any_chain = false;
         for (int q = 0; q < G; q++) any_chain |= gs[q].phase == 1;
         if (!any_chain) break;
-        steps++;
+        CI_DIAG(steps++;)
 
         // ---- (2) idle lanes take the next offsets of their group
         const CiGroup sg = gs[g];
@@ -1739,7 +1745,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
             }
             if (gl == 0 && sg.phase == 1) {
                 gs[g].nxt = nx0 + 2u * (uint32_t)max(nspec, 0);
-                ph[5] += (unsigned long long)(max(nspec, 0) + re);   // candidate trajectories issued
+                CI_DIAG(ph[5] += (unsigned long long)(max(nspec, 0) + re);)   // candidate trajectories issued
                 if (re) gs[g].reissue = 0;
             }
             if (o != kNoOff) {
@@ -1820,7 +1826,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
                     s.phase = 2;
                     break;
                 }
-                atomicAdd(&dh[min(d / 2u, 63u)], 1u);
+                CI_DIAG(atomicAdd(&dh[min(d / 2u, 63u)], 1u);)
                 s.kh++;
                 s.head += d;
                 if (s.kh >= n) {   // every sample of the pixel has its offset; the next StartPixel starts here
@@ -1844,11 +1850,16 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
         }
         mark(4);
     }
+#ifdef PBRT_CI_DIAG
     __syncthreads();
     if (tid < 64 && dh[tid]) atomicAdd(&ctr->dhist[tid], (unsigned long long)dh[tid]);
     if (tid == 0) {
         atomicAdd(&ctr->windows, steps);
         for (int k = 0; k < 8; k++) atomicAdd(&ctr->phase[k], ph[k]);
+    }
+#endif
+#undef CI_DIAG
+    if (tid == 0) {
         if (ticks && G == 1 && bs < nslots_batch) ticks[bs] = (uint32_t)min(wall_clock64() - t_begin, (uint64_t)0xFFFFFFFFu);
     }
 }

@@ -13,6 +13,8 @@ GPU is visible, construction raises.
 """
 import ctypes as C
 import os
+import struct
+import zlib
 
 import numpy as np
 
@@ -455,3 +457,44 @@ def film_to_rgba8(film):
     if rc:
         raise PbrtError(rc, "film_to_rgba8")
     return out
+
+
+def write_png(path, film):
+    """Film.WriteImage (film.go:142-179): the fp64 XYZ film as an 8-bit PNG.
+
+    Pixels are pbrt_film_to_rgba8's (uint8(Clamp(v, 0, 1) * 255) per channel,
+    no XYZ->RGB, no gamma, alpha 255). Every pixel is opaque, so the image is
+    written as 8-bit truecolour without alpha, the colour type Go's png.Encode
+    picks for an opaque NRGBA image; scanlines use filter 0 (Go picks filters
+    adaptively, so the file bytes differ while the decoded pixels are the same)."""
+    rgba = film_to_rgba8(film)
+    h, w, _ = rgba.shape
+    raw = np.zeros((h, 1 + 3 * w), np.uint8)
+    raw[:, 1:] = rgba[:, :, :3].reshape(h, 3 * w)
+
+    def chunk(tag, data):
+        return struct.pack(">I", len(data)) + tag + data + struct.pack(">I", zlib.crc32(tag + data) & 0xFFFFFFFF)
+
+    png = (b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, 2, 0, 0, 0))
+           + chunk(b"IDAT", zlib.compress(raw.tobytes(), 6)) + chunk(b"IEND", b""))
+    with open(path, "wb") as f:
+        f.write(png)
+    return rgba
+
+
+def read_png_rgb(path):
+    """Decode an 8-bit truecolour PNG with filter-0 scanlines (write_png's) -> (h, w, 3) uint8."""
+    data = open(path, "rb").read()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    pos, idat, w, h = 8, b"", 0, 0
+    while pos < len(data):
+        n, tag = struct.unpack(">I4s", data[pos:pos + 8])
+        body = data[pos + 8:pos + 8 + n]
+        if tag == b"IHDR":
+            w, h = struct.unpack(">II", body[:8])
+        elif tag == b"IDAT":
+            idat += body
+        pos += 12 + n
+    raw = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(h, 1 + 3 * w)
+    assert (raw[:, 0] == 0).all()
+    return raw[:, 1:].reshape(h, w, 3)

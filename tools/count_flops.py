@@ -4,7 +4,11 @@ reference algorithm that reaches an output = 1 FLOP; compare/Max/Min/abs/
 Nextafter bit steps = 0). Deterministic for (scene, config); the result is
 committed under profiles/ and read by bench.py for the roofline.
 
-    python tools/count_flops.py [--width 1920 --height 1080 --spp 8]
+    python tools/count_flops.py [--scene readme|cornell --width 1920 --height 1080 --spp 8 --max-depth 10
+                                 --tile-stride 1]
+
+--tile-stride S counts every S-th tile (an evenly spread sample; per-path
+figures are then sample means, stated in the output).
 """
 import argparse
 import json
@@ -25,16 +29,20 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=8)
     ap.add_argument("--threads", type=int, default=os.cpu_count())
+    ap.add_argument("--scene", default="readme", choices=["readme", "cornell"])
+    ap.add_argument("--max-depth", type=int, default=10)
+    ap.add_argument("--tile-stride", type=int, default=1)
     a = ap.parse_args()
-    sc = O.OracleScene.readme(a.width, a.height)
-    rd = abi.render_desc(a.spp, a.spp)
+    sc = getattr(O.OracleScene, a.scene)(a.width, a.height)
+    rd = abi.render_desc(a.spp, a.spp, max_depth=a.max_depth, tile_begin=0, tile_stride=a.tile_stride)
     t = time.time()
     rc, film, st = O.render(sc.desc, rd, threads=a.threads, flops=True)
     dt = time.time() - t
     assert rc == 0
     out = {
-        "scene": "readme", "width": a.width, "height": a.height, "sampler": f"Stratified({a.spp},{a.spp})",
-        "integrator": "Path(10, rr=1, Uniform)", "tiles": int(st.tiles), "paths": int(st.paths),
+        "scene": a.scene, "width": a.width, "height": a.height, "sampler": f"Stratified({a.spp},{a.spp})",
+        "integrator": f"Path({a.max_depth}, rr=1, Uniform)", "tiles": int(st.tiles), "paths": int(st.paths),
+        "tile_sample": "every tile" if a.tile_stride == 1 else f"every {a.tile_stride}-th tile (tile_stride)",
         "flops": int(st.flops), "flops_per_path": st.flops / st.paths,
         "flops_light_per_path": st.flops_light / st.paths,
         "flops_trajectory_per_path": (st.flops - st.flops_light) / st.paths,
@@ -43,7 +51,7 @@ def main():
         "definition": "fp64 add/sub/mul/div/sqrt executed by the reference algorithm on values that reach "
                       "the film (oracle/_build/liboracle_flops.so)",
     }
-    path = os.path.join(REPO, "profiles", f"flops_readme_{a.width}x{a.height}_s{a.spp}x{a.spp}.json")
+    path = os.path.join(REPO, "profiles", f"flops_{a.scene}_{a.width}x{a.height}_s{a.spp}x{a.spp}.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))
