@@ -36,12 +36,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--config", default="B", choices=["B", "C", "D"],
+    ap.add_argument("--width", type=int, default=0, help="0 = the config's (1920, or 3840 for E)")
+    ap.add_argument("--height", type=int, default=0, help="0 = the config's (1080, or 2160 for E)")
+    ap.add_argument("--shard", default="", help="R/N: on ONE GPU, render only tiles t mod N == R, the share of "
+                                                "rank R of an N-GPU job (reported as such)")
+    ap.add_argument("--config", default="B", choices=["B", "C", "D", "E"],
                     help="BASELINE config: B = README sphere scene, Stratified(8,8), Path(10); "
                          "C = Cornell (SURVEY 8(d)), Stratified(16,16), Path(8); "
-                         "D = 999 698-triangle height field (extension), Stratified(8,8), Path(10)")
+                         "D = 999 698-triangle height field (extension), Stratified(8,8), Path(10); "
+                         "E = 9 999 392-triangle height field, 3840x2160, Stratified(32,32), Path(10)")
     ap.add_argument("--spp", type=int, default=0, help="Stratified(spp, spp) (0 = the config's)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "serial", "wave", "wavefront", "wave_ci"])
     ap.add_argument("--tiles-per-wave", type=int, default=0, help="k_chain lane groups per wave (0 = library default)")
@@ -89,7 +92,7 @@ def host_cpu():
     return {"nproc": nproc, "affinity": affinity, "share": share, "cpu_model": model}
 
 
-def cpu_baseline(args, scene_name, rd_kwargs, product_scene=None):
+def cpu_baseline(args, scene_name, rd_kwargs, W, H, product_scene=None):
     """The oracle (C restatement of the Go path, oracle/) on the same frame's
     tiles, on this box's host cores: the whole frame when it fits the budget,
     else an evenly spread tile sample (bit-reversed stride-64 batches, so every
@@ -103,7 +106,7 @@ def cpu_baseline(args, scene_name, rd_kwargs, product_scene=None):
     if scene_name == "heightfield":   # the fixture is data: the oracle renders the product-built descriptor
         sc = product_scene
     else:
-        sc = (O.OracleScene.readme if scene_name == "readme" else O.OracleScene.cornell)(args.width, args.height)
+        sc = (O.OracleScene.readme if scene_name == "readme" else O.OracleScene.cornell)(W, H)
     n_tiles = int(O.lib().oracle_num_tiles(sc.desc, abi.render_desc(**rd_kwargs)))
     stride = 64
     offsets = [int(format(i, "06b")[::-1], 2) for i in range(stride)]
@@ -189,6 +192,10 @@ CONFIGS = {
     "D": dict(scene="heightfield", quads=707, spp=8, max_depth=10,
               text="height field 999698 triangles (device LBVH) + README lights/camera {W}x{H}, "
                    "Stratified({S},{S}) = {T} traced paths/px, Path(maxDepth 10, rr 1, Uniform), tile 16"),
+    # BASELINE.json configs[4] (8 GPUs): the same generator at 2236 x 2236 quads, 4K, 1024 spp
+    "E": dict(scene="heightfield", quads=2236, spp=32, max_depth=10, width=3840, height=2160,
+              text="height field 9999392 triangles (device LBVH) + README lights/camera {W}x{H}, "
+                   "Stratified({S},{S}) = {T} traced paths/px, Path(maxDepth 10, rr 1, Uniform), tile 16"),
 }
 
 
@@ -200,12 +207,12 @@ def make_scene(G, cfg, W, H):
     return G.Scene.heightfield(W, H, quads=cfg["quads"], seed=1)
 
 
-def mesh_roofline(cfg, W, H, S, mode, stats_ms):
-    """HBM roofline of the mesh traversal: the kernel's algorithmic bytes per
-    launch (nodes x 32 B + triangles x 36 B, counted once by
-    tools/count_mesh_bytes.py into profiles/meshbytes_*.json) over its
-    duration measured here with HIP events; the dominant of k_chain_ci /
-    k_paths_ci by time."""
+def mesh_roofline(cfg, W, H, S, mode, stats_ms, paths):
+    """HBM roofline of the mesh traversal: the kernel's algorithmic bytes
+    (nodes x 32 B + triangles x 36 B per path, counted by
+    tools/count_mesh_bytes.py into profiles/meshbytes_*.json) x the paths of
+    this frame, over the kernel's duration measured here with HIP events; the
+    dominant of k_chain_ci / k_paths_ci by time."""
     mb = load_json(os.path.join(REPO, "profiles", f"meshbytes_heightfield{cfg['quads']}_{W}x{H}_s{S}x{S}_{mode}.json"))
     if not mb:
         return None
@@ -216,11 +223,12 @@ def mesh_roofline(cfg, W, H, S, mode, stats_ms):
     k = mb["kernels"].get(name)
     if not k or ms <= 0:
         return None
-    achieved = k["bytes_per_launch"] / (ms / 1e3) / 1e9
+    frame_bytes = k["bytes_per_path"] * paths
+    achieved = frame_bytes / (ms / 1e3) / 1e9
     traffic = (pmc.get(name.replace("_mb", "")) or {}).get("hbm_bytes_per_launch")
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": name, "kernel_ms": ms,
-            "bytes_per_launch": k["bytes_per_launch"],
+            "bytes_per_launch": frame_bytes, "bytes_per_path": k["bytes_per_path"],
             "per_walk": {q: {"nodes": k[q]["nodes_per_walk"], "triangles": k[q]["triangles_per_walk"]}
                          for q in ("closest", "any") if q in k},
             "pipeline": {"kernels_ms": stats_ms["kernels"], "k_chain_ms": stats_ms["chain"],
@@ -244,7 +252,12 @@ def main():
     import pbrtgpu as G
 
     cfg = CONFIGS[args.config]
-    W, H = args.width, args.height
+    W, H = args.width or cfg.get("width", 1920), args.height or cfg.get("height", 1080)
+    shard_r, shard_n = rank, world
+    if args.shard:
+        if world > 1:
+            raise SystemExit("--shard is a one-GPU simulation of a rank; not under torch.distributed")
+        shard_r, shard_n = (int(x) for x in args.shard.split("/"))
     S = args.spp or cfg["spp"]
     rd_kwargs = dict(spp_x=S, spp_y=S, max_depth=cfg["max_depth"])
     scene = make_scene(G, cfg, W, H)
@@ -266,7 +279,7 @@ def main():
             dist.barrier(device_ids=[local])
 
     def make_step(mode):
-        rd = G.render_desc(**rd_kwargs, tile_begin=rank, tile_stride=world, mode=modes[mode])
+        rd = G.render_desc(**rd_kwargs, tile_begin=shard_r, tile_stride=shard_n, mode=modes[mode])
 
         def step():
             rstream.wait_stream(torch.cuda.current_stream(dev))
@@ -279,12 +292,18 @@ def main():
 
     def timed(mode, steps, warmup):
         step = make_step(mode)
-        for _ in range(warmup):
-            step()
+        for i in range(warmup):
+            st = step()
+            if rank == 0:
+                print(f"[bench] {mode} warmup {i}: kernels {st.kernel_ms:.0f} ms", file=sys.stderr, flush=True)
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        stats = [step() for _ in range(steps)]
+        stats = []
+        for i in range(steps):
+            stats.append(step())
+            if rank == 0:   # progress on stderr (long frames: config E); stdout holds the one JSON line
+                print(f"[bench] {mode} step {i}: kernels {stats[-1].kernel_ms:.0f} ms", file=sys.stderr, flush=True)
         torch.cuda.synchronize()
         barrier()
         elapsed = time.perf_counter() - t0
@@ -331,7 +350,8 @@ def main():
     if rank == 0:
         value = paths_total / elapsed / 1e6
         if cfg["scene"] == "heightfield":
-            roof = mesh_roofline(cfg, W, H, S, args.mode, {"chain": chain_ms, "paths": paths_ms, "kernels": kern_ms})
+            roof = mesh_roofline(cfg, W, H, S, args.mode, {"chain": chain_ms, "paths": paths_ms, "kernels": kern_ms},
+                                 paths_local / len(stats))
         else:
             roof = roofline(cfg["scene"], W, H, S, paths_local / len(stats), kernel_kind, kern_ms, chain_ms,
                             paths_ms, merge_ms, args.mode)
@@ -356,7 +376,9 @@ def main():
                 "baseline_config": args.config,
                 "width": W, "height": H, "spp": S * S, "traced_spp": S * S - 1, "max_depth": cfg["max_depth"],
                 "paths_per_frame": int(paths_total / args.steps), "mode": args.mode,
-                "parallelism": f"tiles mod {world}" + (" + RCCL film reduce" if world > 1 else ""),
+                "parallelism": f"tiles mod {world}" + (" + RCCL film reduce" if world > 1 else "")
+                               + (f"; ONE GPU rendering rank {shard_r}'s shard of {shard_n} (tiles t mod {shard_n} == "
+                                  f"{shard_r})" if args.shard else ""),
                 "kernel": {1: "serial", 2: "wave", 3: "wavefront", 4: "wave_ci"}.get(kernel_kind, "?"),
             },
             "pipeline_ms": {"kernels": kern_ms, "chain": chain_ms, "paths": paths_ms, "merge": merge_ms},
@@ -367,7 +389,7 @@ def main():
         if side:
             out["side_mode"] = side
         if not args.no_cpu_baseline and world == 1:
-            cb = cpu_baseline(args, cfg["scene"], rd_kwargs, scene)
+            cb = cpu_baseline(args, cfg["scene"], rd_kwargs, W, H, scene)
             cb["gpu_over_cpu"] = value / cb["value"]
             out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)

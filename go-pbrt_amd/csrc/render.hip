@@ -772,9 +772,12 @@ __host__ __device__ constexpr int paths_group_lds(int per) {   // bytes, per wav
 }
 // kMB: THROUGHPUT mode, sample k of pixel pi starts from its own stream
 // mb_state(tile, pi, k) instead of the chain's offset state.
+// s1d_lds: the group's stratified values are staged in LDS (else read from
+// their global records: large spp, e.g. config E's 1024).
 template <int P, bool kMB = false>
 __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderParams& rp, const WaveBufs& wb, int64_t slot_base,
-                            int64_t rec0, int64_t rec_end, Counters* __restrict__ ctr, unsigned char* wlds) {
+                            int64_t rec0, int64_t rec_end, Counters* __restrict__ ctr, unsigned char* wlds,
+                            int s1d_lds) {
     const int lane = threadIdx.x & (kWave - 1);
     const int n = rp.spp, ndims = rp.ndims, nl = sc.n_lights;
     const int per = ndims * n;
@@ -803,7 +806,7 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
         meta[P].cum = cum;
     }
     wave_sync();
-    for (int idx = lane; idx < P * per; idx += kWave) {
+    for (int idx = lane; s1d_lds && idx < P * per; idx += kWave) {
         const int j = idx / per;
         if (meta[j].nv > 0) s1d[idx] = wb.s1d[(rec0 + j) * wb.s1d_stride + (idx - j * per)];
     }
@@ -880,7 +883,7 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
             // a path taken this iteration runs its bounce 1 from the pixel cache
             // (no traversal) and then, with every other live path, one traced
             // bounce: the cheap first step does not cost the wave an iteration
-            const SpecSampler ss{s1d + j * per, n, ndims};
+            const SpecSampler ss{s1d_lds ? s1d + j * per : wb.s1d + (rec0 + j) * wb.s1d_stride, n, ndims};
             bool done = false;
             if (ps.first) done = path_step<1>(sc, pcs[j], ss, c, ps, rp.max_depth, rp.rr_threshold, nullptr, pnc, bnc);
             if (!done) done = path_step<2>(sc, pcs[j], ss, c, ps, rp.max_depth, rp.rr_threshold, nullptr, pnc, bnc);
@@ -925,10 +928,11 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
 
 template <int P, bool kMB = false>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kPathsWaves, 8))) void k_paths_ci(
-    DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr) {
+    DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr,
+    int s1d_lds) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];   // paths_group_lds<P>
     stage_nodes(sc);
-    paths_group<P, kMB>(sc, rp, wb, slot_base, (int64_t)blockIdx.x * P, nrec, ctr, lds);
+    paths_group<P, kMB>(sc, rp, wb, slot_base, (int64_t)blockIdx.x * P, nrec, ctr, lds, s1d_lds);
 }
 
 // THROUGHPUT mode setup for k_paths_ci<P, true>, one wave per pixel record:
@@ -1582,7 +1586,9 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
     const int64_t blk = order ? (int64_t)order[blockIdx.x] : (int64_t)blockIdx.x;
     const uint32_t R = (uint32_t)ring_size;   // a power of two (host: 256 / G or 256 * kW entries)
     const PcgJump& J = *jump;
-    double* s1d = (double*)(lds + lay.s1d);
+    // StartPixel's values: staged in LDS, or (lay.s1d < 0: large spp, serial
+    // StartPixel) written by it straight to the pixel's global record
+    double* s1d = lay.s1d >= 0 ? (double*)(lds + lay.s1d) : nullptr;
     uint16_t* other = (uint16_t*)(lds + lay.other);
     uint32_t* vbuf = (uint32_t*)(lds + lay.vbuf);
     RingEnt* ring = (RingEnt*)(lds + lay.ring) + (size_t)g * R;
@@ -1662,12 +1668,14 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
                 int64_t x0, y0, x1, y1;
                 tile_bounds(rp, tile, x0, y0, x1, y1);
                 const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
-                const uint64_t S1 = start_pixel_wave(rp, J, gs[q].S, incq, s1d, other, vbuf, &sh_state);
                 double* gs1d = wb.s1d + rec * wb.s1d_stride;
-                for (int idx = tid; idx < ndims * n; idx += kT) gs1d[idx] = s1d[idx];
+                double* sp = s1d ? s1d : gs1d;
+                const uint64_t S1 = start_pixel_wave(rp, J, gs[q].S, incq, sp, other, vbuf, &sh_state);
+                if (s1d)
+                    for (int idx = tid; idx < ndims * n; idx += kT) gs1d[idx] = s1d[idx];
                 // the first traced sample's camera time value (read before the ring
                 // clear: with one tile per workgroup the StartPixel staging aliases the ring)
-                const double time_u = s1d[1 < n ? 1 : 0];
+                const double time_u = sp[1 < n ? 1 : 0];
                 __syncthreads();
                 RingEnt* rq = (RingEnt*)(lds + lay.ring) + (size_t)q * R;
                 for (uint32_t i = (uint32_t)tid; i < R; i += kT) rq[i].tag = kNoOff;
@@ -2328,8 +2336,13 @@ bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Rend
     L.ring = 0;
     // k_chain_ci: the same staging without the window buffers, then the ring
     off = 0;
-    Lci.s1d = put(nd * n * 8);
-    Lci.other = put(nd * n * 2);
+    if (rp.sp_serial) {   // large spp: the serial StartPixel writes the values straight to wb.s1d
+        Lci.s1d = -1;
+        Lci.other = put(16);
+    } else {
+        Lci.s1d = put(nd * n * 8);
+        Lci.other = put(nd * n * 2);
+    }
     Lci.sbuf = Lci.dbuf = 0;
     Lci.vbuf = put(rp.sp_serial ? 4 : (int64_t)rp.sp_draws * 4);
     Lci.staging = (int)off;
@@ -2414,6 +2427,8 @@ uint64_t schedule_key(const RenderParams& rp, int kw) {
 // lane per (pixel, light) for the bounce-1 estimates. PBRT_PATHS_CI=0 keeps
 // the one-pixel-per-wave k_paths.
 // Returns the pixels per wave (2, 4 or 8; PBRT_PATHS_CI overrides, 0 = off).
+// k_paths_ci stages the stratified values of its P pixels in LDS when they take <= 16 KB
+bool paths_ci_s1d_lds(const RenderParams& rp, int P) { return (int64_t)P * rp.ndims * rp.spp * 8 <= 16 * 1024; }
 int paths_ci_pixels(const pbrt_gpu_ctx* c, const RenderParams& rp) {
     int pp = 4;
     bool forced = false;
@@ -2423,25 +2438,26 @@ int paths_ci_pixels(const pbrt_gpu_ctx* c, const RenderParams& rp) {
         if (v == 2 || v == 4 || v == 8) pp = v, forced = true;
     }
     auto fits = [&](int p) {
-        return c->host_scene.n_nodes <= kLdsNodes && p * c->host_scene.n_lights <= kWave &&
-               (int64_t)p * rp.ndims * rp.spp * 8 <= 16 * 1024;
+        return c->host_scene.n_nodes <= kLdsNodes && p * c->host_scene.n_lights <= kWave;
     };
     if (forced) return fits(pp) ? pp : 0;
-    // 4 pixels per wave where their stratified values fit, else 2 (config C, 256 spp)
-    return fits(4) ? 4 : fits(2) ? 2 : 0;
+    // 4 pixels per wave where their stratified values fit in LDS, else 2
+    // (config C, 256 spp), else 4 reading them from global memory (config E)
+    return paths_ci_s1d_lds(rp, 4) && fits(4) ? 4 : paths_ci_s1d_lds(rp, 2) && fits(2) ? 2 : fits(4) ? 4 : 0;
 }
 
 // Carve the per-batch buffers of the wave path. Budget: PBRT_WAVE_BUFFER_GB,
-// default min(48 GB, half the free HBM) -- config C (1080p, 256 spp, ~34 GB)
-// is then one batch on a 288 GB MI355X, so its whole frame is one launch per
-// kernel and gets the heaviest-first schedule.
+// default min(96 GB, half the free HBM) -- config C (1080p, 256 spp, ~34 GB)
+// and one rank's 1/8 shard of config E (4K, 1024 spp, ~68 GB) are then one
+// batch on a 288 GB MI355X, so the whole frame is one launch per kernel and
+// gets the heaviest-first schedule.
 int wave_buffers(pbrt_gpu_ctx* c) {
     const RenderParams& rp = c->rp;
     const int64_t ppt = rp.tile_size * rp.tile_size, n = rp.spp, nd = rp.ndims > 0 ? rp.ndims : 1;
     auto al = [](int64_t b) { return (b + 255) & ~int64_t(255); };
     const int64_t per_tile = al(ppt * (int64_t)sizeof(PixelRec)) + al(ppt * nd * n * 8) + al(ppt * n * 8) +
                              al(ppt * n * 24) + al(ppt * (int64_t)sizeof(PanicRec)) + al(4);
-    double gb = 48.0;
+    double gb = 96.0;
     {
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
@@ -2859,7 +2875,7 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                                 c->cost_cap = npad;
                             }
                             HIPCHK(c, hipMemsetAsync(c->d_cost_keys, 0xFF, sizeof(uint64_t) * (size_t)npad, c->stream));
-                            hipLaunchKernelGGL(k_tile_cost, dim3((unsigned)nb), dim3(kWave), 0, c->stream, with_slot(sc, 7),
+                            hipLaunchKernelGGL(k_tile_cost, dim3((unsigned)nb), dim3(kWave), 0, c->stream, with_slot(sc, 0),
                                                rp, c->wb, sb, nb, c->d_cost, c->d_cost_keys);
                             bitonic_sort_u64(c->d_cost_keys, (uint32_t)npad, c->stream);
                             hipLaunchKernelGGL(k_order_of_keys, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0,
@@ -2934,11 +2950,12 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                                        (unsigned)c->lay.total, c->stream, with_slot(sc, 4), rp, c->lay, c->d_jump, c->wb, sb, nb);
                     const int pp = paths_ci_pixels(c, rp) >= 4 ? 4 : 2;
                     auto kern = pp == 4 ? k_paths_ci<4, true> : k_paths_ci<2, true>;
-                    const int lds = pp == 4 ? paths_group_lds<4>(rp.ndims * rp.spp)
-                                            : paths_group_lds<2>(rp.ndims * rp.spp);
+                    const int sl = paths_ci_s1d_lds(rp, pp) ? 1 : 0;
+                    const int lds = pp == 4 ? paths_group_lds<4>(sl * rp.ndims * rp.spp)
+                                            : paths_group_lds<2>(sl * rp.ndims * rp.spp);
                     hipLaunchKernelGGL(kern, dim3((unsigned)((nb * c->wb.ppt + pp - 1) / pp)), dim3(kWave),
                                        (unsigned)lds, c->stream, with_slot(sc, 5), rp, c->wb, sb, nb * c->wb.ppt,
-                                       c->d_ctr);
+                                       c->d_ctr, sl);
                 } else if (rp.mode == PBRT_MODE_THROUGHPUT)
                     hipLaunchKernelGGL((k_paths<true, kPathsWaves>), dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
                                        (unsigned)c->lay.total, c->stream, with_slot(sc, 5), rp, c->lay, c->d_jump, c->wb, sb,
@@ -2946,11 +2963,12 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                 else if (const int pp = paths_ci_pixels(c, rp)) {
                     const int per = rp.ndims * rp.spp;
                     auto kern = pp == 8 ? k_paths_ci<8> : pp == 2 ? k_paths_ci<2> : k_paths_ci<4>;
-                    const int lds = pp == 8 ? paths_group_lds<8>(per) : pp == 2 ? paths_group_lds<2>(per)
-                                                                                : paths_group_lds<4>(per);
+                    const int sl = paths_ci_s1d_lds(rp, pp) ? 1 : 0;
+                    const int lds = pp == 8 ? paths_group_lds<8>(sl * per) : pp == 2 ? paths_group_lds<2>(sl * per)
+                                                                                     : paths_group_lds<4>(sl * per);
                     hipLaunchKernelGGL(kern, dim3((unsigned)((nb * c->wb.ppt + pp - 1) / pp)), dim3(kWave),
                                        (unsigned)lds, c->stream, with_slot(sc, 3), rp, c->wb, sb, nb * c->wb.ppt,
-                                       c->d_ctr);
+                                       c->d_ctr, sl);
                 }
                 else
                     hipLaunchKernelGGL((k_paths<false, kPathsWaves>), dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),

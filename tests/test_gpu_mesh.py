@@ -155,3 +155,25 @@ def test_config_D_full_size_properties_and_heaviest_tiles():
             g, _ = r.render(one)
         rc, o, _ = O.render(scene.desc, one, threads=1)
         assert rc == 0 and same_bits(g, o), t
+
+
+@pytest.mark.slow
+def test_config_E_full_mesh_sampled_tiles_bitexact():
+    """BASELINE config E: the 9 999 392-triangle height field, 3840x2160,
+    Stratified(32,32) (1023 traced paths per pixel), Path(10). The device
+    LBVH of the full mesh renders an evenly spread sample of 24 of the 32 400
+    tiles (tile_stride 1350, several batches at 1023 spp), bit for bit against
+    the oracle's own BVH over the same mesh."""
+    W, H = 3840, 2160
+    scene = G.Scene.heightfield(W, H, quads=2236, seed=1)
+    rd = abi.render_desc(32, 32, tile_begin=0, tile_stride=1350)
+    with G.Renderer(scene) as r:
+        info = r.mesh_info()
+        film, st = r.render(rd)
+    assert info["tris"] == 9999392
+    print(f"config E LBVH: {info}; sampled frame: {st.kernel_ms:.0f} ms, {st.batches} batches")
+    assert st.tiles_rendered == 24 and st.paths_traced == 24 * 256 * 1023
+    assert np.isfinite(film).all() and film.max() > 0
+    rc, ofilm, ost = O.render(scene.desc, rd, threads=THREADS)
+    assert rc == 0 and ost.paths == st.paths_traced
+    assert same_bits(film, ofilm), int((bits(film) != bits(ofilm)).any(axis=2).sum())

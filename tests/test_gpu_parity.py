@@ -689,3 +689,15 @@ def test_leaf_culling_groups_keep_bits(cull, monkeypatch):
     scene = G.Scene.readme(96, 64)
     check(scene, abi.render_desc(4, 4))
     check(scene, abi.render_desc(3, 3, mode=MB))
+
+
+@pytest.mark.parametrize("spp", [24, 32])
+def test_wave_ci_large_spp_global_start_pixel_values(spp):
+    """Stratified(24,24) / (32,32): StartPixel's draws exceed the wave kernel's
+    LDS staging, so it runs serially and k_chain_ci writes the pixel's
+    stratified values straight to their global record (config E's sampler).
+    Several batches; bit for bit the oracle's."""
+    scene = G.Scene.readme(40, 24)
+    rd = abi.render_desc(spp, spp, max_depth=6)
+    film, st = check(scene, rd, kernel="wave_ci")
+    assert st.kernel == abi.PBRT_KERNEL_WAVE_CI

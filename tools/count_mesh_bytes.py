@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=8)
     ap.add_argument("--mode", default="exact", choices=["exact", "throughput"])
+    ap.add_argument("--max-depth", type=int, default=10)
+    ap.add_argument("--shard", default="", help="R/N: count the tiles t mod N == R only (per-path figures)")
     a = ap.parse_args()
     import pbrtgpu as G
     L = G.lib()
@@ -39,12 +41,14 @@ def main():
     mode = G.abi.PBRT_MODE_EXACT if a.mode == "exact" else G.abi.PBRT_MODE_THROUGHPUT
     with G.Renderer(scene) as r:
         info = r.mesh_info()
-        _, st = r.render(G.render_desc(a.spp, a.spp, mode=mode))
+        r0, n0 = (int(x) for x in a.shard.split("/")) if a.shard else (0, 1)
+        _, st = r.render(G.render_desc(a.spp, a.spp, mode=mode, max_depth=a.max_depth, tile_begin=r0,
+                                       tile_stride=n0))
     L.pbrt_gpu_mesh_counters(buf, 48, 1)
     v = list(buf)
     out = {"scene": f"heightfield quads={a.quads} seed=1", "triangles": info["tris"], "nodes": info["nodes"],
            "depth": info["depth"], "width": a.width, "height": a.height, "sampler": f"Stratified({a.spp},{a.spp})",
-           "mode": a.mode, "paths": int(st.paths_traced), "bytes_per_node": 32, "bytes_per_triangle": 36,
+           "mode": a.mode, "paths": int(st.paths_traced), "tiles": a.shard or "all", "bytes_per_node": 32, "bytes_per_triangle": 36,
            "definition": "per launch: nodes fetched x 32 B + triangles tested x 36 B over every mesh walk "
                          "of the kernel (libpbrt_gpu_meshcount.so counters)", "kernels": {}}
     for slot, name in SLOTS.items():
