@@ -1186,7 +1186,8 @@ __global__ __launch_bounds__(kWave) void k_wf_primary(DevScene sc, RenderParams 
     BSDF b0;
     b0.n_bxdfs = 0;
     Ray ray = camera_ray(*sc.camera, (double)px + 0.0, (double)py + 0.0, 0.0, V2{0.0, 0.0});
-    if (rp.spp > 1 && 1 < rp.max_depth) {
+    // Path.Li traces bounce 1 only below maxDepth (path.go:66); DirectLighting always
+    if (rp.spp > 1 && (1 < rp.max_depth || rp.integrator == PBRT_INTEGRATOR_DIRECT_LIGHTING)) {
         hit0 = bvh_traverse<false>(sc, ray, &si0, stack_lds + threadIdx.x, panic0) ? 1 : 0;
         if (!panic0 && hit0 && compute_bsdf(sc, si0, b0) < 0) panic0 = -1;
     }
@@ -1197,6 +1198,197 @@ __global__ __launch_bounds__(kWave) void k_wf_primary(DevScene sc, RenderParams 
     pr.hit = panic0 ? 0 : hit0;
     pr.panic0 = panic0;
     pr.nvalid = rp.spp;
+}
+
+// ------------------------------------------- DirectLighting, wave-parallel
+// DirectLighting.Li (directlighting.go:62-104) has no chain problem: with
+// n_dims >= 1 (and n_dims >= 2 or a pinhole camera) every sample of a pixel
+// traces the same camera ray, so hit or miss -- the only thing the number of
+// PCG32 draws of a sample depends on -- is per pixel, and sample k of the
+// pixel starts at the state after StartPixel advanced by (k - 1) * D.
+// k_dl_setup replays the tile's pixels in order (StartPixel, then jump-ahead
+// over the pixel's samples); k_dl_samples runs every (pixel, sample) at once.
+//
+// Draws of one DirectLighting sample (pixel.go:60-80 counters): the camera's
+// Get2D pFilm, Get2D pLens, Get1D time (camera.go via integrator.go:240-255),
+// then on a hit UniformSampleAllLights' two Get2D per light (clones carry no
+// sample arrays, #23) or UniformSampleOneLight's Get1D + 2 Get2D, then the two
+// Get2D of SpecularReflect / SpecularTransmit when maxDepth > 1.
+__device__ __forceinline__ uint32_t dl_draws(const RenderParams& rp, int hit, int n_lights) {
+    int c1 = 0, c2 = 0;
+    uint32_t d = 0;
+    auto g1 = [&]() { if (c1 < rp.ndims) c1++; else d += 1; };
+    auto g2 = [&]() { if (c2 < rp.ndims) c2++; else d += 2; };
+    g2();
+    g2();
+    g1();
+    if (hit) {
+        if (n_lights > 0) {
+            if (rp.dl_strategy == PBRT_DL_UNIFORM_SAMPLE_ALL) {
+                for (int j = 0; j < n_lights; j++) {
+                    g2();
+                    g2();
+                }
+            } else {
+                g1();
+                g2();
+                g2();
+            }
+        }
+        if (1 < rp.max_depth) {
+            g2();
+            g2();
+        }
+    }
+    return d;
+}
+
+// One wave per tile slot: the tile's pixels in order. Leaves each pixel's
+// stratified values in wb.s1d, the PCG32 state of each of its samples in
+// wb.memb (slot 0 of a pixel: its panic key, reset here), and the pixels
+// with records in wb.tile_npx (a camera-ray panic ends the tile, as in
+// k_chain_ci). THROUGHPUT mode: each pixel and sample on its own stream.
+__global__ __launch_bounds__(kWave) void k_dl_setup(DevScene sc, RenderParams rp, ChainLayout lay,
+                                                    const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
+                                                    int64_t nb) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ uint64_t sh_state;
+    const int64_t bs = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (bs >= nb) return;
+    const PcgJump& J = *jump;
+    const int64_t tile = tile_of_slot(rp, slot_base + bs);
+    int64_t x0, y0, x1, y1;
+    tile_bounds(rp, tile, x0, y0, x1, y1);
+    const int64_t npx = (x1 - x0) * (y1 - y0);
+    const uint64_t inc = pcg_inc_of((uint64_t)tile);
+    const bool mb = rp.mode == PBRT_MODE_THROUGHPUT;
+    const int n = rp.spp;
+    double* s1d = lay.s1d >= 0 ? (double*)(lds + lay.s1d) : nullptr;
+    uint16_t* other = (uint16_t*)(lds + lay.other);
+    uint32_t* vbuf = (uint32_t*)(lds + lay.vbuf);
+    Pcg seed;
+    pcg_seed(seed, (uint64_t)tile);   // Sampler.Clone(tile), integrator.go:318,328
+    uint64_t S = seed.state;
+    int64_t used = npx;
+    for (int64_t pi = 0; pi < npx; pi++) {
+        const int64_t rec = bs * wb.ppt + pi;
+        double* gs1d = wb.s1d + rec * wb.s1d_stride;
+        double* sp = s1d ? s1d : gs1d;
+        const uint64_t S1 =
+            start_pixel_wave(rp, J, mb ? mb_state((uint64_t)tile, (uint64_t)pi, 0) : S, inc, sp, other, vbuf, &sh_state);
+        if (s1d)
+            for (int idx = lane; idx < rp.ndims * n; idx += kWave) gs1d[idx] = s1d[idx];
+        PixelRec& pr = wb.prec[rec];
+        const int hit = pr.hit, panic0 = pr.panic0;
+        const uint64_t D = dl_draws(rp, hit, sc.n_lights);
+        uint64_t* mst = wb.memb + rec * n;
+        for (int k = 1 + lane; k < n; k += kWave)
+            mst[k] = mb ? mb_state((uint64_t)tile, (uint64_t)pi, (uint64_t)k) : pcg_advance(J, S1, inc, (uint64_t)(k - 1) * D);
+        if (lane == 0) {
+            mst[0] = ~0ULL;
+            if (hit) {   // the camera ray's time (Get1D, dim 0) of the pixel's first traced sample
+                const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
+                pr.si.time = camera_ray(*sc.camera, (double)px, (double)py, sp[1 < n ? 1 : 0], V2{0.0, 0.0}).time;
+            }
+            pr.nvalid = n;
+        }
+        __syncthreads();   // the StartPixel staging is reused by the next pixel
+        if (panic0) {      // its first traced sample panics at bounce 1: the tile ends here
+            used = pi + 1;
+            break;
+        }
+        S = pcg_advance(J, S1, inc, (uint64_t)(n - 1) * D);
+    }
+    if (lane == 0) wb.tile_npx[bs] = (int32_t)used;
+}
+
+// One lane per (pixel record, traced sample): DirectLighting.Li at depth 0
+// from the pixel's bounce-1 record, with the sample's own PCG32 state.
+// Radiance to wb.L; a panic lowers the pixel's key (sample << 32 | kind + 1)
+// in wb.memb[rec * spp + 0] (the first panic in sample order wins).
+__global__ __launch_bounds__(kWave) void k_dl_samples(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
+                                                      int64_t nrec) {
+    __shared__ uint16_t stack_lds[64 * kStackStride];
+    stage_nodes(sc);
+    const int n = rp.spp;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n < 2 || idx >= nrec * (n - 1)) return;
+    const int64_t rec = idx / (n - 1);
+    const int k = 1 + (int)(idx - rec * (n - 1));
+    const int64_t bs = rec / wb.ppt, pi = rec % wb.ppt;
+    if (pi >= wb.tile_npx[bs]) return;
+    const PixelRec& pr = wb.prec[rec];
+    double* o = wb.L + (rec * n + k) * 3;
+    Spec L = spec(0);
+    int panic = pr.panic0;
+    if (!panic && pr.hit) {
+        Cursor c;
+        c.rng.state = wb.memb[rec * n + k];
+        c.rng.inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + bs));
+        c.draws = 0;
+        c.cur1d = c.cur2d = 0;
+        c.k = k;
+        c.kdep = 0;
+        const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, n, rp.ndims};
+        c_get2d(c, ss);   // camera: pFilm, pLens, time
+        c_get2d(c, ss);
+        c_get1d(c, ss);
+        L = L + spec(0);   // si.Le(si.Wo): no primitive carries an area light
+        const int nl = sc.n_lights;
+        if (nl > 0) {
+            if (rp.dl_strategy == PBRT_DL_UNIFORM_SAMPLE_ALL) {   // integrator.go:23-46
+                Spec acc = spec(0);
+                for (int j = 0; j < nl && !panic; j++) {
+                    const V2 ul = c_get2d(c, ss);
+                    c_get2d(c, ss);
+                    acc = acc + estimate_direct(sc, stack_lds + threadIdx.x, panic, pr.si, pr.b, j, ul);
+                }
+                L = L + acc;
+            } else {   // UniformSampleOneLight with no distribution (integrator.go:48-77)
+                const int ln = (int)gomath::to_int(gomath::min(c_get1d(c, ss) * (double)nl, (double)(nl - 1)));
+                const V2 ul = c_get2d(c, ss);
+                c_get2d(c, ss);
+                const Spec s = estimate_direct(sc, stack_lds + threadIdx.x, panic, pr.si, pr.b, ln, ul);
+                if (!panic && max_component(s) > 10) panic = PBRT_PANIC_LD_GT_10;
+                L = L + s;
+            }
+        }
+        // SpecularReflect / SpecularTransmit: black for a Lambertian-only BSDF
+    }
+    o[0] = L.r;
+    o[1] = L.g;
+    o[2] = L.b;
+    if (panic)
+        atomicMin((unsigned long long*)&wb.memb[rec * n],
+                  ((unsigned long long)k << 32) | (unsigned long long)((panic + 1) & 0xFF));
+}
+
+// Per pixel record: its first panic (sample order) -> wb.ppanic, and the
+// traced-path counters of pixels that finish (as paths_group counts them).
+__global__ void k_dl_panics(RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr) {
+    const int64_t rec = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (rec >= nrec) return;
+    const int64_t bs = rec / wb.ppt, pi = rec % wb.ppt;
+    if (pi >= wb.tile_npx[bs]) return;
+    int64_t x0, y0, x1, y1;
+    tile_bounds(rp, tile_of_slot(rp, slot_base + bs), x0, y0, x1, y1);
+    PanicRec p{0, 0, 0, 0, x0 + pi % (x1 - x0), y0 + pi / (x1 - x0)};
+    const uint64_t key = rp.spp >= 2 ? wb.memb[rec * rp.spp] : ~0ULL;
+    if (wb.prec[rec].panic0) {
+        p.kind = wb.prec[rec].panic0;
+        p.sample = 1;
+        p.bounce = 1;
+    } else if (key != ~0ULL) {
+        p.kind = (int)(key & 0xFF) - 1;
+        p.sample = (int)(key >> 32);
+        p.bounce = 1;
+    }
+    wb.ppanic[rec] = p;
+    if (!p.kind && rp.spp > 1) {
+        atomicAdd(&ctr->paths, (unsigned long long)(rp.spp - 1));
+        atomicAdd(&ctr->camera_samples, (unsigned long long)(rp.spp - 1));
+    }
 }
 
 // Cold-frame schedule of k_chain_ci. Workgroups start in launch order, so a
@@ -1976,6 +2168,7 @@ struct pbrt_gpu_ctx {
     // wavefront chain (k_wf_*)
     bool use_wf = false;
     bool use_ci = false;   // k_chain_ci instead of k_chain
+    bool use_dl = false;   // DirectLighting on k_dl_setup / k_dl_samples
     ChainLayout lay_ci{};
     WfBufs wf{};
     unsigned char* d_wf = nullptr;
@@ -2308,10 +2501,15 @@ const PcgJump& pcg_jump_table() {
 // Can the wave-parallel kernels replay this render exactly? (conditions: pbrt_spec.h)
 bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const RenderParams& rp, ChainLayout& L,
                    ChainLayout& Lci) {
-    if (rd->integrator != PBRT_INTEGRATOR_PATH || rd->n_dims < 3 || rd->max_depth > 2048) return false;   // D < 2^32
+    const bool dl = rd->integrator == PBRT_INTEGRATOR_DIRECT_LIGHTING;
+    if (dl) {   // k_dl_*: the camera ray must be per pixel (pFilm stratified; pLens stratified or unused)
+        if (rd->n_dims < 1 || (rd->n_dims < 2 && c->host_scene.camera.lens_radius > 0)) return false;
+    } else if (rd->integrator != PBRT_INTEGRATOR_PATH || rd->n_dims < 3 || rd->max_depth > 2048) {
+        return false;   // D < 2^32
+    }
     const int nl = c->host_scene.n_lights;
-    if (nl > kMaxCachedLights) return false;
-    if (nl > 0) {
+    if (!dl && nl > kMaxCachedLights) return false;
+    if (!dl && nl > 0) {
         const pbrt_distribution_desc& d = c->host_dist;
         if (!(d.func_int > 0)) return false;
         for (int i = 0; i < d.count; i++)
@@ -2656,14 +2854,19 @@ int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
     if ((c->kernel_req == PBRT_KERNEL_WAVE || c->kernel_req == PBRT_KERNEL_WAVEFRONT ||
          c->kernel_req == PBRT_KERNEL_WAVE_CI) && !c->use_spec)
         return set_err(c, PBRT_E_UNSUPPORTED, "render not eligible for the wave-parallel kernels");
-    c->use_wf = c->use_spec && c->kernel_req == PBRT_KERNEL_WAVEFRONT;
+    c->use_dl = c->use_spec && rd->integrator == PBRT_INTEGRATOR_DIRECT_LIGHTING;
+    if (c->use_dl && c->kernel_req != PBRT_KERNEL_AUTO && c->kernel_req != PBRT_KERNEL_WAVE_DL)
+        return set_err(c, PBRT_E_UNSUPPORTED, "DirectLighting runs on the serial or the k_dl_* kernels");
+    if (!c->use_dl && c->kernel_req == PBRT_KERNEL_WAVE_DL)
+        return set_err(c, PBRT_E_UNSUPPORTED, "render not eligible for the DirectLighting wave kernels");
+    c->use_wf = c->use_spec && !c->use_dl && c->kernel_req == PBRT_KERNEL_WAVEFRONT;
     // (dynamic LDS of one 1-wave tile, staging aliased with the ring: <= 20 KB keeps
     // 5+ workgroups per CU; config C at 256 spp needs 19.3 KB)
     const bool ci_fits = c->host_scene.n_nodes <= kLdsNodes &&
                          std::max(c->lay_ci.staging, kCiRingBytes) <= 20 * 1024;
     // AUTO: the continuous-issue chain wherever it fits (measured ~8% faster
     // than the window chain on config B), else the window chain
-    c->use_ci = c->use_spec && (c->kernel_req == PBRT_KERNEL_WAVE_CI ||
+    c->use_ci = c->use_spec && !c->use_dl && (c->kernel_req == PBRT_KERNEL_WAVE_CI ||
                                 (c->kernel_req == PBRT_KERNEL_AUTO && ci_fits));
     if (c->use_ci && !ci_fits)
         return set_err(c, PBRT_E_UNSUPPORTED, "render not eligible for the continuous-issue chain kernel");
@@ -2712,7 +2915,7 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
     }
     if (opts && (opts->occupancy == 2 || opts->occupancy == 4 || opts->occupancy == 8)) c->min_waves = opts->occupancy;
     if (opts) c->occ_req = opts->occupancy;
-    if (opts && (opts->kernel < PBRT_KERNEL_AUTO || opts->kernel > PBRT_KERNEL_WAVE_CI)) {
+    if (opts && (opts->kernel < PBRT_KERNEL_AUTO || opts->kernel > PBRT_KERNEL_WAVE_DL)) {
         delete c;
         return PBRT_E_INVALID;
     }
@@ -2811,7 +3014,7 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
     if (rp.n_slots > 0) {
         DevScene sc = dev_scene(c, rd->integrator == PBRT_INTEGRATOR_PATH);
         if (c->use_spec) {
-            c->last_kernel = rp.mode == PBRT_MODE_THROUGHPUT ? PBRT_KERNEL_WAVE
+            c->last_kernel = c->use_dl ? PBRT_KERNEL_WAVE_DL : rp.mode == PBRT_MODE_THROUGHPUT ? PBRT_KERNEL_WAVE
                              : c->use_wf ? PBRT_KERNEL_WAVEFRONT : c->use_ci ? PBRT_KERNEL_WAVE_CI : PBRT_KERNEL_WAVE;
             c->wf_iters = 0;
             const bool lds_nodes = c->host_scene.n_nodes <= kLdsNodes;
@@ -2830,7 +3033,14 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                 const int64_t nb = std::min<int64_t>(c->wave_batch, rp.n_slots - sb);
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 0], c->stream));
                 const int G = c->tiles_per_wave;
-                if (rp.mode == PBRT_MODE_THROUGHPUT) {
+                if (c->use_dl) {
+                    hipLaunchKernelGGL(k_wf_primary, dim3((unsigned)((nb * c->wb.ppt + kWave - 1) / kWave)),
+                                       dim3(kWave), 0, c->stream, with_slot(sc, 1), rp, c->wb, sb, nb);
+                    unsigned lds = 0;
+                    const ChainLayout lw = ci_layout(c->lay_ci, 1, 1, lds);
+                    hipLaunchKernelGGL(k_dl_setup, dim3((unsigned)nb), dim3(kWave), lds, c->stream, sc, rp, lw,
+                                       c->d_jump, c->wb, sb, nb);
+                } else if (rp.mode == PBRT_MODE_THROUGHPUT) {
                     // no offset chain: every sample's stream is known up front
                 } else if (c->use_wf) {
                     int rcc = wf_chain(c, sc, sb, nb);
@@ -2944,7 +3154,14 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                                        c->lay, c->d_jump, c->wb, sb, nb, kWave / G, c->d_ctr);
                 }
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 1], c->stream));
-                if (rp.mode == PBRT_MODE_THROUGHPUT && paths_ci_pixels(c, rp) > 0) {
+                if (c->use_dl) {
+                    const int64_t nrec = nb * c->wb.ppt;
+                    if (rp.spp > 1)
+                        hipLaunchKernelGGL(k_dl_samples, dim3((unsigned)((nrec * (rp.spp - 1) + kWave - 1) / kWave)),
+                                           dim3(kWave), 0, c->stream, with_slot(sc, 3), rp, c->wb, sb, nrec);
+                    hipLaunchKernelGGL(k_dl_panics, dim3((unsigned)((nrec + 255) / 256)), dim3(256), 0, c->stream, rp,
+                                       c->wb, sb, nrec, c->d_ctr);
+                } else if (rp.mode == PBRT_MODE_THROUGHPUT && paths_ci_pixels(c, rp) > 0) {
                     // setup (StartPixel + bounce 1 per pixel), then lane-refill paths
                     hipLaunchKernelGGL(k_mb_setup, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
                                        (unsigned)c->lay.total, c->stream, with_slot(sc, 4), rp, c->lay, c->d_jump, c->wb, sb, nb);

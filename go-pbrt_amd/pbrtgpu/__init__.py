@@ -309,7 +309,8 @@ class Renderer:
     """pbrt_gpu_ctx: the scene resident on one GPU."""
 
     KERNELS = {"auto": abi.PBRT_KERNEL_AUTO, "serial": abi.PBRT_KERNEL_SERIAL, "wave": abi.PBRT_KERNEL_WAVE,
-               "wavefront": abi.PBRT_KERNEL_WAVEFRONT, "wave_ci": abi.PBRT_KERNEL_WAVE_CI}
+               "wavefront": abi.PBRT_KERNEL_WAVEFRONT, "wave_ci": abi.PBRT_KERNEL_WAVE_CI,
+               "wave_dl": abi.PBRT_KERNEL_WAVE_DL}
 
     def __init__(self, scene, device=-1, lanes_per_wave=0, occupancy=0, kernel="auto"):
         desc = scene.desc if isinstance(scene, Scene) else scene

@@ -36,6 +36,7 @@ PBRT_KERNEL_SERIAL = 1
 PBRT_KERNEL_WAVE = 2
 PBRT_KERNEL_WAVEFRONT = 3
 PBRT_KERNEL_WAVE_CI = 4
+PBRT_KERNEL_WAVE_DL = 5
 PBRT_FLAG_SERIAL_START_PIXEL = 1
 
 PBRT_PANIC_NONE = 0

@@ -282,7 +282,8 @@ typedef struct pbrt_gpu_opts {
 #define PBRT_FLAG_SERIAL_START_PIXEL 1
 
 enum { PBRT_KERNEL_AUTO = 0, PBRT_KERNEL_SERIAL = 1, PBRT_KERNEL_WAVE = 2, PBRT_KERNEL_WAVEFRONT = 3,
-       PBRT_KERNEL_WAVE_CI = 4 /* wave pipeline, continuous-issue offset chain */ };
+       PBRT_KERNEL_WAVE_CI = 4, /* wave pipeline, continuous-issue offset chain */
+       PBRT_KERNEL_WAVE_DL = 5  /* DirectLighting: pixel-order StartPixel + jump-ahead, one lane per sample */ };
 
 typedef struct pbrt_gpu_ctx pbrt_gpu_ctx;
 

@@ -42,12 +42,19 @@ def gpu_render(scene, rd, lanes_per_wave=0, kernel="auto"):
         assert st.kernel == abi.PBRT_KERNEL_WAVEFRONT
     elif kernel == "wave_ci":
         assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
+    elif kernel == "wave_dl":
+        assert st.kernel == abi.PBRT_KERNEL_WAVE_DL
     return film, st
 
 
 def wave_eligible(rd):
     return (rd.integrator == abi.PBRT_INTEGRATOR_PATH and rd.n_dims >= 3
             and rd.light_strategy == abi.PBRT_LIGHT_STRATEGY_UNIFORM)
+
+
+def dl_wave_eligible(rd):
+    """DirectLighting on k_dl_*: the camera ray per pixel (the scenes here are pinhole)."""
+    return rd.integrator == abi.PBRT_INTEGRATOR_DIRECT_LIGHTING and rd.n_dims >= 1
 
 
 def oracle_render(scene, rd):
@@ -59,7 +66,8 @@ def oracle_render(scene, rd):
 def check(scene, rd, **kw):
     film, st = gpu_render(scene, rd, **kw)
     if kw.get("kernel", "auto") == "auto":
-        want = (abi.PBRT_KERNEL_WAVE, abi.PBRT_KERNEL_WAVE_CI) if wave_eligible(rd) else (abi.PBRT_KERNEL_SERIAL,)
+        want = (abi.PBRT_KERNEL_WAVE, abi.PBRT_KERNEL_WAVE_CI) if wave_eligible(rd) else \
+            (abi.PBRT_KERNEL_WAVE_DL,) if dl_wave_eligible(rd) else (abi.PBRT_KERNEL_SERIAL,)
         assert st.kernel in want
     ofilm, ost = oracle_render(scene, rd)
     assert st.paths_traced == ost.paths
@@ -245,7 +253,10 @@ def test_golden_fixtures(name, kernel):
     scene = G.Scene.readme(w, h) if case["scene"] == "readme" else G.Scene.cornell(w, h)
     rd = abi.render_desc(**case["render"])
     if kernel in ("wavefront", "wave_ci") and not wave_eligible(rd):
-        pytest.skip("not eligible for the wave-parallel kernels")
+        if dl_wave_eligible(rd):
+            kernel = "wave_dl"   # DirectLighting's wave kernels instead of the path chain
+        else:
+            pytest.skip("not eligible for the wave-parallel kernels")
     film, st = gpu_render(scene, rd, kernel=kernel)
     gold = np.load(os.path.join(HERE, "golden", name + ".npz"))["film"]
     assert same_bits(film, gold)
@@ -266,13 +277,64 @@ def test_config_A_traces_nothing():
     assert not film.any()
 
 
-def test_config_A_prime_direct_lighting():
-    check(G.Scene.readme(256, 256), abi.render_desc(2, 2, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING))
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_config_A_prime_direct_lighting(kernel):
+    check(G.Scene.readme(256, 256), abi.render_desc(2, 2, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING),
+          kernel=kernel)
 
 
-def test_direct_lighting_sample_one():
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_direct_lighting_sample_one(kernel):
     check(G.Scene.readme(64, 64), abi.render_desc(2, 2, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING,
-                                                  dl_strategy=abi.PBRT_DL_UNIFORM_SAMPLE_ONE))
+                                                  dl_strategy=abi.PBRT_DL_UNIFORM_SAMPLE_ONE), kernel=kernel)
+
+
+DL = abi.PBRT_INTEGRATOR_DIRECT_LIGHTING
+
+
+@pytest.mark.parametrize("kw", [
+    dict(spp_x=8, spp_y=8),
+    dict(spp_x=5, spp_y=3, jitter=True),
+    dict(spp_x=4, spp_y=4, n_dims=1),
+    dict(spp_x=4, spp_y=4, n_dims=2),
+    dict(spp_x=4, spp_y=4, n_dims=7),
+    dict(spp_x=4, spp_y=4, max_depth=1),
+    dict(spp_x=4, spp_y=4, dl_strategy=abi.PBRT_DL_UNIFORM_SAMPLE_ONE, n_dims=2),
+    dict(spp_x=3, spp_y=3, tile_size=13),
+    dict(spp_x=3, spp_y=3, tile_begin=2, tile_stride=3),
+    dict(spp_x=24, spp_y=24, max_depth=3),
+    dict(spp_x=4, spp_y=4, mode=abi.PBRT_MODE_THROUGHPUT),
+    dict(spp_x=4, spp_y=4, mode=abi.PBRT_MODE_THROUGHPUT, dl_strategy=abi.PBRT_DL_UNIFORM_SAMPLE_ONE),
+])
+@pytest.mark.parametrize("scene", ["readme", "cornell"])
+def test_direct_lighting_wave_kernel_bitexact(scene, kw):
+    """DirectLighting on k_dl_setup + k_dl_samples (pixel-order StartPixel and
+    jump-ahead, then one lane per sample): bit for bit the oracle's serial
+    replay, in both modes, both strategies and every sampler shape it takes."""
+    sc = G.Scene.readme(72, 40) if scene == "readme" else G.Scene.cornell(72, 40)
+    rd = abi.render_desc(integrator=DL, **kw)
+    film, st = check(sc, rd, kernel="wave_dl")
+    assert st.kernel == abi.PBRT_KERNEL_WAVE_DL
+    if rd.sampler_x * rd.sampler_y > 1:
+        assert film.max() > 0
+
+
+def test_direct_lighting_wave_kernel_n_dims_0_falls_back_to_serial():
+    """n_dims = 0: pFilm comes from the RNG, so the camera ray is per sample."""
+    rd = abi.render_desc(3, 3, integrator=DL, n_dims=0)
+    film, st = check(G.Scene.readme(40, 24), rd)
+    assert st.kernel == abi.PBRT_KERNEL_SERIAL
+    with G.Renderer(G.Scene.readme(40, 24), kernel="wave_dl") as r:
+        with pytest.raises(G.PbrtError) as ei:
+            r.render(rd)
+    assert ei.value.code == abi.PBRT_E_UNSUPPORTED
+
+
+def test_direct_lighting_wave_kernel_1080p_64spp_vs_oracle():
+    """Config B's frame under DirectLighting (UniformSampleAll): the whole
+    1080p / 64 spp film bit for bit."""
+    scene = G.Scene.readme(1920, 1080)
+    check(scene, abi.render_desc(8, 8, integrator=DL), kernel="wave_dl")
 
 
 @pytest.mark.parametrize("kw", [
@@ -624,7 +686,7 @@ def test_throughput_mode_bitexact_vs_oracle(case, kernel):
     check(scene, abi.render_desc(**kw, mode=MB), kernel=kernel)
 
 
-@pytest.mark.parametrize("kw", [dict(n_dims=1), dict(integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING),
+@pytest.mark.parametrize("kw", [dict(n_dims=1), dict(integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING, n_dims=0),
                                 dict(light_strategy=abi.PBRT_LIGHT_STRATEGY_POWER)])
 def test_throughput_mode_serial_fallback(kw):
     """Renders the wave path cannot take run Mode B on the serial kernel."""
@@ -701,3 +763,21 @@ def test_wave_ci_large_spp_global_start_pixel_values(spp):
     rd = abi.render_desc(spp, spp, max_depth=6)
     film, st = check(scene, rd, kernel="wave_ci")
     assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
+
+
+@pytest.mark.parametrize("mode", [abi.PBRT_MODE_EXACT, abi.PBRT_MODE_THROUGHPUT])
+@pytest.mark.parametrize("kernel", ["serial", "wave_dl"])
+def test_direct_lighting_panic_is_reported_like_the_oracle(kernel, mode):
+    """DirectLighting with UniformSampleOne on the panic scene: Ld > 10
+    (integrator.go:73-75); kind, tile, pixel, sample and bounce as the oracle's."""
+    scene = panic_scene()
+    rd = abi.render_desc(3, 3, integrator=DL, dl_strategy=abi.PBRT_DL_UNIFORM_SAMPLE_ONE, mode=mode)
+    rc, _, ost = O.render(scene.desc, rd, threads=1)
+    assert rc == abi.PBRT_E_REF_PANIC and ost.panic_kind == abi.PBRT_PANIC_LD_GT_10
+    with G.Renderer(scene, kernel=kernel) as r:
+        with pytest.raises(G.PbrtError) as ei:
+            r.render(rd)
+    st = ei.value.stats
+    assert ei.value.code == abi.PBRT_E_REF_PANIC
+    assert (st.panic_kind, st.panic_tile, st.panic_pixel_x, st.panic_pixel_y, st.panic_sample, st.panic_bounce) == (
+        ost.panic_kind, ost.panic_tile, ost.panic_px, ost.panic_py, ost.panic_sample, ost.panic_bounce)
