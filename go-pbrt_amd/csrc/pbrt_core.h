@@ -169,7 +169,7 @@ struct EF {
 GO_HD void ef_check(const EF& f, int& panic) {
     // !(|lo| < Inf) is true for ±Inf and NaN
     const bool bad = (int)!(gomath::abs(f.lo) < kInf) | (int)!(gomath::abs(f.hi) < kInf) | (int)(f.lo > f.hi);
-    panic = bad ? 1 : panic;
+    panic = bad ? (int)PBRT_PANIC_EFLOAT : panic;
 }
 GO_HD EF ef_new(double v, double err, int& panic) {
     EF f{v, v, v};

@@ -978,6 +978,47 @@ __device__ inline Spec estimate_direct(const DevScene& sc, uint16_t* stack, int&
     return ld_vis;
 }
 
+// Sphere.PdfWi (sphere.go:350-363): the cone pdf from outside the sphere;
+// from inside, the generic Shape PdfWi (shape.go:29-47): the spawned ray's
+// Sphere.Intersect (EFloat: can panic), 0 on a miss or an infinite pdf.
+__device__ inline double sphere_pdf_wi(const pbrt_shape_desc& s, const SI& ref, V3 wi, int& panic) {
+    const V3 pc = xf_point(s.object_to_world.m, V3{0, 0, 0}, V3{0, 0, 0}, nullptr);
+    const V3 po = offset_ray_origin(ref.p, ref.perr, ref.n, ref.p - pc);
+    if (dist2(po, pc) <= s.radius * s.radius) {
+        const Ray r{offset_ray_origin(ref.p, ref.perr, ref.n, wi), wi, kInf, ref.time};   // SpawnRay
+        double t;
+        V3 ph;
+        if (!shape_hit(s, r, t, ph, panic) || panic) return 0.0;
+        SI hs;
+        shape_si(s, r, ph, hs);
+        const double area = s.phi_max * s.radius * (s.z_max - s.z_min);
+        const double pdf = dist2(ref.p, hs.p) / absdot(hs.n, muls(muls(wi, -1), area));
+        return gomath::is_inf(pdf) ? 0.0 : pdf;
+    }
+    const double sin2max = s.radius * s.radius / dist2(ref.p, pc);
+    const double cosmax = gomath::sqrt(gomath::max(0, 1.0 - sin2max));
+    return 1.0 / (2.0 * gomath::kPi * (1.0 - cosmax));   // UniformConePdf
+}
+
+// PBRT_FLAG_PANIC_FIDELITY: EstimateDirect's BSDF-sampled half for an area
+// light (integrator.go:132-192). Its radiance is always 0 (no primitive
+// carries an area light, primitive.go:33), but Sphere.PdfWi and the spawned
+// ray's closest hit run in the reference and can panic; only that is kept.
+__device__ inline void estimate_direct_mis_ray(const DevScene& sc, uint16_t* stack, int& panic, const SI& si,
+                                               const BSDF& b, int li, V2 u_scat) {
+    const pbrt_light_desc& L = sc.lights[li];
+    if (L.type != PBRT_LIGHT_DIFFUSE_AREA) return;   // IsDeltaLight
+    V3 wi;
+    double pdf;
+    const Spec f = bsdf_sample_f(b, si.wo, u_scat, wi, pdf);   // local-frame wi (#7)
+    if (is_black(f) || !(pdf > 0.0)) return;
+    const double lpdf = sphere_pdf_wi(sc.shapes[L.shape], si, wi, panic);
+    if (panic || lpdf == 0) return;
+    Ray r{offset_ray_origin(si.p, si.perr, si.n, wi), wi, kInf, si.time};
+    SI tmp;
+    (void)bvh_traverse<false>(sc, r, &tmp, stack, panic);
+}
+
 // Distribution1D.SampleDiscrete + FindInterval (sampling.go:42-55, math.go:64-80)
 __device__ inline int sample_discrete(const pbrt_distribution_desc& d, double u, double& pdf) {
     int size = d.count + 1, first = 0, len = size;
@@ -994,7 +1035,7 @@ __device__ inline int sample_discrete(const pbrt_distribution_desc& d, double u,
 
 // UniformSampleOneLight (integrator.go:48-77): no /lightPdf, panic if > 10 (#10)
 __device__ inline Spec uniform_sample_one_light(const DevScene& sc, Thread& t, const SI& si, const BSDF& b,
-                                                const pbrt_distribution_desc* dist) {
+                                                const pbrt_distribution_desc* dist, bool fidelity = false) {
     const int n = sc.n_lights;
     if (n == 0) return spec(0);
     int ln;
@@ -1006,10 +1047,11 @@ __device__ inline Spec uniform_sample_one_light(const DevScene& sc, Thread& t, c
         ln = (int)gomath::to_int(gomath::min(get1d(t) * (double)n, (double)(n - 1)));
     }
     V2 ul = get2d(t);
-    get2d(t);   // uScattering: only the (skipped) MIS half reads it
+    const V2 us = get2d(t);   // uScattering: only the MIS half reads it
     t.shadow_rays++;
     Spec s = estimate_direct(sc, t.stack, t.panic, si, b, ln, ul);
-    if (max_component(s) > 10) t.panic = PBRT_PANIC_LD_GT_10;
+    if (fidelity && !t.panic) estimate_direct_mis_ray(sc, t.stack, t.panic, si, b, ln, us);
+    if (!t.panic && max_component(s) > 10) t.panic = PBRT_PANIC_LD_GT_10;
     return s;
 }
 
@@ -1017,14 +1059,25 @@ __device__ inline Spec uniform_sample_one_light(const DevScene& sc, Thread& t, c
 // Path.Li (path.go:32-157). Out of line in the serial kernel: fully inlined
 // into k_render_exact the compiler produced a kernel that faulted only after
 // other kernels had run on the device (an uninitialized-register read).
-__device__ __noinline__ Spec path_li(const DevScene& sc, Thread& t, Ray ray, int max_depth, double rr_threshold) {
+// fidelity (PBRT_FLAG_PANIC_FIDELITY): also trace the rays whose results never
+// reach the film but can panic in the reference -- the closest hit at
+// bounces == maxDepth (path.go:44-45, 66) and the MIS half of EstimateDirect.
+__device__ __noinline__ Spec path_li(const DevScene& sc, Thread& t, Ray ray, int max_depth, double rr_threshold,
+                                     bool fidelity) {
     Spec L = spec(0), beta = spec(1);
     int32_t bounces = 0;
     const double eta_scale = 1.0;
     for (;;) {
         bounces++;
         t.bounce = bounces;
-        if (bounces >= max_depth) break;   // path.go:66 breaks whether or not the ray hits
+        if (bounces >= max_depth) {   // path.go:66 breaks whether or not the ray hits
+            if (fidelity) {
+                SI tmp;
+                t.closest_rays++;
+                (void)bvh_traverse<false>(sc, ray, &tmp, t.stack, t.panic);
+            }
+            break;
+        }
         SI isect;
         t.closest_rays++;
         if (!bvh_traverse<false>(sc, ray, &isect, t.stack, t.panic)) break;
@@ -1032,7 +1085,7 @@ __device__ __noinline__ Spec path_li(const DevScene& sc, Thread& t, Ray ray, int
         BSDF b;
         if (compute_bsdf(sc, isect, b) < 0) { t.panic = -1; break; }
         if (b.n_bxdfs > 0) {   // NumComponents(BSDFAll &^ BSDFSpecular) > 0
-            Spec ld = uniform_sample_one_light(sc, t, isect, b, sc.dist);
+            Spec ld = uniform_sample_one_light(sc, t, isect, b, sc.dist, fidelity);
             if (t.panic) break;
             L = L + smul(beta, ld);
         }
@@ -1060,7 +1113,8 @@ __device__ __noinline__ Spec path_li(const DevScene& sc, Thread& t, Ray ray, int
 }
 
 // DirectLighting.Li at depth 0 (directlighting.go:62-104)
-__device__ __noinline__ Spec direct_li(const DevScene& sc, Thread& t, Ray ray, int max_depth, int strategy) {
+__device__ __noinline__ Spec direct_li(const DevScene& sc, Thread& t, Ray ray, int max_depth, int strategy,
+                                       bool fidelity) {
     Spec L = spec(0);
     SI si;
     t.bounce = 1;
@@ -1079,14 +1133,15 @@ __device__ __noinline__ Spec direct_li(const DevScene& sc, Thread& t, Ray ray, i
             Spec acc = spec(0);
             for (int j = 0; j < sc.n_lights; j++) {
                 V2 ul = get2d(t);
-                get2d(t);
+                const V2 us = get2d(t);
                 t.shadow_rays++;
                 acc = acc + estimate_direct(sc, t.stack, t.panic, si, b, j, ul);
+                if (fidelity && !t.panic) estimate_direct_mis_ray(sc, t.stack, t.panic, si, b, j, us);
                 if (t.panic) return L;
             }
             L = L + acc;
         } else {
-            L = L + uniform_sample_one_light(sc, t, si, b, nullptr);
+            L = L + uniform_sample_one_light(sc, t, si, b, nullptr, fidelity);
         }
     }
     if (0 + 1 < max_depth) {

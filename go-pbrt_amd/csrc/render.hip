@@ -191,8 +191,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kMinWaves
                 V2 plens = get2d(t);
                 double tu = get1d(t);
                 Ray ray = camera_ray(cam, (double)px + u0.x, (double)py + u0.y, tu, plens);
-                Spec L = (rp.integrator == PBRT_INTEGRATOR_PATH) ? path_li(sc, t, ray, rp.max_depth, rp.rr_threshold)
-                                                                 : direct_li(sc, t, ray, rp.max_depth, rp.dl_strategy);
+                const bool fid = (rp.flags & PBRT_FLAG_PANIC_FIDELITY) != 0;
+                Spec L = (rp.integrator == PBRT_INTEGRATOR_PATH)
+                             ? path_li(sc, t, ray, rp.max_depth, rp.rr_threshold, fid)
+                             : direct_li(sc, t, ray, rp.max_depth, rp.dl_strategy, fid);
                 paths++;
                 if (t.panic) {
                     PanicRec pr;
@@ -2501,6 +2503,7 @@ const PcgJump& pcg_jump_table() {
 // Can the wave-parallel kernels replay this render exactly? (conditions: pbrt_spec.h)
 bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const RenderParams& rp, ChainLayout& L,
                    ChainLayout& Lci) {
+    if (rd->flags & PBRT_FLAG_PANIC_FIDELITY) return false;   // the serial kernel traces the extra rays
     const bool dl = rd->integrator == PBRT_INTEGRATOR_DIRECT_LIGHTING;
     if (dl) {   // k_dl_*: the camera ray must be per pixel (pFilm stratified; pLens stratified or unused)
         if (rd->n_dims < 1 || (rd->n_dims < 2 && c->host_scene.camera.lens_radius > 0)) return false;

@@ -38,6 +38,7 @@ PBRT_KERNEL_WAVEFRONT = 3
 PBRT_KERNEL_WAVE_CI = 4
 PBRT_KERNEL_WAVE_DL = 5
 PBRT_FLAG_SERIAL_START_PIXEL = 1
+PBRT_FLAG_PANIC_FIDELITY = 2
 
 PBRT_PANIC_NONE = 0
 PBRT_PANIC_LD_GT_10 = 1

@@ -280,6 +280,11 @@ typedef struct pbrt_gpu_opts {
 /* WAVE kernel: always replay StartPixel serially (the path normally taken
  * only after a pcg_bounded rejection); results are identical. */
 #define PBRT_FLAG_SERIAL_START_PIXEL 1
+/* Panic fidelity: also trace the rays whose results never reach the film but
+ * whose traversal can panic in the reference -- EstimateDirect's BSDF-sampled
+ * MIS ray for an area light (integrator.go:132-192, incl. Sphere.PdfWi) and
+ * the closest hit at bounces == maxDepth (path.go:44-45,66). Serial kernel. */
+#define PBRT_FLAG_PANIC_FIDELITY 2
 
 enum { PBRT_KERNEL_AUTO = 0, PBRT_KERNEL_SERIAL = 1, PBRT_KERNEL_WAVE = 2, PBRT_KERNEL_WAVEFRONT = 3,
        PBRT_KERNEL_WAVE_CI = 4, /* wave pipeline, continuous-issue offset chain */

@@ -7,13 +7,15 @@
  * pbrt_scene_desc the device path does and is used ONLY as the parity checker
  * (tests/, __graft_entry__.smoke) and as bench.py's cpu_baseline ("port").
  *
- * Deliberate deviations (none changes a film value):
+ * Deliberate deviations (none changes a film value), both undone by the
+ * render flag PBRT_FLAG_PANIC_FIDELITY (or ORACLE_FLAG_MIS_RAY for the first):
  *  - EstimateDirect's BSDF-sampling (MIS) branch for the area light is
- *    skipped unless ORACLE_FLAG_MIS_RAY is set: in every scene the reference
- *    can build, no primitive carries an area light (primitive.go:33), so the
- *    branch always adds 0 (integrator.go:132-192). It costs one closest-hit ray.
+ *    skipped: in every scene the reference can build, no primitive carries an
+ *    area light (primitive.go:33), so the branch always adds 0
+ *    (integrator.go:132-192). It costs Sphere.PdfWi and one closest-hit ray,
+ *    either of which can panic in EFloat.Check.
  *  - the closest-hit ray at bounces == maxDepth is not traced: path.go:66
- *    breaks there whether or not it hit.
+ *    breaks there whether or not it hit (its traversal can panic too).
  *  - tile films are merged in tile-index order (the reference merges in
  *    goroutine completion order under a mutex, film.go:115-132).
  */
@@ -707,6 +709,30 @@ static intr_t sphere_sample_at(const pbrt_shape_desc* s, const si_t* ref, v2 u, 
     return it;
 }
 
+/* sphere.go:350-363 Sphere.PdfWi: the cone pdf from outside; from inside the
+ * generic shape.go:29-47 PdfWi (SpawnRay + Sphere.Intersect, may panic) */
+static double sphere_pdf_wi(orc_ctx* oc, const pbrt_shape_desc* s, const si_t* ref, v3 wi) {
+    v3 pc = xf_point(&s->object_to_world, V3(0, 0, 0), V3(0, 0, 0), NULL);
+    v3 po = offset_ray_origin(ref->p, ref->perr, ref->n, v_sub(ref->p, pc));
+    if (v_dist2(po, pc) <= s->radius * s->radius) {
+        ray_t r;
+        r.o = offset_ray_origin(ref->p, ref->perr, ref->n, wi);
+        r.d = wi; r.tmax = INFINITY; r.time = ref->time;
+        si_t hs;
+        double t;
+        if (!sphere_intersect(&oc->pc, s, &r, &hs, &t)) return 0;
+        double area = s->phi_max * s->radius * (s->z_max - s->z_min);
+        double pdf = v_dist2(ref->p, hs.p) / v_absdot(hs.n, v_muls(v_muls(wi, -1), area));
+        return gm_isinf(pdf, 0) ? 0 : pdf;
+    }
+    double sin2max = s->radius * s->radius / v_dist2(ref->p, pc);
+    double cosmax = sqrt(go_max(0, 1.0 - sin2max));
+    return 1.0 / (2.0 * go_Pi * (1.0 - cosmax));
+}
+static int panic_fidelity(const orc_ctx* oc) {
+    return (oc->flags & ORACLE_FLAG_MIS_RAY) || (oc->rd->flags & PBRT_FLAG_PANIC_FIDELITY);
+}
+
 /* interaction.go:91-102 SpawnRayToInteraction: Origin is the UN-offset point (#14) */
 static ray_t spawn_ray_to(const si_t* from, v3 to_p, v3 to_perr, v3 to_n) {
     v3 origin = offset_ray_origin(from->p, from->perr, from->n, v_sub(to_p, from->p));
@@ -785,13 +811,16 @@ static spec estimate_direct(orc_ctx* oc, const si_t* si, const bsdf_t* b, v2 u_s
             }
         }
     }
-    if (!is_delta && (oc->flags & ORACLE_FLAG_MIS_RAY)) {
+    if (!is_delta && panic_fidelity(oc)) {
         /* integrator.go:132-192: BSDF-sampled ray toward the area light. No
-         * primitive has an area light, so Li is always 0 here; the ray is
-         * traced only for fidelity (panics). */
+         * primitive has an area light, so Li is always 0 here; PdfLi and the
+         * ray are evaluated only for fidelity (panics). */
         v3 wi2; double spdf;
+        FL_OFF_BEGIN;
         spec f2 = bsdf_sample_f(b, si->wo, u_scat, flags, &wi2, &spdf);
-        if (!s_is_black(f2) && spdf > 0.0) {
+        double lpdf = (!s_is_black(f2) && spdf > 0.0) ? sphere_pdf_wi(oc, &sc->shapes[L->shape], si, wi2) : 0;
+        FL_OFF_END;
+        if (!s_is_black(f2) && spdf > 0.0 && lpdf != 0) {
             ray_t r2;
             r2.o = offset_ray_origin(si->p, si->perr, si->n, wi2);
             r2.d = wi2; r2.tmax = INFINITY; r2.time = si->time;
@@ -855,7 +884,14 @@ static spec path_li(orc_ctx* oc, sampler_t* smp, ray_t ray) {
     for (;;) {
         bounces++;
         oc->cur_bounce = bounces;
-        if (bounces >= rd->max_depth) break;     /* path.go:66 (hit or miss)  */
+        if (bounces >= rd->max_depth) {          /* path.go:66 (hit or miss)  */
+            if (panic_fidelity(oc)) {            /* traced by path.go:45 first */
+                si_t tmp;
+                oc->closest_rays++;
+                orc_bvh_intersect(oc, &ray, &tmp);
+            }
+            break;
+        }
         si_t isect;
         oc->closest_rays++;
         if (!orc_bvh_intersect(oc, &ray, &isect)) break;
