@@ -572,7 +572,8 @@ __device__ __forceinline__ int leaf_prims(const DevScene& sc, uint32_t first, ui
 // per lane, kStride apart), structured "while-while" for 64-lane waves: loop
 // A walks interior nodes until the lane reaches a leaf whose box it hits,
 // loop B tests that leaf's primitives.
-template <bool kAny, int kStride = kStackStride>
+// kLB: leaf boxes tested per scan iteration (LDS-staged trees).
+template <bool kAny, int kStride = kStackStride, int kLB = 4>
 __device__ inline bool bvh_walk_analytic(const DevScene& sc, Ray& ray, uint16_t* stack, int& panic, int& best,
                                          V3& best_ph) {
     best = -1;
@@ -600,35 +601,39 @@ __device__ inline bool bvh_walk_analytic(const DevScene& sc, Ray& ray, uint16_t*
             }
             for (;;) {
                 // A: the next candidate in the octant's leaf preorder whose box the
-                // ray enters; four per iteration (independent loads and slab tests;
+                // ray enters; kLB per iteration (independent loads and slab tests;
                 // a later result is used only if the earlier ones miss, same TMax)
                 bool leaf = false;
                 uint32_t first = 0, np = 0;
                 while (cand) {
-                    const int j0 = __builtin_ctz(cand);
-                    const uint32_t r1 = cand & (cand - 1);
-                    const int j1 = r1 ? __builtin_ctz(r1) : j0;
-                    const uint32_t r2 = r1 & (r1 - 1);
-                    const int j2 = r2 ? __builtin_ctz(r2) : j0;
-                    const uint32_t r3 = r2 & (r2 - 1);
-                    const int j3 = r3 ? __builtin_ctz(r3) : j0;
-                    const NodeView n0 = load_node(sc, leaves[j0]);
-                    const NodeView n1 = load_node(sc, leaves[j1]);
-                    const NodeView n2 = load_node(sc, leaves[j2]);
-                    const NodeView n3 = load_node(sc, leaves[j3]);
-                    const bool h0 = node_hit(n0, ray, inv, nx, ny, nz);
-                    const bool h1 = j1 != j0 && node_hit(n1, ray, inv, nx, ny, nz);
-                    const bool h2 = j2 != j0 && node_hit(n2, ray, inv, nx, ny, nz);
-                    const bool h3 = j3 != j0 && node_hit(n3, ray, inv, nx, ny, nz);
-                    if (h0 | h1 | h2 | h3) {
+                    int js[kLB];
+                    uint32_t rest[kLB];   // rest[q]: cand without its q + 1 lowest bits
+                    uint32_t r = cand;
+#pragma unroll
+                    for (int q = 0; q < kLB; q++) {
+                        js[q] = r ? __builtin_ctz(r) : js[0];
+                        r = r & (r - 1);
+                        rest[q] = r;
+                    }
+                    NodeView nv[kLB];
+#pragma unroll
+                    for (int q = 0; q < kLB; q++) nv[q] = load_node(sc, leaves[js[q]]);
+                    int qh = -1;
+#pragma unroll
+                    for (int q = kLB - 1; q >= 0; q--)
+                        if ((q == 0 || js[q] != js[0]) && node_hit(nv[q], ray, inv, nx, ny, nz)) qh = q;
+                    if (qh >= 0) {
                         leaf = true;
-                        const int q = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
-                        first = q == 0 ? n0.offset : q == 1 ? n1.offset : q == 2 ? n2.offset : n3.offset;
-                        np = q == 0 ? n0.n_prims : q == 1 ? n1.n_prims : q == 2 ? n2.n_prims : n3.n_prims;
-                        cand = q == 0 ? r1 : q == 1 ? r2 : q == 2 ? r3 : (r3 & (r3 - 1));
+#pragma unroll
+                        for (int q = 0; q < kLB; q++)
+                            if (q == qh) {
+                                first = nv[q].offset;
+                                np = nv[q].n_prims;
+                                cand = rest[q];
+                            }
                         break;
                     }
-                    cand = r3 & (r3 - 1);
+                    cand = rest[kLB - 1];
                 }
                 STEP_T(if (!kAny) tt.mark(5);)
                 if (!leaf) break;
@@ -642,30 +647,31 @@ __device__ inline bool bvh_walk_analytic(const DevScene& sc, Ray& ray, uint16_t*
         }
         int j = 0;
         for (;;) {
-            // A: the next leaf in the octant's preorder whose box the ray enters
+            // A: the next leaf in the octant's preorder whose box the ray enters,
+            // kLB leaves per iteration: independent loads and slab tests overlap;
+            // a later result is used only if the earlier leaves miss (same TMax)
             bool leaf = false;
             uint32_t first = 0, np = 0;
-            // four leaves per iteration: independent loads and slab tests overlap;
-            // a later result is used only if the earlier leaves miss (same TMax)
             while (j < nl) {
-                const int j1 = j + 1 < nl ? j + 1 : j, j2 = j + 2 < nl ? j + 2 : j, j3 = j + 3 < nl ? j + 3 : j;
-                const NodeView n0 = load_node(sc, leaves[j]);
-                const NodeView n1 = load_node(sc, leaves[j1]);
-                const NodeView n2 = load_node(sc, leaves[j2]);
-                const NodeView n3 = load_node(sc, leaves[j3]);
-                const bool h0 = node_hit(n0, ray, inv, nx, ny, nz);
-                const bool h1 = j1 > j && node_hit(n1, ray, inv, nx, ny, nz);
-                const bool h2 = j2 > j && node_hit(n2, ray, inv, nx, ny, nz);
-                const bool h3 = j3 > j && node_hit(n3, ray, inv, nx, ny, nz);
-                if (h0 | h1 | h2 | h3) {
+                NodeView nv[kLB];
+#pragma unroll
+                for (int q = 0; q < kLB; q++) nv[q] = load_node(sc, leaves[j + q < nl ? j + q : j]);
+                int qh = -1;
+#pragma unroll
+                for (int q = kLB - 1; q >= 0; q--)
+                    if ((q == 0 || j + q < nl) && node_hit(nv[q], ray, inv, nx, ny, nz)) qh = q;
+                if (qh >= 0) {
                     leaf = true;
-                    const int q = h0 ? 0 : h1 ? 1 : h2 ? 2 : 3;
-                    first = q == 0 ? n0.offset : q == 1 ? n1.offset : q == 2 ? n2.offset : n3.offset;
-                    np = q == 0 ? n0.n_prims : q == 1 ? n1.n_prims : q == 2 ? n2.n_prims : n3.n_prims;
-                    j += q + 1;
+#pragma unroll
+                    for (int q = 0; q < kLB; q++)
+                        if (q == qh) {
+                            first = nv[q].offset;
+                            np = nv[q].n_prims;
+                        }
+                    j += qh + 1;
                     break;
                 }
-                j += 4;
+                j += kLB;
             }
             STEP_T(if (!kAny) tt.mark(5);)
             if (!leaf) break;
@@ -722,9 +728,9 @@ __device__ inline bool bvh_walk_analytic(const DevScene& sc, Ray& ray, uint16_t*
 // the triangle meshes (extension) with the TMax it left; a triangle wins only
 // with a strictly smaller t, so an analytic primitive keeps a tie. A mesh hit
 // is reported as best = n_prims + its leaf slot.
-template <bool kAny, int kStride = kStackStride>
+template <bool kAny, int kStride = kStackStride, int kLB = 4>
 __device__ inline bool bvh_walk(const DevScene& sc, Ray& ray, uint16_t* stack, int& panic, int& best, V3& best_ph) {
-    const bool hit = bvh_walk_analytic<kAny, kStride>(sc, ray, stack, panic, best, best_ph);
+    const bool hit = bvh_walk_analytic<kAny, kStride, kLB>(sc, ray, stack, panic, best, best_ph);
     if (sc.mesh.n_nodes == 0 || panic || (kAny && hit)) return hit;
     double tm = ray.tmax;
     int32_t slot = -1, gid = -1;
@@ -735,11 +741,11 @@ __device__ inline bool bvh_walk(const DevScene& sc, Ray& ray, uint16_t* stack, i
     return true;
 }
 
-template <bool kAny>
+template <bool kAny, int kLB = 4>
 __device__ inline bool bvh_traverse(const DevScene& sc, Ray& ray, SI* si, uint16_t* stack, int& panic) {
     int best;
     V3 best_ph{0, 0, 0};
-    const bool hit = bvh_walk<kAny>(sc, ray, stack, panic, best, best_ph);
+    const bool hit = bvh_walk<kAny, kStackStride, kLB>(sc, ray, stack, panic, best, best_ph);
     STEP_T(StepTimer tt; tt.start();)
     if (!kAny && best >= 0) prim_si(sc, best, ray, best_ph, *si);
     STEP_T(if (!kAny) tt.mark(7);)

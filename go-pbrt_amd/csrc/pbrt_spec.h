@@ -216,6 +216,9 @@ __device__ inline Spec spec_path(const DevScene& sc, const Cache& pc, const Spec
 // loop-carried state is PathState + the Cursor; `bounce` reports the bounce
 // of a panic like spec_path. Returns true when the path has ended (radiance
 // in s.L). Arithmetic and draw order are spec_path<true>'s, step for step.
+#ifndef PBRT_PATHS_LB
+#define PBRT_PATHS_LB 4   // leaf boxes per scan iteration in path_step's traversals (build option)
+#endif
 struct PathState {
     Spec L, beta;
     Ray ray;
@@ -246,7 +249,7 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
         s.bounces++;
         bounce = s.bounces;
         if (s.bounces >= max_depth) return true;
-        const bool hit = bvh_traverse<false>(sc, s.ray, &isect, stack, panic);
+        const bool hit = bvh_traverse<false, PBRT_PATHS_LB>(sc, s.ray, &isect, stack, panic);
         if (!hit) return true;
         if (panic) return true;
         if (compute_bsdf(sc, isect, b) < 0) {
@@ -317,7 +320,7 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
     if (pending) {
         Spec ld = spec(0);
         if (shadow) {
-            const bool occluded = bvh_traverse<true>(sc, sr, nullptr, stack, panic);
+            const bool occluded = bvh_traverse<true, PBRT_PATHS_LB>(sc, sr, nullptr, stack, panic);
             if (panic) return true;
             if (!occluded) ld = ld_vis;
         }

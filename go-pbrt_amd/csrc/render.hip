@@ -937,6 +937,382 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kPathsWav
     paths_group<P, kMB>(sc, rp, wb, slot_base, (int64_t)blockIdx.x * P, nrec, ctr, lds, s1d_lds);
 }
 
+// ------------------------------------------------- path wavefront (k_pw_*)
+// The full-path stage (k_paths_ci's work: every (pixel, sample) path from its
+// RNG state, with light sampling) as per-bounce launches over queues of live
+// paths, compacted every bounce and, between the closest-hit trace and the
+// shading, counting-sorted by the hit's material (SURVEY §8 north_star: "rays
+// compacted and sorted by material between bounces"):
+//   k_pw_cache   bounce-1 EstimateDirect per (pixel, light), uLight = (0,0)
+//   k_pw_start   per path: bounce 1 from the pixel record (path_step<1>),
+//                then the next bounce's depth test -> trace queue or done
+//   k_pw_trace   closest hit of every queued ray; a miss or a panic ends the
+//                path, a hit goes to the hit queue with its material key
+//   k_pw_count / k_pw_scan / k_pw_scatter   counting sort of the hit queue
+//   k_pw_shade   interaction, BSDF, light-sample draws up to the shadow ray,
+//                BSDF sample, throughput and Russian roulette
+//   k_pw_shadow  the deferred shadow ray, L += beta0 * Ld, then the depth
+//                test -> trace queue or done
+//   k_pw_panics  per pixel record: its first panic (sample order) + counters
+// Each step is path_step<2>'s code split at its two traversals, in its order,
+// so L per (pixel, sample) is bit-identical to k_paths_ci's. Grid-stride
+// kernels read the queue lengths on the device (no host round trip).
+struct alignas(16) PwPath {
+    Ray ray;         // next closest-hit ray (tmax: after the walk, for prim_si)
+    Spec L, beta;
+    Ray sr;          // deferred shadow ray
+    Spec beta0, ld;  // its throughput and unoccluded Ld
+    V3 ph;           // object-space hit point of the closest hit
+    uint64_t rng;    // PCG32 state (the increment is the tile's)
+    int64_t rec;     // pixel record in the batch
+    int32_t k, cur1d, cur2d, kdep;
+    int32_t bounces, best, flags, pnc;
+    int32_t bnc, pad0, pad1, pad2;
+};
+constexpr int kPwPending = 1, kPwShadow = 2, kPwDone = 4;
+constexpr int kPwMaxKeys = 64;   // material keys of the sort (more materials share the last)
+struct PwQueues {
+    uint32_t* q[3];          // trace queue (current / next) and the hit queue, path ids
+    uint32_t* sorted;        // hit queue in material order
+    uint32_t* cnt;           // [0] trace, [1] next trace, [2] hits, [3..3+kPwMaxKeys) key counts, then offsets
+    int64_t cap;
+};
+__device__ __forceinline__ uint32_t pw_push(uint32_t* cnt, uint32_t* q, uint32_t v) {
+    const unsigned long long m = __ballot(1);
+    const int lead = __ffsll((long long)m) - 1, lane = threadIdx.x & (kWave - 1);
+    uint32_t base = 0;
+    if (lane == lead) base = atomicAdd(cnt, (uint32_t)__popcll(m));
+    base = __shfl(base, lead);
+    const uint32_t pos = base + (uint32_t)__popcll(m & ((1ULL << lane) - 1ULL));
+    q[pos] = v;
+    return pos;
+}
+// atomicAdd(&ctr[key], 1) for every active lane, aggregated per distinct key
+// of the wave (few materials: a handful of atomics per wave instead of one per
+// lane on the same few addresses); returns the lane's old-count position
+__device__ __forceinline__ uint32_t pw_add_by_key(uint32_t* ctr, int key) {
+    const int lane = threadIdx.x & (kWave - 1);
+    uint32_t pos = 0;
+    unsigned long long todo = __ballot(1);
+    for (;;) {
+        const int lead = __ffsll((long long)todo) - 1;
+        const int k0 = __shfl(key, lead);
+        const unsigned long long m = __ballot(key == k0) & todo;
+        uint32_t base = 0;
+        if (lane == lead) base = atomicAdd(&ctr[k0], (uint32_t)__popcll(m));
+        base = __shfl(base, lead);
+        if (key == k0 && ((todo >> lane) & 1ULL)) pos = base + (uint32_t)__popcll(m & ((1ULL << lane) - 1ULL));
+        todo &= ~m;
+        if (!todo) break;
+    }
+    return pos;
+}
+// a finished path: its radiance, and its panic into the pixel's key
+__device__ __forceinline__ void pw_finish(const WaveBufs& wb, int n, const PwPath& p, unsigned long long* pkey) {
+    double* o = wb.L + (p.rec * n + p.k) * 3;
+    o[0] = p.L.r;
+    o[1] = p.L.g;
+    o[2] = p.L.b;
+    if (p.pnc)
+        atomicMin(&pkey[p.rec], ((unsigned long long)p.k << 32) | ((unsigned long long)(p.bnc & 0xFFFFFF) << 8) |
+                                    (unsigned long long)((p.pnc + 1) & 0xFF));
+}
+// path_step's loop-top depth test; false: the path is done
+__device__ __forceinline__ bool pw_next_bounce(PwPath& p, int max_depth) {
+    p.bounces++;
+    p.bnc = p.bounces;
+    return p.bounces < max_depth;
+}
+// the bounce-1 light estimates of the pixel record (global-memory PixelCache)
+struct PwCache {
+    SI si;
+    BSDF b;
+    V3 wo;
+    const Spec* ld;
+    const int* ld_panic;
+};
+
+__global__ __launch_bounds__(kWave) void k_pw_cache(DevScene sc, WaveBufs wb, int64_t rec0, int64_t nrec,
+                                                    Spec* __restrict__ ldc, int* __restrict__ ldp) {
+    __shared__ uint16_t stack_lds[64 * kStackStride];
+    stage_nodes(sc);
+    const int nl = sc.n_lights;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nrec * nl) return;
+    const int64_t r = i / nl;
+    const int l = (int)(i - r * nl);
+    const PixelRec& pr = wb.prec[rec0 + r];
+    if (!(pr.hit && pr.b.n_bxdfs > 0)) return;
+    int pl = 0;
+    const Spec ld = estimate_direct(sc, stack_lds + threadIdx.x, pl, pr.si, pr.b, l, V2{0.0, 0.0});
+    if (!pl && max_component(ld) > 10) pl = PBRT_PANIC_LD_GT_10;
+    ldc[i] = ld;
+    ldp[i] = pl;
+}
+
+template <bool kMB>
+__global__ __launch_bounds__(kWave) void k_pw_start(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
+                                                    int64_t rec0, int64_t nrec, const Spec* __restrict__ ldc,
+                                                    const int* __restrict__ ldp, PwPath* __restrict__ paths,
+                                                    PwQueues qs, unsigned long long* __restrict__ pkey) {
+    const int n = rp.spp;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n < 2 || i >= nrec * (n - 1)) return;
+    const int64_t r = i / (n - 1);
+    const int k = 1 + (int)(i - r * (n - 1));
+    const int64_t rec = rec0 + r, bs = rec / wb.ppt, pi = rec % wb.ppt;
+    if (k == 1) pkey[rec] = ~0ULL;
+    if (pi >= wb.tile_npx[bs]) return;
+    const PixelRec& pr = wb.prec[rec];
+    if (k >= pr.nvalid) return;
+    PwPath p;
+    p.rec = rec;
+    p.k = k;
+    p.L = spec(0);
+    p.pnc = 0;
+    p.bnc = 1;
+    if (!pr.hit) {   // no traced bounce: the sample's radiance is 0
+        pw_finish(wb, n, p, pkey);
+        return;
+    }
+    const uint64_t tile = (uint64_t)tile_of_slot(rp, slot_base + bs);
+    Cursor c;
+    c.rng.state = kMB ? mb_state(tile, (uint64_t)pi, (uint64_t)k) : wb.memb[rec * n + k];
+    c.rng.inc = pcg_inc_of(tile);
+    c.draws = 0;
+    c.cur1d = 1;   // camera: Get2D pFilm, Get2D pLens, Get1D time (stratified)
+    c.cur2d = 2;
+    c.k = k;
+    c.kdep = 0;
+    PathState s;
+    s.L = spec(0);
+    s.beta = spec(1);
+    s.bounces = 1;
+    s.first = 1;
+    const PwCache pc{pr.si, pr.b, pr.wo, ldc + r * sc.n_lights, ldp + r * sc.n_lights};
+    const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, n, rp.ndims};
+    int pnc = 0, bnc = 1;
+    bool done = path_step<1>(sc, pc, ss, c, s, rp.max_depth, rp.rr_threshold, nullptr, pnc, bnc);
+    p.L = s.L;
+    p.beta = s.beta;
+    p.ray = s.ray;
+    p.bounces = s.bounces;
+    p.rng = c.rng.state;
+    p.cur1d = c.cur1d;
+    p.cur2d = c.cur2d;
+    p.kdep = c.kdep;
+    p.pnc = pnc;
+    p.bnc = bnc;
+    if (!done) done = !pw_next_bounce(p, rp.max_depth);
+    paths[i] = p;
+    if (done)
+        pw_finish(wb, n, p, pkey);
+    else
+        pw_push(&qs.cnt[0], qs.q[0], (uint32_t)i);
+}
+
+// in: trace queue `qin` (count cnt[cin]); out: hits (cnt[2], qs.q[2]) with
+// their material key counted in cnt[3 + key]
+__global__ __launch_bounds__(kWave) void k_pw_trace(DevScene sc, RenderParams rp, WaveBufs wb, PwPath* __restrict__ paths,
+                                                    PwQueues qs, int cin, int n_keys,
+                                                    unsigned long long* __restrict__ pkey) {
+    __shared__ uint16_t stack_lds[64 * kStackStride];
+    stage_nodes(sc);
+    const uint32_t* qin = qs.q[cin];
+    const uint32_t nq = qs.cnt[cin];
+    if (blockIdx.x == 0 && threadIdx.x == 0) qs.cnt[1] = 0;   // k_pw_shade's output, consumed after this pass's shadow step
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nq; t += gridDim.x * blockDim.x) {
+        const uint32_t id = qin[t];
+        PwPath& p = paths[id];
+        Ray ray = p.ray;
+        int panic = 0, best;
+        V3 ph{0, 0, 0};
+        const bool hit = bvh_walk<false>(sc, ray, stack_lds + threadIdx.x, panic, best, ph);
+        if (!hit || panic) {   // path_step: a miss or a traversal panic ends the path
+            if (panic) p.pnc = panic;
+            pw_finish(wb, rp.spp, p, pkey);
+            continue;
+        }
+        p.ray.tmax = ray.tmax;
+        p.best = best;
+        p.ph = ph;
+        int key = best < sc.n_prims ? sc.prims[best].material : sc.mesh.mesh_mat[tri_mesh(sc, best - sc.n_prims)];
+        key = min(max(key, 0), n_keys - 1);
+        p.flags = key;
+        pw_push(&qs.cnt[2], qs.q[2], id);
+        if (n_keys > 1) (void)pw_add_by_key(qs.cnt + 3, key);
+    }
+}
+// exclusive scan of the key counts into offsets (one thread; n_keys <= 64)
+__global__ void k_pw_scan(PwQueues qs, int n_keys) {
+    uint32_t acc = 0;
+    for (int k = 0; k < n_keys; k++) {
+        qs.cnt[3 + kPwMaxKeys + k] = acc;
+        acc += qs.cnt[3 + k];
+    }
+}
+__global__ __launch_bounds__(256) void k_pw_scatter(const PwPath* __restrict__ paths, PwQueues qs) {
+    const uint32_t nh = qs.cnt[2];
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nh; t += gridDim.x * blockDim.x) {
+        const uint32_t id = qs.q[2][t];
+        qs.sorted[pw_add_by_key(qs.cnt + 3 + kPwMaxKeys, paths[id].flags)] = id;
+    }
+}
+
+__global__ __launch_bounds__(kWave) void k_pw_shade(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
+                                                    PwPath* __restrict__ paths, PwQueues qs, int sorted,
+                                                    unsigned long long* __restrict__ pkey) {
+    const uint32_t* qin = sorted ? qs.sorted : qs.q[2];
+    const uint32_t nh = qs.cnt[2];
+    const int n = rp.spp;
+    if (blockIdx.x == 0 && threadIdx.x == 0) qs.cnt[0] = 0;   // k_pw_shadow's output (this pass's trace has read it)
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nh; t += gridDim.x * blockDim.x) {
+        const uint32_t id = qin[t];
+        PwPath& p = paths[id];
+        SI isect;
+        prim_si(sc, p.best, p.ray, p.ph, isect);
+        BSDF b;
+        if (compute_bsdf(sc, isect, b) < 0) {
+            p.pnc = -1;
+            pw_finish(wb, n, p, pkey);
+            continue;
+        }
+        const V3 wo = p.ray.d;
+        const int64_t bs = p.rec / wb.ppt;
+        Cursor c;
+        c.rng.state = p.rng;
+        c.rng.inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + bs));
+        c.draws = 0;
+        c.cur1d = p.cur1d;
+        c.cur2d = p.cur2d;
+        c.k = p.k;
+        c.kdep = p.kdep;
+        const SpecSampler ss{wb.s1d + p.rec * wb.s1d_stride, n, rp.ndims};
+        // path_step<2> after its closest-hit traversal (pbrt_spec.h)
+        int flags = 0;
+        const Spec beta0 = p.beta;
+        const int nl = sc.n_lights;
+        if (b.n_bxdfs > 0) {   // UniformSampleOneLight (integrator.go:48-77)
+            if (nl == 0) {
+                p.L = p.L + smul(p.beta, spec(0));
+            } else {
+                int ln;
+                if (sc.dist) {
+                    double lpdf;
+                    ln = sample_discrete(*sc.dist, c_get1d(c, ss), lpdf);
+                } else {
+                    ln = (int)gomath::to_int(gomath::min(c_get1d(c, ss) * (double)nl, (double)(nl - 1)));
+                }
+                V2 ul = c_get2d(c, ss);
+                c_get2d(c, ss);
+                flags |= kPwPending;
+                Ray sr;
+                Spec ld_vis = spec(0);
+                if (estimate_direct_begin(sc, isect, b, ln, ul, sr, ld_vis)) flags |= kPwShadow;
+                p.sr = sr;
+                p.ld = ld_vis;
+            }
+        }
+        {
+            V2 u = c_get2d(c, ss);
+            V3 wi;
+            double pdf;
+            Spec f = bsdf_sample_f(b, wo, u, wi, pdf);
+            if (is_black(f) || pdf == 0.0) {
+                flags |= kPwDone;
+            } else {
+                double wp = absdot(wi, isect.sn) / pdf;
+                p.beta = smul(p.beta, smuls(f, wp));
+                p.ray.o = offset_ray_origin(isect.p, isect.perr, isect.n, wi);
+                p.ray.d = wi;
+                p.ray.tmax = kInf;
+                p.ray.time = isect.time;
+                Spec rr = smuls(p.beta, 1.0);
+                if (max_component(rr) < rp.rr_threshold && p.bounces > 3) {
+                    double q = gomath::max(0.05, 1 - max_component(rr));
+                    double u1 = c_get1d(c, ss);
+                    if (c.kdep || u1 < q) flags |= kPwDone;
+                    else p.beta = sdivs(p.beta, 1 - q);
+                }
+            }
+        }
+        p.beta0 = beta0;
+        p.rng = c.rng.state;
+        p.cur1d = c.cur1d;
+        p.cur2d = c.cur2d;
+        p.kdep = c.kdep;
+        p.flags = flags;
+        pw_push(&qs.cnt[1], qs.q[1], id);   // every shaded path passes the shadow step
+    }
+}
+
+// in: the shaded paths (cnt[1], q[1]); out: the next trace queue (cnt[0], q[0])
+__global__ __launch_bounds__(kWave) void k_pw_shadow(DevScene sc, RenderParams rp, WaveBufs wb,
+                                                     PwPath* __restrict__ paths, PwQueues qs,
+                                                     unsigned long long* __restrict__ pkey) {
+    __shared__ uint16_t stack_lds[64 * kStackStride];
+    stage_nodes(sc);
+    const uint32_t ns = qs.cnt[1];
+    if (blockIdx.x == 0)   // hits and key counts, for the next pass
+        for (int i = threadIdx.x; i < 1 + kPwMaxKeys; i += blockDim.x) qs.cnt[2 + i] = 0;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < ns; t += gridDim.x * blockDim.x) {
+        const uint32_t id = qs.q[1][t];
+        PwPath& p = paths[id];
+        if (p.flags & kPwPending) {
+            Spec ld = spec(0);
+            if (p.flags & kPwShadow) {
+                int panic = 0;
+                Ray sr = p.sr;
+                const bool occluded = bvh_traverse<true>(sc, sr, nullptr, stack_lds + threadIdx.x, panic);
+                if (panic) {
+                    p.pnc = panic;
+                    pw_finish(wb, rp.spp, p, pkey);
+                    continue;
+                }
+                if (!occluded) ld = p.ld;
+            }
+            if (max_component(ld) > 10) {
+                p.pnc = PBRT_PANIC_LD_GT_10;
+                pw_finish(wb, rp.spp, p, pkey);
+                continue;
+            }
+            p.L = p.L + smul(p.beta0, ld);
+        }
+        if ((p.flags & kPwDone) || !pw_next_bounce(p, rp.max_depth))
+            pw_finish(wb, rp.spp, p, pkey);
+        else
+            pw_push(&qs.cnt[0], qs.q[0], id);
+    }
+}
+
+// per pixel record: paths_group's epilogue (first panic in sample order, counters)
+__global__ void k_pw_panics(RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t rec0, int64_t nrec,
+                            const unsigned long long* __restrict__ pkey, Counters* __restrict__ ctr) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrec) return;
+    const int64_t rec = rec0 + r, bs = rec / wb.ppt, pi = rec % wb.ppt;
+    if (pi >= wb.tile_npx[bs]) return;
+    int64_t x0, y0, x1, y1;
+    tile_bounds(rp, tile_of_slot(rp, slot_base + bs), x0, y0, x1, y1);
+    PanicRec p{0, 0, 0, 0, x0 + pi % (x1 - x0), y0 + pi / (x1 - x0)};
+    const PixelRec& pr = wb.prec[rec];
+    const unsigned long long key = rp.spp >= 2 ? pkey[rec] : ~0ULL;
+    if (pr.panic0) {
+        p.kind = pr.panic0;
+        p.sample = 1;
+        p.bounce = 1;
+    } else if (key != ~0ULL) {
+        p.kind = (int)(key & 0xFF) - 1;
+        p.bounce = (int)((key >> 8) & 0xFFFFFF);
+        p.sample = (int)(key >> 32);
+    }
+    wb.ppanic[rec] = p;
+    if (!p.kind && pr.nvalid > 1) {
+        atomicAdd(&ctr->paths, (unsigned long long)(pr.nvalid - 1));
+        atomicAdd(&ctr->camera_samples, (unsigned long long)(pr.nvalid - 1));
+    }
+}
+
 // THROUGHPUT mode setup for k_paths_ci<P, true>, one wave per pixel record:
 // StartPixel on the pixel's own stream mb_state(tile, pi, 0) and bounce 1
 // (camera ray, first hit, BSDF), written to the PixelRec / s1d buffers the
@@ -2210,6 +2586,10 @@ struct pbrt_gpu_ctx {
     uint32_t* d_slot_order = nullptr;
     int64_t ticks_cap = 0;
     std::vector<uint32_t> h_slot_order;
+    // path wavefront (k_pw_*, PBRT_PATHS_WF=1): path records, queues, counters,
+    // bounce-1 light estimates, per-pixel panic keys (grown on demand)
+    unsigned char* d_pw = nullptr;
+    size_t pw_cap = 0;
     // cold-frame schedule (k_tile_cost): per-slot features and sort keys
     float* d_cost = nullptr;
     uint64_t* d_cost_keys = nullptr;
@@ -2645,6 +3025,91 @@ int paths_ci_pixels(const pbrt_gpu_ctx* c, const RenderParams& rp) {
     // 4 pixels per wave where their stratified values fit in LDS, else 2
     // (config C, 256 spp), else 4 reading them from global memory (config E)
     return paths_ci_s1d_lds(rp, 4) && fits(4) ? 4 : paths_ci_s1d_lds(rp, 2) && fits(2) ? 2 : fits(4) ? 4 : 0;
+}
+
+// The full-path stage on the path wavefront (k_pw_*) instead of k_paths_ci:
+// PBRT_PATHS_WF=1 / 0 forces it on / off; by default it runs for scenes with
+// triangle meshes, where it measured faster (config D: 385 -> 343 ms EXACT,
+// 420 -> 381 ms THROUGHPUT), and not for the analytic scenes, where the
+// monolithic lane-refill kernel is twice as fast (config B: 118 vs 212-245 ms;
+// profiles/r02/path_wavefront_ab.json). PBRT_PW_SORT=1 adds the material sort
+// between trace and shade: a loss on every scene measured (B 212 -> 245 ms: a
+// few matte materials leave no shading divergence to remove), so off by default.
+bool paths_wf_enabled(const pbrt_gpu_ctx* c) {
+    if (const char* e = getenv("PBRT_PATHS_WF")) return atoi(e) == 1;
+    return c->mesh.n_nodes > 0;
+}
+int paths_wavefront(pbrt_gpu_ctx* c, const DevScene& sc, int64_t sb, int64_t nb) {
+    const RenderParams& rp = c->rp;
+    const int64_t nrec = nb * c->wb.ppt, per = rp.spp - 1;
+    const int nl = sc.n_lights;
+    const char* se = getenv("PBRT_PW_SORT");
+    const int sort = (se && atoi(se) == 1) ? 1 : 0;
+    const int n_keys = std::max(1, std::min(c->host_scene.n_materials, kPwMaxKeys));
+    double gb = 24.0;
+    if (const char* e = getenv("PBRT_PW_GB")) gb = atof(e) > 0 ? atof(e) : gb;
+    const int64_t per_path = (int64_t)sizeof(PwPath) + 4 * 4;   // record + 4 queue slots
+    int64_t chunk = per > 0 ? std::max<int64_t>(1, (int64_t)(gb * 1073741824.0) / (per_path * per)) : nrec;
+    chunk = std::min(chunk, nrec);
+    if (per > 0) chunk = std::min<int64_t>(chunk, (int64_t)0xFFFFFFF0 / per);
+    const int64_t cap = std::max<int64_t>(1, chunk * std::max<int64_t>(per, 1));
+    auto al = [](int64_t b) { return (b + 255) & ~int64_t(255); };
+    const int64_t ncnt = 3 + 2 * kPwMaxKeys;
+    const size_t need = (size_t)(al(cap * (int64_t)sizeof(PwPath)) + 4 * al(cap * 4) + al(ncnt * 4) +
+                                 al(chunk * std::max(nl, 1) * (int64_t)sizeof(Spec)) + al(chunk * std::max(nl, 1) * 4) +
+                                 al(nrec * 8));
+    if (c->pw_cap < need || !c->d_pw) {
+        if (c->d_pw) (void)hipFree(c->d_pw);
+        c->d_pw = nullptr;
+        c->pw_cap = 0;
+        HIPCHK(c, hipMalloc((void**)&c->d_pw, need));
+        c->pw_cap = need;
+    }
+    unsigned char* p = c->d_pw;
+    auto take = [&](int64_t bytes) {
+        unsigned char* q = p;
+        p += al(bytes);
+        return q;
+    };
+    PwPath* paths = (PwPath*)take(cap * (int64_t)sizeof(PwPath));
+    PwQueues qs;
+    for (int i = 0; i < 3; i++) qs.q[i] = (uint32_t*)take(cap * 4);
+    qs.sorted = (uint32_t*)take(cap * 4);
+    qs.cnt = (uint32_t*)take(ncnt * 4);
+    qs.cap = cap;
+    Spec* ldc = (Spec*)take(chunk * std::max(nl, 1) * (int64_t)sizeof(Spec));
+    int* ldp = (int*)take(chunk * std::max(nl, 1) * 4);
+    unsigned long long* pkey = (unsigned long long*)take(nrec * 8);
+    const unsigned G = (unsigned)std::max<int64_t>(64, (int64_t)c->n_simd * 8);   // grid-stride blocks
+    HIPCHK(c, hipMemsetAsync(pkey, 0xFF, (size_t)nrec * 8, c->stream));
+    const bool mb = rp.mode == PBRT_MODE_THROUGHPUT;
+    for (int64_t r0 = 0; r0 < nrec; r0 += chunk) {
+        const int64_t nr = std::min(chunk, nrec - r0);
+        if (per > 0) {
+            HIPCHK(c, hipMemsetAsync(qs.cnt, 0, (size_t)ncnt * 4, c->stream));
+            if (nl > 0)
+                hipLaunchKernelGGL(k_pw_cache, dim3((unsigned)((nr * nl + kWave - 1) / kWave)), dim3(kWave), 0,
+                                   c->stream, sc, c->wb, r0, nr, ldc, ldp);
+            auto start = mb ? k_pw_start<true> : k_pw_start<false>;
+            hipLaunchKernelGGL(start, dim3((unsigned)((nr * per + kWave - 1) / kWave)), dim3(kWave), 0, c->stream,
+                               sc, rp, c->wb, sb, r0, nr, ldc, ldp, paths, qs, pkey);
+            for (int pass = 0; pass + 1 < rp.max_depth; pass++) {
+                hipLaunchKernelGGL(k_pw_trace, dim3(G), dim3(kWave), 0, c->stream, sc, rp, c->wb, paths, qs, 0,
+                                   n_keys, pkey);
+                if (sort && n_keys > 1) {
+                    hipLaunchKernelGGL(k_pw_scan, dim3(1), dim3(1), 0, c->stream, qs, n_keys);
+                    hipLaunchKernelGGL(k_pw_scatter, dim3(G / 4), dim3(256), 0, c->stream, paths, qs);
+                }
+                hipLaunchKernelGGL(k_pw_shade, dim3(G), dim3(kWave), 0, c->stream, sc, rp, c->wb, sb, paths, qs,
+                                   sort && n_keys > 1 ? 1 : 0, pkey);
+                hipLaunchKernelGGL(k_pw_shadow, dim3(G), dim3(kWave), 0, c->stream, sc, rp, c->wb, paths, qs, pkey);
+            }
+        }
+        hipLaunchKernelGGL(k_pw_panics, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, c->stream, rp, c->wb, sb, r0,
+                           nr, pkey, c->d_ctr);
+    }
+    HIPCHK(c, hipGetLastError());
+    return PBRT_OK;
 }
 
 // Carve the per-batch buffers of the wave path. Budget: PBRT_WAVE_BUFFER_GB,
@@ -3164,6 +3629,13 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                                            dim3(kWave), 0, c->stream, with_slot(sc, 3), rp, c->wb, sb, nrec);
                     hipLaunchKernelGGL(k_dl_panics, dim3((unsigned)((nrec + 255) / 256)), dim3(256), 0, c->stream, rp,
                                        c->wb, sb, nrec, c->d_ctr);
+                } else if (paths_wf_enabled(c)) {
+                    if (rp.mode == PBRT_MODE_THROUGHPUT)
+                        hipLaunchKernelGGL(k_mb_setup, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
+                                           (unsigned)c->lay.total, c->stream, with_slot(sc, 4), rp, c->lay, c->d_jump,
+                                           c->wb, sb, nb);
+                    const int rcp = paths_wavefront(c, with_slot(sc, rp.mode == PBRT_MODE_THROUGHPUT ? 5 : 3), sb, nb);
+                    if (rcp != PBRT_OK) return rcp;
                 } else if (rp.mode == PBRT_MODE_THROUGHPUT && paths_ci_pixels(c, rp) > 0) {
                     // setup (StartPixel + bounce 1 per pixel), then lane-refill paths
                     hipLaunchKernelGGL(k_mb_setup, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
@@ -3401,7 +3873,7 @@ void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
     void* bufs[] = {c->d_shapes, c->d_materials, c->d_prims, c->d_nodes, c->d_order, c->d_lights, c->d_camera, c->d_film,
                     c->d_dist,   c->d_films,     c->d_s1d,   c->d_panics, c->d_ctr,   c->d_out,    c->d_jump,
                     c->d_wave,   c->d_fprims, c->d_wf,     c->d_ticks, c->d_slot_order, c->d_groups,
-                    c->d_gmasks, c->d_cost,   c->d_cost_keys};
+                    c->d_gmasks, c->d_cost,   c->d_cost_keys, c->d_pw};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     mesh_bvh_free(c->mesh);

@@ -114,10 +114,17 @@ MESH_CASES = [
 ]
 
 
+@pytest.mark.parametrize("paths_wf", ["default", "0"])
 @pytest.mark.parametrize("kernel", ["serial", "auto"])
 @pytest.mark.parametrize("mode", [abi.PBRT_MODE_EXACT, abi.PBRT_MODE_THROUGHPUT])
 @pytest.mark.parametrize("case", MESH_CASES, ids=lambda c: f"q{c[0]}{'s' if c[1] else ''}-{c[2]}")
-def test_render_mesh_bitexact(case, mode, kernel):
+def test_render_mesh_bitexact(case, mode, kernel, paths_wf, monkeypatch):
+    """Mesh scenes run their full paths on the path wavefront by default
+    (k_pw_*); PBRT_PATHS_WF=0 keeps k_paths_ci. Both bit for bit."""
+    if paths_wf != "default":
+        if kernel == "serial":
+            pytest.skip("the serial kernel has no path stage")
+        monkeypatch.setenv("PBRT_PATHS_WF", paths_wf)
     quads, spheres, kw = case
     scene = G.Scene.heightfield(48, 32, quads=quads, seed=1, spheres=spheres)
     rd = abi.render_desc(**kw, mode=mode)

@@ -781,3 +781,45 @@ def test_direct_lighting_panic_is_reported_like_the_oracle(kernel, mode):
     assert ei.value.code == abi.PBRT_E_REF_PANIC
     assert (st.panic_kind, st.panic_tile, st.panic_pixel_x, st.panic_pixel_y, st.panic_sample, st.panic_bounce) == (
         ost.panic_kind, ost.panic_tile, ost.panic_px, ost.panic_py, ost.panic_sample, ost.panic_bounce)
+
+
+PW_CASES = [
+    ("readme", 96, 64, dict(spp_x=4, spp_y=4)),
+    ("readme", 64, 48, dict(spp_x=3, spp_y=3, max_depth=12, rr_threshold=0.5)),
+    ("readme", 40, 24, dict(spp_x=2, spp_y=2, max_depth=1)),
+    ("readme", 48, 32, dict(spp_x=24, spp_y=24, max_depth=4)),
+    ("cornell", 48, 32, dict(spp_x=4, spp_y=4, max_depth=8)),
+    ("cornell", 32, 32, dict(spp_x=3, spp_y=3, light_strategy=abi.PBRT_LIGHT_STRATEGY_POWER)),
+]
+
+
+@pytest.mark.parametrize("sort", ["1", "0"])
+@pytest.mark.parametrize("mode", [abi.PBRT_MODE_EXACT, abi.PBRT_MODE_THROUGHPUT])
+@pytest.mark.parametrize("case", PW_CASES, ids=lambda c: f"{c[0]}{c[1]}x{c[2]}-{c[3]}")
+def test_path_wavefront_bitexact(case, mode, sort, monkeypatch):
+    """PBRT_PATHS_WF=1: the full paths as per-bounce compacted queues, sorted
+    by material between trace and shade (PBRT_PW_SORT) -- bit for bit the
+    oracle's film in both modes."""
+    monkeypatch.setenv("PBRT_PATHS_WF", "1")
+    monkeypatch.setenv("PBRT_PW_SORT", sort)
+    name, w, h, kw = case
+    scene = G.Scene.readme(w, h) if name == "readme" else G.Scene.cornell(w, h)
+    check(scene, abi.render_desc(**kw, mode=mode))
+
+
+@pytest.mark.parametrize("mode", [abi.PBRT_MODE_EXACT, abi.PBRT_MODE_THROUGHPUT])
+def test_path_wavefront_chunked_and_panics(mode, monkeypatch):
+    """A path-record budget small enough to force several chunks; and the
+    panic scene's report through the wavefront."""
+    monkeypatch.setenv("PBRT_PATHS_WF", "1")
+    monkeypatch.setenv("PBRT_PW_GB", "0.01")
+    check(G.Scene.readme(80, 48), abi.render_desc(5, 5, mode=mode))
+    scene = panic_scene()
+    rd = abi.render_desc(2, 2, mode=mode)
+    rc, _, ost = O.render(scene.desc, rd, threads=1)
+    with G.Renderer(scene) as r:
+        with pytest.raises(G.PbrtError) as ei:
+            r.render(rd)
+    st = ei.value.stats
+    assert (st.panic_kind, st.panic_tile, st.panic_pixel_x, st.panic_pixel_y, st.panic_sample, st.panic_bounce) == (
+        ost.panic_kind, ost.panic_tile, ost.panic_px, ost.panic_py, ost.panic_sample, ost.panic_bounce)
