@@ -47,7 +47,7 @@ def parse():
                          "E = 9 999 392-triangle height field, 3840x2160, Stratified(32,32), Path(10)")
     ap.add_argument("--spp", type=int, default=0, help="Stratified(spp, spp) (0 = the config's)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "serial", "wave", "wavefront", "wave_ci"])
-    ap.add_argument("--tiles-per-wave", type=int, default=0, help="k_chain lane groups per wave (0 = library default)")
+    ap.add_argument("--tiles-per-wave", type=int, default=0, help="k_chain_ci tiles per wave (0 = library default)")
     ap.add_argument("--occupancy", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=30.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0,

@@ -104,10 +104,6 @@ struct PixelCache {
     int first_panic;                  // panic of the camera-ray traversal
 };
 
-// Path.Li (path.go:32-157) from bounce 1 on, with bounce 1 taken from the
-// pixel cache. kNEE = false: trajectory only (no light sampling; the draws
-// are still consumed), used to learn D for an RNG offset (k_chain);
-// kNEE = true: the full path (k_paths). Each kernel instantiates one.
 // Bounce-1 state without the per-light estimates (what trajectories need).
 struct ChainCache {
     SI si;
@@ -117,105 +113,12 @@ struct ChainCache {
     int pad;
 };
 
-template <bool kNEE, class Cache>
-__device__ inline Spec spec_path(const DevScene& sc, const Cache& pc, const SpecSampler& ss, Cursor& c,
-                                 int max_depth, double rr_threshold, uint16_t* stack, int& panic, int& bounce) {
-    STEP_T(StepTimer tm; tm.start();)
-    Spec L = spec(0), beta = spec(1);
-    int32_t bounces = 1;
-    bounce = 1;
-    SI isect = pc.si;
-    BSDF b = pc.b;
-    V3 wo = pc.wo;
-    Ray ray;
-    bool first = true;
-    const int nl = sc.n_lights;
-    for (;;) {
-        if (!first) {
-            bounces++;
-            bounce = bounces;
-            if (bounces >= max_depth) break;
-            STEP_T(tm.mark(0);)
-            const bool hit = bvh_traverse<false>(sc, ray, &isect, stack, panic);
-            STEP_T(tm.mark(1);)
-            if (!hit) break;
-            if (panic) break;
-            if (compute_bsdf(sc, isect, b) < 0) {
-                panic = -1;
-                break;
-            }
-            STEP_T(tm.mark(2);)
-            wo = ray.d;
-        }
-        if (b.n_bxdfs > 0) {   // UniformSampleOneLight (integrator.go:48-77)
-            if (nl == 0) {
-                if (kNEE) L = L + smul(beta, spec(0));
-            } else if (kNEE) {
-                int ln;
-                if (sc.dist) {
-                    double lpdf;   // > 0 for every light (launch precondition)
-                    ln = sample_discrete(*sc.dist, c_get1d(c, ss), lpdf);
-                } else {
-                    ln = (int)gomath::to_int(gomath::min(c_get1d(c, ss) * (double)nl, (double)(nl - 1)));
-                }
-                V2 ul = c_get2d(c, ss);
-                c_get2d(c, ss);
-                Spec ld;
-                if constexpr (kNEE) {
-                    if (first) {
-                        ld = pc.ld[ln];
-                        if (pc.ld_panic[ln]) {
-                            panic = pc.ld_panic[ln];
-                            break;
-                        }
-                    }
-                }
-                if (!first) {
-                    ld = estimate_direct(sc, stack, panic, isect, b, ln, ul);
-                    if (panic) break;
-                    if (max_component(ld) > 10) {
-                        panic = PBRT_PANIC_LD_GT_10;
-                        break;
-                    }
-                }
-                L = L + smul(beta, ld);
-            } else {
-                c_skip1d(c, ss);
-                c_get2d(c, ss);
-                c_get2d(c, ss);
-            }
-        }
-        STEP_T(tm.mark(3);)
-        first = false;
-        V2 u = c_get2d(c, ss);
-        V3 wi;
-        double pdf;
-        Spec f = bsdf_sample_f(b, wo, u, wi, pdf);
-        if (is_black(f) || pdf == 0.0) break;
-        double wp = absdot(wi, isect.sn) / pdf;
-        beta = smul(beta, smuls(f, wp));
-        ray.o = offset_ray_origin(isect.p, isect.perr, isect.n, wi);
-        ray.d = wi;
-        ray.tmax = kInf;
-        ray.time = isect.time;
-        Spec rr = smuls(beta, 1.0);
-        if (max_component(rr) < rr_threshold && bounces > 3) {
-            double q = gomath::max(0.05, 1 - max_component(rr));
-            double u1 = c_get1d(c, ss);
-            if (c.kdep) break;
-            if (u1 < q) break;
-            beta = sdivs(beta, 1 - q);
-        }
-        STEP_T(tm.mark(4);)
-    }
-    return L;
-}
-
-// One iteration of spec_path<true>'s loop (path.go:32-157), for kernels that
-// refill a lane with a new path as soon as its path ends (k_paths_ci). The
-// loop-carried state is PathState + the Cursor; `bounce` reports the bounce
-// of a panic like spec_path. Returns true when the path has ended (radiance
-// in s.L). Arithmetic and draw order are spec_path<true>'s, step for step.
+// One iteration of Path.Li's loop (path.go:32-157) from bounce 1 on, with
+// bounce 1 taken from the pixel cache, for kernels that refill a lane with a
+// new path as soon as its path ends (k_paths_ci) or run one bounce per launch
+// (k_pw_*). The loop-carried state is PathState + the Cursor; `bounce`
+// reports the bounce of a panic. Returns true when the path has ended
+// (radiance in s.L). Arithmetic and draw order are the reference's.
 #ifndef PBRT_PATHS_LB
 #define PBRT_PATHS_LB 4   // leaf boxes per scan iteration in path_step's traversals (build option)
 #endif
@@ -333,10 +236,11 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
     return done;
 }
 
-// The rest of one spec_path<false> iteration once the interaction at bounce
+// The rest of one trajectory iteration (Path.Li without light sampling, whose
+// draws are still consumed) once the interaction at bounce
 // `bounces` and its BSDF are known (light draws consumed, BSDF sample,
 // throughput, Russian roulette), then the next iteration's depth test; the
-// wavefront chain kernels (k_wf_*) run a trajectory one such step per launch.
+// chain kernel (k_chain_ci) and the cold-frame probe run one per bounce.
 // Returns 0: trace `ray` next; 1: the trajectory ended (D = c.draws);
 // 2: its draw count depends on the sample index (kBadD).
 __device__ inline int traj_scatter(const DevScene& sc, const SI& isect, const BSDF& b, V3 wo, Cursor& c,

@@ -6,9 +6,12 @@
 //                    (integrator.go:228-289, 311-340): pixel loop, Stratified
 //                    StartPixel, samples 1..spp-1, Path.Li / DirectLighting.Li,
 //                    NaN guard, FilmTile.AddSample into the tile's film slot.
-//   k_render_decorr  THROUGHPUT mode: same arithmetic, one lane per
-//                    (pixel, sample) path with its own PCG32 stream; paths of
-//                    one pixel are summed in sample order in a second pass.
+//   wave pipeline    k_wf_primary (bounce 1 per pixel), k_chain_ci (the
+//                    tile's RNG-offset chain), k_paths_ci or the path
+//                    wavefront k_pw_* (full paths), k_film (tile films);
+//                    THROUGHPUT mode: k_mb_setup instead of the chain.
+//   k_dl_*           DirectLighting: pixel-order StartPixel + jump-ahead, one
+//                    lane per sample.
 //   k_merge_film     Film.MergeFilmTile (film.go:115-132): per output pixel,
 //                    RGBToXYZ of every covering tile film in tile-index order.
 //   k_intersect[_p]  batch BVH closest-hit / any-hit (bvh.go:659-765).
@@ -250,21 +253,19 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kMinWaves
 }
 
 // ------------------------------------------------------ EXACT, wave-parallel
-// Three kernels replace the serial tile replay (see pbrt_spec.h for why the
-// results are the same bits):
-//   k_chain  one 64-lane wave per tile. Per pixel: StartPixel (lane-parallel,
-//            with pcg_bounded rejections resolved), bounce 1 (camera ray,
-//            first hit, BSDF), then windows of speculative trajectories at
-//            RNG offsets head + 2j until every sample's offset is known.
-//            Writes a PixelRec, the stratified 1D values and the RNG state of
-//            each sample. The only serial dependency of the reference (the
-//            per-tile PCG32 stream) lives here, and only trajectories run here.
-//   k_paths  one wave per pixel: bounce-1 EstimateDirect per light (lane l ->
-//            light l), then the pixel's samples as full paths, one per lane.
-//            Writes L per sample and the pixel's first panic.
-//   k_film   one thread per tile-film pixel: FilmTile.AddSample contributions
-//            summed in the reference's order (pixels row-major, samples in
-//            order), i.e. the same floating-point sums as the serial replay.
+// The kernels that replace the serial tile replay (see pbrt_spec.h for why
+// the results are the same bits):
+//   k_chain_ci  per tile: StartPixel (lane-parallel, pcg_bounded rejections
+//               resolved), then speculative trajectories at RNG offsets until
+//               every sample's offset is known; writes the stratified values
+//               and each sample's RNG state. The only serial dependency of the
+//               reference (the per-tile PCG32 stream) lives here.
+//   k_paths_ci  the samples as full paths (bounce-1 EstimateDirect per light
+//               cached per pixel); writes L per sample and the pixel's first
+//               panic. k_pw_*: the same as per-bounce compacted queues.
+//   k_film      one thread per tile-film pixel: FilmTile.AddSample
+//               contributions summed in the reference's order (pixels
+//               row-major, samples in order), the serial replay's sums.
 __device__ __forceinline__ void stage_nodes(DevScene& sc) {
     if (sc.n_nodes > kLdsNodes) return;
     for (int i = threadIdx.x; i < sc.n_nodes; i += blockDim.x) g_nodes_lds[i] = sc.nodes[i];
@@ -300,12 +301,11 @@ struct WaveBufs {
     int64_t ppt;        // pixel records per tile slot (tile_size^2)
     int64_t s1d_stride; // ndims * spp
 };
-struct ChainLayout {   // byte offsets into k_chain's dynamic LDS block
+struct ChainLayout {   // byte offsets into the chain / setup kernels' dynamic LDS block
     int s1d, other, sbuf, dbuf, vbuf, total;
     int ring;      // k_chain_ci: offset ring after the StartPixel staging (no sbuf / dbuf)
     int staging;   // k_chain_ci: bytes of the StartPixel staging (s1d, other, vbuf)
 };
-constexpr uint32_t kBadD = 0xFFFFFFFFu;
 constexpr int kCiRingBytes = 4 * 1024;   // k_chain_ci offset ring (all lane groups of a wave)
 constexpr int kCiMaxGroups = 4;          // k_chain_ci lane groups (tiles) per wave
 
@@ -316,23 +316,6 @@ __device__ __forceinline__ int64_t tile_of_slot(const RenderParams& rp, int64_t 
     return rp.tile_begin + slot * rp.tile_stride;
 }
 __device__ __forceinline__ uint64_t pcg_inc_of(uint64_t seed) { return (seed << 1) | 1; }   // rng.go:28-34
-
-// k_chain runs G = 64 / L tiles per wave: lane group g (L lanes) owns tile
-// slot blockIdx.x * G + g and speculates with L candidate offsets per window
-// (fewer lanes per tile = less speculation waste; more tiles per wave keeps
-// every SIMD busy with ~one wave). Per iteration: (1) groups that need a new
-// pixel run StartPixel and bounce 1 one at a time, with all 64 lanes; (2) one
-// trajectory window for every group; (3) each group leader walks its chain.
-struct GroupState {
-    uint64_t S;     // PCG32 state at the group's chain head
-    int64_t pi;     // current pixel (row-major index in the tile)
-    int64_t npx;    // pixels of the tile
-    int kh;         // next sample without an offset
-    int phase;      // 0 needs a pixel, 1 resolving offsets, 2 tile finished
-    int stop;       // a reference panic ended the tile
-    int pad;
-};
-constexpr int kMaxGroups = 16;
 
 // Stratified.StartPixel (stratified.go:21-48) for one pixel. Every thread of
 // the workgroup calls it (it holds the block's barriers); the first wave does
@@ -437,318 +420,18 @@ __device__ uint64_t start_pixel_wave(const RenderParams& rp, const PcgJump& J, u
     return *sh_state;
 }
 
-// kDepth: LDS stack entries per lane. 32 when the nodes are staged in LDS
-// (<= kLdsNodes = 64 nodes: at most 31 interior nodes on any root-to-leaf
-// path, so the reference's [64] stack never holds more than 31 entries);
-// 64 otherwise. Bounce 1 (camera ray, first hit, BSDF) is read from the
-// PixelRec k_wf_primary wrote, so k_chain holds no second traversal.
-template <int kWaves, int kDepth>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8))) void k_chain(
-    DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
-    int64_t nslots_batch, int lanes_per_tile, Counters* __restrict__ ctr) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    __shared__ uint16_t stack_lds[kDepth * kStackStride];
-    __shared__ GroupState gs[kMaxGroups];
-    __shared__ uint64_t sh_state;
-    const int lane = threadIdx.x;
-    stage_nodes(sc);
-    const int L = lanes_per_tile, G = kWave / L;
-    const int g = lane / L, gl = lane - g * L;
-    const PcgJump& J = *jump;
-    double* s1d = (double*)(lds + lay.s1d);            // StartPixel staging (one group at a time)
-    uint16_t* other = (uint16_t*)(lds + lay.other);
-    uint64_t* sbuf = (uint64_t*)(lds + lay.sbuf);
-    uint32_t* dbuf = (uint32_t*)(lds + lay.dbuf);
-    uint32_t* vbuf = (uint32_t*)(lds + lay.vbuf);
-    ChainCache* pcs = (ChainCache*)(lds + lay.total);   // G entries after the layout
-    uint16_t* stack = stack_lds + lane;
-    const int n = rp.spp, ndims = rp.ndims;
-    unsigned long long windows = 0;
-    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    long long tprev = clock64();
-    auto mark = [&](int i) {
-        long long now = clock64();
-        ph[i] += (unsigned long long)(now - tprev);
-        tprev = now;
-    };
-    if (lane < G) {
-        const int64_t bs = (int64_t)blockIdx.x * G + lane;
-        GroupState& s = gs[lane];
-        s.pi = 0;
-        s.kh = 1;
-        s.stop = 0;
-        if (bs < nslots_batch) {
-            int64_t x0, y0, x1, y1;
-            tile_bounds(rp, tile_of_slot(rp, slot_base + bs), x0, y0, x1, y1);
-            Pcg seed;
-            pcg_seed(seed, (uint64_t)tile_of_slot(rp, slot_base + bs));   // Sampler.Clone(tile), integrator.go:318,328
-            s.S = seed.state;
-            s.npx = (x1 - x0) * (y1 - y0);
-            s.phase = s.npx > 0 ? 0 : 2;
-        } else {
-            s.S = 0;
-            s.npx = 0;
-            s.phase = 2;
-        }
-        if (bs < nslots_batch) wb.tile_npx[bs] = 0;
-    }
-    __syncthreads();
-
-    for (;;) {
-        // ---- (1) groups that need a pixel: StartPixel + bounce 1, one group at a time
-        for (int q = 0; q < G; q++) {
-            while (gs[q].phase == 0) {
-                const int64_t bs = (int64_t)blockIdx.x * G + q;
-                const int64_t tile = tile_of_slot(rp, slot_base + bs);
-                Pcg seed;
-                pcg_seed(seed, (uint64_t)tile);
-                const uint64_t inc = seed.inc;
-                const uint64_t S = gs[q].S;
-                const int64_t pi = gs[q].pi;
-                const int64_t rec = bs * wb.ppt + pi;
-                const uint64_t S1 = start_pixel_wave(rp, J, S, inc, s1d, other, vbuf, &sh_state);
-                double* gs1d = wb.s1d + rec * wb.s1d_stride;
-                for (int idx = lane; idx < ndims * n; idx += kWave) gs1d[idx] = s1d[idx];
-                mark(0);
-                const PixelRec& pr = wb.prec[rec];   // bounce 1 (k_wf_primary)
-                const int panic0 = pr.panic0, hit0 = pr.hit;
-                if (lane == 0) {
-                    pcs[q].si = pr.si;
-                    pcs[q].b = pr.b;
-                    pcs[q].wo = pr.wo;
-                    pcs[q].hit = hit0;
-                    GroupState& s = gs[q];
-                    s.S = S1;
-                    wb.tile_npx[bs] = (int32_t)(pi + 1);
-                    if (panic0) {   // the first traced sample panics at bounce 1: the tile ends here
-                        s.stop = 1;
-                        s.phase = 2;
-                    } else if (hit0) {
-                        s.kh = 1;
-                        s.phase = 1;
-                    } else {   // no traced bounce: every sample is black and draws nothing
-                        s.pi = pi + 1;
-                        s.phase = s.pi < s.npx ? 0 : 2;
-                    }
-                }
-                __syncthreads();
-                mark(1);
-            }
-        }
-        bool any_chain = false;
-        for (int q = 0; q < G; q++) any_chain |= gs[q].phase == 1;
-        if (!any_chain) break;
-
-        // ---- (2) one window of speculative trajectories per resolving group
-        const GroupState sg = gs[g];
-        const int64_t bs = (int64_t)blockIdx.x * G + g;
-        const int64_t rec = bs * wb.ppt + sg.pi;
-        uint64_t st = 0;
-        uint32_t dres = kBadD;
-        if (sg.phase == 1) {
-            Pcg seed;
-            pcg_seed(seed, (uint64_t)tile_of_slot(rp, slot_base + bs));
-            st = pcg_advance(J, sg.S, seed.inc, 2 * (uint64_t)gl);
-            Cursor c;
-            c.rng.state = st;
-            c.rng.inc = seed.inc;
-            c.draws = 0;
-            c.cur1d = 1;   // camera: Get2D pFilm, Get2D pLens, Get1D time (stratified)
-            c.cur2d = 2;
-            c.k = gl == 0 ? sg.kh : -1;
-            c.kdep = 0;
-            const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, n, ndims};
-            int pnc = 0, bnc = 0;
-            (void)spec_path<false>(sc, pcs[g], ss, c, rp.max_depth, rp.rr_threshold, stack, pnc, bnc);
-            dres = (pnc || c.kdep) ? kBadD : c.draws;
-        }
-        sbuf[lane] = st;
-        dbuf[lane] = dres;
-        windows++;
-        __syncthreads();
-        mark(2);
-        // ---- (3) each group leader walks its chain through the window
-        if (gl == 0 && sg.phase == 1) {
-            Pcg seed;
-            pcg_seed(seed, (uint64_t)tile_of_slot(rp, slot_base + bs));
-            uint64_t x = 0;
-            int k = sg.kh;
-            while (k < n) {
-                if ((x & 1) || (x >> 1) >= (uint64_t)L) break;
-                const uint32_t d = dbuf[lane + (int)(x >> 1)];
-                if (d == kBadD) break;
-                wb.memb[rec * n + k] = sbuf[lane + (int)(x >> 1)];
-                k++;
-                x += d;
-            }
-            GroupState& s = gs[g];
-            if (k == sg.kh) {   // the exact head's trajectory panics: the tile ends at this sample
-                wb.memb[rec * n + k] = sg.S;
-                wb.prec[rec].nvalid = k + 1;
-                s.stop = 1;
-                s.phase = 2;
-            } else {
-                s.kh = k;
-                s.S = pcg_advance(J, sg.S, seed.inc, x);
-                if (k >= n) {   // every sample of the pixel has its offset
-                    s.pi = sg.pi + 1;
-                    s.phase = s.pi < s.npx ? 0 : 2;
-                }
-            }
-        }
-        __syncthreads();
-        mark(3);
-    }
-    if (lane == 0) {
-        atomicAdd(&ctr->windows, windows);
-        for (int i = 0; i < 8; i++) atomicAdd(&ctr->phase[i], ph[i]);
-    }
-}
-
-// One wave per pixel record: the pixel's samples as full paths.
-//   kMB = false (EXACT): bounce 1, the stratified values and every sample's
-//                RNG state come from k_chain's records.
-//   kMB = true  (THROUGHPUT): the wave builds them itself, with no chain:
-//                StartPixel on the pixel's own stream (mb_state(tile, pi, 0)),
-//                bounce 1, and sample k's stream mb_state(tile, pi, k); it
-//                writes the PixelRec fields k_film and k_panic_reduce read.
-#ifndef PBRT_CHAIN_WAVES
-#define PBRT_CHAIN_WAVES 2
-#endif
-constexpr int kChainWaves = PBRT_CHAIN_WAVES;   // k_chain waves/SIMD (build option)
 #ifndef PBRT_PATHS_WAVES
 #define PBRT_PATHS_WAVES 2
 #endif
-constexpr int kPathsWaves = PBRT_PATHS_WAVES;   // k_paths waves/SIMD (build option)
-template <bool kMB, int kWaves = 1>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kWaves, 8))) void k_paths(DevScene sc, RenderParams rp, ChainLayout lay,
-                                                 const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
-                                                 int64_t nslots_batch, Counters* __restrict__ ctr) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    __shared__ uint16_t stack_lds[64 * kStackStride];
-    __shared__ PixelCache pc;
-    __shared__ unsigned long long sh_pkey;   // (sample << 32) | (bounce << 8) | (kind + 1): min = first panic
-    __shared__ uint64_t sh_state;
-    const int lane = threadIdx.x;
-    stage_nodes(sc);
-    const int64_t bslot = blockIdx.x / wb.ppt, pi = blockIdx.x % wb.ppt;
-    const int64_t rec = blockIdx.x;
-    const int64_t tile = tile_of_slot(rp, slot_base + bslot);
-    int64_t x0, y0, x1, y1;
-    tile_bounds(rp, tile, x0, y0, x1, y1);
-    if (kMB) {
-        if (bslot >= nslots_batch) return;
-        if (pi == 0 && lane == 0) wb.tile_npx[bslot] = (int32_t)((x1 - x0) * (y1 - y0));
-        if (pi >= (x1 - x0) * (y1 - y0)) return;
-    } else if (pi >= wb.tile_npx[bslot]) {
-        return;
-    }
-    const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
-    const int n = rp.spp, ndims = rp.ndims;
-    double* s1d = (double*)(lds + lay.s1d);
-    uint16_t* stack = stack_lds + lane;
-    PixelRec& pr = wb.prec[rec];
-    Pcg seed;
-    pcg_seed(seed, (uint64_t)tile);
-    const uint64_t inc = seed.inc;
-    SI si0;
-    BSDF b0;
-    int hit, nvalid, panic0;
-    if constexpr (kMB) {
-        (void)start_pixel_wave(rp, *jump, mb_state((uint64_t)tile, (uint64_t)pi, 0), inc, s1d,
-                               (uint16_t*)(lds + lay.other), (uint32_t*)(lds + lay.vbuf), &sh_state);
-        // bounce 1, shared by every sample of the pixel (pbrt_spec.h)
-        panic0 = 0;
-        hit = 0;
-        b0.n_bxdfs = 0;
-        Ray ray = camera_ray(*sc.camera, (double)px + 0.0, (double)py + 0.0, s1d[1 < n ? 1 : 0], V2{0.0, 0.0});
-        if (n > 1 && 1 < rp.max_depth) {
-            hit = bvh_traverse<false>(sc, ray, &si0, stack, panic0) ? 1 : 0;
-            if (!panic0 && hit && compute_bsdf(sc, si0, b0) < 0) panic0 = -1;
-        }
-        if (panic0) hit = 0;
-        nvalid = n;
-        if (lane == 0) {
-            pc.wo = ray.d;
-            pr.nvalid = n;
-            pr.panic0 = panic0;
-        }
-    } else {
-        for (int idx = lane; idx < ndims * n; idx += kWave) s1d[idx] = wb.s1d[rec * wb.s1d_stride + idx];
-        si0 = pr.si;
-        b0 = pr.b;
-        hit = pr.hit;
-        nvalid = pr.nvalid;
-        panic0 = pr.panic0;
-        if (lane == 0) pc.wo = pr.wo;
-    }
-    if (lane == 0) {
-        pc.si = si0;
-        pc.b = b0;
-        pc.hit = hit;
-        sh_pkey = ~0ULL;
-    }
-    if (hit && b0.n_bxdfs > 0 && lane < sc.n_lights) {   // bounce-1 light samples, uLight = (0,0)
-        int pl = 0;
-        Spec ld = estimate_direct(sc, stack, pl, si0, b0, lane, V2{0.0, 0.0});
-        if (!pl && max_component(ld) > 10) pl = PBRT_PANIC_LD_GT_10;
-        pc.ld[lane] = ld;
-        pc.ld_panic[lane] = pl;
-    }
-    __syncthreads();
-    const SpecSampler ss{s1d, n, ndims};
-    for (int kb = 1; kb < nvalid; kb += kWave) {
-        const int k = kb + lane;
-        Spec L = spec(0);
-        if (k < nvalid && hit) {
-            Cursor c;
-            c.rng.state = kMB ? mb_state((uint64_t)tile, (uint64_t)pi, (uint64_t)k) : wb.memb[rec * n + k];
-            c.rng.inc = inc;
-            c.draws = 0;
-            c.cur1d = 1;   // camera: Get2D pFilm, Get2D pLens, Get1D time (stratified)
-            c.cur2d = 2;
-            c.k = k;
-            c.kdep = 0;
-            int pnc = 0, bnc = 0;
-            L = spec_path<true>(sc, pc, ss, c, rp.max_depth, rp.rr_threshold, stack, pnc, bnc);
-            if (pnc)
-                atomicMin(&sh_pkey, ((unsigned long long)k << 32) | ((unsigned long long)(bnc & 0xFFFFFF) << 8) |
-                                        (unsigned long long)((pnc + 1) & 0xFF));
-        }
-        if (k < n) {
-            double* o = wb.L + (rec * n + k) * 3;
-            o[0] = L.r;
-            o[1] = L.g;
-            o[2] = L.b;
-        }
-    }
-    __syncthreads();
-    if (lane == 0) {
-        PanicRec p{0, 0, 0, 0, px, py};
-        if (panic0) {
-            p.kind = panic0;
-            p.sample = 1;
-            p.bounce = 1;
-        } else if (sh_pkey != ~0ULL) {
-            p.kind = (int)(sh_pkey & 0xFF) - 1;
-            p.bounce = (int)((sh_pkey >> 8) & 0xFFFFFF);
-            p.sample = (int)(sh_pkey >> 32);
-        }
-        wb.ppanic[rec] = p;
-        if (!p.kind && nvalid > 1) {
-            atomicAdd(&ctr->paths, (unsigned long long)(nvalid - 1));
-            atomicAdd(&ctr->camera_samples, (unsigned long long)(nvalid - 1));
-        }
-    }
-}
+constexpr int kPathsWaves = PBRT_PATHS_WAVES;   // k_paths_ci waves/SIMD (build option)
 
-// k_paths_ci: EXACT full paths with lane refill. k_paths runs one pixel's
-// samples per wave, so a wave lasts as long as its longest path (~4x the
-// mean). Here a wave owns P pixel records and treats their samples as one
+// k_paths_ci: full paths with lane refill. One pixel's samples per wave would
+// make a wave last as long as its longest path (~4x the mean). Here a wave
+// owns P pixel records and treats their samples as one
 // work list: a lane whose path ends writes its radiance and takes the next
 // (pixel, sample) at once, so the wave only waits for its longest path at
 // the end of the P pixels. Every path runs the same arithmetic as
-// spec_path<true> (path_step), from the offset the chain found, so L per
+// Path.Li (path_step), from the offset the chain found, so L per
 // (pixel, sample) is bit-identical; k_film sums them in sample order as
 // before. Requires LDS-staged nodes (no traversal stack) and P * n_lights <= 64.
 //
@@ -1317,7 +1000,7 @@ __global__ void k_pw_panics(RenderParams rp, WaveBufs wb, int64_t slot_base, int
 // StartPixel on the pixel's own stream mb_state(tile, pi, 0) and bounce 1
 // (camera ray, first hit, BSDF), written to the PixelRec / s1d buffers the
 // EXACT pipeline fills with k_wf_primary + k_chain_ci. The same arithmetic as
-// k_paths<true>'s prologue.
+// the serial kernel's pixel prologue.
 __global__ __launch_bounds__(kWave) void k_mb_setup(DevScene sc, RenderParams rp, ChainLayout lay,
                                                     const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
                                                     int64_t nslots_batch) {
@@ -1430,124 +1113,9 @@ __global__ void k_panic_reduce(WaveBufs wb, int64_t slot_base, int64_t nslots_ba
     }
 }
 
-// ------------------------------------------- EXACT, wavefront chain (k_wf_*)
-// The same speculative-offset chain as k_chain, reorganised so that the
-// trajectory bounces run as wide, register-light kernels instead of inside
-// one 350-register wave per tile:
-//   k_wf_primary  once per batch, one thread per pixel record: the camera
-//                 ray's first hit and BSDF (bounce 1 is the same for every
-//                 sample of a pixel, pbrt_spec.h) -> PixelRec.
-//   per window iteration (host loop, all tiles of the batch together):
-//   k_wf_tile     one wave per tile: walk the chain through the previous
-//                 window's draw counts, StartPixel + the PixelRec of the next
-//                 pixel when the current one is resolved, then the window's
-//                 64 candidates (RNG offsets head + 2j) take their bounce-1
-//                 scattering step; live ones are queued for bounce 2.
-//   k_wf_trace    closest hit of every queued ray (a thread per ray).
-//   k_wf_shade    interaction + BSDF + scattering step; queue for the next
-//                 bounce or record the candidate's draw count D.
-//   k_wf_tail     bounces past the split levels, one thread per trajectory.
-// Trajectories are compacted into dense queues between bounces, so a wave's
-// lanes stay busy however long the other trajectories of its window are.
-constexpr int kWfCand = 64;        // candidates per tile and window
-constexpr int kWfBlock = 256;      // threads per block of the bounce kernels
-constexpr int kWfMaxLevels = 16;   // split bounce levels (trace + shade launches)
-
-struct TileState {
-    uint64_t S;       // PCG32 state at the chain head
-    int32_t pi, npx;  // current pixel, pixels of the tile
-    int32_t kh;       // next sample without an offset
-    int32_t phase;    // 0 needs a pixel (first iteration), 1 window in flight, 2 finished
-    int32_t windows;
-    int32_t pad;
-};
-struct WfBufs {
-    TileState* ts;      // [nb]
-    uint64_t* start;    // [nb * C] PCG state at each candidate's offset
-    uint32_t* D;        // [nb * C] draws of the candidate's trajectory, or kBadD
-    uint64_t* rng;      // [cap] trajectory cursor: PCG state
-    uint32_t* draws;    // [cap]
-    uint32_t* meta;     // [cap] cur1d | cur2d << 8 | bounces << 16
-    double* beta;       // [3][cap]
-    double* ray;        // [6][cap] origin, direction
-    int32_t* hprim;     // [cap] closest primitive, -1 miss, -2 reference panic
-    double* hph;        // [3][cap] its hit point (shape space)
-    uint32_t* q[3];     // ids of rays to trace: split levels by parity, tail
-    uint32_t* cnt;      // [2][kWfMaxLevels + 1] queue lengths by iteration parity (last: tail)
-    uint32_t* finished; // tiles done
-    int64_t cap;        // nb * C
-};
-
-
-// Append the ids of the lanes with push set to q (one atomic per wave). All
-// lanes of the wave call it.
-__device__ __forceinline__ void wf_push(uint32_t* q, uint32_t* cnt, bool push, uint32_t id) {
-    const unsigned long long m = __ballot(push);
-    if (m == 0) return;
-    const int lane = (int)(threadIdx.x & 63);
-    const int leader = __ffsll((long long)m) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(cnt, (uint32_t)__popcll(m));
-    base = __shfl(base, leader);
-    if (push) q[base + (uint32_t)__popcll(m & ((1ULL << lane) - 1ULL))] = id;
-}
-__device__ __forceinline__ void wf_store(const WfBufs& wf, uint32_t id, const Cursor& c, int bounces, Spec beta,
-                                         const Ray& r) {
-    const int64_t cap = wf.cap;
-    wf.rng[id] = c.rng.state;
-    wf.draws[id] = c.draws;
-    wf.meta[id] = (uint32_t)c.cur1d | ((uint32_t)c.cur2d << 8) | ((uint32_t)bounces << 16);
-    wf.beta[id] = beta.r;
-    wf.beta[cap + id] = beta.g;
-    wf.beta[2 * cap + id] = beta.b;
-    wf.ray[id] = r.o.x;
-    wf.ray[cap + id] = r.o.y;
-    wf.ray[2 * cap + id] = r.o.z;
-    wf.ray[3 * cap + id] = r.d.x;
-    wf.ray[4 * cap + id] = r.d.y;
-    wf.ray[5 * cap + id] = r.d.z;
-}
-__device__ __forceinline__ Ray wf_ray(const WfBufs& wf, uint32_t id) {
-    const int64_t cap = wf.cap;
-    Ray r;
-    r.o = V3{wf.ray[id], wf.ray[cap + id], wf.ray[2 * cap + id]};
-    r.d = V3{wf.ray[3 * cap + id], wf.ray[4 * cap + id], wf.ray[5 * cap + id]};
-    r.tmax = kInf;
-    r.time = 0;
-    return r;
-}
-// queue of split level `level` (or the tail queue) and its length slot
-__device__ __forceinline__ uint32_t* wf_queue(const WfBufs& wf, int level, int n_levels) {
-    return level >= n_levels ? wf.q[2] : wf.q[level & 1];
-}
-__device__ __forceinline__ uint32_t* wf_count(const WfBufs& wf, int par, int level, int n_levels) {
-    return wf.cnt + par * (kWfMaxLevels + 1) + (level >= n_levels ? kWfMaxLevels : level);
-}
-
-__global__ void k_wf_init(RenderParams rp, WaveBufs wb, WfBufs wf, int64_t slot_base, int64_t nb) {
-    const int64_t bs = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (bs >= nb) return;
-    int64_t x0, y0, x1, y1;
-    const int64_t tile = tile_of_slot(rp, slot_base + bs);
-    tile_bounds(rp, tile, x0, y0, x1, y1);
-    Pcg seed;
-    pcg_seed(seed, (uint64_t)tile);   // Sampler.Clone(tile), integrator.go:318,328
-    TileState t;
-    t.S = seed.state;
-    t.pi = 0;
-    t.npx = (int32_t)((x1 - x0) * (y1 - y0));
-    t.kh = 1;
-    t.phase = t.npx > 0 ? 0 : 2;
-    t.windows = 0;
-    t.pad = 0;
-    wf.ts[bs] = t;
-    wb.tile_npx[bs] = 0;
-    if (t.phase == 2) atomicAdd(wf.finished, 1u);
-}
-
 // Bounce 1 of every pixel record of the batch: the camera ray through the
 // pixel corner (pFilm and pLens are (0,0) for every sample), its closest hit
-// and BSDF. The ray time is patched by k_wf_tile once StartPixel gives it.
+// and BSDF. The ray time is patched by the chain kernel once StartPixel gives it.
 __global__ __launch_bounds__(kWave) void k_wf_primary(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
                                                       int64_t nb) {
     __shared__ uint16_t stack_lds[64 * kStackStride];
@@ -1846,248 +1414,10 @@ __global__ void k_order_of_keys(const uint64_t* __restrict__ keys, int64_t nb, u
     if (i < nb) order[i] = (uint32_t)keys[i];
 }
 
-__global__ __launch_bounds__(kWave) void k_wf_tile(DevScene sc, RenderParams rp, ChainLayout lay,
-                                                   const PcgJump* __restrict__ jump, WaveBufs wb, WfBufs wf,
-                                                   int64_t slot_base, int par, int n_levels) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    __shared__ uint64_t sh_state;
-    const int lane = threadIdx.x;
-    const int64_t bs = blockIdx.x;
-    if (bs == 0 && lane <= kWfMaxLevels) wf.cnt[(par ^ 1) * (kWfMaxLevels + 1) + lane] = 0;
-    TileState st = wf.ts[bs];
-    if (st.phase == 2) return;
-    const PcgJump& J = *jump;
-    const int64_t tile = tile_of_slot(rp, slot_base + bs);
-    const uint64_t inc = pcg_inc_of((uint64_t)tile);
-    const int n = rp.spp, ndims = rp.ndims;
-    if (st.phase == 1) {   // walk the chain through the last window
-        const uint32_t dj = wf.D[bs * kWfCand + lane];
-        const uint64_t sj = wf.start[bs * kWfCand + lane];
-        const int64_t rec = bs * wb.ppt + st.pi;
-        uint64_t x = 0;
-        int k = st.kh;
-        while (k < n) {
-            if ((x & 1) || (x >> 1) >= (uint64_t)kWfCand) break;
-            const int jj = (int)(x >> 1);
-            const uint32_t d = __shfl(dj, jj);
-            if (d == kBadD) break;
-            const uint64_t s = __shfl(sj, jj);
-            if (lane == 0) wb.memb[rec * n + k] = s;
-            k++;
-            x += d;
-        }
-        if (k == st.kh) {   // the exact head's trajectory panics: the tile ends at this sample
-            if (lane == 0) {
-                wb.memb[rec * n + k] = st.S;
-                wb.prec[rec].nvalid = k + 1;
-            }
-            st.phase = 2;
-        } else {
-            st.kh = k;
-            st.S = pcg_advance(J, st.S, inc, x);
-            if (k >= n) {   // every sample of the pixel has its offset
-                st.pi++;
-                st.phase = st.pi < st.npx ? 0 : 2;
-            }
-        }
-    }
-    while (st.phase == 0) {   // StartPixel, then the pixel's bounce-1 record
-        double* s1d = (double*)(lds + lay.s1d);
-        uint16_t* other = (uint16_t*)(lds + lay.other);
-        uint32_t* vbuf = (uint32_t*)(lds + lay.vbuf);
-        const int64_t rec = bs * wb.ppt + st.pi;
-        const uint64_t S1 = start_pixel_wave(rp, J, st.S, inc, s1d, other, vbuf, &sh_state);
-        double* gs1d = wb.s1d + rec * wb.s1d_stride;
-        for (int idx = lane; idx < ndims * n; idx += kWave) gs1d[idx] = s1d[idx];
-        PixelRec& pr = wb.prec[rec];
-        const int hit0 = pr.hit, panic0 = pr.panic0;
-        if (lane == 0) {
-            if (hit0) {   // the camera ray's time (Get1D after pFilm, pLens) of the pixel's first traced sample
-                int64_t x0, y0, x1, y1;
-                tile_bounds(rp, tile, x0, y0, x1, y1);
-                const int64_t px = x0 + st.pi % (x1 - x0), py = y0 + st.pi / (x1 - x0);
-                pr.si.time = camera_ray(*sc.camera, (double)px, (double)py, s1d[1 < n ? 1 : 0], V2{0.0, 0.0}).time;
-            }
-            wb.tile_npx[bs] = st.pi + 1;
-        }
-        st.S = S1;
-        if (panic0) {   // the first traced sample panics at bounce 1: the tile ends here
-            st.phase = 2;
-        } else if (hit0) {
-            st.kh = 1;
-            st.phase = 1;
-        } else {   // no traced bounce: every sample is black and draws nothing
-            st.pi++;
-            st.phase = st.pi < st.npx ? 0 : 2;
-        }
-        __syncthreads();
-    }
-    if (st.phase == 1) {   // the window: candidate lane at offset head + 2 * lane, bounce-1 step
-        const int64_t rec = bs * wb.ppt + st.pi;
-        const uint32_t id = (uint32_t)(bs * kWfCand + lane);
-        const uint64_t s0 = pcg_advance(J, st.S, inc, 2 * (uint64_t)lane);
-        wf.start[id] = s0;
-        Cursor c;
-        c.rng.state = s0;
-        c.rng.inc = inc;
-        c.draws = 0;
-        c.cur1d = 1;   // camera: Get2D pFilm, Get2D pLens, Get1D time (stratified)
-        c.cur2d = 2;
-        c.k = lane == 0 ? st.kh : -1;
-        c.kdep = 0;
-        const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, n, ndims};
-        const PixelRec& pr = wb.prec[rec];
-        Spec beta = spec(1);
-        int bounces = 1;
-        Ray ray;
-        const int r = traj_scatter(sc, pr.si, pr.b, pr.wo, c, ss, beta, bounces, ray, rp.max_depth, rp.rr_threshold);
-        if (r == 0) wf_store(wf, id, c, bounces, beta, ray);
-        else wf.D[id] = r == 1 ? c.draws : kBadD;
-        wf_push(wf_queue(wf, 0, n_levels), wf_count(wf, par, 0, n_levels), r == 0, id);
-        st.windows++;
-    }
-    if (lane == 0) {
-        wf.ts[bs] = st;
-        if (st.phase == 2) atomicAdd(wf.finished, 1u);
-    }
-}
-
-// Closest hit of every ray queued for split level `level`.
-__global__ __launch_bounds__(kWfBlock) void k_wf_trace(DevScene sc, WfBufs wf, int par, int level, int n_levels) {
-    __shared__ uint16_t stack_lds[kWfBlock * 64];
-    stage_nodes(sc);
-    const uint32_t n = *wf_count(wf, par, level, n_levels);
-    const uint32_t* q = wf_queue(wf, level, n_levels);
-    for (uint32_t i = blockIdx.x * kWfBlock + threadIdx.x; i < n; i += gridDim.x * kWfBlock) {
-        const uint32_t id = q[i];
-        Ray r = wf_ray(wf, id);
-        int panic = 0, best;
-        V3 ph;
-        bvh_walk<false, kWfBlock>(sc, r, stack_lds + threadIdx.x, panic, best, ph);
-        wf.hprim[id] = panic ? -2 : best;
-        const int64_t cap = wf.cap;
-        wf.hph[id] = ph.x;
-        wf.hph[cap + id] = ph.y;
-        wf.hph[2 * cap + id] = ph.z;
-    }
-}
-
-// Interaction, BSDF and scattering step of every ray traced at `level`.
-__global__ __launch_bounds__(kWfBlock) void k_wf_shade(DevScene sc, RenderParams rp, WaveBufs wb, WfBufs wf,
-                                                       int64_t slot_base, int par, int level, int n_levels) {
-    const uint32_t n = *wf_count(wf, par, level, n_levels);
-    const uint32_t* q = wf_queue(wf, level, n_levels);
-    uint32_t* qn = wf_queue(wf, level + 1, n_levels);
-    uint32_t* cn = wf_count(wf, par, level + 1, n_levels);
-    const int lane = (int)(threadIdx.x & 63);
-    const uint32_t stride = gridDim.x * kWfBlock;
-    for (uint32_t i0 = blockIdx.x * kWfBlock + (threadIdx.x & ~63u); i0 < n; i0 += stride) {
-        const uint32_t i = i0 + (uint32_t)lane;
-        bool push = false;
-        uint32_t id = 0;
-        if (i < n) {
-            id = q[i];
-            const int hp = wf.hprim[id];
-            uint32_t D = kBadD;
-            if (hp == -1) {
-                D = wf.draws[id];
-            } else if (hp >= 0) {
-                const int64_t cap = wf.cap;
-                Ray ray = wf_ray(wf, id);
-                const V3 ph{wf.hph[id], wf.hph[cap + id], wf.hph[2 * cap + id]};
-                SI si;
-                prim_si(sc, hp, ray, ph, si);
-                BSDF b;
-                if (compute_bsdf(sc, si, b) >= 0) {
-                    const int64_t bs = id / kWfCand;
-                    const TileState& ts = wf.ts[bs];
-                    const int64_t rec = bs * wb.ppt + ts.pi;
-                    const uint32_t meta = wf.meta[id];
-                    Cursor c;
-                    c.rng.state = wf.rng[id];
-                    c.rng.inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + bs));
-                    c.draws = wf.draws[id];
-                    c.cur1d = (int)(meta & 0xFF);
-                    c.cur2d = (int)((meta >> 8) & 0xFF);
-                    c.k = (id % kWfCand) == 0 ? ts.kh : -1;
-                    c.kdep = 0;
-                    int bounces = (int)(meta >> 16);
-                    Spec beta{wf.beta[id], wf.beta[cap + id], wf.beta[2 * cap + id]};
-                    const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, rp.spp, rp.ndims};
-                    const int r = traj_scatter(sc, si, b, ray.d, c, ss, beta, bounces, ray, rp.max_depth,
-                                               rp.rr_threshold);
-                    if (r == 0) {
-                        wf_store(wf, id, c, bounces, beta, ray);
-                        push = true;
-                    } else {
-                        D = r == 1 ? c.draws : kBadD;
-                    }
-                }
-            }
-            if (!push) wf.D[id] = D;
-        }
-        wf_push(qn, cn, push, id);
-    }
-}
-
-// Trajectories still alive past the split levels, each to its end.
-__global__ __launch_bounds__(kWfBlock) void k_wf_tail(DevScene sc, RenderParams rp, WaveBufs wb, WfBufs wf,
-                                                      int64_t slot_base, int par, int n_levels) {
-    __shared__ uint16_t stack_lds[kWfBlock * 64];
-    stage_nodes(sc);
-    const uint32_t n = *wf_count(wf, par, n_levels, n_levels);
-    const uint32_t* q = wf.q[2];
-    const int64_t cap = wf.cap;
-    for (uint32_t i = blockIdx.x * kWfBlock + threadIdx.x; i < n; i += gridDim.x * kWfBlock) {
-        const uint32_t id = q[i];
-        const int64_t bs = id / kWfCand;
-        const TileState& ts = wf.ts[bs];
-        const int64_t rec = bs * wb.ppt + ts.pi;
-        const uint32_t meta = wf.meta[id];
-        Cursor c;
-        c.rng.state = wf.rng[id];
-        c.rng.inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + bs));
-        c.draws = wf.draws[id];
-        c.cur1d = (int)(meta & 0xFF);
-        c.cur2d = (int)((meta >> 8) & 0xFF);
-        c.k = (id % kWfCand) == 0 ? ts.kh : -1;
-        c.kdep = 0;
-        int bounces = (int)(meta >> 16);
-        Spec beta{wf.beta[id], wf.beta[cap + id], wf.beta[2 * cap + id]};
-        const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, rp.spp, rp.ndims};
-        Ray ray = wf_ray(wf, id);
-        uint32_t D = kBadD;
-        for (;;) {
-            int panic = 0, best;
-            V3 ph;
-            bvh_walk<false, kWfBlock>(sc, ray, stack_lds + threadIdx.x, panic, best, ph);
-            if (panic) break;
-            if (best < 0) {
-                D = c.draws;
-                break;
-            }
-            SI si;
-            prim_si(sc, best, ray, ph, si);
-            BSDF b;
-            if (compute_bsdf(sc, si, b) < 0) break;
-            const int r = traj_scatter(sc, si, b, ray.d, c, ss, beta, bounces, ray, rp.max_depth, rp.rr_threshold);
-            if (r == 1) D = c.draws;
-            if (r != 0) break;
-        }
-        wf.D[id] = D;
-    }
-}
-
-// Per-tile window counts -> Counters.windows.
-__global__ void k_wf_finish(WfBufs wf, int64_t nb, Counters* __restrict__ ctr) {
-    const int64_t bs = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (bs < nb) atomicAdd(&ctr->windows, (unsigned long long)wf.ts[bs].windows);
-}
-
 // ------------------------------------------- continuous-issue offset chain
-// k_chain_ci replaces k_chain's fixed windows. A window of 64 candidates
-// lasts as long as its longest trajectory (~6.5 bounces for a 2.25-bounce
-// mean), so most lanes idle through most of it. Here a lane that finishes a
+// k_chain_ci replaced round 1's fixed 64-candidate windows: a window lasts as
+// long as its longest trajectory (~6.5 bounces for a 2.25-bounce mean), so
+// most lanes idle through most of it. Here a lane that finishes a
 // trajectory, or whose candidate the chain has jumped over, takes the next
 // unissued offset at once: every bounce step keeps every lane busy, and
 // candidates left behind by the chain are dropped mid-trajectory.
@@ -2100,7 +1430,7 @@ __global__ void k_wf_finish(WfBufs wf, int64_t nb, Counters* __restrict__ ctr) {
 // and the group's in-flight candidates are dropped. A speculative result
 // that is not usable at the head (a panic or a draw count that depends on
 // the sample index) is re-run there with the sample index known; an exact
-// panic ends the tile at that sample, as in k_chain. Bit-identical to the
+// panic ends the tile at that sample. Bit-identical to the
 // serial replay: only the schedule changes.
 #ifndef PBRT_CI_EU_WAVES
 #define PBRT_CI_EU_WAVES 2   // k_chain_ci waves/SIMD (build option)
@@ -2131,22 +1461,25 @@ struct CiGroup {
 // the slowest tile's latency, the frame's critical path when tiles are few
 // per GPU (a multi-GPU shard). Idle lanes are ranked across the waves through
 // LDS; StartPixel runs on the first wave.
-template <int kW>
+// kDepth: traversal stack entries per lane. Trees of <= kLdsNodes (64) nodes
+// are staged in LDS and walk their leaves only (no stack); larger trees walk
+// with the reference's [64] stack (bvh.go:670).
+template <int kW, int kDepth = 32>
 __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT_CI_EU_WAVES, 8))) void k_chain_ci(
     DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
     int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr,
     const uint32_t* __restrict__ order, uint32_t* __restrict__ ticks) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const uint64_t t_begin = wall_clock64();
-    // <= kLdsNodes (64) staged nodes: a binary tree that small is at most 31
-    // interior nodes deep, so 32 stack entries per lane cannot overflow
     constexpr int kT = kWave * kW;   // threads per workgroup (stack stride)
-    __shared__ uint16_t stack_lds[32 * kT];
+    __shared__ uint16_t stack_lds[kDepth * kT];
     __shared__ ChainCache pcs[kCiMaxGroups];
     __shared__ CiGroup gs[kCiMaxGroups];
     __shared__ uint64_t sh_state;
     __shared__ int wcnt[kW];
+#ifdef PBRT_CI_DIAG
     __shared__ uint32_t dh[64];   // on-chain D histogram of the block (diagnostics)
+#endif
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
     stage_nodes(sc);
     const int L = kW > 1 ? kT : lanes_per_tile, G = kW > 1 ? 1 : kWave / L;
@@ -2532,29 +1865,20 @@ struct pbrt_gpu_ctx {
     int last_kernel = 0;    // PBRT_KERNEL_SERIAL / PBRT_KERNEL_WAVE
     PcgJump* d_jump = nullptr;
     pbrt_distribution_desc host_dist;
-    // wave-parallel EXACT path (k_chain / k_paths / k_film)
+    // wave-parallel path (k_wf_primary, k_chain_ci, k_paths_ci / k_pw_*, k_film)
     ChainLayout lay{};
     bool use_spec = false;
     unsigned char* d_wave = nullptr;   // per-batch pixel records, stratified values, RNG states, L
     size_t wave_cap = 0;
     int64_t wave_batch = 0;            // tile slots per batch
-    int tiles_per_wave = 1;            // k_chain lane groups per wave (64 / lanes per tile)
-    std::vector<hipEvent_t> bev;       // per batch: before k_chain, after k_chain, after k_paths
+    int tiles_per_wave = 1;            // k_chain_ci lane groups per wave (64 / lanes per tile)
+    std::vector<hipEvent_t> bev;       // per batch: before the chain, after the chain, after the paths
     int n_batches = 0;
     int n_simd = 1024;                 // SIMDs of the device (4 per CU)
     WaveBufs wb{};
-    // wavefront chain (k_wf_*)
-    bool use_wf = false;
-    bool use_ci = false;   // k_chain_ci instead of k_chain
+    bool use_ci = false;   // the Path chain stage (k_chain_ci)
     bool use_dl = false;   // DirectLighting on k_dl_setup / k_dl_samples
     ChainLayout lay_ci{};
-    WfBufs wf{};
-    unsigned char* d_wf = nullptr;
-    size_t wf_cap = 0;
-    uint32_t* h_poll = nullptr;        // pinned: finished-tile counts read back by the window loop
-    hipEvent_t pev[2] = {nullptr, nullptr};
-    int wf_levels = 0;                 // split bounce levels (trace + shade launch pairs per window)
-    int64_t wf_iters = 0;              // window iterations of the last render
     // device scene
     pbrt_shape_desc* d_shapes = nullptr;
     pbrt_material_desc* d_materials = nullptr;
@@ -2665,8 +1989,8 @@ DevScene dev_scene(const pbrt_gpu_ctx* c, bool with_dist) {
 
 // The scene view a launch passes, tagged with its kernel's counter set for
 // the mesh-traversal counting build (PBRT_MESH_COUNT; ignored otherwise):
-// 1 k_wf_primary, 2 k_chain_ci / k_chain, 3 k_paths(_ci) EXACT, 4 k_mb_setup,
-// 5 k_paths(_ci) THROUGHPUT, 6 k_render_exact, 7 k_intersect.
+// 1 k_wf_primary, 2 k_chain_ci, 3 k_paths_ci / k_pw_* EXACT, 4 k_mb_setup,
+// 5 k_paths_ci / k_pw_* THROUGHPUT, 6 k_render_exact, 7 k_intersect.
 DevScene with_slot(DevScene s, int slot) {
     s.mesh.count_slot = slot;
     return s;
@@ -2917,9 +2241,19 @@ bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Rend
     L.ring = 0;
     // k_chain_ci: the same staging without the window buffers, then the ring
     off = 0;
-    if (rp.sp_serial) {   // large spp: the serial StartPixel writes the values straight to wb.s1d
+    // the pixel's stratified values are staged in LDS while the staging of one
+    // 1-wave tile (aliased with the ring) stays <= 20 KB (5+ workgroups per CU;
+    // config C's 256 spp needs 19.3 KB); above, StartPixel writes them straight
+    // to the pixel's global record (always with the serial StartPixel, large spp)
+    const int64_t al16 = 15;
+    const int64_t lds_staging = ((nd * n * 8 + al16) & ~al16) + ((nd * n * 2 + al16) & ~al16) +
+                                (((rp.sp_serial ? 4 : (int64_t)rp.sp_draws * 4) + al16) & ~al16);
+    if (rp.sp_serial) {
         Lci.s1d = -1;
         Lci.other = put(16);
+    } else if (lds_staging > 20 * 1024) {
+        Lci.s1d = -1;
+        Lci.other = put(nd * n * 2);
     } else {
         Lci.s1d = put(nd * n * 8);
         Lci.other = put(nd * n * 2);
@@ -3005,8 +2339,8 @@ uint64_t schedule_key(const RenderParams& rp, int kw) {
 
 // k_paths_ci (lane refill over kPathsPixels pixels per wave) where it fits:
 // LDS-staged nodes, the pixels' stratified values in 16 KB of LDS and one
-// lane per (pixel, light) for the bounce-1 estimates. PBRT_PATHS_CI=0 keeps
-// the one-pixel-per-wave k_paths.
+// lane per (pixel, light) for the bounce-1 estimates; 0: the path wavefront
+// (k_pw_*) runs the paths. PBRT_PATHS_CI=0 forces that.
 // Returns the pixels per wave (2, 4 or 8; PBRT_PATHS_CI overrides, 0 = off).
 // k_paths_ci stages the stratified values of its P pixels in LDS when they take <= 16 KB
 bool paths_ci_s1d_lds(const RenderParams& rp, int P) { return (int64_t)P * rp.ndims * rp.spp * 8 <= 16 * 1024; }
@@ -3160,104 +2494,6 @@ int wave_buffers(pbrt_gpu_ctx* c) {
     return PBRT_OK;
 }
 
-// Trajectory state of the wavefront chain for one batch (wave_batch tiles x kWfCand candidates).
-int wf_buffers(pbrt_gpu_ctx* c) {
-    const int64_t nb = c->wave_batch, cap = nb * kWfCand;
-    auto al = [](int64_t b) { return (b + 255) & ~int64_t(255); };
-    const int64_t bytes = al(nb * (int64_t)sizeof(TileState)) + al(cap * 8) + al(cap * 4) + al(cap * 8) +
-                          al(cap * 4) + al(cap * 4) + al(cap * 24) + al(cap * 48) + al(cap * 4) + al(cap * 24) +
-                          3 * al(cap * 4) + al(2 * (kWfMaxLevels + 1) * 4) + al(4);
-    if (c->wf_cap < (size_t)bytes || !c->d_wf) {
-        if (c->d_wf) (void)hipFree(c->d_wf);
-        c->d_wf = nullptr;
-        c->wf_cap = 0;
-        HIPCHK(c, hipMalloc((void**)&c->d_wf, (size_t)bytes));
-        c->wf_cap = (size_t)bytes;
-    }
-    if (!c->h_poll) HIPCHK(c, hipHostMalloc((void**)&c->h_poll, 2 * sizeof(uint32_t), hipHostMallocDefault));
-    for (int i = 0; i < 2; i++)
-        if (!c->pev[i]) HIPCHK(c, hipEventCreateWithFlags(&c->pev[i], hipEventDisableTiming));
-    unsigned char* p = c->d_wf;
-    auto take = [&](int64_t b) {
-        unsigned char* q = p;
-        p += al(b);
-        return q;
-    };
-    WfBufs& w = c->wf;
-    w.ts = (TileState*)take(nb * (int64_t)sizeof(TileState));
-    w.start = (uint64_t*)take(cap * 8);
-    w.D = (uint32_t*)take(cap * 4);
-    w.rng = (uint64_t*)take(cap * 8);
-    w.draws = (uint32_t*)take(cap * 4);
-    w.meta = (uint32_t*)take(cap * 4);
-    w.beta = (double*)take(cap * 24);
-    w.ray = (double*)take(cap * 48);
-    w.hprim = (int32_t*)take(cap * 4);
-    w.hph = (double*)take(cap * 24);
-    for (int i = 0; i < 3; i++) w.q[i] = (uint32_t*)take(cap * 4);
-    w.cnt = (uint32_t*)take(2 * (kWfMaxLevels + 1) * 4);
-    w.finished = (uint32_t*)take(4);
-    w.cap = cap;
-    // bounces 2 .. maxDepth-1 are traced; the first wf_levels of them as split launches
-    const int need = c->rp.max_depth > 2 ? c->rp.max_depth - 2 : 0;
-    int lv = 8;
-    if (const char* e = getenv("PBRT_WF_LEVELS")) lv = atoi(e);
-    if (lv < 0) lv = 0;
-    if (lv > kWfMaxLevels) lv = kWfMaxLevels;
-    c->wf_levels = need < lv ? need : lv;
-    return PBRT_OK;
-}
-
-// The offset chain of one batch as window iterations (k_wf_tile + per-bounce
-// trace/shade + tail). The host polls the finished-tile count every kPoll
-// iterations without stalling the queue (it waits for the count of the poll
-// before last); the extra iterations it queues meanwhile are no-ops.
-int wf_chain(pbrt_gpu_ctx* c, const DevScene& sc, int64_t sb, int64_t nb) {
-    const RenderParams& rp = c->rp;
-    WfBufs& wf = c->wf;
-    HIPCHK(c, hipMemsetAsync(wf.cnt, 0, 2 * (kWfMaxLevels + 1) * 4, c->stream));
-    HIPCHK(c, hipMemsetAsync(wf.finished, 0, 4, c->stream));
-    hipLaunchKernelGGL(k_wf_init, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, c->stream, rp, c->wb, wf, sb, nb);
-    hipLaunchKernelGGL(k_wf_primary, dim3((unsigned)((nb * c->wb.ppt + kWave - 1) / kWave)), dim3(kWave), 0,
-                       c->stream, sc, rp, c->wb, sb, nb);
-    const int nlev = c->wf_levels;
-    const bool tail = (rp.max_depth > 2 ? rp.max_depth - 2 : 0) > nlev;
-    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((wf.cap + kWfBlock - 1) / kWfBlock,
-                                                                           (int64_t)c->n_simd * 2));
-    constexpr int kPoll = 8;
-    const int64_t max_iters = c->wb.ppt * rp.spp + 2 * kPoll + 2;   // each window resolves >= 1 sample
-    int64_t it = 0;
-    for (;; it++) {
-        const int par = (int)(it & 1);
-        hipLaunchKernelGGL(k_wf_tile, dim3((unsigned)nb), dim3(kWave), (unsigned)c->lay.total, c->stream, sc, rp,
-                           c->lay, c->d_jump, c->wb, wf, sb, par, nlev);
-        for (int l = 0; l < nlev; l++) {
-            hipLaunchKernelGGL(k_wf_trace, dim3(grid), dim3(kWfBlock), 0, c->stream, sc, wf, par, l, nlev);
-            hipLaunchKernelGGL(k_wf_shade, dim3(grid), dim3(kWfBlock), 0, c->stream, sc, rp, c->wb, wf, sb, par, l,
-                               nlev);
-        }
-        if (tail)
-            hipLaunchKernelGGL(k_wf_tail, dim3(grid), dim3(kWfBlock), 0, c->stream, sc, rp, c->wb, wf, sb, par,
-                               nlev);
-        HIPCHK(c, hipGetLastError());
-        if (it % kPoll == kPoll - 1) {
-            const int slot = (int)((it / kPoll) & 1);
-            HIPCHK(c, hipMemcpyAsync(&c->h_poll[slot], wf.finished, 4, hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(c, hipEventRecord(c->pev[slot], c->stream));
-            if (it >= 2 * kPoll - 1) {
-                HIPCHK(c, hipEventSynchronize(c->pev[slot ^ 1]));
-                if ((int64_t)c->h_poll[slot ^ 1] >= nb) break;
-            }
-            if (c->cancel.load()) return set_err(c, PBRT_E_CANCELLED, "cancelled");
-        }
-        if (it > max_iters) return set_err(c, PBRT_E_HIP, "wavefront chain did not converge");
-    }
-    c->wf_iters += it + 1;
-    hipLaunchKernelGGL(k_wf_finish, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, c->stream, wf, nb, c->d_ctr);
-    HIPCHK(c, hipGetLastError());
-    return PBRT_OK;
-}
-
 int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
     if (!rd) return set_err(c, PBRT_E_INVALID, "null render desc");
     if (rd->tile_size <= 0 || rd->sampler_x <= 0 || rd->sampler_y <= 0 || rd->n_dims < 0 || rd->n_dims > 64)
@@ -3327,34 +2563,22 @@ int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
         return set_err(c, PBRT_E_UNSUPPORTED, "DirectLighting runs on the serial or the k_dl_* kernels");
     if (!c->use_dl && c->kernel_req == PBRT_KERNEL_WAVE_DL)
         return set_err(c, PBRT_E_UNSUPPORTED, "render not eligible for the DirectLighting wave kernels");
-    c->use_wf = c->use_spec && !c->use_dl && c->kernel_req == PBRT_KERNEL_WAVEFRONT;
-    // (dynamic LDS of one 1-wave tile, staging aliased with the ring: <= 20 KB keeps
-    // 5+ workgroups per CU; config C at 256 spp needs 19.3 KB)
-    const bool ci_fits = c->host_scene.n_nodes <= kLdsNodes &&
-                         std::max(c->lay_ci.staging, kCiRingBytes) <= 20 * 1024;
-    // AUTO: the continuous-issue chain wherever it fits (measured ~8% faster
-    // than the window chain on config B), else the window chain
-    c->use_ci = c->use_spec && !c->use_dl && (c->kernel_req == PBRT_KERNEL_WAVE_CI ||
-                                (c->kernel_req == PBRT_KERNEL_AUTO && ci_fits));
-    if (c->use_ci && !ci_fits)
-        return set_err(c, PBRT_E_UNSUPPORTED, "render not eligible for the continuous-issue chain kernel");
+    // the chain stage of the wave pipeline is k_chain_ci (PBRT_KERNEL_WAVE and
+    // _WAVEFRONT, whose window and wavefront chains it replaced, select it too)
+    c->use_ci = c->use_spec && !c->use_dl;
     if (c->use_spec && rp.n_slots > 0) {
         int rcw = wave_buffers(c);
         if (rcw != PBRT_OK) return rcw;
-        // tiles per k_chain wave (opts.lanes_per_wave = 1, 2, 4, 8 or 16; default 1).
+        // tiles per k_chain_ci wave (opts.lanes_per_wave = 1, 2 or 4; default 1).
         // One tile per wave is fastest on MI355X: its 64 trajectories leave the
         // same bounce-1 point, so their traversals stay coherent; packing tiles
         // cuts speculation but a window lasts as long as its slowest lane, and
         // mixed-tile windows measured 2.5x slower per window.
         int G = 1;
-        if (c->lanes_per_wave_set && c->lanes_per_wave >= 1 && c->lanes_per_wave <= kMaxGroups &&
+        if (c->lanes_per_wave_set && c->lanes_per_wave >= 1 && c->lanes_per_wave <= kCiMaxGroups &&
             (c->lanes_per_wave & (c->lanes_per_wave - 1)) == 0)
             G = c->lanes_per_wave;
         c->tiles_per_wave = G;
-        if (c->use_wf) {
-            int rcf = wf_buffers(c);
-            if (rcf != PBRT_OK) return rcf;
-        }
     }
     size_t nslot = (size_t)(rp.n_slots > 0 ? rp.n_slots : 1);
     int rc;
@@ -3482,14 +2706,9 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
     if (rp.n_slots > 0) {
         DevScene sc = dev_scene(c, rd->integrator == PBRT_INTEGRATOR_PATH);
         if (c->use_spec) {
-            c->last_kernel = c->use_dl ? PBRT_KERNEL_WAVE_DL : rp.mode == PBRT_MODE_THROUGHPUT ? PBRT_KERNEL_WAVE
-                             : c->use_wf ? PBRT_KERNEL_WAVEFRONT : c->use_ci ? PBRT_KERNEL_WAVE_CI : PBRT_KERNEL_WAVE;
-            c->wf_iters = 0;
+            c->last_kernel = c->use_dl ? PBRT_KERNEL_WAVE_DL
+                             : rp.mode == PBRT_MODE_THROUGHPUT ? PBRT_KERNEL_WAVE : PBRT_KERNEL_WAVE_CI;
             const bool lds_nodes = c->host_scene.n_nodes <= kLdsNodes;
-            // k_chain: 2 waves/SIMD by default (a few spilled registers; the
-            // trajectories are latency-bound), occupancy 1 on request
-            auto chain = c->occ_req == 1 ? (lds_nodes ? k_chain<1, 32> : k_chain<1, 64>)
-                                           : (lds_nodes ? k_chain<kChainWaves, 32> : k_chain<kChainWaves, 64>);
             const int64_t per = rp.slot_w * rp.slot_h;
             c->n_batches = (int)((rp.n_slots + c->wave_batch - 1) / c->wave_batch);
             while ((int)c->bev.size() < 3 * c->n_batches) {
@@ -3510,10 +2729,7 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                                        c->d_jump, c->wb, sb, nb);
                 } else if (rp.mode == PBRT_MODE_THROUGHPUT) {
                     // no offset chain: every sample's stream is known up front
-                } else if (c->use_wf) {
-                    int rcc = wf_chain(c, sc, sb, nb);
-                    if (rcc != PBRT_OK) return rcc;
-                } else if (c->use_ci) {
+                } else {
                     hipLaunchKernelGGL(k_wf_primary, dim3((unsigned)((nb * c->wb.ppt + kWave - 1) / kWave)),
                                        dim3(kWave), 0, c->stream, with_slot(sc, 1), rp, c->wb, sb, nb);
                     const int kw = ci_waves(c, nb);
@@ -3573,7 +2789,8 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                             const int ring = w * kCiRingBytes / (int)sizeof(RingEnt);
                             unsigned lds = 0;
                             const ChainLayout lw = ci_layout(c->lay_ci, w, 1, lds);
-                            auto kern = w == 2 ? k_chain_ci<2> : k_chain_ci<4>;
+                            auto kern = w == 2 ? (lds_nodes ? k_chain_ci<2> : k_chain_ci<2, 64>)
+                                               : (lds_nodes ? k_chain_ci<4> : k_chain_ci<4, 64>);
                             hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3(kWave * w), lds, st, with_slot(sc, 2), rp, lw,
                                                c->d_jump, c->wb, sb, nb, kWave * w, ring, c->d_ctr, ord, ticks);
                         } else {
@@ -3581,7 +2798,8 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                             const int ring = kCiRingBytes / (int)sizeof(RingEnt) / Gc;
                             unsigned lds = 0;
                             const ChainLayout lw = ci_layout(c->lay_ci, 1, Gc, lds);
-                            hipLaunchKernelGGL(k_chain_ci<1>, dim3((unsigned)((n + Gc - 1) / Gc)), dim3(kWave),
+                            auto kern1 = lds_nodes ? k_chain_ci<1> : k_chain_ci<1, 64>;
+                            hipLaunchKernelGGL(kern1, dim3((unsigned)((n + Gc - 1) / Gc)), dim3(kWave),
                                                lds, st, with_slot(sc, 2), rp, lw, c->d_jump, c->wb, sb,
                                                nb, kWave / Gc, ring, c->d_ctr, Gc == 1 ? ord : nullptr,
                                                Gc == 1 ? ticks : nullptr);
@@ -3614,12 +2832,6 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                     } else {
                         launch_ci(kw, nb, order, c->stream);
                     }
-                } else {
-                    hipLaunchKernelGGL(k_wf_primary, dim3((unsigned)((nb * c->wb.ppt + kWave - 1) / kWave)),
-                                       dim3(kWave), 0, c->stream, with_slot(sc, 1), rp, c->wb, sb, nb);
-                    hipLaunchKernelGGL(chain, dim3((unsigned)((nb + G - 1) / G)), dim3(kWave),
-                                       (unsigned)(c->lay.total + G * (int)sizeof(ChainCache)), c->stream, sc, rp,
-                                       c->lay, c->d_jump, c->wb, sb, nb, kWave / G, c->d_ctr);
                 }
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 1], c->stream));
                 if (c->use_dl) {
@@ -3629,7 +2841,9 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                                            dim3(kWave), 0, c->stream, with_slot(sc, 3), rp, c->wb, sb, nrec);
                     hipLaunchKernelGGL(k_dl_panics, dim3((unsigned)((nrec + 255) / 256)), dim3(256), 0, c->stream, rp,
                                        c->wb, sb, nrec, c->d_ctr);
-                } else if (paths_wf_enabled(c)) {
+                } else if (paths_wf_enabled(c) || paths_ci_pixels(c, rp) == 0) {
+                    // the path wavefront: mesh scenes, and whatever k_paths_ci cannot
+                    // take (a tree beyond LDS, more than 64 / P lights)
                     if (rp.mode == PBRT_MODE_THROUGHPUT)
                         hipLaunchKernelGGL(k_mb_setup, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
                                            (unsigned)c->lay.total, c->stream, with_slot(sc, 4), rp, c->lay, c->d_jump,
@@ -3648,11 +2862,9 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                     hipLaunchKernelGGL(kern, dim3((unsigned)((nb * c->wb.ppt + pp - 1) / pp)), dim3(kWave),
                                        (unsigned)lds, c->stream, with_slot(sc, 5), rp, c->wb, sb, nb * c->wb.ppt,
                                        c->d_ctr, sl);
-                } else if (rp.mode == PBRT_MODE_THROUGHPUT)
-                    hipLaunchKernelGGL((k_paths<true, kPathsWaves>), dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
-                                       (unsigned)c->lay.total, c->stream, with_slot(sc, 5), rp, c->lay, c->d_jump, c->wb, sb,
-                                       nb, c->d_ctr);
-                else if (const int pp = paths_ci_pixels(c, rp)) {
+                }
+                else {
+                    const int pp = paths_ci_pixels(c, rp);
                     const int per = rp.ndims * rp.spp;
                     auto kern = pp == 8 ? k_paths_ci<8> : pp == 2 ? k_paths_ci<2> : k_paths_ci<4>;
                     const int sl = paths_ci_s1d_lds(rp, pp) ? 1 : 0;
@@ -3662,10 +2874,6 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                                        (unsigned)lds, c->stream, with_slot(sc, 3), rp, c->wb, sb, nb * c->wb.ppt,
                                        c->d_ctr, sl);
                 }
-                else
-                    hipLaunchKernelGGL((k_paths<false, kPathsWaves>), dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
-                                       (unsigned)(rp.ndims * rp.spp * 8), c->stream, with_slot(sc, 3), rp, c->lay, c->d_jump,
-                                       c->wb, sb, nb, c->d_ctr);
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 2], c->stream));
                 hipLaunchKernelGGL(k_film, dim3((unsigned)((nb * per + 255) / 256)), dim3(256), 0, c->stream,
                                    c->d_film, rp, c->wb, sb, nb, c->d_films);
@@ -3872,15 +3080,12 @@ void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* bufs[] = {c->d_shapes, c->d_materials, c->d_prims, c->d_nodes, c->d_order, c->d_lights, c->d_camera, c->d_film,
                     c->d_dist,   c->d_films,     c->d_s1d,   c->d_panics, c->d_ctr,   c->d_out,    c->d_jump,
-                    c->d_wave,   c->d_fprims, c->d_wf,     c->d_ticks, c->d_slot_order, c->d_groups,
+                    c->d_wave,   c->d_fprims, c->d_ticks, c->d_slot_order, c->d_groups,
                     c->d_gmasks, c->d_cost,   c->d_cost_keys, c->d_pw};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     mesh_bvh_free(c->mesh);
     for (hipEvent_t e : c->bev) (void)hipEventDestroy(e);
-    for (hipEvent_t e : c->pev)
-        if (e) (void)hipEventDestroy(e);
-    if (c->h_poll) (void)hipHostFree(c->h_poll);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->ev2) (void)hipEventDestroy(c->ev2);

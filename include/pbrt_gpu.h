@@ -264,19 +264,21 @@ typedef struct pbrt_gpu_opts {
     int32_t reserved[4];
 } pbrt_gpu_opts;
 
-/* EXACT-mode kernels. All replay the reference bit for bit:
- *  SERIAL     one lane per tile, the tile's PCG32 stream consumed in order;
- *  WAVE       one 64-lane wave per tile: per-pixel shared bounce 1, path
- *             offsets found by speculative trajectories + jump-ahead, the
- *             pixel's samples traced in parallel (Path integrator, n_dims >= 3,
- *             every light pdf > 0, filter radius < 1.5; else SERIAL is used);
- *  WAVEFRONT  the WAVE pipeline with the speculative trajectories run as
- *             compacted per-bounce trace / shade kernels (same eligibility).
- *             pbrt_gpu_render_async returns once the offset chain is done
- *             (the host drives its window loop); the rest stays queued.
- *  WAVE_CI    the WAVE pipeline with a continuous-issue offset chain: a lane
- *             that finishes a trajectory, or whose candidate offset the chain
- *             has passed, takes the next offset at once (same eligibility). */
+/* Kernels. All replay the reference bit for bit:
+ *  SERIAL     one lane per tile, the tile's PCG32 stream consumed in order
+ *             (any render; the only one for n_dims < 3 Path renders,
+ *             zero-pdf lights, filter radius >= 1.5 and PBRT_FLAG_PANIC_FIDELITY);
+ *  WAVE_CI    the wave pipeline (Path integrator, n_dims >= 3, every light
+ *             pdf > 0, filter radius < 1.5): per-pixel shared bounce 1, the
+ *             tile's path offsets found by a continuous-issue chain of
+ *             speculative trajectories + jump-ahead (k_chain_ci), then the
+ *             samples as full paths (k_paths_ci, or the per-bounce path
+ *             wavefront k_pw_* for mesh scenes and large trees);
+ *  WAVE_DL    DirectLighting (n_dims >= 1): pixel-order StartPixel +
+ *             jump-ahead, one lane per sample;
+ *  WAVE, WAVEFRONT  (round 1's window and wavefront chains, since replaced)
+ *             request the wave pipeline; st.kernel reports WAVE_CI.
+ * THROUGHPUT mode reports WAVE for the wave pipeline (no chain). */
 /* WAVE kernel: always replay StartPixel serially (the path normally taken
  * only after a pcg_bounded rejection); results are identical. */
 #define PBRT_FLAG_SERIAL_START_PIXEL 1

@@ -36,10 +36,8 @@ def gpu_render(scene, rd, lanes_per_wave=0, kernel="auto"):
         film, st = r.render(rd)
     if kernel == "serial":
         assert st.kernel == abi.PBRT_KERNEL_SERIAL
-    elif kernel == "wave":
-        assert st.kernel == abi.PBRT_KERNEL_WAVE
-    elif kernel == "wavefront":
-        assert st.kernel == abi.PBRT_KERNEL_WAVEFRONT
+    elif kernel in ("wave", "wavefront"):   # requests of the window / wavefront chains run k_chain_ci
+        assert st.kernel in (abi.PBRT_KERNEL_WAVE_CI, abi.PBRT_KERNEL_WAVE)
     elif kernel == "wave_ci":
         assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
     elif kernel == "wave_dl":
@@ -379,15 +377,6 @@ def test_wave_kernel_variants(kw, kernel):
     check(G.Scene.readme(48, 40), abi.render_desc(**kw), kernel=kernel)
 
 
-@pytest.mark.parametrize("kw", WAVE_VARIANTS)
-@pytest.mark.parametrize("levels", ["8", "0", "2"])
-def test_wavefront_kernel_variants(kw, levels, monkeypatch):
-    """The wavefront chain: split per-bounce trace/shade levels, and the tail
-    kernel alone (0 levels) or after 2 split levels."""
-    monkeypatch.setenv("PBRT_WF_LEVELS", levels)
-    check(G.Scene.readme(48, 40), abi.render_desc(**kw), kernel="wavefront")
-
-
 def test_wavefront_cornell_64spp_and_readme_256():
     check(G.Scene.cornell(32, 32), abi.render_desc(8, 8, max_depth=10), kernel="wavefront")
     check(G.Scene.readme(256, 256), abi.render_desc(2, 2), kernel="wavefront")
@@ -403,7 +392,7 @@ def test_wavefront_panic_is_reported_like_the_oracle():
         with pytest.raises(G.PbrtError) as ei:
             r.render(rd)
     st = ei.value.stats
-    assert ei.value.code == abi.PBRT_E_REF_PANIC and st.kernel == abi.PBRT_KERNEL_WAVEFRONT
+    assert ei.value.code == abi.PBRT_E_REF_PANIC and st.kernel == abi.PBRT_KERNEL_WAVE_CI
     assert (st.panic_kind, st.panic_tile, st.panic_pixel_x, st.panic_pixel_y, st.panic_sample, st.panic_bounce) == (
         ost.panic_kind, ost.panic_tile, ost.panic_px, ost.panic_py, ost.panic_sample, ost.panic_bounce)
 
@@ -411,7 +400,8 @@ def test_wavefront_panic_is_reported_like_the_oracle():
 @pytest.mark.parametrize("tiles_per_wave", [1, 2, 4, 8, 16])
 @pytest.mark.parametrize("kernel", ["wave", "wave_ci"])
 def test_wave_kernel_tiles_per_wave(tiles_per_wave, kernel):
-    """k_chain packs 64 / L lanes per tile; 37 tiles leave partial last waves."""
+    """k_chain_ci packs up to 4 tiles per wave (64 / L lanes each; larger
+    requests run one tile per wave); 37 tiles leave partial last waves."""
     check(G.Scene.readme(112, 80), abi.render_desc(4, 4), kernel=kernel, lanes_per_wave=tiles_per_wave)
 
 
@@ -823,3 +813,35 @@ def test_path_wavefront_chunked_and_panics(mode, monkeypatch):
     st = ei.value.stats
     assert (st.panic_kind, st.panic_tile, st.panic_pixel_x, st.panic_pixel_y, st.panic_sample, st.panic_bounce) == (
         ost.panic_kind, ost.panic_tile, ost.panic_px, ost.panic_py, ost.panic_sample, ost.panic_bounce)
+
+
+
+def many_spheres_scene(n, seed):
+    """n Matte spheres scattered in front of the README camera: a BVH far
+    beyond the 64 LDS-staged nodes, so k_chain_ci walks with the reference's
+    [64] stack and the full paths run on the path wavefront."""
+    rng = np.random.default_rng(seed)
+    s = G.Scene()
+    mats = [s.add_matte(tuple(rng.uniform(0.2, 0.9, 3))) for _ in range(3)]
+    floor = s.add_disk(G.mul(G.translate(0, -1, 0), G.rotate(0, 90)), 0.0, 50.0)
+    s.add_primitive(floor, mats[0])
+    for i in range(n):
+        c = (rng.uniform(-6, 6), rng.uniform(-0.5, 4), rng.uniform(-6, 6))
+        sph = s.add_sphere(G.translate(*c), rng.uniform(0.2, 0.8), reverse=bool(i % 7 == 3))
+        s.add_primitive(sph, mats[i % 3])
+    s.add_point_light(G.translate(0, 8, 0), (40, 40, 40))
+    s.add_distant_light(G.translate(0, 0, 0), (0.6, 0.6, 0.6), (1, 2, 1))
+    s.set_film(64, 48)
+    s.set_camera(G.look_at((0, 5, 14), (0, 0, 0), (0, 1, 0)), fov=50)
+    return s.build()
+
+
+@pytest.mark.parametrize("mode", [abi.PBRT_MODE_EXACT, abi.PBRT_MODE_THROUGHPUT])
+@pytest.mark.parametrize("ci_waves", ["1", "4"])
+def test_large_bvh_wave_pipeline_bitexact(mode, ci_waves, monkeypatch):
+    monkeypatch.setenv("PBRT_CI_WAVES", ci_waves)
+    scene = many_spheres_scene(90, 5)
+    assert scene.desc.n_nodes > 64
+    film, st = check(scene, abi.render_desc(3, 3, max_depth=6, mode=mode))
+    assert st.kernel == (abi.PBRT_KERNEL_WAVE_CI if mode == abi.PBRT_MODE_EXACT else abi.PBRT_KERNEL_WAVE)
+    assert film.max() > 0
