@@ -120,7 +120,7 @@ struct ChainCache {
 // reports the bounce of a panic. Returns true when the path has ended
 // (radiance in s.L). Arithmetic and draw order are the reference's.
 #ifndef PBRT_PATHS_LB
-#define PBRT_PATHS_LB 4   // leaf boxes per scan iteration in path_step's traversals (build option)
+#define PBRT_PATHS_LB 1   // leaf boxes per scan iteration in path_step's traversals (build option)
 #endif
 struct PathState {
     Spec L, beta;

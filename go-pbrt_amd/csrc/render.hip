@@ -1435,6 +1435,9 @@ __global__ void k_order_of_keys(const uint64_t* __restrict__ keys, int64_t nb, u
 #ifndef PBRT_CI_EU_WAVES
 #define PBRT_CI_EU_WAVES 2   // k_chain_ci waves/SIMD (build option)
 #endif
+#ifndef PBRT_CHAIN_LB
+#define PBRT_CHAIN_LB 1   // leaf boxes per scan iteration in k_chain_ci's traversal (build option)
+#endif
 constexpr uint32_t kNoOff = 0xFFFFFFFFu;
 constexpr uint32_t kBadSpecD = 0xFFFFFFFEu;   // speculative lane could not resolve D
 constexpr uint32_t kBadExactD = 0xFFFFFFFDu;  // the exact head's trajectory panics
@@ -1688,7 +1691,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
         if (tracing) {
             int panic = 0, best;
             V3 ph;
-            bvh_walk<false, kT>(sc, ray, stack, panic, best, ph);
+            bvh_walk<false, kT, PBRT_CHAIN_LB>(sc, ray, stack, panic, best, ph);
             mark(2);
             uint32_t d = kNoOff;
             if (panic) {

@@ -845,3 +845,32 @@ def test_large_bvh_wave_pipeline_bitexact(mode, ci_waves, monkeypatch):
     film, st = check(scene, abi.render_desc(3, 3, max_depth=6, mode=mode))
     assert st.kernel == (abi.PBRT_KERNEL_WAVE_CI if mode == abi.PBRT_MODE_EXACT else abi.PBRT_KERNEL_WAVE)
     assert film.max() > 0
+
+
+def test_throughput_mode_statistical_equivalence_at_config_B():
+    """THROUGHPUT (Mode B, the >= 6x scaling vehicle) is checked
+    for statistical equivalence with EXACT on config B's frame (1080p, 64 spp):
+    against a high-spp EXACT render (Stratified(16,16)) its clipped RMS error
+    matches EXACT's own (same spp) within 10%, and its clipped mean / median
+    sit inside the spread of EXACT renders with different tile seeds. The
+    estimator is heavy-tailed (BSDF.SampleF returns the local wi, ledger #7),
+    hence the clipped statistics."""
+    scene = G.Scene.readme(1920, 1080)
+    with G.Renderer(scene) as r:
+        a16, _ = r.render(abi.render_desc(8, 8))
+        a8, _ = r.render(abi.render_desc(8, 8, tile_size=8))
+        b16, st = r.render(abi.render_desc(8, 8, mode=abi.PBRT_MODE_THROUGHPUT))
+        ref, _ = r.render(abi.render_desc(16, 16))
+    assert st.paths_traced == 1920 * 1080 * 63
+    inner = (slice(1, -1), slice(1, -1))
+    a16, a8, b16 = a16[inner], a8[inner], b16[inner]
+    ref = ref[inner] * (63.0 / 255.0)   # film sums: scale the 255-path reference to 63 paths
+    cap = np.percentile(ref, 95)
+    clip = lambda x: np.clip(x, 0, cap)   # noqa: E731
+    err_a = np.sqrt(np.mean((clip(a16) - clip(ref)) ** 2))
+    err_b = np.sqrt(np.mean((clip(b16) - clip(ref)) ** 2))
+    assert 0.9 < err_b / err_a < 1.1, (err_a, err_b)
+    for stat in (np.median, lambda x: clip(x).mean()):
+        sa16, sa8, sb = stat(a16), stat(a8), stat(b16)
+        spread = abs(sa16 - sa8) + 0.002 * abs(sa16)
+        assert abs(sb - 0.5 * (sa16 + sa8)) < 3 * spread, (sa16, sa8, sb)
