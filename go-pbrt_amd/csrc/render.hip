@@ -306,7 +306,10 @@ struct ChainLayout {   // byte offsets into the chain / setup kernels' dynamic L
     int ring;      // k_chain_ci: offset ring after the StartPixel staging (no sbuf / dbuf)
     int staging;   // k_chain_ci: bytes of the StartPixel staging (s1d, other, vbuf)
 };
-constexpr int kCiRingBytes = 4 * 1024;   // k_chain_ci offset ring (all lane groups of a wave)
+#ifndef PBRT_CI_RING_KB
+#define PBRT_CI_RING_KB 4
+#endif
+constexpr int kCiRingBytes = PBRT_CI_RING_KB * 1024;   // k_chain_ci offset ring (all lane groups of a wave)
 constexpr int kCiMaxGroups = 4;          // k_chain_ci lane groups (tiles) per wave
 
 __device__ __forceinline__ double pcg_float_of(uint32_t v) {
@@ -2092,8 +2095,12 @@ int cull_groups(const pbrt_scene_desc* s, const std::vector<uint32_t>& order, st
     for (int v : leaves)
         if (!(diag2(v) > 0.25 * root)) rest.push_back(v);
     std::vector<std::vector<int>> groups;
+    // leaves per group at most: 4 measured best on config B (chain 420 -> 404 ms against 8;
+    // 2: 450, 3: 403, 5: 418, 16: 492; profiles/r02/cull_group_ab.json). PBRT_CULL_GROUP overrides.
+    size_t gmax = 4;
+    if (const char* e = getenv("PBRT_CULL_GROUP")) gmax = (size_t)std::max(2, atoi(e));
     std::function<void(std::vector<int>)> split = [&](std::vector<int> g) {
-        if (g.size() <= 8) {
+        if (g.size() <= gmax) {
             if (g.size() > 1) groups.push_back(g);
             return;
         }
