@@ -2120,7 +2120,9 @@ int cull_groups(const pbrt_scene_desc* s, const std::vector<uint32_t>& order, st
     const int G = (int)groups.size();
     // worth it only when the groups can skip a fair share of the leaf tests
     // (README: 21 of 23 leaves grouped; Cornell: 2 of 8, not grouped)
-    if (G == 0 || G > kMaxCullGroups || 2 * (int)rest.size() < (int)leaves.size()) return 0;
+    int min_frac2 = 2;   // grouped leaves must be at least half of all (PBRT_CULL_MIN=0: any)
+    if (const char* e = getenv("PBRT_CULL_MIN")) min_frac2 = std::max(0, atoi(e));
+    if (G == 0 || G > kMaxCullGroups || min_frac2 * (int)rest.size() < (int)leaves.size()) return 0;
     boxes.assign((size_t)G * 6, 0.0);
     for (int gi = 0; gi < G; gi++) {
         for (int k = 0; k < 3; k++) {
