@@ -2355,7 +2355,13 @@ uint64_t schedule_key(const RenderParams& rp, int kw) {
 // (k_pw_*) runs the paths. PBRT_PATHS_CI=0 forces that.
 // Returns the pixels per wave (2, 4 or 8; PBRT_PATHS_CI overrides, 0 = off).
 // k_paths_ci stages the stratified values of its P pixels in LDS when they take <= 16 KB
-bool paths_ci_s1d_lds(const RenderParams& rp, int P) { return (int64_t)P * rp.ndims * rp.spp * 8 <= 16 * 1024; }
+// Off by default: read from their global records (L2-resident; config B
+// 111.0 -> 109.9 ms EXACT, 136.0 -> 134.8 ms THROUGHPUT against LDS staging).
+// PBRT_PATHS_S1D=lds stages them where they fit (experiments).
+bool paths_ci_s1d_lds(const RenderParams& rp, int P) {
+    const char* e = getenv("PBRT_PATHS_S1D");
+    return e && std::strcmp(e, "lds") == 0 && (int64_t)P * rp.ndims * rp.spp * 8 <= 16 * 1024;
+}
 int paths_ci_pixels(const pbrt_gpu_ctx* c, const RenderParams& rp) {
     int pp = 4;
     bool forced = false;
@@ -2368,9 +2374,10 @@ int paths_ci_pixels(const pbrt_gpu_ctx* c, const RenderParams& rp) {
         return c->host_scene.n_nodes <= kLdsNodes && p * c->host_scene.n_lights <= kWave;
     };
     if (forced) return fits(pp) ? pp : 0;
-    // 4 pixels per wave where their stratified values fit in LDS, else 2
-    // (config C, 256 spp), else 4 reading them from global memory (config E)
-    return paths_ci_s1d_lds(rp, 4) && fits(4) ? 4 : paths_ci_s1d_lds(rp, 2) && fits(2) ? 2 : fits(4) ? 4 : 0;
+    // 4 pixels per wave; their stratified values in LDS where they fit, else
+    // read from global memory (config C at 256 spp: 4 pixels with global values
+    // 868 ms against 2 pixels with LDS values 1150 ms; config E)
+    return fits(4) ? 4 : 0;
 }
 
 // The full-path stage on the path wavefront (k_pw_*) instead of k_paths_ci:
