@@ -2374,10 +2374,11 @@ int paths_ci_pixels(const pbrt_gpu_ctx* c, const RenderParams& rp) {
         return c->host_scene.n_nodes <= kLdsNodes && p * c->host_scene.n_lights <= kWave;
     };
     if (forced) return fits(pp) ? pp : 0;
-    // 4 pixels per wave; their stratified values in LDS where they fit, else
-    // read from global memory (config C at 256 spp: 4 pixels with global values
-    // 868 ms against 2 pixels with LDS values 1150 ms; config E)
-    return fits(4) ? 4 : 0;
+    // 8 pixels per wave where their lights fit one wave, else 4; stratified
+    // values read from global memory (config B EXACT paths 109.9 -> 104.8 ms
+    // for 8 against 4; config C at 256 spp 872 -> 869 ms, where 4 pixels with
+    // global values already beat 2 with LDS values, 1150 ms)
+    return fits(8) ? 8 : fits(4) ? 4 : 0;
 }
 
 // The full-path stage on the path wavefront (k_pw_*) instead of k_paths_ci:
@@ -2873,11 +2874,12 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                     // setup (StartPixel + bounce 1 per pixel), then lane-refill paths
                     hipLaunchKernelGGL(k_mb_setup, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
                                        (unsigned)c->lay.total, c->stream, with_slot(sc, 4), rp, c->lay, c->d_jump, c->wb, sb, nb);
-                    const int pp = paths_ci_pixels(c, rp) >= 4 ? 4 : 2;
-                    auto kern = pp == 4 ? k_paths_ci<4, true> : k_paths_ci<2, true>;
+                    const int pp = paths_ci_pixels(c, rp);
+                    const int per = rp.ndims * rp.spp;
+                    auto kern = pp == 8 ? k_paths_ci<8, true> : pp == 2 ? k_paths_ci<2, true> : k_paths_ci<4, true>;
                     const int sl = paths_ci_s1d_lds(rp, pp) ? 1 : 0;
-                    const int lds = pp == 4 ? paths_group_lds<4>(sl * rp.ndims * rp.spp)
-                                            : paths_group_lds<2>(sl * rp.ndims * rp.spp);
+                    const int lds = pp == 8 ? paths_group_lds<8>(sl * per) : pp == 2 ? paths_group_lds<2>(sl * per)
+                                                                                     : paths_group_lds<4>(sl * per);
                     hipLaunchKernelGGL(kern, dim3((unsigned)((nb * c->wb.ppt + pp - 1) / pp)), dim3(kWave),
                                        (unsigned)lds, c->stream, with_slot(sc, 5), rp, c->wb, sb, nb * c->wb.ppt,
                                        c->d_ctr, sl);
