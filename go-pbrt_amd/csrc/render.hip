@@ -1474,9 +1474,10 @@ template <int kW, int kDepth = 32>
 __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT_CI_EU_WAVES, 8))) void k_chain_ci(
     DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
     int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr,
-    const uint32_t* __restrict__ order, uint32_t* __restrict__ ticks) {
+    const uint32_t* __restrict__ order, uint32_t* __restrict__ ticks, int cstride) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const uint64_t t_begin = wall_clock64();
+    const uint32_t cs = cstride == 1 ? 1u : 2u;   // candidate offsets head + cs * j
     constexpr int kT = kWave * kW;   // threads per workgroup (stack stride)
     __shared__ uint16_t stack_lds[kDepth * kT];
     __shared__ ChainCache pcs[kCiMaxGroups];
@@ -1647,7 +1648,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
             const int re = (sg.reissue && nidle > 0) ? 1 : 0;
             const uint32_t nx0 = sg.nxt;
             // offsets < head + R keep the ring collision-free
-            const int avail = nx0 < sg.head + R ? (int)((sg.head + R - nx0 + 1) / 2) : 0;
+            const int avail = nx0 < sg.head + R ? (int)((sg.head + R - nx0 + cs - 1) / cs) : 0;
             const int nspec = min(nidle - re, avail);
             uint32_t o = kNoOff;
             bool exact = false;
@@ -1657,11 +1658,11 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
                     exact = true;
                 } else {
                     rank -= re;
-                    if (rank < nspec) o = nx0 + 2u * (uint32_t)rank;
+                    if (rank < nspec) o = nx0 + cs * (uint32_t)rank;
                 }
             }
             if (gl == 0 && sg.phase == 1) {
-                gs[g].nxt = nx0 + 2u * (uint32_t)max(nspec, 0);
+                gs[g].nxt = nx0 + cs * (uint32_t)max(nspec, 0);
                 CI_DIAG(ph[5] += (unsigned long long)(max(nspec, 0) + re);)   // candidate trajectories issued
                 if (re) gs[g].reissue = 0;
             }
@@ -1753,14 +1754,14 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
                     break;
                 }
             }
-            if (s.nxt < s.head || ((s.nxt ^ s.head) & 1u)) s.nxt = s.head;
+            if (s.nxt < s.head || (cs == 2u && ((s.nxt ^ s.head) & 1u))) s.nxt = s.head;
             gs[g] = s;
         }
         __syncthreads();
         // ---- (5) drop candidates the chain has left behind
         if (off != kNoOff) {
             const CiGroup s2 = gs[g];
-            if (s2.phase != 1 || off < s2.head || ((off ^ s2.head) & 1u) || s2.pi != sg.pi) {
+            if (s2.phase != 1 || off < s2.head || (cs == 2u && ((off ^ s2.head) & 1u)) || s2.pi != sg.pi) {
                 off = kNoOff;
                 tracing = false;
             }
@@ -2301,7 +2302,7 @@ ChainLayout ci_layout(const ChainLayout& base, int w, int G, unsigned& lds_bytes
 int ci_waves(const pbrt_gpu_ctx* c, int64_t nb) {
     if (const char* e = getenv("PBRT_CI_WAVES")) {
         const int v = atoi(e);
-        if (v == 1 || v == 2 || v == 4) return v;
+        if (v == 1 || v == 2 || v == 4 || v == 8) return v;
     }
     if (c->tiles_per_wave > 1) return 1;
     // measured on config B shards (tools/shard_sim.py): 8160 tiles -> 1,
@@ -2330,6 +2331,21 @@ bool ci_split_enabled() {
 int64_t ci_heavy_override() {
     const char* e = getenv("PBRT_CI_HEAVY");
     return e ? (int64_t)atoll(e) : -1;
+}
+// k_chain_ci candidate stride: 2 issues candidates at the chain head's parity
+// only (dropped when an odd draw count flips it), 1 at every offset (twice
+// the candidates, none dropped). PBRT_CI_STRIDE = 1 / 2 overrides.
+int ci_stride(int w) {
+    if (const char* e = getenv("PBRT_CI_STRIDE")) {
+        const int v = atoi(e);
+        if (v == 1 || v == 2) return v;
+    }
+    return w > 1 ? 1 : 2;
+}
+// PBRT_CI_HEAVY_WAVES = 4 (default) or 8: waves per heavy tile of the split
+int ci_heavy_waves() {
+    const char* e = getenv("PBRT_CI_HEAVY_WAVES");
+    return (e && atoi(e) == 8) ? 8 : 4;
 }
 bool ci_order_enabled() {
     const char* e = getenv("PBRT_CI_ORDER");
@@ -2809,10 +2825,12 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                             const int ring = w * kCiRingBytes / (int)sizeof(RingEnt);
                             unsigned lds = 0;
                             const ChainLayout lw = ci_layout(c->lay_ci, w, 1, lds);
-                            auto kern = w == 2 ? (lds_nodes ? k_chain_ci<2> : k_chain_ci<2, 64>)
-                                               : (lds_nodes ? k_chain_ci<4> : k_chain_ci<4, 64>);
+                            auto kern = w == 2   ? (lds_nodes ? k_chain_ci<2> : k_chain_ci<2, 64>)
+                                        : w == 4 ? (lds_nodes ? k_chain_ci<4> : k_chain_ci<4, 64>)
+                                                 : (lds_nodes ? k_chain_ci<8> : k_chain_ci<8, 64>);
                             hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3(kWave * w), lds, st, with_slot(sc, 2), rp, lw,
-                                               c->d_jump, c->wb, sb, nb, kWave * w, ring, c->d_ctr, ord, ticks);
+                                               c->d_jump, c->wb, sb, nb, kWave * w, ring, c->d_ctr, ord, ticks,
+                                               ci_stride(w));
                         } else {
                             const int Gc = std::min(G, kCiMaxGroups);
                             const int ring = kCiRingBytes / (int)sizeof(RingEnt) / Gc;
@@ -2822,7 +2840,7 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                             hipLaunchKernelGGL(kern1, dim3((unsigned)((n + Gc - 1) / Gc)), dim3(kWave),
                                                lds, st, with_slot(sc, 2), rp, lw, c->d_jump, c->wb, sb,
                                                nb, kWave / Gc, ring, c->d_ctr, Gc == 1 ? ord : nullptr,
-                                               Gc == 1 ? ticks : nullptr);
+                                               Gc == 1 ? ticks : nullptr, ci_stride(1));
                         }
                     };
                     // the heaviest tiles of the last frame get 4 waves each; they are
@@ -2834,17 +2852,17 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                     // (1020 tiles: 294 -> 307 ms), so smaller launches never split
                     int64_t heavy = (learned && kw > 1 && G == 1 && nb > c->n_simd && ci_split_enabled())
                                         ? std::min<int64_t>(c->heavy_k, nb) : 0;
-                    if (ci_heavy_override() >= 0 && learned && kw > 1 && G == 1)   // tests force the split
+                    if (ci_heavy_override() >= 0 && learned && G == 1)   // tests and experiments force the split
                         heavy = std::min<int64_t>(ci_heavy_override(), nb);
                     if (heavy >= nb) heavy = 0;   // nothing left for the light launch: one launch at kw
                     c->last_heavy = heavy;
                     if (ticks) {   // label every slot with the waves it actually runs at
                         c->h_slot_kw.assign((size_t)nb, (uint8_t)(heavy > 0 ? 1 : kw));
-                        for (int64_t i = 0; i < heavy; i++) c->h_slot_kw[c->h_slot_order[(size_t)i]] = 4;
+                        for (int64_t i = 0; i < heavy; i++) c->h_slot_kw[c->h_slot_order[(size_t)i]] = (uint8_t)ci_heavy_waves();
                     }
                     if (heavy > 0) {
                         HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
-                        launch_ci(4, heavy, order, c->stream);
+                        launch_ci(ci_heavy_waves(), heavy, order, c->stream);
                         HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
                         launch_ci(1, nb - heavy, order + heavy, c->stream2);
                         HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
@@ -2964,7 +2982,7 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
         double sum = 0;
         for (size_t i = 0; i < t.size(); i++) {
             const int w = i < c->h_slot_kw.size() ? c->h_slot_kw[i] : 1;
-            cost[i] = (double)t[i] * (w == 4 ? 1.8 : w == 2 ? 1.3 : 1.0);
+            cost[i] = (double)t[i] * (w == 8 ? 2.3 : w == 4 ? 1.8 : w == 2 ? 1.3 : 1.0);
             sum += cost[i];
         }
         c->h_slot_order.resize(t.size());

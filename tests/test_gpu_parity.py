@@ -420,7 +420,7 @@ def test_wave_ci_readme_256_and_odd_draw_counts(tiles_per_wave):
           lanes_per_wave=tiles_per_wave)
 
 
-@pytest.mark.parametrize("ci_waves", ["1", "2", "4"])
+@pytest.mark.parametrize("ci_waves", ["1", "2", "4", "8"])
 @pytest.mark.parametrize("kw", WAVE_VARIANTS)
 def test_wave_ci_waves_per_tile(kw, ci_waves, monkeypatch):
     """k_chain_ci with 1, 2 or 4 waves cooperating on one tile's chain
@@ -429,14 +429,25 @@ def test_wave_ci_waves_per_tile(kw, ci_waves, monkeypatch):
     check(G.Scene.readme(48, 40), abi.render_desc(**kw), kernel="wave_ci")
 
 
-@pytest.mark.parametrize("ci_waves", ["1", "2", "4"])
+@pytest.mark.parametrize("ci_waves", ["1", "4"])
+def test_wave_ci_stride_1_keeps_bits(ci_waves, monkeypatch):
+    """PBRT_CI_STRIDE=1: chain candidates at every offset (both parities), so
+    an odd draw count drops nothing; only the schedule changes."""
+    monkeypatch.setenv("PBRT_CI_STRIDE", "1")
+    monkeypatch.setenv("PBRT_CI_WAVES", ci_waves)
+    check(G.Scene.readme(112, 80), abi.render_desc(8, 8), kernel="wave_ci")
+    check(G.Scene.readme(48, 40), abi.render_desc(4, 4, jitter=True), kernel="wave_ci")
+    check(G.Scene.cornell(48, 32), abi.render_desc(6, 6, max_depth=12, rr_threshold=0.5), kernel="wave_ci")
+
+
+@pytest.mark.parametrize("ci_waves", ["1", "2", "4", "8"])
 def test_wave_ci_waves_per_tile_larger_frames(ci_waves, monkeypatch):
     monkeypatch.setenv("PBRT_CI_WAVES", ci_waves)
     check(G.Scene.readme(112, 80), abi.render_desc(8, 8), kernel="wave_ci")
     check(G.Scene.cornell(48, 32), abi.render_desc(6, 6, max_depth=12, rr_threshold=0.5), kernel="wave_ci")
 
 
-@pytest.mark.parametrize("ci_waves", ["1", "2", "4"])
+@pytest.mark.parametrize("ci_waves", ["1", "2", "4", "8"])
 def test_wave_ci_heaviest_first_schedule_keeps_bits(ci_waves, monkeypatch):
     """The second frame of a configuration launches its tiles in the
     heaviest-first order measured on the first; only the schedule changes."""
@@ -453,7 +464,7 @@ def test_wave_ci_heaviest_first_schedule_keeps_bits(ci_waves, monkeypatch):
 
 
 @pytest.mark.parametrize("heavy", ["3", "12"])
-@pytest.mark.parametrize("ci_waves", ["2", "4"])
+@pytest.mark.parametrize("ci_waves", ["2", "4", "8"])
 def test_wave_ci_heavy_light_split_keeps_bits(ci_waves, heavy, monkeypatch):
     heavy_env = heavy
     """Shard mode: from the second frame the heaviest tiles run at 4 waves in
@@ -461,6 +472,8 @@ def test_wave_ci_heavy_light_split_keeps_bits(ci_waves, heavy, monkeypatch):
     stream; only the schedule changes."""
     monkeypatch.setenv("PBRT_CI_WAVES", ci_waves)
     monkeypatch.setenv("PBRT_CI_HEAVY", heavy)
+    if ci_waves == "8":   # heavy tiles at 8 waves (PBRT_CI_HEAVY_WAVES)
+        monkeypatch.setenv("PBRT_CI_HEAVY_WAVES", "8")
     scene = G.Scene.readme(112, 80)
     rds = [abi.render_desc(8, 8), abi.render_desc(4, 4, tile_begin=1, tile_stride=2),
            abi.render_desc(6, 6, max_depth=12, rr_threshold=0.5)]
@@ -714,7 +727,7 @@ def test_throughput_mode_1080p_sampled_tiles_and_shards():
 
 
 # ------------------------------------------- config C sampler (256 spp) at small size
-@pytest.mark.parametrize("ci_waves", ["1", "2", "4"])
+@pytest.mark.parametrize("ci_waves", ["1", "2", "4", "8"])
 def test_cornell_256spp_wave_ci(ci_waves, monkeypatch):
     """Stratified(16,16) as config C: the continuous-issue chain with its
     StartPixel staging aliased on the offset ring (19 KB of LDS) and k_paths_ci
