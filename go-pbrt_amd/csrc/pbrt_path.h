@@ -850,6 +850,123 @@ __device__ inline Spec bsdf_sample_f(const BSDF& b, V3 woW, V2 u, V3& wi, double
     return f;
 }
 
+// --------------------------------------------- Mirror and smooth Glass (serial kernel)
+// The BSDF of a Mirror (mirror.go:21-32) or Glass (glass.go:28-75) material. Its
+// single BxDF has F = 0 and Pdf = 0 (reflection.go:486-488, 534-536, 553-555,
+// 572-574), so light sampling sees it exactly as a BSDF without components: the
+// shared estimate_direct/bsdf_f/bsdf_pdf run on `b` with n_bxdfs = 0. Only
+// sampling (and the Path.Li bookkeeping) needs the kind.
+constexpr int BXDF_TRANSMISSION = 2;
+enum { BXDF_KIND_LAMBERT = 0, BXDF_KIND_SPEC_REFL = 1, BXDF_KIND_FRESNEL_SPEC = 2 };
+struct BSDFX {
+    int kind;       // BXDF_KIND_*; LAMBERT: `b` is the whole BSDF
+    int n;          // 0 or 1 BxDFs of that kind
+    Spec r, t;
+    double eta;     // NewBSDF(si, eta)
+};
+// NumComponents(BSDFAll &^ BSDFSpecular) > 0: SpecularReflection is typed
+// Reflection|Diffuse (reflection.go:538-544), FresnelSpecular is specular
+__device__ __forceinline__ bool bsdfx_nonspecular(const BSDF& b, const BSDFX& x) {
+    return x.kind == BXDF_KIND_LAMBERT ? b.n_bxdfs > 0 : (x.kind == BXDF_KIND_SPEC_REFL && x.n > 0);
+}
+__device__ inline int compute_bsdf_x(const DevScene& sc, const SI& si, BSDF& b, BSDFX& x) {
+    const pbrt_material_desc& m =
+        sc.materials[si.prim < sc.n_prims ? sc.prims[si.prim].material
+                                          : sc.mesh.mesh_mat[tri_mesh(sc, si.prim - sc.n_prims)]];
+    x.kind = BXDF_KIND_LAMBERT;
+    x.n = 0;
+    x.eta = 1.0;
+    if (m.type == PBRT_MAT_MATTE) return compute_bsdf(sc, si, b);
+    b.ns = si.sn;
+    b.ng = si.n;
+    b.ss = normalized(si.sdpdu);
+    b.ts = cross(b.ns, b.ss);
+    b.n_bxdfs = 0;
+    if (m.type == PBRT_MAT_MIRROR) {
+        Spec r = spec3(m.kr);
+        r.r = gomath::clamp(r.r, 0, kInf);
+        r.g = gomath::clamp(r.g, 0, kInf);
+        r.b = gomath::clamp(r.b, 0, kInf);
+        x.kind = BXDF_KIND_SPEC_REFL;
+        x.n = is_black(r) ? 0 : 1;
+        x.r = r;
+        return 0;
+    }
+    Spec R = spec3(m.kr), T = spec3(m.kt);
+    R.r = gomath::clamp(R.r, 0, 1); R.g = gomath::clamp(R.g, 0, 1); R.b = gomath::clamp(R.b, 0, 1);
+    T.r = gomath::clamp(T.r, 0, 1); T.g = gomath::clamp(T.g, 0, 1); T.b = gomath::clamp(T.b, 0, 1);
+    x.kind = BXDF_KIND_FRESNEL_SPEC;
+    x.eta = m.eta;
+    x.r = R;
+    x.t = T;
+    if (is_black(R) && is_black(T)) return 0;
+    if (!(m.u_roughness == 0 && m.v_roughness == 0)) return -1;   // microfacets: unsupported
+    x.n = 1;
+    return 0;
+}
+// FrDielectric (reflection.go:21-42)
+__device__ inline double fr_dielectric(double cos_i, double eta_i, double eta_t) {
+    cos_i = gomath::clamp(cos_i, -1, 1);
+    if (!(cos_i > 0)) {
+        const double tmp = eta_i;
+        eta_i = eta_t;
+        eta_t = tmp;
+        cos_i = gomath::abs(cos_i);
+    }
+    const double sin_i = gomath::sqrt(gomath::max(0.0, 1 - cos_i * cos_i));
+    const double sin_t = eta_i / eta_t * sin_i;
+    if (sin_t >= 1) return 1;
+    const double cos_t = gomath::sqrt(gomath::max(0.0, 1 - sin_t * sin_t));
+    const double rparl = ((eta_t * cos_i) - (eta_i * cos_t)) / ((eta_t * cos_i) + (eta_i * cos_t));
+    const double rperp = ((eta_i * cos_i) - (eta_t * cos_t)) / ((eta_i * cos_i) + (eta_t * cos_t));
+    return (rparl * rparl + rperp * rperp) / 2;
+}
+// BSDF.SampleF (reflection.go:188-253) over any BSDFX, flags BSDFAll (Path.Li),
+// returning the LOCAL-frame wi (#7) and the sampled type
+__device__ inline Spec bsdfx_sample_f(const BSDF& b, const BSDFX& x, V3 woW, V2 u, V3& wi, double& pdf, int& type) {
+    type = 0;
+    if (x.kind == BXDF_KIND_LAMBERT) return bsdf_sample_f(b, woW, u, wi, pdf);   // sampleF's type is 0
+    wi = V3{0, 0, 0};
+    pdf = 0;
+    if (x.n == 0) return spec(0);
+    const double comp = gomath::min(gomath::floor(u.x * 1.0), 1.0 - 1);
+    const V2 ur{gomath::min(u.x * 1.0 - comp, gomath::kOneMinusEpsilon), u.y};
+    const V3 wo = w2l(b, woW);
+    if (wo.z == 0.0) return spec(0);
+    if (x.kind == BXDF_KIND_SPEC_REFL) {   // SpecularReflection.SampleF, FresnelNoOp (reflection.go:557-562)
+        wi = V3{-wo.x, -wo.y, wo.z};
+        pdf = 1.0;
+        return sdivs(smul(spec(1.0), x.r), gomath::abs(wi.z));
+    }
+    // FresnelSpecular.SampleF (reflection.go:489-524), incl. its (etaT / etaT) radiance scale
+    const double F = fr_dielectric(wo.z, 1.0, x.eta);
+    if (ur.x < F) {
+        wi = V3{-wo.x, -wo.y, wo.z};
+        pdf = F;
+        type = BXDF_SPECULAR | BXDF_REFLECTION;
+        return sdivs(smuls(x.r, F), gomath::abs(wi.z));
+    }
+    double eta_i, eta_t;
+    if (wo.z > 0) { eta_i = 1.0; eta_t = x.eta; } else { eta_i = x.eta; eta_t = 1.0; }
+    V3 n{0, 0, 1};
+    if (dot(n, wo) < 0.0) n = muls(n, -1);   // FaceForward (geometry.go:111-116)
+    const double eta = eta_i / eta_t;        // Refract (reflection.go:106-118)
+    const double cos_i = dot(n, wo);
+    const double sin2_i = gomath::max(0.0, 1 - cos_i * cos_i);
+    const double sin2_t = eta * eta * sin2_i;
+    if (sin2_t >= 1) return spec(0);         // total internal reflection: pdf 0
+    const double cos_t = gomath::sqrt(1 - sin2_t);
+    const V3 w = muls(wo, -eta) + muls(n, eta * cos_i - cos_t);
+    Spec ft = smuls(x.t, 1 - F);
+    ft = smuls(ft, (eta_i * eta_i) / (eta_t / eta_t));   // mode == Radiance
+    const double p = 1 - F;
+    if (p == 0.0) return spec(0);
+    wi = w;
+    pdf = p;
+    type = BXDF_SPECULAR | BXDF_TRANSMISSION;
+    return sdivs(ft, gomath::abs(w.z));
+}
+
 // ------------------------------------------------------------------- lights
 struct LightSample {
     Spec Li;
@@ -1072,7 +1189,7 @@ __device__ __noinline__ Spec path_li(const DevScene& sc, Thread& t, Ray ray, int
                                      bool fidelity) {
     Spec L = spec(0), beta = spec(1);
     int32_t bounces = 0;
-    const double eta_scale = 1.0;
+    double eta_scale = 1.0;
     for (;;) {
         bounces++;
         t.bounce = bounces;
@@ -1089,8 +1206,9 @@ __device__ __noinline__ Spec path_li(const DevScene& sc, Thread& t, Ray ray, int
         if (!bvh_traverse<false>(sc, ray, &isect, t.stack, t.panic)) break;
         if (t.panic) break;
         BSDF b;
-        if (compute_bsdf(sc, isect, b) < 0) { t.panic = -1; break; }
-        if (b.n_bxdfs > 0) {   // NumComponents(BSDFAll &^ BSDFSpecular) > 0
+        BSDFX x;
+        if (compute_bsdf_x(sc, isect, b, x) < 0) { t.panic = -1; break; }
+        if (bsdfx_nonspecular(b, x)) {   // NumComponents(BSDFAll &^ BSDFSpecular) > 0
             Spec ld = uniform_sample_one_light(sc, t, isect, b, sc.dist, fidelity);
             if (t.panic) break;
             L = L + smul(beta, ld);
@@ -1099,10 +1217,16 @@ __device__ __noinline__ Spec path_li(const DevScene& sc, Thread& t, Ray ray, int
         V2 u = get2d(t);
         V3 wi;
         double pdf;
-        Spec f = bsdf_sample_f(b, wo, u, wi, pdf);
+        int flags;
+        Spec f = bsdfx_sample_f(b, x, wo, u, wi, pdf, flags);
         if (is_black(f) || pdf == 0.0) break;
         double wp = absdot(wi, isect.sn) / pdf;
         beta = smul(beta, smuls(f, wp));
+        if ((flags & BXDF_SPECULAR) && (flags & BXDF_TRANSMISSION)) {   // path.go:106-117
+            const double eta = x.eta;
+            if (dot(wo, isect.n) > 0) eta_scale *= eta * eta;
+            else eta_scale *= 1 / (eta * eta);
+        }
         // SpawnRay (interaction.go:68-77)
         ray.o = offset_ray_origin(isect.p, isect.perr, isect.n, wi);
         ray.d = wi;
@@ -1131,7 +1255,8 @@ __device__ __noinline__ Spec direct_li(const DevScene& sc, Thread& t, Ray ray, i
     }
     if (t.panic) return L;
     BSDF b;
-    if (compute_bsdf(sc, si, b) < 0) { t.panic = -1; return L; }
+    BSDFX x;   // Mirror/Glass: F and Pdf are 0 and SpecularReflect/Transmit match no lobe
+    if (compute_bsdf_x(sc, si, b, x) < 0) { t.panic = -1; return L; }
     L = L + spec(0);   // si.Le(si.Wo): no primitive carries an area light
     if (sc.n_lights > 0) {
         if (strategy == PBRT_DL_UNIFORM_SAMPLE_ALL) {

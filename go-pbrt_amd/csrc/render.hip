@@ -1903,6 +1903,7 @@ struct pbrt_gpu_ctx {
     pbrt_distribution_desc* d_dist = nullptr;
     pbrt_scene_desc host_scene;   // counts + film/camera (pointer fields are not kept)
     std::vector<pbrt_light_desc> host_lights;
+    bool non_matte = false;       // a Mirror or Glass material: serial kernel only
     // per-render buffers (grown on demand)
     double* d_films = nullptr;
     size_t films_cap = 0;
@@ -2181,6 +2182,8 @@ int validate_scene(const pbrt_scene_desc* s) {
         if (n.n_prims > 0 && (int64_t)n.offset + n.n_prims > s->n_prims) return PBRT_E_INVALID;
         if (n.n_prims == 0 && (n.offset >= (uint32_t)s->n_nodes || n.axis > 2)) return PBRT_E_INVALID;
     }
+    for (int i = 0; i < s->n_materials; i++)
+        if (s->materials[i].type < PBRT_MAT_MATTE || s->materials[i].type > PBRT_MAT_GLASS) return PBRT_E_UNSUPPORTED;
     if (s->n_meshes < 0 || (s->n_meshes > 0 && !s->meshes)) return PBRT_E_INVALID;
     for (int i = 0; i < s->n_meshes; i++) {
         const pbrt_mesh_desc& m = s->meshes[i];
@@ -2221,6 +2224,9 @@ const PcgJump& pcg_jump_table() {
 bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const RenderParams& rp, ChainLayout& L,
                    ChainLayout& Lci) {
     if (rd->flags & PBRT_FLAG_PANIC_FIDELITY) return false;   // the serial kernel traces the extra rays
+    // Mirror and Glass change a path's draw count per bounce (no light sample on
+    // glass) and its direction rule: the serial kernel renders such scenes
+    if (c->non_matte) return false;
     const bool dl = rd->integrator == PBRT_INTEGRATOR_DIRECT_LIGHTING;
     if (dl) {   // k_dl_*: the camera ray must be per pixel (pFilm stratified; pLens stratified or unused)
         if (rd->n_dims < 1 || (rd->n_dims < 2 && c->host_scene.camera.lens_radius > 0)) return false;
@@ -2546,6 +2552,8 @@ int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
     if (f.filter_radius_x <= 0 || f.filter_radius_y <= 0 || f.filter_radius_x >= (double)rd->tile_size ||
         f.filter_radius_y >= (double)rd->tile_size)
         return set_err(c, PBRT_E_UNSUPPORTED, "filter radius must be in (0, tile_size)");
+    if ((rd->flags & PBRT_FLAG_PANIC_FIDELITY) && c->non_matte)
+        return set_err(c, PBRT_E_UNSUPPORTED, "panic fidelity covers Matte scenes only");
     RenderParams& rp = c->rp;
     std::memset(&rp, 0, sizeof(rp));
     rp.film_min_x = f.crop_min_x;
@@ -2669,6 +2677,8 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
         return PBRT_E_INVALID;
     }
     c->host_scene = *scene;
+    c->non_matte = false;
+    for (int i = 0; i < scene->n_materials; i++) c->non_matte |= scene->materials[i].type != PBRT_MAT_MATTE;
     c->h_node_prims.resize((size_t)scene->n_nodes);
     for (int i = 0; i < scene->n_nodes; i++) c->h_node_prims[i] = scene->nodes[i].n_prims;
     c->host_scene.shapes = nullptr;
@@ -3012,7 +3022,7 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
             break;
         }
         if (st.panic_kind == -1) {
-            rc = set_err(c, PBRT_E_UNSUPPORTED, "material not on the hot path (OrenNayar)");
+            rc = set_err(c, PBRT_E_UNSUPPORTED, "material not on the hot path (OrenNayar, rough Glass)");
             st.panic_kind = 0;
         } else {
             rc = set_err(c, PBRT_E_REF_PANIC, "the Go reference panics on this input");

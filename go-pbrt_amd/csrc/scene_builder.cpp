@@ -395,6 +395,23 @@ void pbrt_make_matte_checkerboard(const double vs[3], const double vt[3], double
     out->ds = ds; out->dt = dt;
     out->sigma = sigma;
 }
+void pbrt_make_mirror(const double kr[3], pbrt_material_desc* out) {   // mirror.go:9-14 (NewMirror: Kr 0.9)
+    std::memset(out, 0, sizeof(*out));
+    out->type = PBRT_MAT_MIRROR;
+    for (int i = 0; i < 3; i++) out->kr[i] = kr[i];
+}
+void pbrt_make_glass(const double kr[3], const double kt[3], double u_roughness, double v_roughness, double eta,
+                     pbrt_material_desc* out) {   // glass.go:15-26 (remapRoughness false)
+    std::memset(out, 0, sizeof(*out));
+    out->type = PBRT_MAT_GLASS;
+    for (int i = 0; i < 3; i++) {
+        out->kr[i] = kr[i];
+        out->kt[i] = kt[i];
+    }
+    out->u_roughness = u_roughness;
+    out->v_roughness = v_roughness;
+    out->eta = eta;
+}
 void pbrt_make_point_light(const pbrt_transform* l2w, const double I[3], pbrt_light_desc* out) {  // point.go:19-30
     std::memset(out, 0, sizeof(*out));
     out->type = PBRT_LIGHT_POINT;

@@ -95,6 +95,10 @@ def lib():
     L.pbrt_make_matte_constant.restype = None
     L.pbrt_make_matte_checkerboard.argtypes = [P(d), P(d), d, d, P(d), P(d), d, P(abi.MaterialDesc)]
     L.pbrt_make_matte_checkerboard.restype = None
+    L.pbrt_make_mirror.argtypes = [P(d), P(abi.MaterialDesc)]
+    L.pbrt_make_mirror.restype = None
+    L.pbrt_make_glass.argtypes = [P(d), P(d), d, d, d, P(abi.MaterialDesc)]
+    L.pbrt_make_glass.restype = None
     L.pbrt_make_point_light.argtypes = [T, P(d), P(abi.LightDesc)]
     L.pbrt_make_point_light.restype = None
     L.pbrt_make_distant_light.argtypes = [T, P(d), P(d), P(abi.LightDesc)]
@@ -237,6 +241,18 @@ class Scene:
     def add_checker(self, vs, vt, ds, dt, tex1, tex2, sigma=0.0):
         m = abi.MaterialDesc()
         lib().pbrt_make_matte_checkerboard(_d3(vs), _d3(vt), ds, dt, _d3(tex1), _d3(tex2), sigma, C.byref(m))
+        return lib().pbrt_sb_add_material(self.h, C.byref(m))
+
+    def add_mirror(self, kr=(0.9, 0.9, 0.9)):
+        """materials.NewMirror (mirror.go:9-14; Kr 0.9 by default)."""
+        m = abi.MaterialDesc()
+        lib().pbrt_make_mirror(_d3(kr), C.byref(m))
+        return lib().pbrt_sb_add_material(self.h, C.byref(m))
+
+    def add_glass(self, kr=(0.5, 0.5, 0.5), kt=(0.5, 0.5, 0.5), u_roughness=0.0, v_roughness=0.0, eta=1.5):
+        """materials.NewGlass (glass.go:15-26); defaults are server.go:80-87's glass."""
+        m = abi.MaterialDesc()
+        lib().pbrt_make_glass(_d3(kr), _d3(kt), u_roughness, v_roughness, eta, C.byref(m))
         return lib().pbrt_sb_add_material(self.h, C.byref(m))
 
     def add_primitive(self, shape, material, prim_to_world=None):

@@ -18,6 +18,7 @@ PBRT_SHAPE_SPHERE = 1
 PBRT_SHAPE_DISK = 2
 PBRT_TEX_CONSTANT = 1
 PBRT_TEX_CHECKERBOARD2D = 2
+PBRT_MAT_MATTE, PBRT_MAT_MIRROR, PBRT_MAT_GLASS = 0, 1, 2
 PBRT_PRIM_GEOMETRIC = 1
 PBRT_PRIM_TRANSFORMED = 2
 PBRT_LIGHT_POINT = 1
@@ -77,7 +78,7 @@ class ShapeDesc(C.Structure):
 class MaterialDesc(C.Structure):
     _fields_ = [
         ("kd_type", C.c_int32),
-        ("pad0", C.c_int32),
+        ("type", C.c_int32),
         ("kd", C.c_double * 3),
         ("vs", C.c_double * 3),
         ("vt", C.c_double * 3),
@@ -86,6 +87,11 @@ class MaterialDesc(C.Structure):
         ("tex1", C.c_double * 3),
         ("tex2", C.c_double * 3),
         ("sigma", C.c_double),
+        ("kr", C.c_double * 3),
+        ("kt", C.c_double * 3),
+        ("eta", C.c_double),
+        ("u_roughness", C.c_double),
+        ("v_roughness", C.c_double),
     ]
 
 

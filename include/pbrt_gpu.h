@@ -77,18 +77,27 @@ typedef struct pbrt_shape_desc {
 
 /* --------------------------------------------------------------- materials */
 enum { PBRT_TEX_CONSTANT = 1, PBRT_TEX_CHECKERBOARD2D = 2 };
+enum { PBRT_MAT_MATTE = 0, PBRT_MAT_MIRROR = 1, PBRT_MAT_GLASS = 2 };
 
-/* pkg/materials/matte.go:8-37 MatteMaterial with Kd either a
+/* type PBRT_MAT_MATTE: pkg/materials/matte.go:8-37 MatteMaterial with Kd either a
  * ConstantSpectrumTexture (pkg/pbrt/texture.go:133-145) or a Checkerboard2D
  * over PlanarMapping2D (pkg/textures/checkerboard.go, texture.go:105-123) whose
- * two sub-textures are constants. sigma is a ConstantFloatTexture. */
+ * two sub-textures are constants. sigma is a ConstantFloatTexture.
+ * type PBRT_MAT_MIRROR: pkg/materials/mirror.go:9-32 (constant Kr; NewMirror uses 0.9).
+ * type PBRT_MAT_GLASS: pkg/materials/glass.go:15-75 with constant Kr, Kt, index
+ * (eta) and roughness textures. Path.Li asks for multiple lobes (path.go:74), so
+ * smooth glass (both roughnesses 0) is one FresnelSpecular lobe; rough glass
+ * (TrowbridgeReitz microfacets) is PBRT_E_UNSUPPORTED. The serial kernel renders
+ * scenes holding a Mirror or Glass material. */
 typedef struct pbrt_material_desc {
     int32_t kd_type;
-    int32_t pad0;
+    int32_t type;                  /* PBRT_MAT_* (0 = Matte)                  */
     double kd[3];
     double vs[3], vt[3], ds, dt;
     double tex1[3], tex2[3];
     double sigma;
+    double kr[3], kt[3];           /* Mirror: Kr; Glass: Kr, Kt               */
+    double eta, u_roughness, v_roughness;   /* Glass                          */
 } pbrt_material_desc;
 
 /* -------------------------------------------------------------- primitives */

@@ -508,11 +508,17 @@ static int prim_material(const pbrt_scene_desc* sc, int prim) {
     return 0;
 }
 
-/* ============================================================ BSDF (Matte) */
+/* ========================================== BSDF (Matte, Mirror, Glass) */
+/* kind of the single BxDF: LambertianReflection (matte.go), SpecularReflection
+ * with FresnelNoOp (mirror.go), or FresnelSpecular (smooth glass with multiple
+ * lobes allowed, glass.go:46-47 -- Path.Li passes allowMultipleLobes true). */
+enum { BXDF_KIND_LAMBERT = 0, BXDF_KIND_SPEC_REFL = 1, BXDF_KIND_FRESNEL_SPEC = 2 };
 typedef struct {
     v3 ns, ng, ss, ts;
-    int n_bxdfs;        /* 0 or 1 (LambertianReflection)                      */
-    spec r;
+    int n_bxdfs;        /* 0 or 1                                             */
+    int kind;           /* BXDF_KIND_*                                        */
+    spec r, t;          /* Lambert/mirror R; glass R and T                    */
+    double eta;         /* NewBSDF(si, eta): 1 for matte/mirror, index for glass */
 } bsdf_t;
 
 #define BXDF_REFLECTION 1
@@ -522,6 +528,10 @@ typedef struct {
 #define BXDF_SPECULAR 16
 #define BXDF_ALL 31
 #define LAMBERT_TYPE (BXDF_REFLECTION | BXDF_DIFFUSE)
+/* reflection.go:538-544: SpecularReflection is typed Reflection|Diffuse (not
+ * Specular), so it counts as a non-specular component and its sampled type is 0 */
+#define SPEC_REFL_TYPE (BXDF_REFLECTION | BXDF_DIFFUSE)
+#define FRESNEL_SPEC_TYPE (BXDF_REFLECTION | BXDF_TRANSMISSION | BXDF_SPECULAR)   /* reflection.go:465-474 */
 
 static double inv_pi(void) { FL(1); return 1.0 / go_Pi; }   /* pkg/math InvPi = 1.0 / Pi */
 static int matches_flags(int t, int flags) { return (t & flags) == t; }
@@ -534,6 +544,33 @@ static int material_bsdf(const pbrt_scene_desc* sc, const si_t* si, bsdf_t* b) {
     b->ss = v_normalized(si->sdpdu);
     b->ts = v_cross(b->ns, b->ss);
     b->n_bxdfs = 0;
+    b->kind = BXDF_KIND_LAMBERT;
+    b->eta = 1.0;
+    if (m->type == PBRT_MAT_MIRROR) {   /* mirror.go:21-32 */
+        spec r = S3(m->kr[0], m->kr[1], m->kr[2]);
+        for (int i = 0; i < 3; i++) r.c[i] = go_clamp(r.c[i], 0, INFINITY);
+        if (!s_is_black(r)) {
+            b->n_bxdfs = 1;
+            b->kind = BXDF_KIND_SPEC_REFL;
+            b->r = r;
+        }
+        return 0;
+    }
+    if (m->type == PBRT_MAT_GLASS) {    /* glass.go:28-75 */
+        spec R = S3(m->kr[0], m->kr[1], m->kr[2]), T = S3(m->kt[0], m->kt[1], m->kt[2]);
+        for (int i = 0; i < 3; i++) {
+            R.c[i] = go_clamp(R.c[i], 0, 1);
+            T.c[i] = go_clamp(T.c[i], 0, 1);
+        }
+        b->eta = m->eta;
+        if (s_is_black(R) && s_is_black(T)) return 0;
+        if (!(m->u_roughness == 0 && m->v_roughness == 0)) return -1;   /* microfacets: unsupported */
+        b->n_bxdfs = 1;
+        b->kind = BXDF_KIND_FRESNEL_SPEC;
+        b->r = R;
+        b->t = T;
+        return 0;
+    }
     spec r;
     if (m->kd_type == PBRT_TEX_CHECKERBOARD2D) {
         double s = m->ds + v_dot(si->p, V3(m->vs[0], m->vs[1], m->vs[2]));
@@ -567,8 +604,10 @@ static spec bsdf_f(const bsdf_t* b, v3 woW, v3 wiW, int flags) {
     int reflect = v_dot(wiW, b->ng) * v_dot(woW, b->ng) > 0;
     FL(1);
     spec f = S3(0, 0, 0);
-    if (b->n_bxdfs && matches_flags(LAMBERT_TYPE, flags) && reflect)
+    if (b->n_bxdfs && b->kind == BXDF_KIND_LAMBERT && matches_flags(LAMBERT_TYPE, flags) && reflect)
         f = s_add(f, s_muls(b->r, inv_pi()));
+    else if (b->n_bxdfs && b->kind != BXDF_KIND_LAMBERT)
+        f = s_add(f, S3(0, 0, 0));   /* reflection.go:486-488, 553-555: F is 0 */
     return f;
 }
 /* reflection.go:343-348 */
@@ -585,7 +624,12 @@ static double bsdf_pdf(const bsdf_t* b, v3 woW, v3 wiW, int flags) {
     if (wo.z == 0) return 0;
     double pdf = 0;
     int matching = 0;
-    if (matches_flags(LAMBERT_TYPE, flags)) { matching++; pdf += lambert_pdf(wo, wi); FL(1); }
+    if (b->kind == BXDF_KIND_LAMBERT) {
+        if (matches_flags(LAMBERT_TYPE, flags)) { matching++; pdf += lambert_pdf(wo, wi); FL(1); }
+    } else {   /* reflection.go:534-536, 572-574: Pdf is 0 */
+        int ty = b->kind == BXDF_KIND_SPEC_REFL ? SPEC_REFL_TYPE : FRESNEL_SPEC_TYPE;
+        if (matches_flags(ty, flags)) { matching++; pdf += 0.0; }
+    }
     if (matching <= 0) return 0;
     FL(1);
     return pdf / (double)matching;
@@ -616,17 +660,79 @@ static v3 cosine_sample_hemisphere(v2 u) {
     FL(5);
     return V3(d.x, d.y, z);
 }
-/* reflection.go:188-253; returns the LOCAL-frame wi (#7) */
-static spec bsdf_sample_f(const bsdf_t* b, v3 woW, v2 u, int t, v3* wi_out, double* pdf_out) {
-    int matching = (b->n_bxdfs && matches_flags(LAMBERT_TYPE, t)) ? 1 : 0;
+/* reflection.go:21-42 FrDielectric */
+static double fr_dielectric(double cos_i, double eta_i, double eta_t) {
+    cos_i = go_clamp(cos_i, -1, 1);
+    if (!(cos_i > 0)) {
+        double tmp = eta_i; eta_i = eta_t; eta_t = tmp;
+        cos_i = gm_abs(cos_i);
+    }
+    double sin_i = sqrt(go_max(0, 1 - cos_i * cos_i));
+    double sin_t = eta_i / eta_t * sin_i;
+    if (sin_t >= 1) return 1;
+    double cos_t = sqrt(go_max(0, 1 - sin_t * sin_t));
+    double rparl = ((eta_t * cos_i) - (eta_i * cos_t)) / ((eta_t * cos_i) + (eta_i * cos_t));
+    double rperp = ((eta_i * cos_i) - (eta_t * cos_t)) / ((eta_i * cos_i) + (eta_t * cos_t));
+    return (rparl * rparl + rperp * rperp) / 2;
+}
+double oracle_fr_dielectric(double cos_i, double eta_i, double eta_t) { return fr_dielectric(cos_i, eta_i, eta_t); }
+/* FresnelSpecular.SampleF (reflection.go:489-524), incl. its (etaT / etaT)
+ * radiance scale; FaceForward (geometry.go:111-116) + Refract (:106-118) */
+static spec fresnel_specular_sample(const bsdf_t* b, v3 wo, v2 u, v3* wi, double* pdf, int* type) {
+    double F = fr_dielectric(wo.z, 1.0, b->eta);
+    if (u.x < F) {
+        *wi = V3(-wo.x, -wo.y, wo.z);
+        *pdf = F;
+        *type = BXDF_SPECULAR | BXDF_REFLECTION;
+        return s_divs(s_muls(b->r, F), gm_abs(wi->z));
+    }
+    double eta_i, eta_t;
+    if (wo.z > 0) { eta_i = 1.0; eta_t = b->eta; } else { eta_i = b->eta; eta_t = 1.0; }
+    v3 n = V3(0, 0, 1);
+    if (v_dot(n, wo) < 0.0) n = v_muls(n, -1);
+    double eta = eta_i / eta_t;
+    double cos_i = v_dot(n, wo);
+    double sin2_i = go_max(0, 1 - cos_i * cos_i);
+    double sin2_t = eta * eta * sin2_i;
+    if (sin2_t >= 1) { *pdf = 0; *type = 0; return S3(0, 0, 0); }
+    double cos_t = sqrt(1 - sin2_t);
+    *wi = v_add(v_muls(wo, -eta), v_muls(n, eta * cos_i - cos_t));
+    spec ft = s_muls(b->t, 1 - F);
+    ft = s_muls(ft, (eta_i * eta_i) / (eta_t / eta_t));   /* mode == Radiance */
+    *pdf = 1 - F;
+    *type = BXDF_SPECULAR | BXDF_TRANSMISSION;
+    return s_divs(ft, gm_abs(wi->z));
+}
+/* reflection.go:188-253; returns the LOCAL-frame wi (#7) and the sampled type */
+static spec bsdf_sample_f_t(const bsdf_t* b, v3 woW, v2 u, int t, v3* wi_out, double* pdf_out, int* type_out) {
+    const int ty = b->kind == BXDF_KIND_LAMBERT ? LAMBERT_TYPE
+                 : b->kind == BXDF_KIND_SPEC_REFL ? SPEC_REFL_TYPE : FRESNEL_SPEC_TYPE;
+    int matching = (b->n_bxdfs && matches_flags(ty, t)) ? 1 : 0;
     *wi_out = V3(0, 0, 0);
     *pdf_out = 0;
+    *type_out = 0;
     if (matching == 0) return S3(0, 0, 0);
     double comp = go_min(floor(u.x * (double)matching), (double)matching - 1);
     v2 ur = {go_min(u.x * (double)matching - comp, GO_ONE_MINUS_EPSILON), u.y};
     FL(4);
     v3 wo = bsdf_w2l(b, woW);
     if (wo.z == 0.0) return S3(0, 0, 0);
+    if (b->kind == BXDF_KIND_SPEC_REFL) {   /* reflection.go:557-562 (FresnelNoOp) */
+        v3 wi = V3(-wo.x, -wo.y, wo.z);
+        spec f = s_divs(s_mul(S3(1, 1, 1), b->r), gm_abs(wi.z));
+        *wi_out = wi;
+        *pdf_out = 1.0;
+        return f;
+    }
+    if (b->kind == BXDF_KIND_FRESNEL_SPEC) {
+        v3 wi; double pdf; int st;
+        spec f = fresnel_specular_sample(b, wo, ur, &wi, &pdf, &st);
+        if (pdf == 0.0) return S3(0, 0, 0);
+        *wi_out = wi;
+        *pdf_out = pdf;
+        *type_out = st;
+        return f;
+    }
     /* reflection.go:305-314 sampleF */
     v3 wi = cosine_sample_hemisphere(ur);
     if (wo.z < 0) { wi.z *= -1; FL(1); }
@@ -636,6 +742,10 @@ static spec bsdf_sample_f(const bsdf_t* b, v3 woW, v2 u, int t, v3* wi_out, doub
     *wi_out = wi;
     *pdf_out = pdf;
     return f;
+}
+static spec bsdf_sample_f(const bsdf_t* b, v3 woW, v2 u, int t, v3* wi_out, double* pdf_out) {
+    int ty;
+    return bsdf_sample_f_t(b, woW, u, t, wi_out, pdf_out, &ty);
 }
 
 /* ================================================================== lights */
@@ -897,7 +1007,7 @@ static spec path_li(orc_ctx* oc, sampler_t* smp, ray_t ray) {
         if (!orc_bvh_intersect(oc, &ray, &isect)) break;
         bsdf_t b;
         if (material_bsdf(sc, &isect, &b) < 0) { oc->unsupported = 1; break; }
-        if (b.n_bxdfs > 0) {   /* NumComponents(BSDFAll &^ BSDFSpecular) > 0 */
+        if (b.n_bxdfs > 0 && b.kind != BXDF_KIND_FRESNEL_SPEC) {   /* NumComponents(BSDFAll &^ BSDFSpecular) > 0 */
 #ifdef ORACLE_COUNT_FLOPS
             const uint64_t f0 = orc_flops;
 #endif
@@ -909,14 +1019,19 @@ static spec path_li(orc_ctx* oc, sampler_t* smp, ray_t ray) {
         }
         v3 wo = ray.d;                           /* path.go:91 (#8)           */
         v2 u = sampler_get2d(smp);
-        v3 wi; double pdf;
-        spec f = bsdf_sample_f(&b, wo, u, BXDF_ALL, &wi, &pdf);
+        v3 wi; double pdf; int flags;
+        spec f = bsdf_sample_f_t(&b, wo, u, BXDF_ALL, &wi, &pdf, &flags);
         if (s_is_black(f) || pdf == 0.0) break;
         double wabs = v_absdot(wi, isect.sn);
         double wp = wabs / pdf;
         FL(1);
         spec fm = s_muls(f, wp);
         beta = s_mul(beta, fm);
+        if ((flags & BXDF_SPECULAR) && (flags & BXDF_TRANSMISSION)) {   /* path.go:106-117 */
+            double eta = b.eta;
+            if (v_dot(wo, isect.n) > 0) eta_scale *= eta * eta;
+            else eta_scale *= 1 / (eta * eta);
+        }
         /* interaction.go:68-77 SpawnRay */
         ray.o = offset_ray_origin(isect.p, isect.perr, isect.n, wi);
         ray.d = wi;

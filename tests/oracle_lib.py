@@ -71,6 +71,7 @@ def _bind(L):
             f = getattr(L, "oracle_go_" + name)
             f.argtypes, f.restype = [d, d], d
         L.oracle_go_f2i.argtypes, L.oracle_go_f2i.restype = [d], C.c_int64
+        L.oracle_fr_dielectric.argtypes, L.oracle_fr_dielectric.restype = [d, d, d], d
         for name in ("oracle_efloat_add", "oracle_efloat_mul", "oracle_efloat_div"):
             getattr(L, name).argtypes = [d, d, d, d, P(d)]
             getattr(L, name).restype = C.c_int

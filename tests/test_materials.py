@@ -1,0 +1,169 @@
+"""Mirror and smooth Glass: pkg/materials/mirror.go:9-32,
+pkg/materials/glass.go:15-75 and their BxDFs in pkg/pbrt/reflection.go
+(FrDielectric :21-42, Refract :106-118, FresnelSpecular :465-536,
+SpecularReflection :538-574), driven by Path.Li's specular bookkeeping
+(pkg/integrator/path.go:82-117).
+
+Quirks restated (and therefore tested here):
+- SpecularReflection is typed Reflection|Diffuse, so a Mirror still samples a
+  light (its F and Pdf are 0) and its sampled type is 0 (no specular bounce);
+- FresnelSpecular's radiance scale is etaI^2 / (etaT / etaT) = etaI^2;
+- smooth glass is a single specular lobe: no light sample, so its paths consume
+  fewer draws per bounce;
+- DirectLighting's SpecularReflect/Transmit match neither lobe, so both
+  materials render there exactly like a black Matte.
+
+No reference test covers these materials and there is no Go toolchain here:
+device-vs-oracle parity is bit-exact but "parity unpinned" against Go itself.
+The oracle's FrDielectric is pinned by closed forms below.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import pbrtgpu as G
+from pbrtgpu import abi
+
+
+def material_scene(kind="both", w=32, h=24, rough=0.0):
+    """A floor, a glass sphere, a mirror sphere and a matte sphere, lit by a
+    point light and an area-light sphere. kind: "both" | "matte" (the two
+    special spheres matte) | "black" (the two special spheres black matte)."""
+    s = G.Scene()
+    chk = s.add_checker((0.2, 0, 0), (0, 0, 0.2), 0, 0, (1, 1, 1), (0.18, 0.18, 0.18))
+    floor = s.add_disk(G.rotate(0, 90), 0.0, 100.0)
+    s.add_primitive(floor, chk)
+    red = s.add_matte((0.6, 0.1, 0.1))
+    if kind == "both":
+        glass = s.add_glass(u_roughness=rough, v_roughness=rough)   # server.go:80-87's glass
+        mirror = s.add_mirror()
+    elif kind == "matte":
+        glass = mirror = s.add_matte((0.5, 0.5, 0.5))
+    else:
+        glass = mirror = s.add_matte((0.0, 0.0, 0.0))
+    for (x, z, m) in ((-2.5, 0.0, glass), (2.5, 0.0, mirror), (0.0, -4.0, red)):
+        sph = s.add_sphere(G.translate(0, 0, 0), 2.0)
+        s.add_primitive(sph, m, G.translate(x, 2.0, z))
+    light = s.add_sphere(G.translate(0, 9, 2), 0.75)
+    s.add_area_light((6, 6, 6), light)
+    s.add_point_light(G.translate(-6, 10, 8), (60, 60, 60))
+    s.set_film(w, h)
+    s.set_camera(G.look_at((0, 7, 12), (0, 1.5, 0), (0, 1, 0)), fov=55)
+    return s.build(max_prims_in_node=1)
+
+
+def bits(a):
+    return a.view(np.uint64)
+
+
+# ------------------------------------------------------------------ CPU tests
+def test_fr_dielectric_closed_forms():
+    """FrDielectric at normal incidence is ((eta-1)/(eta+1))^2, total internal
+    reflection returns 1 (reflection.go:21-42)."""
+    L = O.lib()
+    f = L.oracle_fr_dielectric
+    assert f(1.0, 1.0, 1.5) == pytest.approx(0.04, rel=1e-15)
+    assert f(-1.0, 1.0, 1.5) == pytest.approx(0.04, rel=1e-15)   # leaving: the indices swap
+    assert f(-0.2, 1.0, 1.5) == 1.0                              # sin_t = 1.5 * 0.98 > 1
+    assert 0.04 < f(0.3, 1.0, 1.5) < 1.0
+
+
+def test_oracle_materials_render_deterministically():
+    sc = material_scene()
+    rd = abi.render_desc(3, 3, max_depth=6)
+    rc, f1, st = O.render(sc.desc, rd, threads=1)
+    assert rc == 0 and np.isfinite(f1).all() and f1.max() > 0
+    rc, f8, _ = O.render(sc.desc, rd, threads=8)
+    assert np.array_equal(bits(f1), bits(f8))
+    scm = material_scene("matte")   # the builder owns the desc: keep it alive
+    _, fm, _ = O.render(scm.desc, rd, threads=8)
+    assert not np.array_equal(f1, fm)   # the glass and mirror spheres are in view
+
+
+def test_oracle_direct_lighting_sees_glass_and_mirror_as_black_matte():
+    for strategy in (abi.PBRT_DL_UNIFORM_SAMPLE_ALL, abi.PBRT_DL_UNIFORM_SAMPLE_ONE):
+        rd = abi.render_desc(2, 2, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING, dl_strategy=strategy)
+        sa, sb = material_scene(), material_scene("black")
+        rc, fa, _ = O.render(sa.desc, rd, threads=8)
+        rc2, fb, _ = O.render(sb.desc, rd, threads=8)
+        assert rc == rc2 == 0 and np.array_equal(bits(fa), bits(fb))
+
+
+def test_oracle_rough_glass_is_unsupported():
+    sc = material_scene(rough=0.1)
+    rc, _, _ = O.render(sc.desc, abi.render_desc(2, 2), threads=4)
+    assert rc == abi.PBRT_E_UNSUPPORTED
+
+
+def test_material_desc_layout():
+    m = abi.MaterialDesc()
+    G.lib().pbrt_make_glass((G.C.c_double * 3)(0.5, 0.4, 0.3), (G.C.c_double * 3)(0.2, 0.1, 0.0), 0.0, 0.0, 1.5,
+                            G.C.byref(m))
+    assert m.type == abi.PBRT_MAT_GLASS and list(m.kr) == [0.5, 0.4, 0.3] and list(m.kt) == [0.2, 0.1, 0.0]
+    assert m.eta == 1.5 and m.u_roughness == 0 and m.v_roughness == 0
+    G.lib().pbrt_make_mirror((G.C.c_double * 3)(0.9, 0.9, 0.9), G.C.byref(m))
+    assert m.type == abi.PBRT_MAT_MIRROR and list(m.kr) == [0.9, 0.9, 0.9] and m.eta == 0
+
+
+# ------------------------------------------------------------------ GPU tests
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [abi.PBRT_MODE_EXACT, abi.PBRT_MODE_THROUGHPUT])
+@pytest.mark.parametrize("spp,nd,depth", [(3, 4, 6), (2, 2, 8), (4, 0, 5)])
+def test_device_materials_bitexact_vs_oracle(mode, spp, nd, depth):
+    sc = material_scene()
+    rd = abi.render_desc(spp, spp, n_dims=nd, max_depth=depth, mode=mode)
+    rc, of, _ = O.render(sc.desc, rd, threads=8)
+    assert rc == 0
+    with G.Renderer(sc) as r:
+        film, st = r.render(rd)
+    assert st.kernel == abi.PBRT_KERNEL_SERIAL
+    assert np.array_equal(bits(film), bits(of))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strategy", [abi.PBRT_DL_UNIFORM_SAMPLE_ALL, abi.PBRT_DL_UNIFORM_SAMPLE_ONE])
+def test_device_materials_direct_lighting_vs_oracle(strategy):
+    sc = material_scene()
+    rd = abi.render_desc(3, 3, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING, dl_strategy=strategy)
+    rc, of, _ = O.render(sc.desc, rd, threads=8)
+    assert rc == 0
+    with G.Renderer(sc) as r:
+        film, st = r.render(rd)
+    assert np.array_equal(bits(film), bits(of))
+
+
+@pytest.mark.gpu
+def test_device_materials_power_strategy_and_rr():
+    sc = material_scene(w=40, h=40)
+    rd = abi.render_desc(3, 3, max_depth=12, rr_threshold=0.5, light_strategy=abi.PBRT_LIGHT_STRATEGY_POWER)
+    rc, of, _ = O.render(sc.desc, rd, threads=8)
+    assert rc == 0
+    with G.Renderer(sc) as r:
+        film, _ = r.render(rd)
+    assert np.array_equal(bits(film), bits(of))
+
+
+@pytest.mark.gpu
+def test_device_rough_glass_and_fidelity_are_unsupported():
+    sr = material_scene(rough=0.1)
+    with G.Renderer(sr) as r:
+        with pytest.raises(G.PbrtError) as ei:
+            r.render(abi.render_desc(2, 2))
+    assert ei.value.code == abi.PBRT_E_UNSUPPORTED
+    sc = material_scene()
+    with G.Renderer(sc) as r:
+        with pytest.raises(G.PbrtError) as ei:
+            r.render(abi.render_desc(2, 2, flags=abi.PBRT_FLAG_PANIC_FIDELITY))
+    assert ei.value.code == abi.PBRT_E_UNSUPPORTED
+
+
+@pytest.mark.gpu
+def test_device_matte_scene_keeps_the_wave_kernels():
+    """A scene without Mirror/Glass still takes the wave pipeline."""
+    sc = material_scene("matte")
+    with G.Renderer(sc) as r:
+        film, st = r.render(abi.render_desc(3, 3, max_depth=6))
+    assert st.kernel != abi.PBRT_KERNEL_SERIAL
+    scm = material_scene("matte")
+    _, of, _ = O.render(scm.desc, abi.render_desc(3, 3, max_depth=6), threads=8)
+    assert np.array_equal(bits(film), bits(of))
