@@ -856,25 +856,28 @@ __device__ inline Spec bsdf_sample_f(const BSDF& b, V3 woW, V2 u, V3& wi, double
 // 572-574), so light sampling sees it exactly as a BSDF without components: the
 // shared estimate_direct/bsdf_f/bsdf_pdf run on `b` with n_bxdfs = 0. Only
 // sampling (and the Path.Li bookkeeping) needs the kind.
-constexpr int BXDF_TRANSMISSION = 2;
-enum { BXDF_KIND_LAMBERT = 0, BXDF_KIND_SPEC_REFL = 1, BXDF_KIND_FRESNEL_SPEC = 2 };
+constexpr int BXDF_TRANSMISSION = 2, BXDF_GLOSSY = 8;
+constexpr int MF_REFL_TYPE = BXDF_REFLECTION | BXDF_GLOSSY, MF_TRANS_TYPE = BXDF_TRANSMISSION | BXDF_GLOSSY;
+enum { BXDF_KIND_LAMBERT = 0, BXDF_KIND_SPEC_REFL = 1, BXDF_KIND_FRESNEL_SPEC = 2, BXDF_KIND_MICROFACET = 3 };
 struct BSDFX {
     int kind;       // BXDF_KIND_*; LAMBERT: `b` is the whole BSDF
-    int n;          // 0 or 1 BxDFs of that kind
+    int n;          // number of BxDFs of that kind (MICROFACET: mf_r + mf_t)
+    int mf_r, mf_t; // rough glass: MicrofacetReflection, MicrofacetTransmission
     Spec r, t;
     double eta;     // NewBSDF(si, eta)
+    double ax, ay;  // TrowbridgeReitz alphas (remapRoughness false)
 };
 // NumComponents(BSDFAll &^ BSDFSpecular) > 0: SpecularReflection is typed
 // Reflection|Diffuse (reflection.go:538-544), FresnelSpecular is specular
 __device__ __forceinline__ bool bsdfx_nonspecular(const BSDF& b, const BSDFX& x) {
-    return x.kind == BXDF_KIND_LAMBERT ? b.n_bxdfs > 0 : (x.kind == BXDF_KIND_SPEC_REFL && x.n > 0);
+    return x.kind == BXDF_KIND_LAMBERT ? b.n_bxdfs > 0 : (x.kind != BXDF_KIND_FRESNEL_SPEC && x.n > 0);
 }
 __device__ inline int compute_bsdf_x(const DevScene& sc, const SI& si, BSDF& b, BSDFX& x) {
     const pbrt_material_desc& m =
         sc.materials[si.prim < sc.n_prims ? sc.prims[si.prim].material
                                           : sc.mesh.mesh_mat[tri_mesh(sc, si.prim - sc.n_prims)]];
     x.kind = BXDF_KIND_LAMBERT;
-    x.n = 0;
+    x.n = x.mf_r = x.mf_t = 0;
     x.eta = 1.0;
     if (m.type == PBRT_MAT_MATTE) return compute_bsdf(sc, si, b);
     b.ns = si.sn;
@@ -900,7 +903,15 @@ __device__ inline int compute_bsdf_x(const DevScene& sc, const SI& si, BSDF& b, 
     x.r = R;
     x.t = T;
     if (is_black(R) && is_black(T)) return 0;
-    if (!(m.u_roughness == 0 && m.v_roughness == 0)) return -1;   // microfacets: unsupported
+    if (!(m.u_roughness == 0 && m.v_roughness == 0)) {   // glass.go:49-73
+        x.kind = BXDF_KIND_MICROFACET;
+        x.ax = m.u_roughness;
+        x.ay = m.v_roughness;
+        x.mf_r = is_black(R) ? 0 : 1;
+        x.mf_t = is_black(T) ? 0 : 1;
+        x.n = x.mf_r + x.mf_t;
+        return 0;
+    }
     x.n = 1;
     return 0;
 }
@@ -921,8 +932,103 @@ __device__ inline double fr_dielectric(double cos_i, double eta_i, double eta_t)
     const double rperp = ((eta_i * cos_i) - (eta_t * cos_t)) / ((eta_i * cos_i) + (eta_t * cos_t));
     return (rparl * rparl + rperp * rperp) / 2;
 }
+// TrowbridgeReitz (microfacet.go:36-84, 117-124; sampleVisibleArea true) and
+// the trig helpers (reflection.go:48-100); D's e keeps the reference's
+// alphaX*alphaY under Cos2Phi
+__device__ inline double cos2_theta(V3 w) { return w.z * w.z; }
+__device__ inline double sin2_theta(V3 w) { return gomath::max(0.0, 1 - cos2_theta(w)); }
+__device__ inline double sin_theta(V3 w) { return gomath::sqrt(sin2_theta(w)); }
+__device__ inline double cos_phi(V3 w) {
+    const double st = sin_theta(w);
+    return st == 0 ? 1 : gomath::clamp(w.x / st, -1, 1);
+}
+__device__ inline double sin_phi(V3 w) {
+    const double st = sin_theta(w);
+    return st == 0 ? 0 : gomath::clamp(w.y / st, -1, 1);
+}
+__device__ inline double tr_d(const BSDFX& x, V3 wh) {
+    const double t2 = sin2_theta(wh) / cos2_theta(wh);
+    if (gomath::is_inf(t2)) return 0;
+    const double c4 = cos2_theta(wh) * cos2_theta(wh);
+    const double cp = cos_phi(wh), sp = sin_phi(wh);
+    const double e = (cp * cp / (x.ax * x.ay) + sp * sp / (x.ay * x.ay)) * t2;
+    return 1 / (gomath::kPi * x.ax * x.ay * c4 * (1 + e) * (1 + e));
+}
+__device__ inline double tr_lambda(const BSDFX& x, V3 w) {
+    const double at = gomath::abs(sin_theta(w) / w.z);
+    if (gomath::is_inf(at)) return 0;
+    const double cp = cos_phi(w), sp = sin_phi(w);
+    const double alpha = gomath::sqrt(cp * cp * x.ax * x.ax + sp * sp * x.ay * x.ay);
+    const double a2t2 = (alpha * at) * (alpha * at);
+    return (-1 + gomath::sqrt(1.0 + a2t2)) / 2;
+}
+__device__ inline double tr_g(const BSDFX& x, V3 wo, V3 wi) { return 1 / (1 + tr_lambda(x, wo) + tr_lambda(x, wi)); }
+__device__ inline double tr_pdf(const BSDFX& x, V3 wo, V3 wh) {   // microfacet.go:26-32
+    return tr_d(x, wh) * (1 / (1 + tr_lambda(x, wo))) * absdot(wo, wh) / gomath::abs(wo.z);
+}
+// MicrofacetReflection.F / .Pdf (reflection.go:690-704, 730-736), FresnelDielectric(1, eta)
+__device__ inline Spec mf_refl_f(const BSDFX& x, V3 wo, V3 wi) {
+    const double c0 = gomath::abs(wo.z), c1 = gomath::abs(wi.z);
+    V3 wh = wi + wo;
+    if (c1 == 0 || c0 == 0) return spec(0);
+    if (wh.x == 0 && wh.y == 0 && wh.z == 0) return spec(0);
+    wh = normalized(wh);
+    const double F = fr_dielectric(dot(wi, wh), 1.0, x.eta);
+    return smuls(smul(x.r, spec(F)), tr_d(x, wh) * tr_g(x, wo, wi) / (4 * c1 * c0));
+}
+__device__ inline double mf_refl_pdf(const BSDFX& x, V3 wo, V3 wi) {
+    if (!(wo.z * wi.z > 0)) return 0;
+    const V3 wh = normalized(wo + wi);
+    return tr_pdf(x, wo, wh) / (4 * dot(wo, wh));
+}
+// MicrofacetTransmission.F / .Pdf (reflection.go:758-790, 820-835): F is 0 unless
+// wo and wi share a hemisphere (the reference's inverted test), wh is not
+// normalized, and the mode field is left at its zero value (not Radiance), so
+// factor stays 1
+__device__ inline Spec mf_trans_f(const BSDFX& x, V3 wo, V3 wi) {
+    if (!(wo.z * wi.z > 0)) return spec(0);
+    const double co = wo.z, ci = wi.z;
+    if (ci == 0 || co == 0) return spec(0);
+    const double eta = wo.z > 0 ? 1.0 / x.eta : x.eta / 1.0;
+    V3 wh = wo + muls(wi, eta);
+    if (wh.z < 0) wh = muls(wh, -1);
+    const double F = fr_dielectric(dot(wo, wh), 1.0, x.eta);
+    const double sd = dot(wo, wh) * eta * dot(wi, wh);
+    const double factor = 1.0;
+    return smuls(smul(spec(1 - F), x.t), gomath::abs(tr_d(x, wh) * tr_g(x, wo, wi) * eta * eta * absdot(wi, wh) *
+                                                     absdot(wo, wh) * factor * factor / (ci * co * sd * sd)));
+}
+__device__ inline double mf_trans_pdf(const BSDFX& x, V3 wo, V3 wi) {
+    if (wo.z * wi.z > 0) return 0;
+    const double eta = wo.z > 0 ? 1.0 / x.eta : x.eta / 1.0;
+    const V3 wh = wo + muls(wi, eta);
+    const double sd = dot(wo, wh) + eta * dot(wi, wh);
+    const double dwh = gomath::abs((eta * eta * dot(wi, wh)) / (sd * sd));
+    return tr_pdf(x, wo, wh) * dwh;
+}
+// BSDF.F / BSDF.Pdf (reflection.go:169-186, 255-278) of a rough glass, flags
+// BSDFAll &^ BSDFSpecular (both microfacet lobes match)
+__device__ inline Spec mf_bsdf_f(const BSDF& b, const BSDFX& x, V3 woW, V3 wiW) {
+    const V3 wi = w2l(b, wiW), wo = w2l(b, woW);
+    if (wo.z == 0.0) return spec(0);
+    const bool reflect = dot(wiW, b.ng) * dot(woW, b.ng) > 0;
+    Spec f = spec(0);
+    if (x.mf_r && reflect) f = f + mf_refl_f(x, wo, wi);
+    if (x.mf_t && !reflect) f = f + mf_trans_f(x, wo, wi);
+    return f;
+}
+__device__ inline double mf_bsdf_pdf(const BSDF& b, const BSDFX& x, V3 woW, V3 wiW) {
+    if (x.n == 0) return 0;
+    const V3 wo = w2l(b, woW), wi = w2l(b, wiW);
+    if (wo.z == 0) return 0;
+    double pdf = 0;
+    if (x.mf_r) pdf += mf_refl_pdf(x, wo, wi);
+    if (x.mf_t) pdf += mf_trans_pdf(x, wo, wi);
+    return pdf / (double)x.n;
+}
 // BSDF.SampleF (reflection.go:188-253) over any BSDFX, flags BSDFAll (Path.Li),
-// returning the LOCAL-frame wi (#7) and the sampled type
+// returning the LOCAL-frame wi (#7) and the sampled type; type -1: the
+// reference panics (rough glass: SampleWH's nil wh reaches Reflect/Refract)
 __device__ inline Spec bsdfx_sample_f(const BSDF& b, const BSDFX& x, V3 woW, V2 u, V3& wi, double& pdf, int& type) {
     type = 0;
     if (x.kind == BXDF_KIND_LAMBERT) return bsdf_sample_f(b, woW, u, wi, pdf);   // sampleF's type is 0
@@ -933,6 +1039,10 @@ __device__ inline Spec bsdfx_sample_f(const BSDF& b, const BSDFX& x, V3 woW, V2 
     const V2 ur{gomath::min(u.x * 1.0 - comp, gomath::kOneMinusEpsilon), u.y};
     const V3 wo = w2l(b, woW);
     if (wo.z == 0.0) return spec(0);
+    if (x.kind == BXDF_KIND_MICROFACET) {
+        type = -1;
+        return spec(0);
+    }
     if (x.kind == BXDF_KIND_SPEC_REFL) {   // SpecularReflection.SampleF, FresnelNoOp (reflection.go:557-562)
         wi = V3{-wo.x, -wo.y, wo.z};
         pdf = 1.0;
@@ -1101,6 +1211,42 @@ __device__ inline Spec estimate_direct(const DevScene& sc, uint16_t* stack, int&
     return ld_vis;
 }
 
+// EstimateDirect for the serial kernel's BSDFX: rough glass evaluates its
+// microfacet F and Pdf, and for an area light the BSDF-sampled half's
+// BSDF.SampleF panics (integrator.go:134-139 always runs it); every other BSDF
+// is the shared estimate_direct.
+__device__ inline Spec estimate_direct_x(const DevScene& sc, uint16_t* stack, int& panic, const SI& si, const BSDF& b,
+                                         const BSDFX& x, int li, V2 u_light) {
+    if (x.kind != BXDF_KIND_MICROFACET) return estimate_direct(sc, stack, panic, si, b, li, u_light);
+    const pbrt_light_desc& L = sc.lights[li];
+    const bool is_delta = L.type != PBRT_LIGHT_DIFFUSE_AREA;
+    LightSample ls;
+    sample_li(sc, L, si, u_light, ls);
+    Spec Ld = spec(0);
+    if (ls.pdf > 0 && !is_black(ls.Li)) {
+        const Spec f = smuls(mf_bsdf_f(b, x, si.wo, ls.wi), absdot(ls.wi, si.sn));
+        const double scat_pdf = mf_bsdf_pdf(b, x, si.wo, ls.wi);
+        if (!is_black(f)) {
+            const V3 origin = offset_ray_origin(si.p, si.perr, si.n, ls.tp - si.p);
+            const V3 target = offset_ray_origin(ls.tp, ls.tperr, ls.tn, origin - ls.tp);
+            Ray sr{si.p, target - origin, 1 - 0.0001, si.time};
+            const bool occluded = bvh_traverse<true>(sc, sr, nullptr, stack, panic);
+            if (panic) return spec(0);
+            if (!occluded) {
+                if (is_delta) {
+                    Ld = Ld + sdivs(smul(f, ls.Li), ls.pdf);
+                } else {
+                    const double fp = 1.0 * ls.pdf, gp = 1.0 * scat_pdf;
+                    const double w = (fp * fp) / (fp * fp + gp * gp);
+                    Ld = Ld + sdivs(smuls(smul(f, ls.Li), w), ls.pdf);
+                }
+            }
+        }
+    }
+    if (!is_delta && x.n > 0 && w2l(b, si.wo).z != 0) panic = PBRT_PANIC_NIL_DEREF;
+    return Ld;
+}
+
 // Sphere.PdfWi (sphere.go:350-363): the cone pdf from outside the sphere;
 // from inside, the generic Shape PdfWi (shape.go:29-47): the spawned ray's
 // Sphere.Intersect (EFloat: can panic), 0 on a miss or an infinite pdf.
@@ -1158,7 +1304,8 @@ __device__ inline int sample_discrete(const pbrt_distribution_desc& d, double u,
 
 // UniformSampleOneLight (integrator.go:48-77): no /lightPdf, panic if > 10 (#10)
 __device__ inline Spec uniform_sample_one_light(const DevScene& sc, Thread& t, const SI& si, const BSDF& b,
-                                                const pbrt_distribution_desc* dist, bool fidelity = false) {
+                                                const BSDFX& x, const pbrt_distribution_desc* dist,
+                                                bool fidelity = false) {
     const int n = sc.n_lights;
     if (n == 0) return spec(0);
     int ln;
@@ -1172,7 +1319,7 @@ __device__ inline Spec uniform_sample_one_light(const DevScene& sc, Thread& t, c
     V2 ul = get2d(t);
     const V2 us = get2d(t);   // uScattering: only the MIS half reads it
     t.shadow_rays++;
-    Spec s = estimate_direct(sc, t.stack, t.panic, si, b, ln, ul);
+    Spec s = estimate_direct_x(sc, t.stack, t.panic, si, b, x, ln, ul);
     if (fidelity && !t.panic) estimate_direct_mis_ray(sc, t.stack, t.panic, si, b, ln, us);
     if (!t.panic && max_component(s) > 10) t.panic = PBRT_PANIC_LD_GT_10;
     return s;
@@ -1209,7 +1356,7 @@ __device__ __noinline__ Spec path_li(const DevScene& sc, Thread& t, Ray ray, int
         BSDFX x;
         if (compute_bsdf_x(sc, isect, b, x) < 0) { t.panic = -1; break; }
         if (bsdfx_nonspecular(b, x)) {   // NumComponents(BSDFAll &^ BSDFSpecular) > 0
-            Spec ld = uniform_sample_one_light(sc, t, isect, b, sc.dist, fidelity);
+            Spec ld = uniform_sample_one_light(sc, t, isect, b, x, sc.dist, fidelity);
             if (t.panic) break;
             L = L + smul(beta, ld);
         }
@@ -1219,6 +1366,7 @@ __device__ __noinline__ Spec path_li(const DevScene& sc, Thread& t, Ray ray, int
         double pdf;
         int flags;
         Spec f = bsdfx_sample_f(b, x, wo, u, wi, pdf, flags);
+        if (flags == -1) { t.panic = PBRT_PANIC_NIL_DEREF; break; }
         if (is_black(f) || pdf == 0.0) break;
         double wp = absdot(wi, isect.sn) / pdf;
         beta = smul(beta, smuls(f, wp));
@@ -1266,13 +1414,13 @@ __device__ __noinline__ Spec direct_li(const DevScene& sc, Thread& t, Ray ray, i
                 V2 ul = get2d(t);
                 const V2 us = get2d(t);
                 t.shadow_rays++;
-                acc = acc + estimate_direct(sc, t.stack, t.panic, si, b, j, ul);
+                acc = acc + estimate_direct_x(sc, t.stack, t.panic, si, b, x, j, ul);
                 if (fidelity && !t.panic) estimate_direct_mis_ray(sc, t.stack, t.panic, si, b, j, us);
                 if (t.panic) return L;
             }
             L = L + acc;
         } else {
-            L = L + uniform_sample_one_light(sc, t, si, b, nullptr, fidelity);
+            L = L + uniform_sample_one_light(sc, t, si, b, x, nullptr, fidelity);
         }
     }
     if (0 + 1 < max_depth) {

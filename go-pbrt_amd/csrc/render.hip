@@ -3022,7 +3022,7 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
             break;
         }
         if (st.panic_kind == -1) {
-            rc = set_err(c, PBRT_E_UNSUPPORTED, "material not on the hot path (OrenNayar, rough Glass)");
+            rc = set_err(c, PBRT_E_UNSUPPORTED, "material not on the hot path (OrenNayar)");
             st.panic_kind = 0;
         } else {
             rc = set_err(c, PBRT_E_REF_PANIC, "the Go reference panics on this input");

@@ -45,6 +45,7 @@ PBRT_PANIC_NONE = 0
 PBRT_PANIC_LD_GT_10 = 1
 PBRT_PANIC_EFLOAT = 2
 PBRT_PANIC_BVH_STACK = 3
+PBRT_PANIC_NIL_DEREF = 4
 
 PBRT_MAX_DIST = 64
 

@@ -51,7 +51,11 @@ enum {
     PBRT_PANIC_NONE = 0,
     PBRT_PANIC_LD_GT_10 = 1,     /* integrator.go:73-75                      */
     PBRT_PANIC_EFLOAT = 2,       /* efloat.go:102-111                        */
-    PBRT_PANIC_BVH_STACK = 3     /* bvh.go:670 fixed [64] stack overflow     */
+    PBRT_PANIC_BVH_STACK = 3,    /* bvh.go:670 fixed [64] stack overflow     */
+    PBRT_PANIC_NIL_DEREF = 4     /* rough Glass: TrowbridgeReitz.SampleWH returns nil
+                                    (its wh is shadowed, microfacet.go:79-115), so a
+                                    microfacet BxDF's SampleF dereferences nil in
+                                    Reflect/Refract (reflection.go:102-118, 706-811) */
 };
 
 /* --------------------------------------------------------------- transform */
@@ -86,9 +90,11 @@ enum { PBRT_MAT_MATTE = 0, PBRT_MAT_MIRROR = 1, PBRT_MAT_GLASS = 2 };
  * type PBRT_MAT_MIRROR: pkg/materials/mirror.go:9-32 (constant Kr; NewMirror uses 0.9).
  * type PBRT_MAT_GLASS: pkg/materials/glass.go:15-75 with constant Kr, Kt, index
  * (eta) and roughness textures. Path.Li asks for multiple lobes (path.go:74), so
- * smooth glass (both roughnesses 0) is one FresnelSpecular lobe; rough glass
- * (TrowbridgeReitz microfacets) is PBRT_E_UNSUPPORTED. The serial kernel renders
- * scenes holding a Mirror or Glass material. */
+ * smooth glass (both roughnesses 0) is one FresnelSpecular lobe; rough glass is
+ * MicrofacetReflection + MicrofacetTransmission over TrowbridgeReitz(u, v)
+ * (microfacet.go, reflection.go:670-835), whose sampling panics in the reference
+ * (PBRT_PANIC_NIL_DEREF). The serial kernel renders scenes holding a Mirror or
+ * Glass material. */
 typedef struct pbrt_material_desc {
     int32_t kd_type;
     int32_t type;                  /* PBRT_MAT_* (0 = Matte)                  */

@@ -63,8 +63,7 @@ void pbrt_make_matte_checkerboard(const double vs[3], const double vt[3], double
                                   pbrt_material_desc* out);
 /* pkg/materials/mirror.go:9-32 (NewMirror's Kr is 0.9) */
 void pbrt_make_mirror(const double kr[3], pbrt_material_desc* out);
-/* pkg/materials/glass.go:15-75 with constant textures; rough glass renders as
- * PBRT_E_UNSUPPORTED (see pbrt_material_desc) */
+/* pkg/materials/glass.go:15-75 with constant textures (see pbrt_material_desc) */
 void pbrt_make_glass(const double kr[3], const double kt[3], double u_roughness, double v_roughness,
                      double eta, pbrt_material_desc* out);
 void pbrt_make_point_light(const pbrt_transform* l2w, const double I[3], pbrt_light_desc* out);

@@ -512,11 +512,13 @@ static int prim_material(const pbrt_scene_desc* sc, int prim) {
 /* kind of the single BxDF: LambertianReflection (matte.go), SpecularReflection
  * with FresnelNoOp (mirror.go), or FresnelSpecular (smooth glass with multiple
  * lobes allowed, glass.go:46-47 -- Path.Li passes allowMultipleLobes true). */
-enum { BXDF_KIND_LAMBERT = 0, BXDF_KIND_SPEC_REFL = 1, BXDF_KIND_FRESNEL_SPEC = 2 };
+enum { BXDF_KIND_LAMBERT = 0, BXDF_KIND_SPEC_REFL = 1, BXDF_KIND_FRESNEL_SPEC = 2, BXDF_KIND_MICROFACET = 3 };
 typedef struct {
     v3 ns, ng, ss, ts;
-    int n_bxdfs;        /* 0 or 1                                             */
+    int n_bxdfs;        /* 0 or 1; 0-2 for MICROFACET (mf_r + mf_t)           */
     int kind;           /* BXDF_KIND_*                                        */
+    int mf_r, mf_t;     /* rough glass: MicrofacetReflection / -Transmission  */
+    double ax, ay;      /* TrowbridgeReitz alphas (remapRoughness false)      */
     spec r, t;          /* Lambert/mirror R; glass R and T                    */
     double eta;         /* NewBSDF(si, eta): 1 for matte/mirror, index for glass */
 } bsdf_t;
@@ -532,6 +534,8 @@ typedef struct {
  * Specular), so it counts as a non-specular component and its sampled type is 0 */
 #define SPEC_REFL_TYPE (BXDF_REFLECTION | BXDF_DIFFUSE)
 #define FRESNEL_SPEC_TYPE (BXDF_REFLECTION | BXDF_TRANSMISSION | BXDF_SPECULAR)   /* reflection.go:465-474 */
+#define MF_REFL_TYPE (BXDF_REFLECTION | BXDF_GLOSSY)     /* reflection.go:670-677 */
+#define MF_TRANS_TYPE (BXDF_TRANSMISSION | BXDF_GLOSSY)  /* reflection.go:738-747 */
 
 static double inv_pi(void) { FL(1); return 1.0 / go_Pi; }   /* pkg/math InvPi = 1.0 / Pi */
 static int matches_flags(int t, int flags) { return (t & flags) == t; }
@@ -545,6 +549,7 @@ static int material_bsdf(const pbrt_scene_desc* sc, const si_t* si, bsdf_t* b) {
     b->ts = v_cross(b->ns, b->ss);
     b->n_bxdfs = 0;
     b->kind = BXDF_KIND_LAMBERT;
+    b->mf_r = b->mf_t = 0;
     b->eta = 1.0;
     if (m->type == PBRT_MAT_MIRROR) {   /* mirror.go:21-32 */
         spec r = S3(m->kr[0], m->kr[1], m->kr[2]);
@@ -564,7 +569,17 @@ static int material_bsdf(const pbrt_scene_desc* sc, const si_t* si, bsdf_t* b) {
         }
         b->eta = m->eta;
         if (s_is_black(R) && s_is_black(T)) return 0;
-        if (!(m->u_roughness == 0 && m->v_roughness == 0)) return -1;   /* microfacets: unsupported */
+        if (!(m->u_roughness == 0 && m->v_roughness == 0)) {   /* glass.go:49-73 */
+            b->kind = BXDF_KIND_MICROFACET;
+            b->ax = m->u_roughness;
+            b->ay = m->v_roughness;
+            b->mf_r = !s_is_black(R);
+            b->mf_t = !s_is_black(T);
+            b->n_bxdfs = b->mf_r + b->mf_t;
+            b->r = R;
+            b->t = T;
+            return 0;
+        }
         b->n_bxdfs = 1;
         b->kind = BXDF_KIND_FRESNEL_SPEC;
         b->r = R;
@@ -593,6 +608,93 @@ static int material_bsdf(const pbrt_scene_desc* sc, const si_t* si, bsdf_t* b) {
 }
 static v3 bsdf_w2l(const bsdf_t* b, v3 v) { return V3(v_dot(v, b->ss), v_dot(v, b->ts), v_dot(v, b->ns)); }
 
+/* reflection.go:21-42 FrDielectric */
+static double fr_dielectric(double cos_i, double eta_i, double eta_t) {
+    cos_i = go_clamp(cos_i, -1, 1);
+    if (!(cos_i > 0)) {
+        double tmp = eta_i; eta_i = eta_t; eta_t = tmp;
+        cos_i = gm_abs(cos_i);
+    }
+    double sin_i = sqrt(go_max(0, 1 - cos_i * cos_i));
+    double sin_t = eta_i / eta_t * sin_i;
+    if (sin_t >= 1) return 1;
+    double cos_t = sqrt(go_max(0, 1 - sin_t * sin_t));
+    double rparl = ((eta_t * cos_i) - (eta_i * cos_t)) / ((eta_t * cos_i) + (eta_i * cos_t));
+    double rperp = ((eta_i * cos_i) - (eta_t * cos_t)) / ((eta_i * cos_i) + (eta_t * cos_t));
+    return (rparl * rparl + rperp * rperp) / 2;
+}
+/* TrowbridgeReitz (microfacet.go:36-84, 117-124; sampleVisibleArea true) and the
+ * trig helpers (reflection.go:48-100); D's e keeps the reference's
+ * alphaX*alphaY under Cos2Phi */
+static double cos2_theta(v3 w) { return w.z * w.z; }
+static double sin2_theta(v3 w) { return go_max(0, 1 - cos2_theta(w)); }
+static double sin_theta(v3 w) { return sqrt(sin2_theta(w)); }
+static double tan_theta(v3 w) { return sin_theta(w) / w.z; }
+static double tan2_theta(v3 w) { return sin2_theta(w) / cos2_theta(w); }
+static double cos_phi(v3 w) { double st = sin_theta(w); return st == 0 ? 1 : go_clamp(w.x / st, -1, 1); }
+static double sin_phi(v3 w) { double st = sin_theta(w); return st == 0 ? 0 : go_clamp(w.y / st, -1, 1); }
+static double cos2_phi(v3 w) { return cos_phi(w) * cos_phi(w); }
+static double sin2_phi(v3 w) { return sin_phi(w) * sin_phi(w); }
+static double tr_d(const bsdf_t* b, v3 wh) {
+    double t2 = tan2_theta(wh);
+    if (isinf(t2)) return 0;
+    double c4 = cos2_theta(wh) * cos2_theta(wh);
+    double e = (cos2_phi(wh) / (b->ax * b->ay) + sin2_phi(wh) / (b->ay * b->ay)) * t2;
+    return 1 / (go_Pi * b->ax * b->ay * c4 * (1 + e) * (1 + e));
+}
+static double tr_lambda(const bsdf_t* b, v3 w) {
+    double at = gm_abs(tan_theta(w));
+    if (isinf(at)) return 0;
+    double alpha = sqrt(cos2_phi(w) * b->ax * b->ax + sin2_phi(w) * b->ay * b->ay);
+    double a2t2 = (alpha * at) * (alpha * at);
+    return (-1 + sqrt(1.0 + a2t2)) / 2;
+}
+static double tr_g1(const bsdf_t* b, v3 w) { return 1 / (1 + tr_lambda(b, w)); }
+static double tr_g(const bsdf_t* b, v3 wo, v3 wi) { return 1 / (1 + tr_lambda(b, wo) + tr_lambda(b, wi)); }
+static double tr_pdf(const bsdf_t* b, v3 wo, v3 wh) {   /* microfacet.go:26-32 */
+    return tr_d(b, wh) * tr_g1(b, wo) * v_absdot(wo, wh) / gm_abs(wo.z);
+}
+/* MicrofacetReflection.F / .Pdf (reflection.go:690-704, 730-736), FresnelDielectric(1, eta) */
+static spec mf_refl_f(const bsdf_t* b, v3 wo, v3 wi) {
+    double c0 = gm_abs(wo.z), c1 = gm_abs(wi.z);
+    v3 wh = v_add(wi, wo);
+    if (c1 == 0 || c0 == 0) return S3(0, 0, 0);
+    if (wh.x == 0 && wh.y == 0 && wh.z == 0) return S3(0, 0, 0);
+    wh = v_normalized(wh);
+    double F = fr_dielectric(v_dot(wi, wh), 1.0, b->eta);
+    return s_muls(s_mul(b->r, S3(F, F, F)), tr_d(b, wh) * tr_g(b, wo, wi) / (4 * c1 * c0));
+}
+static double mf_refl_pdf(const bsdf_t* b, v3 wo, v3 wi) {
+    if (!(wo.z * wi.z > 0)) return 0;
+    v3 wh = v_normalized(v_add(wo, wi));
+    return tr_pdf(b, wo, wh) / (4 * v_dot(wo, wh));
+}
+/* MicrofacetTransmission.F / .Pdf (reflection.go:758-790, 820-835): F is 0 unless
+ * wo and wi share a hemisphere (the reference's inverted test), wh is not
+ * normalized, and NewMicrofacetTransmission leaves mode at its zero value (not
+ * Radiance, material.go:10), so factor stays 1 */
+static spec mf_trans_f(const bsdf_t* b, v3 wo, v3 wi) {
+    if (!(wo.z * wi.z > 0)) return S3(0, 0, 0);
+    double co = wo.z, ci = wi.z;
+    if (ci == 0 || co == 0) return S3(0, 0, 0);
+    double eta = wo.z > 0 ? 1.0 / b->eta : b->eta / 1.0;
+    v3 wh = v_add(wo, v_muls(wi, eta));
+    if (wh.z < 0) wh = v_muls(wh, -1);
+    double F = fr_dielectric(v_dot(wo, wh), 1.0, b->eta);
+    double sd = v_dot(wo, wh) * eta * v_dot(wi, wh);
+    double factor = 1.0;
+    spec a = s_mul(S3(1 - F, 1 - F, 1 - F), b->t);
+    return s_muls(a, gm_abs(tr_d(b, wh) * tr_g(b, wo, wi) * eta * eta * v_absdot(wi, wh) * v_absdot(wo, wh) *
+                            factor * factor / (ci * co * sd * sd)));
+}
+static double mf_trans_pdf(const bsdf_t* b, v3 wo, v3 wi) {
+    if (wo.z * wi.z > 0) return 0;
+    double eta = wo.z > 0 ? 1.0 / b->eta : b->eta / 1.0;
+    v3 wh = v_add(wo, v_muls(wi, eta));
+    double sd = v_dot(wo, wh) + eta * v_dot(wi, wh);
+    double dwh = gm_abs((eta * eta * v_dot(wi, wh)) / (sd * sd));
+    return tr_pdf(b, wo, wh) * dwh;
+}
 /* reflection.go:169-186 */
 static spec bsdf_f(const bsdf_t* b, v3 woW, v3 wiW, int flags) {
     FL_OFF_BEGIN;
@@ -604,6 +706,11 @@ static spec bsdf_f(const bsdf_t* b, v3 woW, v3 wiW, int flags) {
     int reflect = v_dot(wiW, b->ng) * v_dot(woW, b->ng) > 0;
     FL(1);
     spec f = S3(0, 0, 0);
+    if (b->kind == BXDF_KIND_MICROFACET) {
+        if (b->mf_r && matches_flags(MF_REFL_TYPE, flags) && reflect) f = s_add(f, mf_refl_f(b, wo, wi));
+        if (b->mf_t && matches_flags(MF_TRANS_TYPE, flags) && !reflect) f = s_add(f, mf_trans_f(b, wo, wi));
+        return f;
+    }
     if (b->n_bxdfs && b->kind == BXDF_KIND_LAMBERT && matches_flags(LAMBERT_TYPE, flags) && reflect)
         f = s_add(f, s_muls(b->r, inv_pi()));
     else if (b->n_bxdfs && b->kind != BXDF_KIND_LAMBERT)
@@ -626,6 +733,9 @@ static double bsdf_pdf(const bsdf_t* b, v3 woW, v3 wiW, int flags) {
     int matching = 0;
     if (b->kind == BXDF_KIND_LAMBERT) {
         if (matches_flags(LAMBERT_TYPE, flags)) { matching++; pdf += lambert_pdf(wo, wi); FL(1); }
+    } else if (b->kind == BXDF_KIND_MICROFACET) {
+        if (b->mf_r && matches_flags(MF_REFL_TYPE, flags)) { matching++; pdf += mf_refl_pdf(b, wo, wi); }
+        if (b->mf_t && matches_flags(MF_TRANS_TYPE, flags)) { matching++; pdf += mf_trans_pdf(b, wo, wi); }
     } else {   /* reflection.go:534-536, 572-574: Pdf is 0 */
         int ty = b->kind == BXDF_KIND_SPEC_REFL ? SPEC_REFL_TYPE : FRESNEL_SPEC_TYPE;
         if (matches_flags(ty, flags)) { matching++; pdf += 0.0; }
@@ -660,21 +770,6 @@ static v3 cosine_sample_hemisphere(v2 u) {
     FL(5);
     return V3(d.x, d.y, z);
 }
-/* reflection.go:21-42 FrDielectric */
-static double fr_dielectric(double cos_i, double eta_i, double eta_t) {
-    cos_i = go_clamp(cos_i, -1, 1);
-    if (!(cos_i > 0)) {
-        double tmp = eta_i; eta_i = eta_t; eta_t = tmp;
-        cos_i = gm_abs(cos_i);
-    }
-    double sin_i = sqrt(go_max(0, 1 - cos_i * cos_i));
-    double sin_t = eta_i / eta_t * sin_i;
-    if (sin_t >= 1) return 1;
-    double cos_t = sqrt(go_max(0, 1 - sin_t * sin_t));
-    double rparl = ((eta_t * cos_i) - (eta_i * cos_t)) / ((eta_t * cos_i) + (eta_i * cos_t));
-    double rperp = ((eta_i * cos_i) - (eta_t * cos_t)) / ((eta_i * cos_i) + (eta_t * cos_t));
-    return (rparl * rparl + rperp * rperp) / 2;
-}
 double oracle_fr_dielectric(double cos_i, double eta_i, double eta_t) { return fr_dielectric(cos_i, eta_i, eta_t); }
 /* FresnelSpecular.SampleF (reflection.go:489-524), incl. its (etaT / etaT)
  * radiance scale; FaceForward (geometry.go:111-116) + Refract (:106-118) */
@@ -703,11 +798,14 @@ static spec fresnel_specular_sample(const bsdf_t* b, v3 wo, v2 u, v3* wi, double
     *type = BXDF_SPECULAR | BXDF_TRANSMISSION;
     return s_divs(ft, gm_abs(wi->z));
 }
-/* reflection.go:188-253; returns the LOCAL-frame wi (#7) and the sampled type */
+/* reflection.go:188-253; returns the LOCAL-frame wi (#7) and the sampled type;
+ * type -1: the reference panics (rough glass, PBRT_PANIC_NIL_DEREF) */
 static spec bsdf_sample_f_t(const bsdf_t* b, v3 woW, v2 u, int t, v3* wi_out, double* pdf_out, int* type_out) {
     const int ty = b->kind == BXDF_KIND_LAMBERT ? LAMBERT_TYPE
                  : b->kind == BXDF_KIND_SPEC_REFL ? SPEC_REFL_TYPE : FRESNEL_SPEC_TYPE;
     int matching = (b->n_bxdfs && matches_flags(ty, t)) ? 1 : 0;
+    if (b->kind == BXDF_KIND_MICROFACET)
+        matching = (b->mf_r && matches_flags(MF_REFL_TYPE, t)) + (b->mf_t && matches_flags(MF_TRANS_TYPE, t));
     *wi_out = V3(0, 0, 0);
     *pdf_out = 0;
     *type_out = 0;
@@ -717,6 +815,10 @@ static spec bsdf_sample_f_t(const bsdf_t* b, v3 woW, v2 u, int t, v3* wi_out, do
     FL(4);
     v3 wo = bsdf_w2l(b, woW);
     if (wo.z == 0.0) return S3(0, 0, 0);
+    if (b->kind == BXDF_KIND_MICROFACET) {   /* SampleWH's nil wh reaches Reflect/Refract */
+        *type_out = -1;
+        return S3(0, 0, 0);
+    }
     if (b->kind == BXDF_KIND_SPEC_REFL) {   /* reflection.go:557-562 (FresnelNoOp) */
         v3 wi = V3(-wo.x, -wo.y, wo.z);
         spec f = s_divs(s_mul(S3(1, 1, 1), b->r), gm_abs(wi.z));
@@ -921,6 +1023,11 @@ static spec estimate_direct(orc_ctx* oc, const si_t* si, const bsdf_t* b, v2 u_s
             }
         }
     }
+    if (!is_delta && b->kind == BXDF_KIND_MICROFACET && b->n_bxdfs > 0 && bsdf_w2l(b, si->wo).z != 0) {
+        /* integrator.go:134-139: BSDF.SampleF runs for every area light */
+        oc->pc.kind = PBRT_PANIC_NIL_DEREF;
+        longjmp(oc->pc.jb, 1);
+    }
     if (!is_delta && panic_fidelity(oc)) {
         /* integrator.go:132-192: BSDF-sampled ray toward the area light. No
          * primitive has an area light, so Li is always 0 here; PdfLi and the
@@ -1021,6 +1128,10 @@ static spec path_li(orc_ctx* oc, sampler_t* smp, ray_t ray) {
         v2 u = sampler_get2d(smp);
         v3 wi; double pdf; int flags;
         spec f = bsdf_sample_f_t(&b, wo, u, BXDF_ALL, &wi, &pdf, &flags);
+        if (flags == -1) {
+            oc->pc.kind = PBRT_PANIC_NIL_DEREF;
+            longjmp(oc->pc.jb, 1);
+        }
         if (s_is_black(f) || pdf == 0.0) break;
         double wabs = v_absdot(wi, isect.sn);
         double wp = wabs / pdf;

@@ -11,7 +11,16 @@ Quirks restated (and therefore tested here):
 - smooth glass is a single specular lobe: no light sample, so its paths consume
   fewer draws per bounce;
 - DirectLighting's SpecularReflect/Transmit match neither lobe, so both
-  materials render there exactly like a black Matte.
+  materials render there exactly like a black Matte;
+- rough glass (MicrofacetReflection + MicrofacetTransmission over
+  TrowbridgeReitz, pkg/pbrt/microfacet.go, reflection.go:670-835): SampleWH
+  shadows its result and returns nil, so any BSDF.SampleF on it dereferences
+  nil in Reflect/Refract -- in Path.Li's bounce sampling and in EstimateDirect's
+  BSDF-sampled half, which runs for every area light (integrator.go:134-139).
+  The reference panics there (PBRT_PANIC_NIL_DEREF); with delta lights only,
+  DirectLighting renders rough glass through the microfacet F and Pdf, whose
+  own quirks (D's alphaX*alphaY, MicrofacetTransmission.F's inverted hemisphere
+  test, its unset TransportMode) are restated.
 
 No reference test covers these materials and there is no Go toolchain here:
 device-vs-oracle parity is bit-exact but "parity unpinned" against Go itself.
@@ -25,7 +34,7 @@ import pbrtgpu as G
 from pbrtgpu import abi
 
 
-def material_scene(kind="both", w=32, h=24, rough=0.0):
+def material_scene(kind="both", w=32, h=24, rough=0.0, area=True, kt=(0.5, 0.5, 0.5)):
     """A floor, a glass sphere, a mirror sphere and a matte sphere, lit by a
     point light and an area-light sphere. kind: "both" | "matte" (the two
     special spheres matte) | "black" (the two special spheres black matte)."""
@@ -35,7 +44,7 @@ def material_scene(kind="both", w=32, h=24, rough=0.0):
     s.add_primitive(floor, chk)
     red = s.add_matte((0.6, 0.1, 0.1))
     if kind == "both":
-        glass = s.add_glass(u_roughness=rough, v_roughness=rough)   # server.go:80-87's glass
+        glass = s.add_glass(kt=kt, u_roughness=rough, v_roughness=0.5 * rough)   # server.go:80-87's glass
         mirror = s.add_mirror()
     elif kind == "matte":
         glass = mirror = s.add_matte((0.5, 0.5, 0.5))
@@ -44,8 +53,9 @@ def material_scene(kind="both", w=32, h=24, rough=0.0):
     for (x, z, m) in ((-2.5, 0.0, glass), (2.5, 0.0, mirror), (0.0, -4.0, red)):
         sph = s.add_sphere(G.translate(0, 0, 0), 2.0)
         s.add_primitive(sph, m, G.translate(x, 2.0, z))
-    light = s.add_sphere(G.translate(0, 9, 2), 0.75)
-    s.add_area_light((6, 6, 6), light)
+    if area:
+        light = s.add_sphere(G.translate(0, 9, 2), 0.75)
+        s.add_area_light((6, 6, 6), light)
     s.add_point_light(G.translate(-6, 10, 8), (60, 60, 60))
     s.set_film(w, h)
     s.set_camera(G.look_at((0, 7, 12), (0, 1.5, 0), (0, 1, 0)), fov=55)
@@ -89,10 +99,27 @@ def test_oracle_direct_lighting_sees_glass_and_mirror_as_black_matte():
         assert rc == rc2 == 0 and np.array_equal(bits(fa), bits(fb))
 
 
-def test_oracle_rough_glass_is_unsupported():
-    sc = material_scene(rough=0.1)
-    rc, _, _ = O.render(sc.desc, abi.render_desc(2, 2), threads=4)
-    assert rc == abi.PBRT_E_UNSUPPORTED
+def test_oracle_rough_glass_panics_like_the_reference():
+    sc = material_scene(rough=0.3)
+    for rd in (abi.render_desc(2, 2),
+               abi.render_desc(2, 2, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING)):
+        rc, _, st = O.render(sc.desc, rd, threads=4)
+        assert rc == abi.PBRT_E_REF_PANIC and st.panic_kind == abi.PBRT_PANIC_NIL_DEREF
+        assert st.panic_bounce == 1
+    sp = material_scene(rough=0.3, area=False)   # Path.Li still samples a bounce
+    rc, _, st = O.render(sp.desc, abi.render_desc(2, 2), threads=4)
+    assert rc == abi.PBRT_E_REF_PANIC and st.panic_kind == abi.PBRT_PANIC_NIL_DEREF
+
+
+def test_oracle_rough_glass_direct_lighting_with_delta_lights():
+    """DirectLighting without area lights never samples the BSDF: rough glass
+    renders through its microfacet F (reflection and transmission lobes)."""
+    rd = abi.render_desc(2, 2, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING)
+    sr, sb = material_scene(rough=0.3, area=False), material_scene("black", area=False)
+    rc, fr, _ = O.render(sr.desc, rd, threads=8)
+    _, fb, _ = O.render(sb.desc, rd, threads=8)
+    assert rc == 0 and np.isfinite(fr).all()
+    assert (fr.sum(axis=2) > fb.sum(axis=2)).sum() > 10   # glossy highlights on the glass sphere
 
 
 def test_material_desc_layout():
@@ -144,12 +171,31 @@ def test_device_materials_power_strategy_and_rr():
 
 
 @pytest.mark.gpu
-def test_device_rough_glass_and_fidelity_are_unsupported():
-    sr = material_scene(rough=0.1)
-    with G.Renderer(sr) as r:
+@pytest.mark.parametrize("integrator", [abi.PBRT_INTEGRATOR_PATH, abi.PBRT_INTEGRATOR_DIRECT_LIGHTING])
+@pytest.mark.parametrize("area", [True, False])
+@pytest.mark.parametrize("mode", [abi.PBRT_MODE_EXACT, abi.PBRT_MODE_THROUGHPUT])
+def test_device_rough_glass_vs_oracle(integrator, area, mode):
+    """Rough glass: the reference's nil-dereference panic site, or (DirectLighting
+    with delta lights) the microfacet film, bit-exact."""
+    sc = material_scene(rough=0.3, area=area)
+    rd = abi.render_desc(3, 3, integrator=integrator, mode=mode)
+    rc, of, ost = O.render(sc.desc, rd, threads=8)
+    with G.Renderer(sc) as r:
+        if rc == 0:
+            film, _ = r.render(rd)
+            assert np.array_equal(bits(film), bits(of))
+            return
+        assert rc == abi.PBRT_E_REF_PANIC and ost.panic_kind == abi.PBRT_PANIC_NIL_DEREF
         with pytest.raises(G.PbrtError) as ei:
-            r.render(abi.render_desc(2, 2))
-    assert ei.value.code == abi.PBRT_E_UNSUPPORTED
+            r.render(rd)
+    assert ei.value.code == abi.PBRT_E_REF_PANIC
+    st = ei.value.stats
+    assert (st.panic_kind, st.panic_tile, st.panic_pixel_x, st.panic_pixel_y, st.panic_sample, st.panic_bounce) == \
+        (ost.panic_kind, ost.panic_tile, ost.panic_px, ost.panic_py, ost.panic_sample, ost.panic_bounce)
+
+
+@pytest.mark.gpu
+def test_device_fidelity_on_mirror_glass_is_unsupported():
     sc = material_scene()
     with G.Renderer(sc) as r:
         with pytest.raises(G.PbrtError) as ei:
