@@ -858,14 +858,15 @@ __device__ inline Spec bsdf_sample_f(const BSDF& b, V3 woW, V2 u, V3& wi, double
 // sampling (and the Path.Li bookkeeping) needs the kind.
 constexpr int BXDF_TRANSMISSION = 2, BXDF_GLOSSY = 8;
 constexpr int MF_REFL_TYPE = BXDF_REFLECTION | BXDF_GLOSSY, MF_TRANS_TYPE = BXDF_TRANSMISSION | BXDF_GLOSSY;
-enum { BXDF_KIND_LAMBERT = 0, BXDF_KIND_SPEC_REFL = 1, BXDF_KIND_FRESNEL_SPEC = 2, BXDF_KIND_MICROFACET = 3 };
+enum { BXDF_KIND_LAMBERT = 0, BXDF_KIND_SPEC_REFL = 1, BXDF_KIND_FRESNEL_SPEC = 2, BXDF_KIND_MICROFACET = 3,
+       BXDF_KIND_OREN_NAYAR = 4 };
 struct BSDFX {
     int kind;       // BXDF_KIND_*; LAMBERT: `b` is the whole BSDF
     int n;          // number of BxDFs of that kind (MICROFACET: mf_r + mf_t)
     int mf_r, mf_t; // rough glass: MicrofacetReflection, MicrofacetTransmission
     Spec r, t;
     double eta;     // NewBSDF(si, eta)
-    double ax, ay;  // TrowbridgeReitz alphas (remapRoughness false)
+    double ax, ay;  // TrowbridgeReitz alphas (remapRoughness false); OrenNayar A, B
 };
 // NumComponents(BSDFAll &^ BSDFSpecular) > 0: SpecularReflection is typed
 // Reflection|Diffuse (reflection.go:538-544), FresnelSpecular is specular
@@ -879,7 +880,37 @@ __device__ inline int compute_bsdf_x(const DevScene& sc, const SI& si, BSDF& b, 
     x.kind = BXDF_KIND_LAMBERT;
     x.n = x.mf_r = x.mf_t = 0;
     x.eta = 1.0;
-    if (m.type == PBRT_MAT_MATTE) return compute_bsdf(sc, si, b);
+    if (m.type == PBRT_MAT_MATTE) {
+        const double sig = gomath::clamp(m.sigma, 0, 90);
+        if (sig == 0) return compute_bsdf(sc, si, b);
+        // OrenNayar (matte.go:30-35, NewOrenNayar reflection.go:616-625; B's
+        // sigma2 * 0.09 kept): sampled and weighted like a Lambertian, its F
+        // differs, so it carries its own kind with b.r = Kd
+        b.ns = si.sn;
+        b.ng = si.n;
+        b.ss = normalized(si.sdpdu);
+        b.ts = cross(b.ns, b.ss);
+        b.n_bxdfs = 0;
+        Spec r;
+        if (m.kd_type == PBRT_TEX_CHECKERBOARD2D) {
+            double s = m.ds + dot(si.p, load3(m.vs));
+            double t = m.dt + dot(si.p, load3(m.vt));
+            int64_t k = gomath::to_int(gomath::floor(s) + gomath::floor(t));
+            r = (k % 2 == 0) ? spec3(m.tex1) : spec3(m.tex2);
+        } else {
+            r = spec3(m.kd);
+        }
+        r.r = gomath::clamp(r.r, 0, kInf);
+        r.g = gomath::clamp(r.g, 0, kInf);
+        r.b = gomath::clamp(r.b, 0, kInf);
+        x.kind = BXDF_KIND_OREN_NAYAR;
+        x.r = r;
+        x.n = is_black(r) ? 0 : 1;
+        const double sr = gomath::radians(sig), s2 = sr * sr;
+        x.ax = 1.0 - (s2 / (2.0 * (s2 + 0.33)));
+        x.ay = 0.45 * s2 / (s2 * 0.09);
+        return 0;
+    }
     b.ns = si.sn;
     b.ng = si.n;
     b.ss = normalized(si.sdpdu);
@@ -1006,6 +1037,25 @@ __device__ inline double mf_trans_pdf(const BSDFX& x, V3 wo, V3 wi) {
     const double dwh = gomath::abs((eta * eta * dot(wi, wh)) / (sd * sd));
     return tr_pdf(x, wo, wh) * dwh;
 }
+// OrenNayar.F (reflection.go:627-652); the else branch's tanBeta keeps sinThetaO
+__device__ inline Spec oren_nayar_f(const BSDFX& x, V3 wo, V3 wi) {
+    const double sin_i = sin_theta(wi), sin_o = sin_theta(wo);
+    double max_cos = 0.0;
+    if (sin_i > 1e-4 && sin_o > 1e-4) {
+        const double sp_i = sin_phi(wi), cp_i = cos_phi(wi), sp_o = sin_phi(wo), cp_o = cos_phi(wo);
+        const double d_cos = cp_i * cp_o + sp_i * sp_o;
+        max_cos = gomath::max(0.0, d_cos);
+    }
+    double sin_alpha, tan_beta;
+    if (gomath::abs(wi.z) > gomath::abs(wo.z)) {
+        sin_alpha = sin_o;
+        tan_beta = sin_o / gomath::abs(wo.z);
+    } else {
+        sin_alpha = sin_i;
+        tan_beta = sin_o / gomath::abs(wo.z);
+    }
+    return smuls(x.r, inv_pi() * (x.ax + x.ay * max_cos * sin_alpha * tan_beta));
+}
 // BSDF.F / BSDF.Pdf (reflection.go:169-186, 255-278) of a rough glass, flags
 // BSDFAll &^ BSDFSpecular (both microfacet lobes match)
 __device__ inline Spec mf_bsdf_f(const BSDF& b, const BSDFX& x, V3 woW, V3 wiW) {
@@ -1013,6 +1063,7 @@ __device__ inline Spec mf_bsdf_f(const BSDF& b, const BSDFX& x, V3 woW, V3 wiW) 
     if (wo.z == 0.0) return spec(0);
     const bool reflect = dot(wiW, b.ng) * dot(woW, b.ng) > 0;
     Spec f = spec(0);
+    if (x.kind == BXDF_KIND_OREN_NAYAR) return (x.n && reflect) ? f + oren_nayar_f(x, wo, wi) : f;
     if (x.mf_r && reflect) f = f + mf_refl_f(x, wo, wi);
     if (x.mf_t && !reflect) f = f + mf_trans_f(x, wo, wi);
     return f;
@@ -1021,6 +1072,7 @@ __device__ inline double mf_bsdf_pdf(const BSDF& b, const BSDFX& x, V3 woW, V3 w
     if (x.n == 0) return 0;
     const V3 wo = w2l(b, woW), wi = w2l(b, wiW);
     if (wo.z == 0) return 0;
+    if (x.kind == BXDF_KIND_OREN_NAYAR) return (0 + lambert_pdf(wo, wi)) / 1.0;
     double pdf = 0;
     if (x.mf_r) pdf += mf_refl_pdf(x, wo, wi);
     if (x.mf_t) pdf += mf_trans_pdf(x, wo, wi);
@@ -1039,6 +1091,17 @@ __device__ inline Spec bsdfx_sample_f(const BSDF& b, const BSDFX& x, V3 woW, V2 
     const V2 ur{gomath::min(u.x * 1.0 - comp, gomath::kOneMinusEpsilon), u.y};
     const V3 wo = w2l(b, woW);
     if (wo.z == 0.0) return spec(0);
+    if (x.kind == BXDF_KIND_OREN_NAYAR) {   // the default sampleF (reflection.go:305-314)
+        const V2 d = concentric_sample_disk(ur);
+        V3 w{d.x, d.y, gomath::sqrt(gomath::max(0.0, 1.0 - d.x * d.x - d.y * d.y))};
+        if (wo.z < 0) w.z *= -1;
+        const double p = lambert_pdf(wo, w);
+        const Spec f = oren_nayar_f(x, wo, w);
+        if (p == 0.0) return spec(0);
+        wi = w;
+        pdf = p;
+        return f;
+    }
     if (x.kind == BXDF_KIND_MICROFACET) {
         type = -1;
         return spec(0);
@@ -1217,7 +1280,8 @@ __device__ inline Spec estimate_direct(const DevScene& sc, uint16_t* stack, int&
 // is the shared estimate_direct.
 __device__ inline Spec estimate_direct_x(const DevScene& sc, uint16_t* stack, int& panic, const SI& si, const BSDF& b,
                                          const BSDFX& x, int li, V2 u_light) {
-    if (x.kind != BXDF_KIND_MICROFACET) return estimate_direct(sc, stack, panic, si, b, li, u_light);
+    if (x.kind != BXDF_KIND_MICROFACET && x.kind != BXDF_KIND_OREN_NAYAR)
+        return estimate_direct(sc, stack, panic, si, b, li, u_light);
     const pbrt_light_desc& L = sc.lights[li];
     const bool is_delta = L.type != PBRT_LIGHT_DIFFUSE_AREA;
     LightSample ls;
@@ -1243,7 +1307,7 @@ __device__ inline Spec estimate_direct_x(const DevScene& sc, uint16_t* stack, in
             }
         }
     }
-    if (!is_delta && x.n > 0 && w2l(b, si.wo).z != 0) panic = PBRT_PANIC_NIL_DEREF;
+    if (x.kind == BXDF_KIND_MICROFACET && !is_delta && x.n > 0 && w2l(b, si.wo).z != 0) panic = PBRT_PANIC_NIL_DEREF;
     return Ld;
 }
 

@@ -1903,7 +1903,7 @@ struct pbrt_gpu_ctx {
     pbrt_distribution_desc* d_dist = nullptr;
     pbrt_scene_desc host_scene;   // counts + film/camera (pointer fields are not kept)
     std::vector<pbrt_light_desc> host_lights;
-    bool non_matte = false;       // a Mirror or Glass material: serial kernel only
+    bool non_matte = false;       // Mirror, Glass or OrenNayar material: serial kernel only
     // per-render buffers (grown on demand)
     double* d_films = nullptr;
     size_t films_cap = 0;
@@ -2678,7 +2678,9 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
     }
     c->host_scene = *scene;
     c->non_matte = false;
-    for (int i = 0; i < scene->n_materials; i++) c->non_matte |= scene->materials[i].type != PBRT_MAT_MATTE;
+    for (int i = 0; i < scene->n_materials; i++)   // Mirror, Glass or OrenNayar (Matte with sigma != 0)
+        c->non_matte |= scene->materials[i].type != PBRT_MAT_MATTE ||
+                        !(std::min(std::max(scene->materials[i].sigma, 0.0), 90.0) == 0);
     c->h_node_prims.resize((size_t)scene->n_nodes);
     for (int i = 0; i < scene->n_nodes; i++) c->h_node_prims[i] = scene->nodes[i].n_prims;
     c->host_scene.shapes = nullptr;
@@ -3022,7 +3024,7 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
             break;
         }
         if (st.panic_kind == -1) {
-            rc = set_err(c, PBRT_E_UNSUPPORTED, "material not on the hot path (OrenNayar)");
+            rc = set_err(c, PBRT_E_UNSUPPORTED, "unsupported material");
             st.panic_kind = 0;
         } else {
             rc = set_err(c, PBRT_E_REF_PANIC, "the Go reference panics on this input");

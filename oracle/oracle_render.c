@@ -512,13 +512,15 @@ static int prim_material(const pbrt_scene_desc* sc, int prim) {
 /* kind of the single BxDF: LambertianReflection (matte.go), SpecularReflection
  * with FresnelNoOp (mirror.go), or FresnelSpecular (smooth glass with multiple
  * lobes allowed, glass.go:46-47 -- Path.Li passes allowMultipleLobes true). */
-enum { BXDF_KIND_LAMBERT = 0, BXDF_KIND_SPEC_REFL = 1, BXDF_KIND_FRESNEL_SPEC = 2, BXDF_KIND_MICROFACET = 3 };
+enum { BXDF_KIND_LAMBERT = 0, BXDF_KIND_SPEC_REFL = 1, BXDF_KIND_FRESNEL_SPEC = 2, BXDF_KIND_MICROFACET = 3,
+       BXDF_KIND_OREN_NAYAR = 4 };
 typedef struct {
     v3 ns, ng, ss, ts;
     int n_bxdfs;        /* 0 or 1; 0-2 for MICROFACET (mf_r + mf_t)           */
     int kind;           /* BXDF_KIND_*                                        */
     int mf_r, mf_t;     /* rough glass: MicrofacetReflection / -Transmission  */
     double ax, ay;      /* TrowbridgeReitz alphas (remapRoughness false)      */
+    double on_a, on_b;  /* OrenNayar A, B (reflection.go:616-625)             */
     spec r, t;          /* Lambert/mirror R; glass R and T                    */
     double eta;         /* NewBSDF(si, eta): 1 for matte/mirror, index for glass */
 } bsdf_t;
@@ -600,9 +602,15 @@ static int material_bsdf(const pbrt_scene_desc* sc, const si_t* si, bsdf_t* b) {
     for (int i = 0; i < 3; i++) r.c[i] = go_clamp(r.c[i], 0, INFINITY);
     double sig = go_clamp(m->sigma, 0, 90);
     if (!s_is_black(r)) {
-        if (sig != 0) return -1;          /* OrenNayar: not on the hot path   */
         b->n_bxdfs = 1;
         b->r = r;
+        if (sig != 0) {   /* NewOrenNayar (reflection.go:616-625): B's sigma2 * 0.09 kept */
+            double s = go_radians(sig);
+            double s2 = s * s;
+            b->kind = BXDF_KIND_OREN_NAYAR;
+            b->on_a = 1.0 - (s2 / (2.0 * (s2 + 0.33)));
+            b->on_b = 0.45 * s2 / (s2 * 0.09);
+        }
     }
     return 0;
 }
@@ -695,6 +703,25 @@ static double mf_trans_pdf(const bsdf_t* b, v3 wo, v3 wi) {
     double dwh = gm_abs((eta * eta * v_dot(wi, wh)) / (sd * sd));
     return tr_pdf(b, wo, wh) * dwh;
 }
+/* OrenNayar.F (reflection.go:627-652); the else branch's tanBeta keeps sinThetaO */
+static spec oren_nayar_f(const bsdf_t* b, v3 wo, v3 wi) {
+    double sin_i = sin_theta(wi), sin_o = sin_theta(wo);
+    double max_cos = 0.0;
+    if (sin_i > 1e-4 && sin_o > 1e-4) {
+        double sp_i = sin_phi(wi), cp_i = cos_phi(wi), sp_o = sin_phi(wo), cp_o = cos_phi(wo);
+        double d_cos = cp_i * cp_o + sp_i * sp_o;
+        max_cos = go_max(0.0, d_cos);
+    }
+    double sin_alpha, tan_beta;
+    if (gm_abs(wi.z) > gm_abs(wo.z)) {
+        sin_alpha = sin_o;
+        tan_beta = sin_o / gm_abs(wo.z);
+    } else {
+        sin_alpha = sin_i;
+        tan_beta = sin_o / gm_abs(wo.z);
+    }
+    return s_muls(b->r, inv_pi() * (b->on_a + b->on_b * max_cos * sin_alpha * tan_beta));
+}
 /* reflection.go:169-186 */
 static spec bsdf_f(const bsdf_t* b, v3 woW, v3 wiW, int flags) {
     FL_OFF_BEGIN;
@@ -713,6 +740,8 @@ static spec bsdf_f(const bsdf_t* b, v3 woW, v3 wiW, int flags) {
     }
     if (b->n_bxdfs && b->kind == BXDF_KIND_LAMBERT && matches_flags(LAMBERT_TYPE, flags) && reflect)
         f = s_add(f, s_muls(b->r, inv_pi()));
+    else if (b->n_bxdfs && b->kind == BXDF_KIND_OREN_NAYAR && matches_flags(LAMBERT_TYPE, flags) && reflect)
+        f = s_add(f, oren_nayar_f(b, wo, bsdf_w2l(b, wiW)));
     else if (b->n_bxdfs && b->kind != BXDF_KIND_LAMBERT)
         f = s_add(f, S3(0, 0, 0));   /* reflection.go:486-488, 553-555: F is 0 */
     return f;
@@ -731,7 +760,7 @@ static double bsdf_pdf(const bsdf_t* b, v3 woW, v3 wiW, int flags) {
     if (wo.z == 0) return 0;
     double pdf = 0;
     int matching = 0;
-    if (b->kind == BXDF_KIND_LAMBERT) {
+    if (b->kind == BXDF_KIND_LAMBERT || b->kind == BXDF_KIND_OREN_NAYAR) {   /* both use pdf() :343-348 */
         if (matches_flags(LAMBERT_TYPE, flags)) { matching++; pdf += lambert_pdf(wo, wi); FL(1); }
     } else if (b->kind == BXDF_KIND_MICROFACET) {
         if (b->mf_r && matches_flags(MF_REFL_TYPE, flags)) { matching++; pdf += mf_refl_pdf(b, wo, wi); }
@@ -801,7 +830,7 @@ static spec fresnel_specular_sample(const bsdf_t* b, v3 wo, v2 u, v3* wi, double
 /* reflection.go:188-253; returns the LOCAL-frame wi (#7) and the sampled type;
  * type -1: the reference panics (rough glass, PBRT_PANIC_NIL_DEREF) */
 static spec bsdf_sample_f_t(const bsdf_t* b, v3 woW, v2 u, int t, v3* wi_out, double* pdf_out, int* type_out) {
-    const int ty = b->kind == BXDF_KIND_LAMBERT ? LAMBERT_TYPE
+    const int ty = (b->kind == BXDF_KIND_LAMBERT || b->kind == BXDF_KIND_OREN_NAYAR) ? LAMBERT_TYPE
                  : b->kind == BXDF_KIND_SPEC_REFL ? SPEC_REFL_TYPE : FRESNEL_SPEC_TYPE;
     int matching = (b->n_bxdfs && matches_flags(ty, t)) ? 1 : 0;
     if (b->kind == BXDF_KIND_MICROFACET)
@@ -839,7 +868,7 @@ static spec bsdf_sample_f_t(const bsdf_t* b, v3 woW, v2 u, int t, v3* wi_out, do
     v3 wi = cosine_sample_hemisphere(ur);
     if (wo.z < 0) { wi.z *= -1; FL(1); }
     double pdf = lambert_pdf(wo, wi);
-    spec f = s_muls(b->r, inv_pi());
+    spec f = b->kind == BXDF_KIND_OREN_NAYAR ? oren_nayar_f(b, wo, wi) : s_muls(b->r, inv_pi());
     if (pdf == 0.0) return S3(0, 0, 0);
     *wi_out = wi;
     *pdf_out = pdf;

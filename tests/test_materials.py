@@ -34,7 +34,7 @@ import pbrtgpu as G
 from pbrtgpu import abi
 
 
-def material_scene(kind="both", w=32, h=24, rough=0.0, area=True, kt=(0.5, 0.5, 0.5)):
+def material_scene(kind="both", w=32, h=24, rough=0.0, area=True, kt=(0.5, 0.5, 0.5), sigma=0.0):
     """A floor, a glass sphere, a mirror sphere and a matte sphere, lit by a
     point light and an area-light sphere. kind: "both" | "matte" (the two
     special spheres matte) | "black" (the two special spheres black matte)."""
@@ -42,7 +42,7 @@ def material_scene(kind="both", w=32, h=24, rough=0.0, area=True, kt=(0.5, 0.5, 
     chk = s.add_checker((0.2, 0, 0), (0, 0, 0.2), 0, 0, (1, 1, 1), (0.18, 0.18, 0.18))
     floor = s.add_disk(G.rotate(0, 90), 0.0, 100.0)
     s.add_primitive(floor, chk)
-    red = s.add_matte((0.6, 0.1, 0.1))
+    red = s.add_matte((0.6, 0.1, 0.1), sigma=sigma)
     if kind == "both":
         glass = s.add_glass(kt=kt, u_roughness=rough, v_roughness=0.5 * rough)   # server.go:80-87's glass
         mirror = s.add_mirror()
@@ -212,4 +212,33 @@ def test_device_matte_scene_keeps_the_wave_kernels():
     assert st.kernel != abi.PBRT_KERNEL_SERIAL
     scm = material_scene("matte")
     _, of, _ = O.render(scm.desc, abi.render_desc(3, 3, max_depth=6), threads=8)
+    assert np.array_equal(bits(film), bits(of))
+
+
+# ------------------------------------------------------------------ OrenNayar
+# Matte with sigma != 0 (matte.go:30-35): OrenNayar (reflection.go:609-668) with
+# the reference's B = 0.45 sigma^2 / (sigma^2 * 0.09) and its else-branch
+# tanBeta = sinThetaO / |cos wo|; sampled like a Lambertian.
+def test_oracle_oren_nayar_renders_and_clamps_sigma():
+    rd = abi.render_desc(3, 3, max_depth=5)
+    s0, s20, s90, s120, sneg = (material_scene("matte", sigma=v) for v in (0.0, 20.0, 90.0, 120.0, -5.0))
+    f0 = O.render(s0.desc, rd, threads=8)[1]
+    rc, f20, _ = O.render(s20.desc, rd, threads=8)
+    assert rc == 0 and np.isfinite(f20).all() and not np.array_equal(f0, f20)
+    assert np.array_equal(bits(O.render(s90.desc, rd, threads=8)[1]), bits(O.render(s120.desc, rd, threads=8)[1]))
+    assert np.array_equal(bits(O.render(sneg.desc, rd, threads=8)[1]), bits(f0))   # Clamp(-5, 0, 90) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("integrator", [abi.PBRT_INTEGRATOR_PATH, abi.PBRT_INTEGRATOR_DIRECT_LIGHTING])
+@pytest.mark.parametrize("mode", [abi.PBRT_MODE_EXACT, abi.PBRT_MODE_THROUGHPUT])
+@pytest.mark.parametrize("sigma", [20.0, 90.0])
+def test_device_oren_nayar_vs_oracle(integrator, mode, sigma):
+    sc = material_scene("matte", sigma=sigma)
+    rd = abi.render_desc(3, 3, max_depth=6, integrator=integrator, mode=mode)
+    rc, of, _ = O.render(sc.desc, rd, threads=8)
+    assert rc == 0
+    with G.Renderer(sc) as r:
+        film, st = r.render(rd)
+    assert st.kernel == abi.PBRT_KERNEL_SERIAL
     assert np.array_equal(bits(film), bits(of))
