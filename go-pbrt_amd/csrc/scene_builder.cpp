@@ -395,6 +395,16 @@ void pbrt_make_matte_checkerboard(const double vs[3], const double vt[3], double
     out->ds = ds; out->dt = dt;
     out->sigma = sigma;
 }
+void pbrt_random_sampler(int32_t samples_per_pixel, pbrt_render_desc* rd) {
+    // sampler.NewRandomSampler (random.go:12-57) == Stratified(ns, 1) with no sampled
+    // dimensions: StartPixel draws nothing, Get1D/Get2D fall through to the same
+    // PCG32 stream, Clone seeds it the same way (tests/test_materials.py pins this
+    // against the oracle's own RandomSampler restatement)
+    rd->sampler_x = samples_per_pixel;
+    rd->sampler_y = 1;
+    rd->n_dims = 0;
+    rd->jitter = 0;
+}
 void pbrt_make_mirror(const double kr[3], pbrt_material_desc* out) {   // mirror.go:9-14 (NewMirror: Kr 0.9)
     std::memset(out, 0, sizeof(*out));
     out->type = PBRT_MAT_MIRROR;

@@ -95,6 +95,8 @@ def lib():
     L.pbrt_make_matte_constant.restype = None
     L.pbrt_make_matte_checkerboard.argtypes = [P(d), P(d), d, d, P(d), P(d), d, P(abi.MaterialDesc)]
     L.pbrt_make_matte_checkerboard.restype = None
+    L.pbrt_random_sampler.argtypes = [C.c_int32, P(abi.RenderDesc)]
+    L.pbrt_random_sampler.restype = None
     L.pbrt_make_mirror.argtypes = [P(d), P(abi.MaterialDesc)]
     L.pbrt_make_mirror.restype = None
     L.pbrt_make_glass.argtypes = [P(d), P(d), d, d, d, P(abi.MaterialDesc)]

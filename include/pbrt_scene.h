@@ -61,6 +61,10 @@ void pbrt_make_matte_constant(double r, double g, double b, double sigma, pbrt_m
 void pbrt_make_matte_checkerboard(const double vs[3], const double vt[3], double ds, double dt,
                                   const double tex1[3], const double tex2[3], double sigma,
                                   pbrt_material_desc* out);
+/* sampler.NewRandomSampler(ns, seed) (pkg/sampler/random.go:12-57): sets the
+ * sampler fields of rd (sampler_x = ns, sampler_y = 1, n_dims = 0, jitter = 0),
+ * under which the Stratified path consumes exactly the RandomSampler's stream */
+void pbrt_random_sampler(int32_t samples_per_pixel, pbrt_render_desc* rd);
 /* pkg/materials/mirror.go:9-32 (NewMirror's Kr is 0.9) */
 void pbrt_make_mirror(const double kr[3], pbrt_material_desc* out);
 /* pkg/materials/glass.go:15-75 with constant textures (see pbrt_material_desc) */

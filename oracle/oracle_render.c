@@ -78,11 +78,17 @@ typedef struct {
     int32_t xs, ys, spp, ndims, jitter;
     int32_t sample_index, cur1d, cur2d;
     double* s1d;   /* ndims * spp */
+    int random;    /* RandomSampler (pkg/sampler/random.go:12-57) */
 } sampler_t;
 
 /* stratified.go:21-48 + sampling.go:101-145 */
 static void sampler_start_pixel(sampler_t* s) {
     int32_t n = s->spp;
+    if (s->random) {   /* random.go:41-55: no sample arrays are requested, so no draws */
+        s->sample_index = 0;
+        s->cur1d = s->cur2d = 0;
+        return;
+    }
     for (int d = 0; d < s->ndims; d++) {
         double* samp = s->s1d + (size_t)d * n;
         double inv = 1.0 / (double)n;
@@ -116,6 +122,7 @@ static int sampler_next_sample(sampler_t* s) {
 }
 /* pixel.go:60-69 */
 static double sampler_get1d(sampler_t* s) {
+    if (s->random) return orc_pcg_float(&s->rng);   /* random.go:21-23 */
     if (s->cur1d < s->ndims) {
         double v = s->s1d[(size_t)s->cur1d * s->spp + s->sample_index];
         s->cur1d++;
@@ -126,6 +133,11 @@ static double sampler_get1d(sampler_t* s) {
 /* pixel.go:71-80 */
 static v2 sampler_get2d(sampler_t* s) {
     v2 v;
+    if (s->random) {   /* random.go:25-27: X then Y */
+        v.x = orc_pcg_float(&s->rng);
+        v.y = orc_pcg_float(&s->rng);
+        return v;
+    }
     if (s->cur2d < s->ndims) {
         s->cur2d++;
         v.x = 0.0; v.y = 0.0;
@@ -1350,7 +1362,11 @@ static int render_tile(orc_ctx* oc, int64_t tile, film_tile_t* ft, double* s1d_b
     memset(&smp, 0, sizeof(smp));
     smp.xs = rd->sampler_x; smp.ys = rd->sampler_y; smp.spp = rd->sampler_x * rd->sampler_y;
     smp.ndims = rd->n_dims; smp.jitter = rd->jitter; smp.s1d = s1d_buf;
-    orc_pcg_set_sequence(&smp.rng, (uint64_t)tile);   /* integrator.go:318,328 */
+    smp.random = (oc->flags & ORACLE_FLAG_RANDOM_SAMPLER) != 0;
+    if (smp.random) smp.ndims = 0;
+    /* integrator.go:318,328; RandomSampler.Clone = NewRNGWithSeed + SetSequence
+     * (random.go:33-37), which resets the state: the same stream */
+    orc_pcg_set_sequence(&smp.rng, (uint64_t)tile);
 
     const int mb = rd->mode == PBRT_MODE_THROUGHPUT;
     oc->pc.kind = 0;

@@ -8,6 +8,7 @@
 #include "oracle_core.h"
 
 #define ORACLE_FLAG_MIS_RAY 1   /* trace EstimateDirect's (no-op) BSDF-sampled ray */
+#define ORACLE_FLAG_RANDOM_SAMPLER 2   /* sampler.RandomSampler (random.go) with spp = sampler_x * sampler_y */
 
 typedef struct { uint64_t state, inc; } orc_pcg;
 uint32_t orc_pcg_next(orc_pcg* r);
