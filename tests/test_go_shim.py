@@ -1,0 +1,62 @@
+"""The cgo shim (integration/go/pbrtgpu/pbrtgpu.go) against the C ABI.
+
+No Go toolchain exists here, so the Go side is not compiled. This test
+compiles the shim's cgo preamble with gcc and checks that every C identifier
+the Go code uses (functions, types, constants, and the struct fields it sets
+or reads) exists in include/pbrt_gpu.h / include/pbrt_scene.h, so the shim
+cannot drift from the headers.
+"""
+import os
+import re
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SHIM = os.path.join(REPO, "integration", "go", "pbrtgpu", "pbrtgpu.go")
+# cgo pseudo-identifiers and C scalar types, not ABI names
+CGO_BUILTINS = {"GoString", "CString", "GoBytes", "int", "int32_t", "int64_t", "uint8_t", "double", "size_t",
+                "uint64_t", "float", "char"}
+
+
+def shim_parts():
+    src = open(SHIM).read()
+    pre = "\n".join(l[3:] for l in src.splitlines() if l.startswith("// #") and not l.startswith("// #cgo"))
+    names = set(re.findall(r"\bC\.([A-Za-z_]\w*)", src)) - CGO_BUILTINS
+    fields = set()
+    for var, ty in re.findall(r"\bvar (\w+) C\.(\w+)", src):
+        for f in re.findall(r"\b%s\.(\w+)\b" % re.escape(var), src):
+            fields.add((ty, f))
+    return pre, names, fields
+
+
+def test_shim_identifiers_exist_in_the_headers(tmp_path):
+    pre, names, fields = shim_parts()
+    assert "pbrt_gpu.h" in pre and "pbrt_scene.h" in pre
+    hdr = open(os.path.join(REPO, "include", "pbrt_gpu.h")).read() + open(
+        os.path.join(REPO, "include", "pbrt_scene.h")).read()
+    funcs = set(re.findall(r"\b(pbrt_\w+)\s*\(", hdr))
+    body = []
+    for n in sorted(names):
+        if n.isupper() or n.startswith("PBRT_"):
+            body.append(f"    (void)({n});")
+        elif n in funcs:
+            body.append(f"    (void)&{n};")
+        else:
+            body.append(f"    {{ {n}* p_ = 0; (void)p_; }}")   # opaque handles included
+    for ty, f in sorted(fields):
+        body.append(f"    (void)sizeof((({ty}*)0)->{f});")
+    c = tmp_path / "shim_check.c"
+    c.write_text(pre + "\n\nvoid shim_check(void) {\n" + "\n".join(body) + "\n}\n")
+    r = subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-fsyntax-only", "-I", os.path.join(REPO, "include"),
+                        str(c)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert len(names) > 30 and len(fields) >= 10
+
+
+def test_shim_covers_the_render_entry_points():
+    _, names, _ = shim_parts()
+    for n in ("pbrt_gpu_create", "pbrt_gpu_render", "pbrt_gpu_cancel", "pbrt_gpu_last_error", "pbrt_gpu_destroy",
+              "pbrt_gpu_intersect", "pbrt_gpu_intersect_p", "pbrt_film_to_rgba8", "pbrt_sb_build",
+              "pbrt_make_glass", "pbrt_make_mirror", "pbrt_random_sampler"):
+        assert n in names, n
