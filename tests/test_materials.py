@@ -242,3 +242,25 @@ def test_device_oren_nayar_vs_oracle(integrator, mode, sigma):
         film, st = r.render(rd)
     assert st.kernel == abi.PBRT_KERNEL_SERIAL
     assert np.array_equal(bits(film), bits(of))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [abi.PBRT_MODE_EXACT, abi.PBRT_MODE_THROUGHPUT])
+def test_device_readme_scene_with_the_commented_out_glass_sphere(mode):
+    """internal/render/server.go:67-91 (commented out): a glass sphere of radius 5
+    at (50, 2.5, 50) with Kr = Kt = 0.5 and index 1.5, added to the README scene;
+    plus a mirror sphere beside it. Rendered on the serial kernel, bit-exact."""
+    sc = G.Scene.readme(96, 64)
+    glass = sc.add_glass()
+    mirror = sc.add_mirror()
+    for (pos, m) in (((50, 2.5, 50), glass), ((35, 5.0, 45), mirror)):
+        sph = sc.add_sphere(G.translate(0, 0, 0), 5.0)
+        sc.add_primitive(sph, m, G.translate(*pos))
+    sc.build(2)
+    rd = abi.render_desc(2, 2, mode=mode)
+    rc, of, _ = O.render(sc.desc, rd, threads=8)
+    assert rc == 0
+    with G.Renderer(sc) as r:
+        film, st = r.render(rd)
+    assert st.kernel == abi.PBRT_KERNEL_SERIAL
+    assert np.array_equal(bits(film), bits(of))
