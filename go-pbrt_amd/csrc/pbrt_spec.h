@@ -128,6 +128,18 @@ struct PathState {
     int bounces;
     int first;
 };
+// k_paths_ci's variant: the radiance sum lives in the lane's LDS slot (it is
+// only added to, never read, inside a bounce), freeing its registers for the
+// traversals
+struct PathStateLds {
+    Spec* L;
+    Spec beta;
+    Ray ray;
+    int bounces;
+    int first;
+};
+__device__ __forceinline__ void add_L(PathState& s, Spec v) { s.L = s.L + v; }
+__device__ __forceinline__ void add_L(PathStateLds& s, Spec v) { *s.L = *s.L + v; }
 // kWhich: 0 any iteration, 1 only the first (s.first == 1: bounce 1 from the
 // pixel cache, no traversal), 2 only later ones (s.first == 0).
 //
@@ -139,9 +151,9 @@ struct PathState {
 // dead by then, so the any-hit traversal runs with their registers free (no
 // scratch spills). Every value and every draw is the reference's; a panic of
 // the shadow ray or Ld > 10 ends the path at this bounce, as it would have.
-template <int kWhich = 0, class Cache>
+template <int kWhich = 0, class Cache, class State>
 __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, const SpecSampler& ss, Cursor& c,
-                                 PathState& s, int max_depth, double rr_threshold, uint16_t* stack, int& panic,
+                                 State& s, int max_depth, double rr_threshold, uint16_t* stack, int& panic,
                                  int& bounce) {
     const bool first = kWhich == 1 ? true : kWhich == 2 ? false : (s.first != 0);
     SI isect;
@@ -171,7 +183,7 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
     const Spec beta0 = s.beta;
     if (b.n_bxdfs > 0) {   // UniformSampleOneLight (integrator.go:48-77)
         if (nl == 0) {
-            s.L = s.L + smul(s.beta, spec(0));
+            add_L(s, smul(s.beta, spec(0)));
         } else {
             int ln;
             if (sc.dist) {
@@ -188,7 +200,7 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
                     panic = pc.ld_panic[ln];
                     return true;
                 }
-                s.L = s.L + smul(s.beta, ld);
+                add_L(s, smul(s.beta, ld));
             } else {
                 pending = true;
                 shadow = estimate_direct_begin(sc, isect, b, ln, ul, sr, ld_vis);
@@ -231,7 +243,7 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
             panic = PBRT_PANIC_LD_GT_10;
             return true;
         }
-        s.L = s.L + smul(beta0, ld);
+        add_L(s, smul(beta0, ld));
     }
     return done;
 }

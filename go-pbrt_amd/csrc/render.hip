@@ -455,8 +455,12 @@ __host__ __device__ constexpr size_t paths_group_meta_off() {
     return (P * sizeof(PixelCache) + P * 8 + 15) & ~(size_t)15;
 }
 template <int P>
+__host__ __device__ constexpr size_t paths_group_l_off() {   // per-lane radiance sums (PathStateLds)
+    return paths_group_meta_off<P>() + (P + 1) * sizeof(PMeta);
+}
+template <int P>
 __host__ __device__ constexpr int paths_group_lds(int per) {   // bytes, per wave
-    return (int)(paths_group_meta_off<P>() + (P + 1) * sizeof(PMeta) + (size_t)P * per * 8);
+    return (int)(paths_group_l_off<P>() + kWave * sizeof(Spec) + (size_t)P * per * 8);
 }
 // kMB: THROUGHPUT mode, sample k of pixel pi starts from its own stream
 // mb_state(tile, pi, k) instead of the chain's offset state.
@@ -473,7 +477,8 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
     unsigned long long* pkey = (unsigned long long*)(wlds + P * sizeof(PixelCache));
     // per-pixel metadata lives in LDS (not in per-lane register arrays)
     PMeta* meta = (PMeta*)(wlds + paths_group_meta_off<P>());
-    double* s1d = (double*)(wlds + paths_group_meta_off<P>() + (P + 1) * sizeof(PMeta));
+    Spec* Lslot = (Spec*)(wlds + paths_group_l_off<P>()) + lane;
+    double* s1d = (double*)(wlds + paths_group_l_off<P>() + kWave * sizeof(Spec));
     if (lane == 0) {
         int cum = 0;
         for (int j = 0; j < P; j++) {
@@ -524,7 +529,8 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
     const int T = meta[P].cum;
     int base = 0;
     int w = -1, j = 0, k = 0;
-    PathState ps;
+    PathStateLds ps;
+    ps.L = Lslot;
     Cursor c;
     int pnc = 0, bnc = 1;
     for (;;) {
@@ -553,7 +559,7 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
                     c.cur2d = 2;
                     c.k = k;
                     c.kdep = 0;
-                    ps.L = spec(0);
+                    *ps.L = spec(0);
                     ps.beta = spec(1);
                     ps.bounces = 1;
                     ps.first = 1;
@@ -578,9 +584,10 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
             if (done) {
                 const int64_t rec = rec0 + j;
                 double* o = wb.L + (rec * n + k) * 3;
-                o[0] = ps.L.r;
-                o[1] = ps.L.g;
-                o[2] = ps.L.b;
+                const Spec Lp = *ps.L;
+                o[0] = Lp.r;
+                o[1] = Lp.g;
+                o[2] = Lp.b;
                 if (pnc)
                     atomicMin(&pkey[j], ((unsigned long long)k << 32) | ((unsigned long long)(bnc & 0xFFFFFF) << 8) |
                                             (unsigned long long)((pnc + 1) & 0xFF));
