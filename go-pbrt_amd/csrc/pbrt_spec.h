@@ -27,6 +27,7 @@
 #pragma clang fp contract(off)
 
 #include "pbrt_path.h"
+#include <type_traits>
 
 namespace pbrt {
 
@@ -133,6 +134,7 @@ struct PathState {
 // traversals
 struct PathStateLds {
     Spec* L;
+    Spec* aux;   // [0] beta0 and [1] ld_vis of a deferred shadow ray, held across the BSDF sample
     Spec beta;
     Ray ray;
     int bounces;
@@ -178,9 +180,11 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
         wo = pc.wo;
     }
     bool pending = false, shadow = false;   // a deferred L += beta0 * Ld (with a shadow ray)
+    constexpr bool kLdsAux = std::is_same<State, PathStateLds>::value;
     Ray sr;
     Spec ld_vis = spec(0);
-    const Spec beta0 = s.beta;
+    Spec beta0 = s.beta;
+    if constexpr (kLdsAux) s.aux[0] = beta0;
     if (b.n_bxdfs > 0) {   // UniformSampleOneLight (integrator.go:48-77)
         if (nl == 0) {
             add_L(s, smul(s.beta, spec(0)));
@@ -204,6 +208,7 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
             } else {
                 pending = true;
                 shadow = estimate_direct_begin(sc, isect, b, ln, ul, sr, ld_vis);
+                if constexpr (kLdsAux) s.aux[1] = ld_vis;
             }
         }
     }
@@ -237,12 +242,16 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
         if (shadow) {
             const bool occluded = bvh_traverse<true, PBRT_PATHS_LB>(sc, sr, nullptr, stack, panic);
             if (panic) return true;
-            if (!occluded) ld = ld_vis;
+            if (!occluded) {
+                if constexpr (kLdsAux) ld = s.aux[1];
+                else ld = ld_vis;
+            }
         }
         if (max_component(ld) > 10) {
             panic = PBRT_PANIC_LD_GT_10;
             return true;
         }
+        if constexpr (kLdsAux) beta0 = s.aux[0];
         add_L(s, smul(beta0, ld));
     }
     return done;

@@ -460,7 +460,7 @@ __host__ __device__ constexpr size_t paths_group_l_off() {   // per-lane radianc
 }
 template <int P>
 __host__ __device__ constexpr int paths_group_lds(int per) {   // bytes, per wave
-    return (int)(paths_group_l_off<P>() + kWave * sizeof(Spec) + (size_t)P * per * 8);
+    return (int)(paths_group_l_off<P>() + 3 * kWave * sizeof(Spec) + (size_t)P * per * 8);
 }
 // kMB: THROUGHPUT mode, sample k of pixel pi starts from its own stream
 // mb_state(tile, pi, k) instead of the chain's offset state.
@@ -478,7 +478,8 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
     // per-pixel metadata lives in LDS (not in per-lane register arrays)
     PMeta* meta = (PMeta*)(wlds + paths_group_meta_off<P>());
     Spec* Lslot = (Spec*)(wlds + paths_group_l_off<P>()) + lane;
-    double* s1d = (double*)(wlds + paths_group_l_off<P>() + kWave * sizeof(Spec));
+    Spec* aux = (Spec*)(wlds + paths_group_l_off<P>()) + kWave + 2 * lane;
+    double* s1d = (double*)(wlds + paths_group_l_off<P>() + 3 * kWave * sizeof(Spec));
     if (lane == 0) {
         int cum = 0;
         for (int j = 0; j < P; j++) {
@@ -531,6 +532,7 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
     int w = -1, j = 0, k = 0;
     PathStateLds ps;
     ps.L = Lslot;
+    ps.aux = aux;
     Cursor c;
     int pnc = 0, bnc = 1;
     for (;;) {
