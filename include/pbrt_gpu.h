@@ -142,7 +142,7 @@ typedef struct pbrt_bvh_node {
  * n_prims + that index. */
 typedef struct pbrt_mesh_desc {
     int32_t n_vertices, n_triangles;
-    int32_t material;              /* index into materials (Matte)              */
+    int32_t material;              /* index into materials                      */
     int32_t reverse_orientation;   /* flips the geometric normal                */
     const float* p;                /* n_vertices * 3 world-space positions     */
     const int32_t* indices;        /* n_triangles * 3 vertex indices            */
