@@ -858,8 +858,12 @@ __device__ inline Spec bsdf_sample_f(const BSDF& b, V3 woW, V2 u, V3& wi, double
 // sampling (and the Path.Li bookkeeping) needs the kind.
 constexpr int BXDF_TRANSMISSION = 2, BXDF_GLOSSY = 8;
 constexpr int MF_REFL_TYPE = BXDF_REFLECTION | BXDF_GLOSSY, MF_TRANS_TYPE = BXDF_TRANSMISSION | BXDF_GLOSSY;
+// SPEC_PAIR: smooth glass under DirectLighting (allowMultipleLobes false,
+// directlighting.go:76): SpecularReflection(R, FresnelDielectric(1, eta)) if R
+// is not black, then SpecularTransmission(T, 1, eta, Radiance) if T is not
+// (glass.go:58-72); mf_r / mf_t say which exist. Both F and Pdf are 0.
 enum { BXDF_KIND_LAMBERT = 0, BXDF_KIND_SPEC_REFL = 1, BXDF_KIND_FRESNEL_SPEC = 2, BXDF_KIND_MICROFACET = 3,
-       BXDF_KIND_OREN_NAYAR = 4 };
+       BXDF_KIND_OREN_NAYAR = 4, BXDF_KIND_SPEC_PAIR = 5 };
 struct BSDFX {
     int kind;       // BXDF_KIND_*; LAMBERT: `b` is the whole BSDF
     int n;          // number of BxDFs of that kind (MICROFACET: mf_r + mf_t)
@@ -873,7 +877,9 @@ struct BSDFX {
 __device__ __forceinline__ bool bsdfx_nonspecular(const BSDF& b, const BSDFX& x) {
     return x.kind == BXDF_KIND_LAMBERT ? b.n_bxdfs > 0 : (x.kind != BXDF_KIND_FRESNEL_SPEC && x.n > 0);
 }
-__device__ inline int compute_bsdf_x(const DevScene& sc, const SI& si, BSDF& b, BSDFX& x) {
+// multi_lobes: ComputeScatteringFunctions' allowMultipleLobes (interaction.go:217-223),
+// true for Path.Li (path.go:74), false for DirectLighting.Li (directlighting.go:76)
+__device__ inline int compute_bsdf_x(const DevScene& sc, const SI& si, BSDF& b, BSDFX& x, bool multi_lobes = true) {
     const pbrt_material_desc& m =
         sc.materials[si.prim < sc.n_prims ? sc.prims[si.prim].material
                                           : sc.mesh.mesh_mat[tri_mesh(sc, si.prim - sc.n_prims)]];
@@ -938,6 +944,13 @@ __device__ inline int compute_bsdf_x(const DevScene& sc, const SI& si, BSDF& b, 
         x.kind = BXDF_KIND_MICROFACET;
         x.ax = m.u_roughness;
         x.ay = m.v_roughness;
+        x.mf_r = is_black(R) ? 0 : 1;
+        x.mf_t = is_black(T) ? 0 : 1;
+        x.n = x.mf_r + x.mf_t;
+        return 0;
+    }
+    if (!multi_lobes) {
+        x.kind = BXDF_KIND_SPEC_PAIR;
         x.mf_r = is_black(R) ? 0 : 1;
         x.mf_t = is_black(T) ? 0 : 1;
         x.n = x.mf_r + x.mf_t;
@@ -1454,47 +1467,107 @@ __device__ __noinline__ Spec path_li(const DevScene& sc, Thread& t, Ray ray, int
     return L;
 }
 
-// DirectLighting.Li at depth 0 (directlighting.go:62-104)
+// SamplerIntegratorSpecularTransmit's BSDF.SampleF(wo, u, Transmission|Specular)
+// (integrator.go:383-385, reflection.go:188-253) on a SPEC_PAIR BSDF: the one
+// matching BxDF is SpecularTransmission (reflection.go:428-451); returns the
+// LOCAL-frame wi (#7). pdf 0: no transmission (no such BxDF, wo.z == 0, or
+// total internal reflection).
+__device__ inline Spec spec_trans_sample(const BSDF& b, const BSDFX& x, V3 woW, V2 u, V3& wi, double& pdf) {
+    wi = V3{0, 0, 0};
+    pdf = 0;
+    if (x.kind != BXDF_KIND_SPEC_PAIR || !x.mf_t) return spec(0);
+    (void)u;   // one matching component: comp 0, u unused by SpecularTransmission
+    const V3 wo = w2l(b, woW);
+    if (wo.z == 0.0) return spec(0);
+    double eta_i, eta_t;
+    if (wo.z > 0) { eta_i = 1.0; eta_t = x.eta; } else { eta_i = x.eta; eta_t = 1.0; }
+    V3 n{0, 0, 1};
+    if (dot(n, wo) < 0.0) n = muls(n, -1);   // FaceForward (geometry.go:111-116)
+    const double eta = eta_i / eta_t;        // Refract (reflection.go:106-118)
+    const double cos_i = dot(n, wo);
+    const double sin2_i = gomath::max(0.0, 1 - cos_i * cos_i);
+    const double sin2_t = eta * eta * sin2_i;
+    if (sin2_t >= 1) return spec(0);
+    const double cos_t = gomath::sqrt(1 - sin2_t);
+    const V3 w = muls(wo, -eta) + muls(n, eta * cos_i - cos_t);
+    const double F = fr_dielectric(w.z, 1.0, x.eta);   // FresnelDielectric(etaA, etaB)
+    Spec ft = smul(x.t, spec(1 - F));
+    ft = smuls(ft, (eta_i * eta_i) / (eta_t * eta_t));  // mode == Radiance
+    wi = w;
+    pdf = 1;
+    return sdivs(ft, gomath::abs(w.z));
+}
+
+// DirectLighting.Li (directlighting.go:62-104) from depth 0. SpecularReflect
+// matches no supported BxDF (none is Reflection|Specular: SpecularReflection is
+// typed Reflection|Diffuse, reflection.go:538-544) and only draws its Get2D;
+// SpecularTransmit recurses into Li at depth + 2 (#23) through a smooth glass's
+// SpecularTransmission. The recursion is linear, so it runs as a loop that
+// keeps each level's own radiance, f and |wi.ns|/pdf, then folds them back
+// innermost first as the reference's returns do: L_k = own_k + (f_k * L_k+1) * w_k.
+constexpr int kDlMaxLevels = 32;   // maxDepth <= 64 (host check)
 __device__ __noinline__ Spec direct_li(const DevScene& sc, Thread& t, Ray ray, int max_depth, int strategy,
                                        bool fidelity) {
-    Spec L = spec(0);
-    SI si;
-    t.bounce = 1;
-    t.closest_rays++;
-    if (!bvh_traverse<false>(sc, ray, &si, t.stack, t.panic)) {
-        for (int i = 0; i < sc.n_lights; i++) L = L + spec(0);
-        return L;
-    }
-    if (t.panic) return L;
-    BSDF b;
-    BSDFX x;   // Mirror/Glass: F and Pdf are 0 and SpecularReflect/Transmit match no lobe
-    if (compute_bsdf_x(sc, si, b, x) < 0) { t.panic = -1; return L; }
-    L = L + spec(0);   // si.Le(si.Wo): no primitive carries an area light
-    if (sc.n_lights > 0) {
-        if (strategy == PBRT_DL_UNIFORM_SAMPLE_ALL) {
-            // UniformSampleAllLights (integrator.go:23-46); clones carry no arrays (#23)
-            Spec acc = spec(0);
-            for (int j = 0; j < sc.n_lights; j++) {
-                V2 ul = get2d(t);
-                const V2 us = get2d(t);
-                t.shadow_rays++;
-                acc = acc + estimate_direct_x(sc, t.stack, t.panic, si, b, x, j, ul);
-                if (fidelity && !t.panic) estimate_direct_mis_ray(sc, t.stack, t.panic, si, b, j, us);
-                if (t.panic) return L;
-            }
-            L = L + acc;
-        } else {
-            L = L + uniform_sample_one_light(sc, t, si, b, x, nullptr, fidelity);
+    Spec own[kDlMaxLevels], fk[kDlMaxLevels];
+    double wk[kDlMaxLevels];
+    int levels = 0;
+    Spec L;
+    for (int depth = 0;; depth += 2) {
+        L = spec(0);
+        SI si;
+        t.bounce = depth + 1;
+        t.closest_rays++;
+        if (!bvh_traverse<false>(sc, ray, &si, t.stack, t.panic)) {
+            for (int i = 0; i < sc.n_lights; i++) L = L + spec(0);
+            break;
         }
-    }
-    if (0 + 1 < max_depth) {
-        // SpecularReflect / SpecularTransmit (integrator.go:352-422): one Get2D
-        // each, black for a Lambertian-only BSDF
-        get2d(t);
+        if (t.panic) break;
+        BSDF b;
+        BSDFX x;   // Mirror: F and Pdf are 0 and SpecularReflect/Transmit match no lobe
+        if (compute_bsdf_x(sc, si, b, x, false) < 0) { t.panic = -1; break; }
+        L = L + spec(0);   // si.Le(si.Wo): no primitive carries an area light
+        if (sc.n_lights > 0) {
+            if (strategy == PBRT_DL_UNIFORM_SAMPLE_ALL) {
+                // UniformSampleAllLights (integrator.go:23-46); clones carry no arrays (#23)
+                Spec acc = spec(0);
+                for (int j = 0; j < sc.n_lights; j++) {
+                    V2 ul = get2d(t);
+                    const V2 us = get2d(t);
+                    t.shadow_rays++;
+                    acc = acc + estimate_direct_x(sc, t.stack, t.panic, si, b, x, j, ul);
+                    if (fidelity && !t.panic) estimate_direct_mis_ray(sc, t.stack, t.panic, si, b, j, us);
+                    if (t.panic) break;
+                }
+                if (t.panic) break;
+                L = L + acc;
+            } else {
+                L = L + uniform_sample_one_light(sc, t, si, b, x, nullptr, fidelity);
+                if (t.panic) break;
+            }
+        }
+        if (!(depth + 1 < max_depth)) break;
+        get2d(t);           // SpecularReflect (integrator.go:352-355): black
         L = L + spec(0);
-        get2d(t);
-        L = L + spec(0);
+        const V2 u = get2d(t);   // SpecularTransmit (integrator.go:383-385)
+        V3 wi;
+        double pdf;
+        const Spec f = spec_trans_sample(b, x, si.wo, u, wi, pdf);
+        const double adn = absdot(wi, si.sn);
+        if (!(pdf > 0 && !is_black(f) && adn != 0.0) || levels == kDlMaxLevels) {
+            L = L + spec(0);
+            break;
+        }
+        own[levels] = L;
+        fk[levels] = f;
+        wk[levels] = adn / pdf;
+        levels++;
+        // SpawnRay (interaction.go:68-77) with the local-frame wi
+        ray.o = offset_ray_origin(si.p, si.perr, si.n, wi);
+        ray.d = wi;
+        ray.tmax = kInf;
+        ray.time = si.time;
     }
+    for (int k = levels - 1; k >= 0; k--) L = own[k] + smuls(smul(fk[k], L), wk[k]);
     return L;
 }
 

@@ -2563,6 +2563,8 @@ int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
         return set_err(c, PBRT_E_UNSUPPORTED, "filter radius must be in (0, tile_size)");
     if ((rd->flags & PBRT_FLAG_PANIC_FIDELITY) && c->non_matte)
         return set_err(c, PBRT_E_UNSUPPORTED, "panic fidelity covers Matte scenes only");
+    if (rd->integrator == PBRT_INTEGRATOR_DIRECT_LIGHTING && c->non_matte && rd->max_depth > 2 * kDlMaxLevels)
+        return set_err(c, PBRT_E_UNSUPPORTED, "DirectLighting through glass: maxDepth must be <= 64");
     RenderParams& rp = c->rp;
     std::memset(&rp, 0, sizeof(rp));
     rp.film_min_x = f.crop_min_x;

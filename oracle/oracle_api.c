@@ -134,6 +134,9 @@ int oracle_render(const pbrt_scene_desc* sc, const pbrt_render_desc* rd, int n_t
     return orc_render(sc, rd, n_threads, flags, film_xyz, stats);
 }
 int64_t oracle_num_tiles(const pbrt_scene_desc* sc, const pbrt_render_desc* rd) { return orc_num_tiles(sc, rd); }
+int oracle_tile_draws(const pbrt_scene_desc* sc, const pbrt_render_desc* rd, int64_t tile, int64_t* out) {
+    return orc_tile_draws(sc, rd, tile, out);
+}
 int oracle_intersect(const pbrt_scene_desc* sc, const double* rays, size_t n, int closest, double* out) {
     return orc_intersect(sc, rays, n, closest, out);
 }

@@ -46,7 +46,11 @@ static __thread uint64_t orc_flops_light;
 #define PCG32_DEFAULT_STATE 0x853c49e6748fea9bULL
 #define PCG32_MULT 0x5851f42d4c957f2dULL
 
+/* PCG32 draws made by this thread (orc_tile_draws: per-pixel draw counts) */
+static __thread uint64_t orc_draws;
+
 uint32_t orc_pcg_next(orc_pcg* r) {
+    orc_draws++;
     uint64_t old = r->state;
     r->state = old * PCG32_MULT + r->inc;
     uint32_t xorshifted = (uint32_t)(((old >> 18) ^ old) >> 27);
@@ -521,11 +525,16 @@ static int prim_material(const pbrt_scene_desc* sc, int prim) {
 }
 
 /* ========================================== BSDF (Matte, Mirror, Glass) */
-/* kind of the single BxDF: LambertianReflection (matte.go), SpecularReflection
- * with FresnelNoOp (mirror.go), or FresnelSpecular (smooth glass with multiple
- * lobes allowed, glass.go:46-47 -- Path.Li passes allowMultipleLobes true). */
+/* kind of the BSDF's BxDFs: LambertianReflection (matte.go), SpecularReflection
+ * with FresnelNoOp (mirror.go), FresnelSpecular (smooth glass with multiple
+ * lobes allowed, glass.go:45-46 -- Path.Li passes allowMultipleLobes true),
+ * rough glass's microfacet pair, OrenNayar, or SPEC_PAIR: smooth glass without
+ * multiple lobes (DirectLighting.Li passes false, directlighting.go:76), i.e.
+ * SpecularReflection(R, FresnelDielectric(1, eta)) if R is not black, then
+ * SpecularTransmission(T, 1, eta, Radiance) if T is not black (glass.go:58-72);
+ * mf_r / mf_t say which of the two exist, in that order. */
 enum { BXDF_KIND_LAMBERT = 0, BXDF_KIND_SPEC_REFL = 1, BXDF_KIND_FRESNEL_SPEC = 2, BXDF_KIND_MICROFACET = 3,
-       BXDF_KIND_OREN_NAYAR = 4 };
+       BXDF_KIND_OREN_NAYAR = 4, BXDF_KIND_SPEC_PAIR = 5 };
 typedef struct {
     v3 ns, ng, ss, ts;
     int n_bxdfs;        /* 0 or 1; 0-2 for MICROFACET (mf_r + mf_t)           */
@@ -550,12 +559,15 @@ typedef struct {
 #define FRESNEL_SPEC_TYPE (BXDF_REFLECTION | BXDF_TRANSMISSION | BXDF_SPECULAR)   /* reflection.go:465-474 */
 #define MF_REFL_TYPE (BXDF_REFLECTION | BXDF_GLOSSY)     /* reflection.go:670-677 */
 #define MF_TRANS_TYPE (BXDF_TRANSMISSION | BXDF_GLOSSY)  /* reflection.go:738-747 */
+#define SPEC_TRANS_TYPE (BXDF_TRANSMISSION | BXDF_SPECULAR)   /* reflection.go:405-415 */
 
 static double inv_pi(void) { FL(1); return 1.0 / go_Pi; }   /* pkg/math InvPi = 1.0 / Pi */
 static int matches_flags(int t, int flags) { return (t & flags) == t; }
 
-/* matte.go:21-37 + reflection.go:128-140 + checkerboard.go:30-40 */
-static int material_bsdf(const pbrt_scene_desc* sc, const si_t* si, bsdf_t* b) {
+/* matte.go:21-37 + reflection.go:128-140 + checkerboard.go:30-40; multi_lobes
+ * is ComputeScatteringFunctions' allowMultipleLobes (interaction.go:217-223):
+ * true for Path.Li (path.go:74), false for DirectLighting.Li (directlighting.go:76) */
+static int material_bsdf(const pbrt_scene_desc* sc, const si_t* si, bsdf_t* b, int multi_lobes) {
     const pbrt_material_desc* m = &sc->materials[prim_material(sc, si->prim)];
     b->ns = si->sn;
     b->ng = si->n;
@@ -594,10 +606,17 @@ static int material_bsdf(const pbrt_scene_desc* sc, const si_t* si, bsdf_t* b) {
             b->t = T;
             return 0;
         }
-        b->n_bxdfs = 1;
-        b->kind = BXDF_KIND_FRESNEL_SPEC;
         b->r = R;
         b->t = T;
+        if (!multi_lobes) {   /* glass.go:58-72 with isSpecular */
+            b->kind = BXDF_KIND_SPEC_PAIR;
+            b->mf_r = !s_is_black(R);
+            b->mf_t = !s_is_black(T);
+            b->n_bxdfs = b->mf_r + b->mf_t;
+            return 0;
+        }
+        b->n_bxdfs = 1;
+        b->kind = BXDF_KIND_FRESNEL_SPEC;
         return 0;
     }
     spec r;
@@ -750,6 +769,11 @@ static spec bsdf_f(const bsdf_t* b, v3 woW, v3 wiW, int flags) {
         if (b->mf_t && matches_flags(MF_TRANS_TYPE, flags) && !reflect) f = s_add(f, mf_trans_f(b, wo, wi));
         return f;
     }
+    if (b->kind == BXDF_KIND_SPEC_PAIR) {   /* both F are 0 (reflection.go:424-426, 553-555) */
+        if (b->mf_r && matches_flags(SPEC_REFL_TYPE, flags) && reflect) f = s_add(f, S3(0, 0, 0));
+        if (b->mf_t && matches_flags(SPEC_TRANS_TYPE, flags) && !reflect) f = s_add(f, S3(0, 0, 0));
+        return f;
+    }
     if (b->n_bxdfs && b->kind == BXDF_KIND_LAMBERT && matches_flags(LAMBERT_TYPE, flags) && reflect)
         f = s_add(f, s_muls(b->r, inv_pi()));
     else if (b->n_bxdfs && b->kind == BXDF_KIND_OREN_NAYAR && matches_flags(LAMBERT_TYPE, flags) && reflect)
@@ -777,6 +801,9 @@ static double bsdf_pdf(const bsdf_t* b, v3 woW, v3 wiW, int flags) {
     } else if (b->kind == BXDF_KIND_MICROFACET) {
         if (b->mf_r && matches_flags(MF_REFL_TYPE, flags)) { matching++; pdf += mf_refl_pdf(b, wo, wi); }
         if (b->mf_t && matches_flags(MF_TRANS_TYPE, flags)) { matching++; pdf += mf_trans_pdf(b, wo, wi); }
+    } else if (b->kind == BXDF_KIND_SPEC_PAIR) {   /* both Pdf are 0 (reflection.go:461-463, 572-574) */
+        if (b->mf_r && matches_flags(SPEC_REFL_TYPE, flags)) { matching++; pdf += 0.0; }
+        if (b->mf_t && matches_flags(SPEC_TRANS_TYPE, flags)) { matching++; pdf += 0.0; }
     } else {   /* reflection.go:534-536, 572-574: Pdf is 0 */
         int ty = b->kind == BXDF_KIND_SPEC_REFL ? SPEC_REFL_TYPE : FRESNEL_SPEC_TYPE;
         if (matches_flags(ty, flags)) { matching++; pdf += 0.0; }
@@ -847,6 +874,8 @@ static spec bsdf_sample_f_t(const bsdf_t* b, v3 woW, v2 u, int t, v3* wi_out, do
     int matching = (b->n_bxdfs && matches_flags(ty, t)) ? 1 : 0;
     if (b->kind == BXDF_KIND_MICROFACET)
         matching = (b->mf_r && matches_flags(MF_REFL_TYPE, t)) + (b->mf_t && matches_flags(MF_TRANS_TYPE, t));
+    if (b->kind == BXDF_KIND_SPEC_PAIR)
+        matching = (b->mf_r && matches_flags(SPEC_REFL_TYPE, t)) + (b->mf_t && matches_flags(SPEC_TRANS_TYPE, t));
     *wi_out = V3(0, 0, 0);
     *pdf_out = 0;
     *type_out = 0;
@@ -865,6 +894,47 @@ static spec bsdf_sample_f_t(const bsdf_t* b, v3 woW, v2 u, int t, v3* wi_out, do
         spec f = s_divs(s_mul(S3(1, 1, 1), b->r), gm_abs(wi.z));
         *wi_out = wi;
         *pdf_out = 1.0;
+        return f;
+    }
+    if (b->kind == BXDF_KIND_SPEC_PAIR) {
+        /* the comp-th matching BxDF, in BSDF order (reflection.go:194-206) */
+        const int refl_ok = b->mf_r && matches_flags(SPEC_REFL_TYPE, t);
+        const int pick_refl = refl_ok && comp == 0.0;
+        v3 wi;
+        spec f;
+        if (pick_refl) {   /* SpecularReflection.SampleF with FresnelDielectric(1, eta) (reflection.go:557-562) */
+            wi = V3(-wo.x, -wo.y, wo.z);
+            double F = fr_dielectric(wi.z, 1.0, b->eta);
+            f = s_divs(s_mul(S3(F, F, F), b->r), gm_abs(wi.z));
+        } else {           /* SpecularTransmission.SampleF (reflection.go:428-451) */
+            double eta_i, eta_t;
+            if (wo.z > 0) { eta_i = 1.0; eta_t = b->eta; } else { eta_i = b->eta; eta_t = 1.0; }
+            v3 n = V3(0, 0, 1);
+            if (v_dot(n, wo) < 0.0) n = v_muls(n, -1);   /* FaceForward (geometry.go:111-116) */
+            double eta = eta_i / eta_t;                   /* Refract (reflection.go:106-118) */
+            double cos_i = v_dot(n, wo);
+            double sin2_i = go_max(0, 1 - cos_i * cos_i);
+            double sin2_t = eta * eta * sin2_i;
+            if (sin2_t >= 1) return S3(0, 0, 0);          /* pdf 0 (reflection.go:440-442, 226-228) */
+            double cos_t = sqrt(1 - sin2_t);
+            wi = v_add(v_muls(wo, -eta), v_muls(n, eta * cos_i - cos_t));
+            double F = fr_dielectric(wi.z, 1.0, b->eta);  /* t.fresnel = FresnelDielectric(etaA, etaB) */
+            spec ft = s_mul(b->t, S3(1 - F, 1 - F, 1 - F));
+            ft = s_muls(ft, (eta_i * eta_i) / (eta_t * eta_t));   /* mode == Radiance (directlighting.go:76) */
+            f = s_divs(ft, gm_abs(wi.z));
+        }
+        double pdf = 1.0;   /* both SampleF return pdf 1 and sampled type 0 */
+        if (matching > 1) {
+            /* reflection.go:233-250: a non-specular pick (SpecularReflection is typed
+             * Reflection|Diffuse) adds the other's Pdf (0) and re-evaluates f as the
+             * sum of the matching F (all 0); either pick divides pdf by matching */
+            if (pick_refl) pdf += 0.0;
+            pdf /= (double)matching;
+            if (pick_refl) f = S3(0, 0, 0);
+        }
+        *wi_out = wi;
+        *pdf_out = pdf;
+        *type_out = 0;
         return f;
     }
     if (b->kind == BXDF_KIND_FRESNEL_SPEC) {
@@ -1154,7 +1224,7 @@ static spec path_li(orc_ctx* oc, sampler_t* smp, ray_t ray) {
         oc->closest_rays++;
         if (!orc_bvh_intersect(oc, &ray, &isect)) break;
         bsdf_t b;
-        if (material_bsdf(sc, &isect, &b) < 0) { oc->unsupported = 1; break; }
+        if (material_bsdf(sc, &isect, &b, 1) < 0) { oc->unsupported = 1; break; }
         if (b.n_bxdfs > 0 && b.kind != BXDF_KIND_FRESNEL_SPEC) {   /* NumComponents(BSDFAll &^ BSDFSpecular) > 0 */
 #ifdef ORACLE_COUNT_FLOPS
             const uint64_t f0 = orc_flops;
@@ -1201,20 +1271,52 @@ static spec path_li(orc_ctx* oc, sampler_t* smp, ray_t ray) {
     return L;
 }
 
-/* pkg/integrator/directlighting.go:62-104 (depth 0 from renderWorker) */
-static spec direct_li(orc_ctx* oc, sampler_t* smp, ray_t ray) {
+/* pkg/integrator/directlighting.go:62-104 DirectLighting.Li at `depth`
+ * (renderWorker calls it with 0). A smooth glass carries SpecularTransmission
+ * (allowMultipleLobes false, directlighting.go:76), so SpecularTransmit
+ * recurses here. */
+static spec direct_li_d(orc_ctx* oc, sampler_t* smp, ray_t ray, int depth);
+
+/* SamplerIntegratorSpecularReflect / -Transmit (integrator.go:352-422) with
+ * BSDF.SampleF flags t = Reflection|Specular or Transmission|Specular. The
+ * Get2D is drawn first (an argument of SampleF); wi is the LOCAL-frame
+ * direction SampleF returns (#7), used for |wi.ns|, SpawnRay and the recursion;
+ * Li runs at depth + 1 where `depth` already is the caller's depth + 1 (#23). */
+static spec specular_bounce(orc_ctx* oc, sampler_t* smp, const si_t* si, const bsdf_t* b, int depth, int t) {
+    v2 u = sampler_get2d(smp);
+    v3 wi; double pdf; int ty;
+    spec f = bsdf_sample_f_t(b, si->wo, u, t, &wi, &pdf, &ty);
+    if (ty == -1) {   /* not reachable: no BxDF of rough glass matches a specular flag set */
+        oc->pc.kind = PBRT_PANIC_NIL_DEREF;
+        longjmp(oc->pc.jb, 1);
+    }
+    double adn = v_absdot(wi, si->sn);
+    if (pdf > 0 && !s_is_black(f) && adn != 0.0) {
+        /* interaction.go:68-77 SpawnRay; the differentials never reach an output (#27) */
+        ray_t rd;
+        rd.o = offset_ray_origin(si->p, si->perr, si->n, wi);
+        rd.d = wi;
+        rd.tmax = INFINITY;
+        rd.time = si->time;
+        spec li = direct_li_d(oc, smp, rd, depth + 1);
+        return s_muls(s_mul(f, li), adn / pdf);
+    }
+    return S3(0, 0, 0);
+}
+
+static spec direct_li_d(orc_ctx* oc, sampler_t* smp, ray_t ray, int depth) {
     const pbrt_scene_desc* sc = oc->scene;
     const pbrt_render_desc* rd = oc->rd;
     spec L = S3(0, 0, 0);
     si_t si;
-    oc->cur_bounce = 1;
+    oc->cur_bounce = depth + 1;   /* panic report: 1 + the recursion depth */
     oc->closest_rays++;
     if (!orc_bvh_intersect(oc, &ray, &si)) {
-        for (int i = 0; i < sc->n_lights; i++) L = s_add(L, S3(0, 0, 0));
+        for (int i = 0; i < sc->n_lights; i++) L = s_add(L, S3(0, 0, 0));   /* Light.Le: 0 */
         return L;
     }
     bsdf_t b;
-    if (material_bsdf(sc, &si, &b) < 0) { oc->unsupported = 1; return L; }
+    if (material_bsdf(sc, &si, &b, 0) < 0) { oc->unsupported = 1; return L; }
     L = s_add(L, S3(0, 0, 0));       /* si.Le(si.Wo): no area-light prims  */
     if (sc->n_lights > 0) {
         if (rd->dl_strategy == PBRT_DL_UNIFORM_SAMPLE_ALL) {
@@ -1230,16 +1332,17 @@ static spec direct_li(orc_ctx* oc, sampler_t* smp, ray_t ray) {
             L = s_add(L, uniform_sample_one_light(oc, smp, &si, &b, NULL));
         }
     }
-    if (0 + 1 < rd->max_depth) {
-        /* integrator.go:352-422: Lambertian has no specular lobe; each call
-         * still consumes one Get2D and returns black. */
-        sampler_get2d(smp);
-        L = s_add(L, S3(0, 0, 0));
-        sampler_get2d(smp);
-        L = s_add(L, S3(0, 0, 0));
+    if (depth + 1 < rd->max_depth) {
+        /* directlighting.go:97-101. No supported BxDF is Reflection|Specular
+         * (SpecularReflection is typed Reflection|Diffuse, reflection.go:538-544),
+         * so SpecularReflect only draws its Get2D; SpecularTransmit follows a
+         * smooth glass's SpecularTransmission. */
+        L = s_add(L, specular_bounce(oc, smp, &si, &b, depth + 1, BXDF_REFLECTION | BXDF_SPECULAR));
+        L = s_add(L, specular_bounce(oc, smp, &si, &b, depth + 1, BXDF_TRANSMISSION | BXDF_SPECULAR));
     }
     return L;
 }
+static spec direct_li(orc_ctx* oc, sampler_t* smp, ray_t ray) { return direct_li_d(oc, smp, ray, 0); }
 
 /* =================================================================== camera */
 /* camera.go:192-242 GenerateRayDifferential (differentials have no effect, #27) */
@@ -1376,6 +1479,7 @@ static int render_tile(orc_ctx* oc, int64_t tile, film_tile_t* ft, double* s1d_b
         for (int64_t px = x0; px < x1; px++) {
             oc->cur_px = px; oc->cur_py = py;
             const uint64_t pi = (uint64_t)((py - y0) * (x1 - x0) + (px - x0));
+            const uint64_t draws0 = orc_draws;
             if (mb) smp.rng.state = mb_state((uint64_t)tile, pi, 0);
             sampler_start_pixel(&smp);
             while (sampler_next_sample(&smp)) {
@@ -1396,9 +1500,31 @@ static int render_tile(orc_ctx* oc, int64_t tile, film_tile_t* ft, double* s1d_b
                 if (s_has_nans(L)) L = S3(0.1, 0.1, 0.1);    /* integrator.go:256-262 */
                 film_tile_add(&sc->film, ft, fx, fy, L, 1.0);
             }
+            if (oc->pixel_draws) oc->pixel_draws[pi] = (int64_t)(orc_draws - draws0);
         }
     }
     return 0;
+}
+
+/* PCG32 draws each pixel of `tile` consumes (StartPixel + its samples), row-major
+ * in the tile; out holds tile_size^2 entries. Returns 0, or the render_tile status. */
+int orc_tile_draws(const pbrt_scene_desc* sc, const pbrt_render_desc* rd, int64_t tile, int64_t* out) {
+    orc_ctx oc;
+    memset(&oc, 0, sizeof(oc));
+    oc.scene = sc; oc.rd = rd;
+    oc.mesh = orc_mesh_get(sc);
+    oc.pixel_draws = out;
+    orc_light_distribution(sc, rd, &oc.dist);
+    const int spp = rd->sampler_x * rd->sampler_y;
+    double* s1d = (double*)malloc(sizeof(double) * (size_t)spp * (size_t)(rd->n_dims > 0 ? rd->n_dims : 1));
+    int64_t maxw = rd->tile_size + 2 * (int64_t)(sc->film.filter_radius_x + 2);
+    int64_t maxh = rd->tile_size + 2 * (int64_t)(sc->film.filter_radius_y + 2);
+    film_tile_t ft;
+    ft.contrib = (double*)malloc(sizeof(double) * (size_t)(maxw * maxh * 3));
+    int rc = render_tile(&oc, tile, &ft, s1d);
+    free(ft.contrib);
+    free(s1d);
+    return rc;
 }
 
 /* ================================================================ driver */

@@ -27,6 +27,7 @@ typedef struct {
     int unsupported;
     uint64_t paths, camera_samples, closest_rays, shadow_rays;
     const struct orc_mesh* mesh;   /* triangle meshes of the scene (extension), or NULL */
+    int64_t* pixel_draws;          /* orc_tile_draws: PCG32 draws per pixel of the tile, or NULL */
 } orc_ctx;
 
 typedef struct {
@@ -46,6 +47,7 @@ void orc_film_tile_bounds(const pbrt_scene_desc* sc, int64_t x0, int64_t y0, int
                           int64_t* px0, int64_t* py0, int64_t* px1, int64_t* py1);
 int orc_render(const pbrt_scene_desc* sc, const pbrt_render_desc* rd, int n_threads, int flags,
                double* film_xyz, orc_stats* stats);
+int orc_tile_draws(const pbrt_scene_desc* sc, const pbrt_render_desc* rd, int64_t tile, int64_t* out);
 int orc_intersect(const pbrt_scene_desc* sc, const double* rays, size_t n, int closest, double* out);
 
 #endif

@@ -108,6 +108,7 @@ def _bind(L):
         L.oracle_num_tiles.argtypes = [P(abi.SceneDesc), P(abi.RenderDesc)]
         L.oracle_num_tiles.restype = C.c_int64
         L.oracle_intersect.argtypes = [P(abi.SceneDesc), P(d), C.c_size_t, C.c_int, P(d)]
+        L.oracle_tile_draws.argtypes = [P(abi.SceneDesc), P(abi.RenderDesc), C.c_int64, P(C.c_int64)]
         L.oracle_light_distribution.argtypes = [P(abi.SceneDesc), P(abi.RenderDesc), P(abi.DistributionDesc)]
         L.oracle_spawn_ray_to.argtypes = [P(d), P(d)]
         L.oracle_triangle_hit.argtypes = [P(d), P(d), P(d)]
@@ -157,6 +158,16 @@ def render(desc, rd, threads=None, flags=0, flops=False):
     st = OracleStats()
     rc = lib(flops).oracle_render(C.byref(desc), C.byref(rd), threads, flags, dptr(film), C.byref(st))
     return rc, film, st
+
+
+def tile_draws(desc, rd, tile):
+    """PCG32 draws per pixel of `tile` (StartPixel + its samples), row-major with the
+    tile's own width, in a tile_size^2 array (a ragged tile leaves the tail 0).
+    Returns (rc, counts)."""
+    ts = int(rd.tile_size)
+    out = np.zeros(ts * ts, dtype=np.int64)
+    rc = lib().oracle_tile_draws(C.byref(desc), C.byref(rd), tile, out.ctypes.data_as(C.POINTER(C.c_int64)))
+    return rc, out
 
 
 def intersect(desc, rays, closest=True):

@@ -10,8 +10,11 @@ Quirks restated (and therefore tested here):
 - FresnelSpecular's radiance scale is etaI^2 / (etaT / etaT) = etaI^2;
 - smooth glass is a single specular lobe: no light sample, so its paths consume
   fewer draws per bounce;
-- DirectLighting's SpecularReflect/Transmit match neither lobe, so both
-  materials render there exactly like a black Matte;
+- DirectLighting asks for one lobe per BxDF (directlighting.go:76), so smooth
+  glass is SpecularReflection + SpecularTransmission there (glass.go:58-72):
+  SpecularReflect matches no lobe (SpecularReflection is Reflection|Diffuse),
+  SpecularTransmit refracts and recurses into Li at depth + 2; a Mirror renders
+  under DirectLighting exactly like a black Matte;
 - rough glass (MicrofacetReflection + MicrofacetTransmission over
   TrowbridgeReitz, pkg/pbrt/microfacet.go, reflection.go:670-835): SampleWH
   shadows its result and returns nil, so any BSDF.SampleF on it dereferences
@@ -26,6 +29,8 @@ No reference test covers these materials and there is no Go toolchain here:
 device-vs-oracle parity is bit-exact but "parity unpinned" against Go itself.
 The oracle's FrDielectric is pinned by closed forms below.
 """
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -34,7 +39,8 @@ import pbrtgpu as G
 from pbrtgpu import abi
 
 
-def material_scene(kind="both", w=32, h=24, rough=0.0, area=True, kt=(0.5, 0.5, 0.5), sigma=0.0):
+def material_scene(kind="both", w=32, h=24, rough=0.0, area=True, kt=(0.5, 0.5, 0.5), sigma=0.0,
+                   glass_kr=(0.5, 0.5, 0.5)):
     """A floor, a glass sphere, a mirror sphere and a matte sphere, lit by a
     point light and an area-light sphere. kind: "both" | "matte" (the two
     special spheres matte) | "black" (the two special spheres black matte)."""
@@ -44,7 +50,7 @@ def material_scene(kind="both", w=32, h=24, rough=0.0, area=True, kt=(0.5, 0.5, 
     s.add_primitive(floor, chk)
     red = s.add_matte((0.6, 0.1, 0.1), sigma=sigma)
     if kind == "both":
-        glass = s.add_glass(kt=kt, u_roughness=rough, v_roughness=0.5 * rough)   # server.go:80-87's glass
+        glass = s.add_glass(kr=glass_kr, kt=kt, u_roughness=rough, v_roughness=0.5 * rough)   # server.go:80-87
         mirror = s.add_mirror()
     elif kind == "matte":
         glass = mirror = s.add_matte((0.5, 0.5, 0.5))
@@ -90,13 +96,65 @@ def test_oracle_materials_render_deterministically():
     assert not np.array_equal(f1, fm)   # the glass and mirror spheres are in view
 
 
-def test_oracle_direct_lighting_sees_glass_and_mirror_as_black_matte():
+def test_oracle_direct_lighting_mirror_is_black_matte():
+    """A Mirror's SpecularReflection is typed Reflection|Diffuse (reflection.go:538-544):
+    DirectLighting's SpecularReflect (Reflection|Specular) and SpecularTransmit match
+    no lobe, its F is 0, and it renders exactly like a black Matte (same draws)."""
     for strategy in (abi.PBRT_DL_UNIFORM_SAMPLE_ALL, abi.PBRT_DL_UNIFORM_SAMPLE_ONE):
         rd = abi.render_desc(2, 2, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING, dl_strategy=strategy)
-        sa, sb = material_scene(), material_scene("black")
+        sa, sb = material_scene(kt=(0, 0, 0), glass_kr=(0, 0, 0)), material_scene("black")
         rc, fa, _ = O.render(sa.desc, rd, threads=8)
         rc2, fb, _ = O.render(sb.desc, rd, threads=8)
         assert rc == rc2 == 0 and np.array_equal(bits(fa), bits(fb))
+
+
+def readme_glass_scene(w=96, h=64, special="glass", mirror=False):
+    """internal/render/server.go:67-91 (commented out): the README scene plus a
+    sphere of radius 5 at (50, 2.5, 50) made of NewGlass(Kr = Kt = 0.5, index 1.5)
+    -- the commented code attaches the checkerboard `m`, the glass it defines is
+    what image.png shows. special = "black": that sphere a black Matte instead.
+    mirror: a Mirror sphere beside it at (35, 5, 45)."""
+    sc = G.Scene.readme(w, h)
+    m = sc.add_glass() if special == "glass" else sc.add_matte((0.0, 0.0, 0.0))
+    spheres = [((50, 2.5, 50), m)]
+    if mirror:
+        spheres.append(((35, 5.0, 45), sc.add_mirror()))
+    for (pos, mat) in spheres:
+        sph = sc.add_sphere(G.translate(0, 0, 0), 5.0)
+        sc.add_primitive(sph, mat, G.translate(*pos))
+    sc.build(2)
+    return sc
+
+
+@pytest.mark.parametrize("strategy", [abi.PBRT_DL_UNIFORM_SAMPLE_ALL, abi.PBRT_DL_UNIFORM_SAMPLE_ONE])
+def test_oracle_direct_lighting_refracts_through_smooth_glass(strategy):
+    """DirectLighting asks for one lobe per BxDF (allowMultipleLobes false,
+    directlighting.go:76): smooth glass is SpecularReflection + SpecularTransmission
+    (glass.go:58-72), and SpecularTransmit (integrator.go:383-422) follows the
+    Transmission|Specular lobe into Li at depth + 2 (#23). So:
+    - the glass sphere is not a black Matte: light refracted from the scene;
+    - with maxDepth 1 no specular call runs and glass renders as a black Matte;
+    - the recursion's light samples consume draws: pixels that see the glass
+      draw more PCG32 numbers than with a black Matte sphere."""
+    rd = abi.render_desc(2, 2, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING, dl_strategy=strategy, max_depth=5)
+    sg, sb = readme_glass_scene(), readme_glass_scene(special="black")
+    rc, fg, _ = O.render(sg.desc, rd, threads=8)
+    rc2, fb, _ = O.render(sb.desc, rd, threads=8)
+    assert rc == rc2 == 0 and np.isfinite(fg).all()
+    assert (fg.sum(axis=2) > fb.sum(axis=2)).sum() > 100   # light through the glass sphere
+    rd1 = abi.render_desc(2, 2, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING, dl_strategy=strategy, max_depth=1)
+    _, g1, _ = O.render(sg.desc, rd1, threads=8)
+    _, b1, _ = O.render(sb.desc, rd1, threads=8)
+    assert np.array_equal(bits(g1), bits(b1))
+    ntiles = O.lib().oracle_num_tiles(C.byref(sg.desc), C.byref(rd))
+    more = same = 0
+    for tile in range(ntiles):
+        rcg, dg = O.tile_draws(sg.desc, rd, tile)
+        rcb, db = O.tile_draws(sb.desc, rd, tile)
+        assert rcg == rcb == 0
+        more += int((dg - db > 4).sum())           # a recursion level draws >= 5 numbers
+        same += int((np.abs(dg - db) <= 2).sum())  # StartPixel rejections move by a draw or two
+    assert more > 20 and same > more   # only the pixels that see the glass draw more
 
 
 def test_oracle_rough_glass_panics_like_the_reference():
@@ -250,13 +308,7 @@ def test_device_readme_scene_with_the_commented_out_glass_sphere(mode):
     """internal/render/server.go:67-91 (commented out): a glass sphere of radius 5
     at (50, 2.5, 50) with Kr = Kt = 0.5 and index 1.5, added to the README scene;
     plus a mirror sphere beside it. Rendered on the serial kernel, bit-exact."""
-    sc = G.Scene.readme(96, 64)
-    glass = sc.add_glass()
-    mirror = sc.add_mirror()
-    for (pos, m) in (((50, 2.5, 50), glass), ((35, 5.0, 45), mirror)):
-        sph = sc.add_sphere(G.translate(0, 0, 0), 5.0)
-        sc.add_primitive(sph, m, G.translate(*pos))
-    sc.build(2)
+    sc = readme_glass_scene(mirror=True)
     rd = abi.render_desc(2, 2, mode=mode)
     rc, of, _ = O.render(sc.desc, rd, threads=8)
     assert rc == 0
@@ -264,3 +316,34 @@ def test_device_readme_scene_with_the_commented_out_glass_sphere(mode):
         film, st = r.render(rd)
     assert st.kernel == abi.PBRT_KERNEL_SERIAL
     assert np.array_equal(bits(film), bits(of))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strategy", [abi.PBRT_DL_UNIFORM_SAMPLE_ALL, abi.PBRT_DL_UNIFORM_SAMPLE_ONE])
+@pytest.mark.parametrize("mode", [abi.PBRT_MODE_EXACT, abi.PBRT_MODE_THROUGHPUT])
+@pytest.mark.parametrize("depth", [2, 5, 10, 64])
+def test_device_direct_lighting_through_glass_vs_oracle(strategy, mode, depth):
+    """DirectLighting's SpecularTransmit recursion through smooth glass
+    (directlighting.go:76,97-101, integrator.go:383-422, glass.go:58-72), on the
+    README scene with server.go's glass sphere and a mirror: device vs oracle
+    bit-exact (the device folds the linear recursion in the reference's order)."""
+    sc = readme_glass_scene(mirror=True)
+    rd = abi.render_desc(3, 3, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING, dl_strategy=strategy,
+                         max_depth=depth, mode=mode)
+    rc, of, _ = O.render(sc.desc, rd, threads=8)
+    assert rc == 0
+    with G.Renderer(sc) as r:
+        film, st = r.render(rd)
+    assert st.kernel == abi.PBRT_KERNEL_SERIAL
+    assert np.array_equal(bits(film), bits(of))
+
+
+@pytest.mark.gpu
+def test_device_direct_lighting_through_glass_depth_limit():
+    """The device keeps at most 32 recursion levels: maxDepth > 64 through glass is
+    refused (PBRT_E_UNSUPPORTED), never truncated."""
+    sc = readme_glass_scene()
+    with G.Renderer(sc) as r:
+        with pytest.raises(G.PbrtError) as ei:
+            r.render(abi.render_desc(2, 2, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING, max_depth=65))
+    assert ei.value.code == abi.PBRT_E_UNSUPPORTED
