@@ -62,7 +62,15 @@ struct DevScene {
     const double* groups;
     const uint32_t* gmasks;
     int n_groups;
+    // pbrt_gpu_cancel's flag for the render in flight (fine-grained host memory,
+    // written by the host while kernels run); polled between units of work
+    const int* cancel;
 };
+// The flag as the whole wave sees it (one system-scope load, lane 0's value).
+__device__ __forceinline__ bool cancel_requested(const DevScene& sc) {
+    const int v = __hip_atomic_load(sc.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return __builtin_amdgcn_readfirstlane(v) != 0;
+}
 
 // ---------------------------------------------------------------- PCG32 (rng.go)
 struct Pcg {

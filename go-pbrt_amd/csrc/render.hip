@@ -29,6 +29,7 @@
 #include <cstring>
 #include <string>
 #include <functional>
+#include <mutex>
 #include <vector>
 
 #include "../../include/pbrt_gpu.h"
@@ -172,6 +173,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kMinWaves
     const bool mb = rp.mode == PBRT_MODE_THROUGHPUT;
     for (int64_t py = y0; py < y1; py++) {
         for (int64_t px = x0; px < x1; px++) {
+            if (__hip_atomic_load(sc.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;   // pbrt_gpu_cancel
             const uint64_t pi = (uint64_t)((py - y0) * (x1 - x0) + (px - x0));
             if (mb) t.rng.state = mb_state((uint64_t)tile, pi, 0);
             start_pixel(t);
@@ -628,6 +630,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kPathsWav
     DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr,
     int s1d_lds) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];   // paths_group_lds<P>
+    if (cancel_requested(sc)) return;   // one wave per workgroup
     stage_nodes(sc);
     paths_group<P, kMB>(sc, rp, wb, slot_base, (int64_t)blockIdx.x * P, nrec, ctr, lds, s1d_lds);
 }
@@ -751,6 +754,7 @@ __global__ __launch_bounds__(kWave) void k_pw_start(DevScene sc, RenderParams rp
                                                     const int* __restrict__ ldp, PwPath* __restrict__ paths,
                                                     PwQueues qs, unsigned long long* __restrict__ pkey) {
     const int n = rp.spp;
+    if (cancel_requested(sc)) return;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (n < 2 || i >= nrec * (n - 1)) return;
     const int64_t r = i / (n - 1);
@@ -812,6 +816,7 @@ __global__ __launch_bounds__(kWave) void k_pw_trace(DevScene sc, RenderParams rp
                                                     PwQueues qs, int cin, int n_keys,
                                                     unsigned long long* __restrict__ pkey) {
     __shared__ uint16_t stack_lds[64 * kStackStride];
+    if (cancel_requested(sc)) return;
     stage_nodes(sc);
     const uint32_t* qin = qs.q[cin];
     const uint32_t nq = qs.cnt[cin];
@@ -857,6 +862,7 @@ __global__ __launch_bounds__(256) void k_pw_scatter(const PwPath* __restrict__ p
 __global__ __launch_bounds__(kWave) void k_pw_shade(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
                                                     PwPath* __restrict__ paths, PwQueues qs, int sorted,
                                                     unsigned long long* __restrict__ pkey) {
+    if (cancel_requested(sc)) return;
     const uint32_t* qin = sorted ? qs.sorted : qs.q[2];
     const uint32_t nh = qs.cnt[2];
     const int n = rp.spp;
@@ -946,6 +952,7 @@ __global__ __launch_bounds__(kWave) void k_pw_shadow(DevScene sc, RenderParams r
                                                      PwPath* __restrict__ paths, PwQueues qs,
                                                      unsigned long long* __restrict__ pkey) {
     __shared__ uint16_t stack_lds[64 * kStackStride];
+    if (cancel_requested(sc)) return;
     stage_nodes(sc);
     const uint32_t ns = qs.cnt[1];
     if (blockIdx.x == 0)   // hits and key counts, for the next pass
@@ -1020,6 +1027,7 @@ __global__ __launch_bounds__(kWave) void k_mb_setup(DevScene sc, RenderParams rp
     __shared__ uint16_t stack_lds[64 * kStackStride];
     __shared__ uint64_t sh_state;
     const int lane = threadIdx.x;
+    if (cancel_requested(sc)) return;
     stage_nodes(sc);
     const int64_t bslot = blockIdx.x / wb.ppt, pi = blockIdx.x % wb.ppt, rec = blockIdx.x;
     if (bslot >= nslots_batch) return;
@@ -1131,6 +1139,7 @@ __global__ void k_panic_reduce(WaveBufs wb, int64_t slot_base, int64_t nslots_ba
 __global__ __launch_bounds__(kWave) void k_wf_primary(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
                                                       int64_t nb) {
     __shared__ uint16_t stack_lds[64 * kStackStride];
+    if (cancel_requested(sc)) return;
     stage_nodes(sc);
     const int64_t rec = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (rec >= nb * wb.ppt) return;
@@ -1213,7 +1222,7 @@ __global__ __launch_bounds__(kWave) void k_dl_setup(DevScene sc, RenderParams rp
     __shared__ uint64_t sh_state;
     const int64_t bs = blockIdx.x;
     const int lane = threadIdx.x;
-    if (bs >= nb) return;
+    if (bs >= nb || cancel_requested(sc)) return;
     const PcgJump& J = *jump;
     const int64_t tile = tile_of_slot(rp, slot_base + bs);
     int64_t x0, y0, x1, y1;
@@ -1268,6 +1277,7 @@ __global__ __launch_bounds__(kWave) void k_dl_setup(DevScene sc, RenderParams rp
 __global__ __launch_bounds__(kWave) void k_dl_samples(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
                                                       int64_t nrec) {
     __shared__ uint16_t stack_lds[64 * kStackStride];
+    if (cancel_requested(sc)) return;
     stage_nodes(sc);
     const int n = rp.spp;
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1368,6 +1378,7 @@ __global__ __launch_bounds__(kWave) void k_tile_cost(DevScene sc, RenderParams r
                                                      int64_t nb, float* __restrict__ feat,
                                                      uint64_t* __restrict__ keys) {
     __shared__ uint16_t stack_lds[64 * kStackStride];
+    if (cancel_requested(sc)) return;
     stage_nodes(sc);
     const int64_t bs = blockIdx.x;
     const int lane = threadIdx.x;
@@ -1557,6 +1568,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
     }
     __syncthreads();
 
+    uint32_t cancel_poll = 0;   // chain steps since the leader last read the cancel flag
     // lane trajectory state
     uint32_t off = kNoOff;
     uint64_t st0 = 0;
@@ -1602,7 +1614,9 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
                 // pixel record by k_wf_primary; only the ray time needs StartPixel
                 PixelRec& pr = wb.prec[rec];
                 const int hit0 = pr.hit, panic0 = pr.panic0;
-                if (tid == 0) {
+                if (tid == 0 && cancel_requested(sc))   // pbrt_gpu_cancel: every group of the workgroup ends
+                    for (int q2 = 0; q2 < G; q2++) gs[q2].phase = 2;
+                if (tid == 0 && gs[q].phase == 0) {
                     if (hit0)   // the camera ray's time (Get1D after pFilm, pLens) of the pixel's first traced sample
                         pr.si.time = camera_ray(cam, (double)px, (double)py, time_u, V2{0.0, 0.0}).time;
                     pcs[q].si = pr.si;
@@ -1738,7 +1752,8 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
         // ---- (4) each group leader walks its chain through the ring
         if (gl == 0 && sg.phase == 1) {
             CiGroup s = gs[g];
-            for (;;) {
+            if ((++cancel_poll & 127u) == 0 && cancel_requested(sc)) s.phase = 2;   // long pixels (large spp)
+            for (; s.phase == 1;) {
                 RingEnt& e = ring[s.head & (R - 1u)];
                 if (e.tag != s.head) break;
                 const uint32_t d = e.d;
@@ -1944,7 +1959,15 @@ struct pbrt_gpu_ctx {
     // last render
     RenderParams rp{};
     bool rendered = false;
-    std::atomic<int> cancel{0};
+    // cancellation (pbrt_gpu_cancel): a flag in fine-grained host memory the
+    // kernels poll; it belongs to the render in flight (render_async entry to
+    // synchronize) and is cleared when that render ends, so a cancel never
+    // outlives its render and never reaches the next one
+    std::mutex cancel_mu;
+    bool in_flight = false;
+    bool cancel_req = false;
+    int* h_cancel = nullptr;   // hipHostMalloc (coherent, mapped)
+    int* d_cancel = nullptr;   // its device address
     std::string err;
     std::chrono::steady_clock::time_point t_start;
 };
@@ -2001,6 +2024,7 @@ DevScene dev_scene(const pbrt_gpu_ctx* c, bool with_dist) {
     s.groups = c->d_groups;
     s.gmasks = c->d_gmasks;
     s.n_groups = c->n_groups;
+    s.cancel = c->d_cancel;
     return s;
 }
 
@@ -2709,6 +2733,12 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
         pbrt_gpu_destroy(c);
         return PBRT_E_HIP;
     }
+    if (hipHostMalloc((void**)&c->h_cancel, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&c->d_cancel, c->h_cancel, 0) != hipSuccess) {
+        pbrt_gpu_destroy(c);
+        return PBRT_E_HIP;
+    }
+    __atomic_store_n(c->h_cancel, 0, __ATOMIC_SEQ_CST);
     if ((rc = upload(c, &c->d_shapes, scene->shapes, scene->n_shapes)) ||
         (rc = upload(c, &c->d_materials, scene->materials, scene->n_materials)) ||
         (rc = upload(c, &c->d_prims, scene->prims, scene->n_prims)) ||
@@ -2750,11 +2780,16 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
 
 int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_device) {
     if (!c) return PBRT_E_INVALID;
-    if (c->cancel.load()) return set_err(c, PBRT_E_CANCELLED, "cancelled");
     HIPCHK(c, hipSetDevice(c->device));
     c->t_start = std::chrono::steady_clock::now();
     int rc = prepare(c, rd);
     if (rc != PBRT_OK) return rc;
+    {   // this render is the one pbrt_gpu_cancel now cancels
+        std::lock_guard<std::mutex> lk(c->cancel_mu);
+        c->in_flight = true;
+        c->cancel_req = false;
+        __atomic_store_n(c->h_cancel, 0, __ATOMIC_SEQ_CST);
+    }
     const RenderParams& rp = c->rp;
     double* out = film_device ? film_device : c->d_out;
     c->film_target = out;
@@ -2972,7 +3007,27 @@ int pbrt_gpu_render_async(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
 int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
     if (!c) return PBRT_E_INVALID;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const hipError_t se = hipStreamSynchronize(c->stream);
+    bool cancelled = false;
+    {   // the render has ended: its cancel flag dies with it
+        std::lock_guard<std::mutex> lk(c->cancel_mu);
+        cancelled = c->in_flight && c->cancel_req;
+        c->in_flight = false;
+        c->cancel_req = false;
+        __atomic_store_n(c->h_cancel, 0, __ATOMIC_SEQ_CST);
+    }
+    HIPCHK(c, se);
+    if (cancelled) {   // the kernels stopped early: the film and the schedule feedback are not valid
+        c->ticks_pending = false;
+        c->rendered = false;
+        if (stats) {
+            std::memset(stats, 0, sizeof(*stats));
+            stats->kernel = c->last_kernel;
+            stats->total_ms =
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c->t_start).count();
+        }
+        return set_err(c, PBRT_E_CANCELLED, "cancelled by pbrt_gpu_cancel");
+    }
     Counters ctr;
     HIPCHK(c, hipMemcpy(&ctr, c->d_ctr, sizeof(ctr), hipMemcpyDeviceToHost));
     float ms = 0, ms_merge = 0;
@@ -3132,7 +3187,11 @@ int pbrt_gpu_intersect_p(pbrt_gpu_ctx* c, const pbrt_ray_soa* rays, size_t n, ui
 }
 
 void pbrt_gpu_cancel(pbrt_gpu_ctx* c) {
-    if (c) c->cancel.store(1);
+    if (!c) return;
+    std::lock_guard<std::mutex> lk(c->cancel_mu);
+    if (!c->in_flight) return;   // nothing to cancel: no render is in flight
+    c->cancel_req = true;
+    __atomic_store_n(c->h_cancel, 1, __ATOMIC_SEQ_CST);
 }
 const char* pbrt_gpu_last_error(const pbrt_gpu_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
@@ -3158,6 +3217,7 @@ void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
         (void)hipStreamDestroy(c->stream2);
     }
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->h_cancel) (void)hipHostFree(c->h_cancel);
     delete c;
 }
 

@@ -338,7 +338,16 @@ int pbrt_gpu_intersect(pbrt_gpu_ctx* ctx, const pbrt_ray_soa* rays, size_t n,
 int pbrt_gpu_intersect_p(pbrt_gpu_ctx* ctx, const pbrt_ray_soa* rays, size_t n,
                          uint8_t* occluded);
 
-void pbrt_gpu_cancel(pbrt_gpu_ctx* ctx);     /* thread-safe                   */
+/* Cancels the render in flight on ctx (from pbrt_gpu_render[_async[_into]]
+ * entry until its pbrt_gpu_synchronize returns): the kernels poll a flag between
+ * units of work (a pixel's chain, every 128 chain steps, a workgroup of paths),
+ * so the frame stops within milliseconds and its synchronize returns
+ * PBRT_E_CANCELLED (the film is then not valid). Like the reference's
+ * errgroup, which stops issuing tiles once ctx is done (integrator.go:332-335),
+ * it ends that render only: the flag is cleared when the render ends, so the
+ * next render on the context runs normally. With no render in flight it does
+ * nothing. Thread-safe. */
+void pbrt_gpu_cancel(pbrt_gpu_ctx* ctx);
 const char* pbrt_gpu_last_error(const pbrt_gpu_ctx* ctx);
 void pbrt_gpu_destroy(pbrt_gpu_ctx* ctx);
 
