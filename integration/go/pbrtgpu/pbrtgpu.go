@@ -193,22 +193,37 @@ func PathDesc(xs, ys int32, jitter bool, nDims, maxDepth int32, rrThreshold floa
 func WithRandomSampler(rd *C.pbrt_render_desc, ns int32) { C.pbrt_random_sampler(C.int32_t(ns), rd) }
 
 // Renderer owns a device-resident scene (one per GPU).
-type Renderer struct{ ctx *C.pbrt_gpu_ctx }
+type Renderer struct {
+	ctx  *C.pbrt_gpu_ctx
+	w, h int // CroppedPixelBounds extent of the scene's film
+}
 
 func NewRenderer(s *SceneBuilder, device int) (*Renderer, error) {
+	if s.desc == nil {
+		return nil, fmt.Errorf("pbrtgpu: scene not built")
+	}
 	var opts C.pbrt_gpu_opts
 	opts.device = C.int32_t(device)
 	var ctx *C.pbrt_gpu_ctx
 	if rc := C.pbrt_gpu_create(s.desc, &opts, &ctx); rc != C.PBRT_OK {
 		return nil, fmt.Errorf("pbrt_gpu_create: status %d", int(rc))
 	}
-	return &Renderer{ctx: ctx}, nil
+	f := s.desc.film
+	return &Renderer{ctx: ctx, w: int(f.crop_max_x - f.crop_min_x), h: int(f.crop_max_y - f.crop_min_y)}, nil
 }
 
 // RenderFrame is pbrt.Render for one frame: film receives the merged XYZ sums
 // Film.MergeFilmTile would hold, row-major W*H*3 float64. ctx cancellation maps
 // to pbrt_gpu_cancel, as errgroup cancels the CPU workers (integrator.go:305-345).
 func (r *Renderer) RenderFrame(ctx context.Context, rd *C.pbrt_render_desc, film []float64) error {
+	if len(film) < r.w*r.h*3 || len(film) == 0 {
+		return fmt.Errorf("pbrtgpu: film holds %d values, the frame needs %d", len(film), r.w*r.h*3)
+	}
+	if err := ctx.Err(); err != nil {
+		return err
+	}
+	// pbrt_gpu_cancel acts on the render in flight only: a cancel that lands
+	// before the render starts or after it ends is a no-op (include/pbrt_gpu.h)
 	done := make(chan struct{})
 	defer close(done)
 	go func() {
@@ -224,7 +239,10 @@ func (r *Renderer) RenderFrame(ctx context.Context, rd *C.pbrt_render_desc, film
 	case C.PBRT_OK:
 		return nil
 	case C.PBRT_E_CANCELLED:
-		return ctx.Err()
+		if err := ctx.Err(); err != nil {
+			return err
+		}
+		return context.Canceled
 	case C.PBRT_E_REF_PANIC: // the CPU reference panics here; keep that contract
 		panic(fmt.Sprintf("go-pbrt panic kind %d at tile %d pixel (%d,%d) sample %d bounce %d",
 			int(st.panic_kind), int(st.panic_tile), int64(st.panic_pixel_x), int64(st.panic_pixel_y),
@@ -244,6 +262,12 @@ func (r *Renderer) Intersect(rays *C.pbrt_ray_soa, n int, hits *C.pbrt_hit_soa) 
 
 // IntersectP is BVH.IntersectP over a batch; occluded[i] is 0 or 1.
 func (r *Renderer) IntersectP(rays *C.pbrt_ray_soa, n int, occluded []uint8) error {
+	if n <= 0 {
+		return nil
+	}
+	if len(occluded) < n {
+		return fmt.Errorf("pbrtgpu: %d results for %d rays", len(occluded), n)
+	}
 	if rc := C.pbrt_gpu_intersect_p(r.ctx, rays, C.size_t(n), (*C.uint8_t)(unsafe.Pointer(&occluded[0]))); rc != C.PBRT_OK {
 		return fmt.Errorf("pbrt_gpu_intersect_p: %s", C.GoString(C.pbrt_gpu_last_error(r.ctx)))
 	}
@@ -255,6 +279,9 @@ func (r *Renderer) Close() { C.pbrt_gpu_destroy(r.ctx) }
 // FilmToRGBA is Film.WriteImage's pixel loop (film.go:156-161): uint8(Clamp(v, 0, 1) * 255)
 // of the XYZ sums, NaN -> 0, alpha 255; encode the result with image/png as WriteImage does.
 func FilmToRGBA(film []float64, w, h int) (*image.RGBA, error) {
+	if w <= 0 || h <= 0 || len(film) < w*h*3 {
+		return nil, fmt.Errorf("pbrtgpu: film holds %d values, %dx%d needs %d", len(film), w, h, w*h*3)
+	}
 	img := image.NewRGBA(image.Rect(0, 0, w, h))
 	if rc := C.pbrt_film_to_rgba8((*C.double)(unsafe.Pointer(&film[0])), C.int64_t(w), C.int64_t(h),
 		(*C.uint8_t)(unsafe.Pointer(&img.Pix[0]))); rc != C.PBRT_OK {

@@ -13,20 +13,24 @@ import subprocess
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SHIM = os.path.join(REPO, "integration", "go", "pbrtgpu", "pbrtgpu.go")
+SHIM_DIR = os.path.join(REPO, "integration", "go", "pbrtgpu")
+SHIMS = sorted(os.path.join(SHIM_DIR, f) for f in os.listdir(SHIM_DIR) if f.endswith(".go"))
+PATCHES = os.path.join(REPO, "integration", "go", "patches")
+REFERENCE = "/root/reference"
 # cgo pseudo-identifiers and C scalar types, not ABI names
 CGO_BUILTINS = {"GoString", "CString", "GoBytes", "int", "int32_t", "int64_t", "uint8_t", "double", "size_t",
-                "uint64_t", "float", "char"}
+                "uint64_t", "float", "char", "int32_t"}
 
 
 def shim_parts():
-    src = open(SHIM).read()
+    src = "\n".join(open(f).read() for f in SHIMS)
     pre = "\n".join(l[3:] for l in src.splitlines() if l.startswith("// #") and not l.startswith("// #cgo"))
     names = set(re.findall(r"\bC\.([A-Za-z_]\w*)", src)) - CGO_BUILTINS
     fields = set()
-    for var, ty in re.findall(r"\bvar (\w+) C\.(\w+)", src):
-        for f in re.findall(r"\b%s\.(\w+)\b" % re.escape(var), src):
-            fields.add((ty, f))
+    for fn in re.split(r"\nfunc ", src):   # a `var x C.T` is scoped to its function
+        for var, ty in re.findall(r"\bvar (\w+) C\.(\w+)", fn):
+            for f in re.findall(r"\b%s\.(\w+)\b" % re.escape(var), fn):
+                fields.add((ty, f))
     return pre, names, fields
 
 
@@ -60,3 +64,37 @@ def test_shim_covers_the_render_entry_points():
               "pbrt_gpu_intersect", "pbrt_gpu_intersect_p", "pbrt_film_to_rgba8", "pbrt_sb_build",
               "pbrt_make_glass", "pbrt_make_mirror", "pbrt_random_sampler"):
         assert n in names, n
+
+
+def test_dropin_types_cover_the_reference_interfaces():
+    """pbrtgpu.Path is a pbrt.Integrator (integrator.go:12-21) with
+    RenderFrame, pbrtgpu.BVH a pbrt.Aggregate (primitive.go:9-20) with batch methods;
+    both embed the CPU implementation for the per-ray methods."""
+    src = open(os.path.join(SHIM_DIR, "dropin.go")).read()
+    assert re.search(r"type Path struct \{\s*pbrt\.Integrator", src)
+    assert re.search(r"type BVH struct \{\s*\*accelerator\.BVH", src)
+    assert "func (p *Path) RenderFrame(ctx context.Context, scene pbrt.Scene, tileSize int64) error" in src
+    for m in ("IntersectBatch", "IntersectPBatch"):
+        assert f"func (b *BVH) {m}(" in src
+    for ctor in ("NewSphereShape", "NewDisk", "NewMatte", "NewCheckerMatte", "NewMirror", "NewGlass",
+                 "NewGeometricPrimitive", "NewTransformedPrimitive", "NewBVH", "NewPoint", "NewDistant",
+                 "NewDiffuseAreaLight", "NewScene", "NewFilm", "NewPerspectiveCamera", "NewPath"):
+        assert f"func (r *Recorder) {ctor}(" in src, ctor
+
+
+@pytest.mark.skipif(not os.path.isdir(REFERENCE) or not os.path.exists("/usr/bin/patch"),
+                    reason="the reference checkout (or patch(1)) is not on this machine")
+def test_patches_apply_to_the_reference(tmp_path):
+    """integration/go/patches/*.patch apply cleanly to the reference checkout
+    (dry run: nothing under /root/reference is written), and the hook patch puts
+    the FrameRenderer check at the top of pbrt.Render (integrator.go:291)."""
+    pats = sorted(f for f in os.listdir(PATCHES) if f.endswith(".patch"))
+    assert len(pats) == 2
+    for f in pats:
+        r = subprocess.run(["patch", "--dry-run", "-p1", "-d", REFERENCE, "-i", os.path.join(PATCHES, f)],
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout + r.stderr
+    hook = open(os.path.join(PATCHES, pats[0])).read()
+    assert "+\tif fr, ok := s.(FrameRenderer); ok {" in hook and "+func RenderTiles(" in hook
+    server = open(os.path.join(PATCHES, pats[1])).read()
+    assert "+\tdli := rec.NewPath(10, camera, sampler, pixelBounds, 1, pbrt.Uniform, 0)" in server
