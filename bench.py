@@ -51,8 +51,8 @@ def parse():
     ap.add_argument("--occupancy", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=30.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="0 = this process's CPU share: OMP_NUM_THREADS if set (the GPU box allots 16 host "
-                         "cores per GPU), else the affinity mask")
+                    help="threads of the CPU baseline's per-GPU timing (0 = nproc / 8: the host's share per "
+                         "GPU of an 8-GPU node); a second timing always uses every host core")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="exact", choices=["exact", "throughput"],
                     help="mode of the headline line (exact = the reference's per-tile RNG, bit-exact)")
@@ -70,7 +70,7 @@ def load_json(path):
 
 
 def host_cpu():
-    """nproc, the affinity mask, the process's CPU share and the CPU model of this host."""
+    """nproc, the affinity mask, the cgroup CPU quota and the CPU model of this host."""
     model = "?"
     try:
         with open("/proc/cpuinfo") as f:
@@ -85,28 +85,24 @@ def host_cpu():
         affinity = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         affinity = nproc
-    share = affinity
-    omp = os.environ.get("OMP_NUM_THREADS", "")
-    if omp.isdigit() and int(omp) > 0:
-        share = min(share, int(omp))
-    return {"nproc": nproc, "affinity": affinity, "share": share, "cpu_model": model}
+    quota = None   # CPUs' worth of time the cgroup grants (cgroup v2 cpu.max), if limited
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    return {"nproc": nproc, "affinity": affinity, "cgroup_cpus": quota, "cpu_model": model}
 
 
-def cpu_baseline(args, scene_name, rd_kwargs, W, H, product_scene=None):
-    """The oracle (C restatement of the Go path, oracle/) on the same frame's
-    tiles, on this box's host cores: the whole frame when it fits the budget,
-    else an evenly spread tile sample (bit-reversed stride-64 batches, so every
-    prefix of batches is spread over the frame) -- stated in `sample`."""
-    sys.path.insert(0, os.path.join(REPO, "tests"))
+def cpu_rate(sc, rd_kwargs, threads, seconds):
+    """Oracle Mpaths/s on `threads` threads over an evenly spread tile sample of
+    the frame (bit-reversed stride-64 batches: every prefix is spread over the
+    frame), stopping after `seconds` of wall time or the whole frame."""
     import oracle_lib as O
     from pbrtgpu import abi
 
-    cpu = host_cpu()
-    threads = args.cpu_threads or cpu["share"]
-    if scene_name == "heightfield":   # the fixture is data: the oracle renders the product-built descriptor
-        sc = product_scene
-    else:
-        sc = (O.OracleScene.readme if scene_name == "readme" else O.OracleScene.cornell)(W, H)
     n_tiles = int(O.lib().oracle_num_tiles(sc.desc, abi.render_desc(**rd_kwargs)))
     stride = 64
     offsets = [int(format(i, "06b")[::-1], 2) for i in range(stride)]
@@ -119,24 +115,51 @@ def cpu_baseline(args, scene_name, rd_kwargs, W, H, product_scene=None):
             raise RuntimeError(f"oracle rc {rc}")
         paths += st.paths
         tiles += st.tiles
-        if time.perf_counter() - t0 >= args.cpu_seconds:
+        if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
     what = "the whole frame" if tiles == n_tiles else \
         f"{tiles} of {n_tiles} tiles of the same frame (evenly spread, stride {stride})"
-    return {
-        "value": paths / dt / 1e6,
+    return paths / dt / 1e6, f"{what}: {paths} paths in {dt:.2f} s on {threads} threads"
+
+
+def cpu_baseline(args, scene_name, rd_kwargs, W, H, product_scene=None, gpus_per_host=8):
+    """The oracle (C restatement of the Go path, oracle/) on the same frame's
+    tiles, on this box's host cores, timed twice (one worker per
+    host core): on the per-GPU share of the host (nproc / 8 threads: the node
+    has 8 GPUs) and on every host core (nproc threads). `value` is the share;
+    `whole_host` the other. The cgroup quota, if any, caps what either can use."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib as O
+
+    cpu = host_cpu()
+    if scene_name == "heightfield":   # the fixture is data: the oracle renders the product-built descriptor
+        sc = product_scene
+    else:
+        sc = (O.OracleScene.readme if scene_name == "readme" else O.OracleScene.cornell)(W, H)
+    share = args.cpu_threads or max(1, cpu["nproc"] // gpus_per_host)
+    whole = cpu["nproc"]
+    budget = args.cpu_seconds / 2
+    v_share, s_share = cpu_rate(sc, rd_kwargs, share, budget)
+    out = {
+        "value": v_share,
         "unit": "Mpaths/s",
-        "cores": threads,
+        "cores": share,
         "kind": "port",
         "nproc": cpu["nproc"],
         "affinity": cpu["affinity"],
+        "cgroup_cpus": cpu["cgroup_cpus"],
         "cpu_model": cpu["cpu_model"],
-        "per_core": paths / dt / 1e6 / threads,
-        "sample": f"{what}: {paths} paths in {dt:.2f} s on {threads} threads (this process's CPU share: "
-                  f"OMP_NUM_THREADS / affinity; nproc {cpu['nproc']}); oracle/ C restatement of the Go path, "
-                  "which has no Go per-op heap allocation, so it is expected to be faster than go-pbrt",
+        "per_core": v_share / share,
+        "sample": f"{s_share} (the per-GPU share of the host: nproc {cpu['nproc']} / {gpus_per_host} GPUs); "
+                  "oracle/ C restatement of the Go path, which has no Go per-op heap allocation, so it is "
+                  "expected to be faster than go-pbrt",
     }
+    if whole != share:
+        v_whole, s_whole = cpu_rate(sc, rd_kwargs, whole, budget)
+        out["whole_host"] = {"value": v_whole, "unit": "Mpaths/s", "cores": whole, "per_core": v_whole / whole,
+                             "sample": s_whole + " (every host core, SURVEY 8(d))"}
+    return out
 
 
 def roofline(scene_name, W, H, S, paths_per_launch, kernel_kind, kern_ms, chain_ms, paths_ms, merge_ms,
@@ -235,6 +258,96 @@ def mesh_roofline(cfg, W, H, S, mode, stats_ms, paths):
                          "k_paths_ms": stats_ms["paths"]}}
 
 
+class GpuBackend:
+    """One process per GPU: torch owns the device, RCCL (the "nccl" backend)
+    reduces the films over xGMI, the renderer's stream is ordered after
+    torch's current stream before every frame."""
+
+    def __init__(self, local):
+        import torch
+        self.torch = torch
+        self.local = local
+        torch.cuda.set_device(local)
+        self.dev = torch.device("cuda", local)
+        self.rstream = None
+
+    def init_process_group(self):
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=self.dev)   # RCCL over xGMI
+
+    def zeros(self, shape):
+        return self.torch.zeros(shape, dtype=self.torch.float64, device=self.dev)
+
+    def attach(self, renderer):
+        # the renderer launches on its own non-blocking HIP stream
+        self.rstream = self.torch.cuda.ExternalStream(renderer.stream(), device=self.dev)
+
+    def order(self):
+        # everything queued on torch's stream (the film's zero fill, the previous
+        # frame's RCCL reduce, which dist.reduce made torch's stream wait for)
+        # precedes the frame
+        self.rstream.wait_stream(self.torch.cuda.current_stream(self.dev))
+
+    def synchronize(self):
+        self.torch.cuda.synchronize()
+
+    def barrier(self, world):
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier(device_ids=[self.local])
+
+    def tensor(self, vals):
+        return self.torch.tensor(vals, dtype=self.torch.float64, device=self.dev)
+
+
+def make_step(renderer, backend, film, rd, world):
+    """One frame: the rank's shard into its full-size film, then (N > 1) one
+    SUM reduce of the films onto rank 0 -- the additive MergeFilmTile."""
+    import torch.distributed as dist
+
+    def step():
+        backend.order()
+        renderer.render_async(rd, film.data_ptr())
+        st = renderer.synchronize()
+        if world > 1:
+            dist.reduce(film, dst=0, op=dist.ReduceOp.SUM)
+        return st
+    return step
+
+
+def timed(step, backend, world, rank, steps, warmup, label="exact", log=sys.stderr):
+    """W untimed warmup frames, then K frames bracketed by barrier +
+    synchronize on both sides; elapsed is the MAX over ranks, paths the SUM."""
+    import torch.distributed as dist
+
+    for i in range(warmup):
+        st = step()
+        if rank == 0:
+            print(f"[bench] {label} warmup {i}: kernels {st.kernel_ms:.0f} ms", file=log, flush=True)
+    backend.barrier(world)
+    backend.synchronize()
+    t0 = time.perf_counter()
+    stats = []
+    for i in range(steps):
+        stats.append(step())
+        if rank == 0:   # progress on stderr (long frames: config E); stdout holds the one JSON line
+            print(f"[bench] {label} step {i}: kernels {stats[-1].kernel_ms:.0f} ms", file=log, flush=True)
+    backend.synchronize()
+    backend.barrier(world)
+    elapsed = time.perf_counter() - t0
+    paths_local = sum(int(s.paths_traced) for s in stats)
+    agg = backend.tensor([elapsed, float(paths_local)])
+    if world > 1:
+        mx = agg.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = agg.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed, paths_total = float(mx[0]), float(sm[1])
+    else:
+        paths_total = float(paths_local)
+    return elapsed, paths_local, paths_total, stats
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -243,11 +356,9 @@ def main():
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
-    import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    backend = GpuBackend(local)
 
     import pbrtgpu as G
 
@@ -266,73 +377,29 @@ def main():
     renderer = G.Renderer(scene, device=local, kernel=args.kernel, lanes_per_wave=args.tiles_per_wave,
                           occupancy=args.occupancy)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)   # RCCL over xGMI
+        backend.init_process_group()
     modes = {"exact": G.abi.PBRT_MODE_EXACT, "throughput": G.abi.PBRT_MODE_THROUGHPUT}
-    film = torch.zeros((H, W, 3), dtype=torch.float64, device=dev)
-    # the renderer launches on its own non-blocking HIP stream: order it after
-    # everything queued on torch's stream (the film's zero fill, the previous
-    # frame's RCCL reduce, which dist.reduce made torch's stream wait for)
-    rstream = torch.cuda.ExternalStream(renderer.stream(), device=dev)
+    film = backend.zeros((H, W, 3))
+    backend.attach(renderer)
 
-    def barrier():
-        if world > 1:
-            dist.barrier(device_ids=[local])
-
-    def make_step(mode):
-        rd = G.render_desc(**rd_kwargs, tile_begin=shard_r, tile_stride=shard_n, mode=modes[mode])
-
-        def step():
-            rstream.wait_stream(torch.cuda.current_stream(dev))
-            renderer.render_async(rd, film.data_ptr())
-            st = renderer.synchronize()
-            if world > 1:
-                dist.reduce(film, dst=0, op=dist.ReduceOp.SUM)
-            return st
-        return step
-
-    def timed(mode, steps, warmup):
-        step = make_step(mode)
-        for i in range(warmup):
-            st = step()
-            if rank == 0:
-                print(f"[bench] {mode} warmup {i}: kernels {st.kernel_ms:.0f} ms", file=sys.stderr, flush=True)
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        stats = []
-        for i in range(steps):
-            stats.append(step())
-            if rank == 0:   # progress on stderr (long frames: config E); stdout holds the one JSON line
-                print(f"[bench] {mode} step {i}: kernels {stats[-1].kernel_ms:.0f} ms", file=sys.stderr, flush=True)
-        torch.cuda.synchronize()
-        barrier()
-        elapsed = time.perf_counter() - t0
-        paths_local = sum(int(s.paths_traced) for s in stats)
-        agg = torch.tensor([elapsed, float(paths_local)], dtype=torch.float64, device=dev)
-        if world > 1:
-            mx = agg.clone()
-            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-            sm = agg.clone()
-            dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-            elapsed, paths_total = float(mx[0]), float(sm[1])
-        else:
-            paths_total = float(paths_local)
-        return elapsed, paths_local, paths_total, stats
+    def rd_of(mode):
+        return G.render_desc(**rd_kwargs, tile_begin=shard_r, tile_stride=shard_n, mode=modes[mode])
 
     # cold frame: a fresh context's first frame (no schedule learned yet), as
     # internal/render/server.go pays it when it builds a scene per RPC
-    barrier()
-    torch.cuda.synchronize()
+    backend.barrier(world)
+    backend.synchronize()
     t0 = time.perf_counter()
-    first = make_step(args.mode)()
-    torch.cuda.synchronize()
+    first = make_step(renderer, backend, film, rd_of(args.mode), world)()
+    backend.synchronize()
     first_ms = (time.perf_counter() - t0) * 1e3
     if world > 1:
-        fm = torch.tensor([first_ms], dtype=torch.float64, device=dev)
+        fm = backend.tensor([first_ms])
         dist.all_reduce(fm, op=dist.ReduceOp.MAX)
         first_ms = float(fm[0])
 
-    elapsed, paths_local, paths_total, stats = timed(args.mode, args.steps, args.warmup)
+    elapsed, paths_local, paths_total, stats = timed(make_step(renderer, backend, film, rd_of(args.mode), world),
+                                                     backend, world, rank, args.steps, args.warmup, args.mode)
     kern_ms = sum(s.kernel_ms for s in stats) / len(stats)
     merge_ms = sum(s.merge_ms for s in stats) / len(stats)
     chain_ms = sum(s.chain_ms for s in stats) / len(stats)
@@ -341,7 +408,8 @@ def main():
     side = None
     if not args.no_side_mode:
         other = "throughput" if args.mode == "exact" else "exact"
-        e2, _, p2, st2 = timed(other, 2, 1)
+        e2, _, p2, st2 = timed(make_step(renderer, backend, film, rd_of(other), world), backend, world, rank,
+                               2, 1, other)
         side = {"mode": other, "value": p2 / e2 / 1e6, "unit": "Mpaths/s", "ms_per_step": e2 / 2 * 1e3,
                 "chain_ms": sum(s.chain_ms for s in st2) / 2, "k_paths_ms": sum(s.paths_ms for s in st2) / 2,
                 "note": "THROUGHPUT = one PCG32 stream per (pixel, sample): same arithmetic, statistically "
@@ -391,6 +459,8 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             cb = cpu_baseline(args, cfg["scene"], rd_kwargs, W, H, scene)
             cb["gpu_over_cpu"] = value / cb["value"]
+            if "whole_host" in cb:
+                cb["whole_host"]["gpu_over_cpu"] = value / cb["whole_host"]["value"]
             out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)
     renderer.close()

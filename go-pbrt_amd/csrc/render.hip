@@ -1239,6 +1239,10 @@ __global__ __launch_bounds__(kWave) void k_dl_setup(DevScene sc, RenderParams rp
     uint64_t S = seed.state;
     int64_t used = npx;
     for (int64_t pi = 0; pi < npx; pi++) {
+        if (cancel_requested(sc)) {   // pbrt_gpu_cancel (large spp: a pixel's StartPixel is long)
+            used = pi;
+            break;
+        }
         const int64_t rec = bs * wb.ppt + pi;
         double* gs1d = wb.s1d + rec * wb.s1d_stride;
         double* sp = s1d ? s1d : gs1d;
@@ -1280,56 +1284,64 @@ __global__ __launch_bounds__(kWave) void k_dl_samples(DevScene sc, RenderParams 
     if (cancel_requested(sc)) return;
     stage_nodes(sc);
     const int n = rp.spp;
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (n < 2 || idx >= nrec * (n - 1)) return;
-    const int64_t rec = idx / (n - 1);
-    const int k = 1 + (int)(idx - rec * (n - 1));
-    const int64_t bs = rec / wb.ppt, pi = rec % wb.ppt;
-    if (pi >= wb.tile_npx[bs]) return;
-    const PixelRec& pr = wb.prec[rec];
-    double* o = wb.L + (rec * n + k) * 3;
-    Spec L = spec(0);
-    int panic = pr.panic0;
-    if (!panic && pr.hit) {
-        Cursor c;
-        c.rng.state = wb.memb[rec * n + k];
-        c.rng.inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + bs));
-        c.draws = 0;
-        c.cur1d = c.cur2d = 0;
-        c.k = k;
-        c.kdep = 0;
-        const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, n, rp.ndims};
-        c_get2d(c, ss);   // camera: pFilm, pLens, time
-        c_get2d(c, ss);
-        c_get1d(c, ss);
-        L = L + spec(0);   // si.Le(si.Wo): no primitive carries an area light
-        const int nl = sc.n_lights;
-        if (nl > 0) {
-            if (rp.dl_strategy == PBRT_DL_UNIFORM_SAMPLE_ALL) {   // integrator.go:23-46
-                Spec acc = spec(0);
-                for (int j = 0; j < nl && !panic; j++) {
+    if (n < 2) return;
+    // grid-stride over every (pixel record, sample): a bounded grid, so a cancel
+    // (polled every 16 passes) ends the kernel quickly at any spp
+    const int64_t total = nrec * (n - 1), stride = (int64_t)gridDim.x * blockDim.x;
+    int pass = 0;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx - threadIdx.x < total; idx += stride) {
+        if ((++pass & 15) == 0 && cancel_requested(sc)) return;
+        if (idx >= total) continue;
+        const int64_t rec = idx / (n - 1);
+        const int k = 1 + (int)(idx - rec * (n - 1));
+        const int64_t bs = rec / wb.ppt, pi = rec % wb.ppt;
+        if (pi >= wb.tile_npx[bs]) continue;
+        const PixelRec& pr = wb.prec[rec];
+        double* o = wb.L + (rec * n + k) * 3;
+        Spec L = spec(0);
+        int panic = pr.panic0;
+        if (!panic && pr.hit) {
+            Cursor c;
+            c.rng.state = wb.memb[rec * n + k];
+            c.rng.inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + bs));
+            c.draws = 0;
+            c.cur1d = c.cur2d = 0;
+            c.k = k;
+            c.kdep = 0;
+            const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, n, rp.ndims};
+            c_get2d(c, ss);   // camera: pFilm, pLens, time
+            c_get2d(c, ss);
+            c_get1d(c, ss);
+            L = L + spec(0);   // si.Le(si.Wo): no primitive carries an area light
+            const int nl = sc.n_lights;
+            if (nl > 0) {
+                if (rp.dl_strategy == PBRT_DL_UNIFORM_SAMPLE_ALL) {   // integrator.go:23-46
+                    Spec acc = spec(0);
+                    for (int j = 0; j < nl && !panic; j++) {
+                        const V2 ul = c_get2d(c, ss);
+                        c_get2d(c, ss);
+                        acc = acc + estimate_direct(sc, stack_lds + threadIdx.x, panic, pr.si, pr.b, j, ul);
+                    }
+                    L = L + acc;
+                } else {   // UniformSampleOneLight with no distribution (integrator.go:48-77)
+                    const int ln = (int)gomath::to_int(gomath::min(c_get1d(c, ss) * (double)nl, (double)(nl - 1)));
                     const V2 ul = c_get2d(c, ss);
                     c_get2d(c, ss);
-                    acc = acc + estimate_direct(sc, stack_lds + threadIdx.x, panic, pr.si, pr.b, j, ul);
+                    const Spec s = estimate_direct(sc, stack_lds + threadIdx.x, panic, pr.si, pr.b, ln, ul);
+                    if (!panic && max_component(s) > 10) panic = PBRT_PANIC_LD_GT_10;
+                    L = L + s;
                 }
-                L = L + acc;
-            } else {   // UniformSampleOneLight with no distribution (integrator.go:48-77)
-                const int ln = (int)gomath::to_int(gomath::min(c_get1d(c, ss) * (double)nl, (double)(nl - 1)));
-                const V2 ul = c_get2d(c, ss);
-                c_get2d(c, ss);
-                const Spec s = estimate_direct(sc, stack_lds + threadIdx.x, panic, pr.si, pr.b, ln, ul);
-                if (!panic && max_component(s) > 10) panic = PBRT_PANIC_LD_GT_10;
-                L = L + s;
             }
+            // SpecularReflect / SpecularTransmit: black for a Lambertian-only BSDF
         }
-        // SpecularReflect / SpecularTransmit: black for a Lambertian-only BSDF
+        o[0] = L.r;
+        o[1] = L.g;
+        o[2] = L.b;
+        if (panic)
+            atomicMin((unsigned long long*)&wb.memb[rec * n],
+                      ((unsigned long long)k << 32) | (unsigned long long)((panic + 1) & 0xFF));
+
     }
-    o[0] = L.r;
-    o[1] = L.g;
-    o[2] = L.b;
-    if (panic)
-        atomicMin((unsigned long long*)&wb.memb[rec * n],
-                  ((unsigned long long)k << 32) | (unsigned long long)((panic + 1) & 0xFF));
 }
 
 // Per pixel record: its first panic (sample order) -> wb.ppanic, and the
@@ -2933,7 +2945,9 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                 if (c->use_dl) {
                     const int64_t nrec = nb * c->wb.ppt;
                     if (rp.spp > 1)
-                        hipLaunchKernelGGL(k_dl_samples, dim3((unsigned)((nrec * (rp.spp - 1) + kWave - 1) / kWave)),
+                        hipLaunchKernelGGL(k_dl_samples,
+                                           dim3((unsigned)std::min<int64_t>((nrec * (rp.spp - 1) + kWave - 1) / kWave,
+                                                                            (int64_t)c->n_simd * 64)),
                                            dim3(kWave), 0, c->stream, with_slot(sc, 3), rp, c->wb, sb, nrec);
                     hipLaunchKernelGGL(k_dl_panics, dim3((unsigned)((nrec + 255) / 256)), dim3(256), 0, c->stream, rp,
                                        c->wb, sb, nrec, c->d_ctr);

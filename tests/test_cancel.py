@@ -22,12 +22,6 @@ def bits(a):
     return np.ascontiguousarray(a).view(np.uint64)
 
 
-def cancel_after(r, seconds):
-    t = threading.Timer(seconds, lambda: G.lib().pbrt_gpu_cancel(r.h))
-    t.start()
-    return t
-
-
 def full_time(r, rd):
     t0 = time.time()
     r.render(rd)
@@ -35,16 +29,27 @@ def full_time(r, rd):
 
 
 def check_cancel_then_render(sc, rd, small_rd, delay=0.4, bound=0.25):
+    """Enqueue the frame (render_async returns with the render in flight), cancel
+    it from another thread after `delay`, and require synchronize to return
+    PBRT_E_CANCELLED within `bound` seconds of the cancel."""
     with G.Renderer(sc) as r:
         G.lib().pbrt_gpu_cancel(r.h)   # nothing in flight: a no-op
-        t0 = time.time()
-        timer = cancel_after(r, delay)
+        r.render_async(rd)
+        t_cancel = []
+
+        def fire():
+            t_cancel.append(time.time())
+            G.lib().pbrt_gpu_cancel(r.h)
+
+        timer = threading.Timer(delay, fire)
+        timer.start()
         with pytest.raises(G.PbrtError) as ei:
-            r.render(rd)
-        dt = time.time() - t0
+            r.synchronize()
+        t_done = time.time()
         timer.join()
         assert ei.value.code == abi.PBRT_E_CANCELLED
-        assert dt < delay + bound, f"the frame ran {dt - delay:.3f} s past the cancel"
+        dt = t_done - t_cancel[0]
+        assert dt < bound, f"the frame ran {dt:.3f} s past the cancel"
         # the cancel died with its render: the next one is exact
         film, st = r.render(small_rd)
     rc, of, _ = O.render(sc.desc, small_rd, threads=min(16, os.cpu_count() or 1))
@@ -76,10 +81,16 @@ def test_cancel_serial_kernel():
 
 
 def test_cancel_direct_lighting_wave():
+    """k_dl_* is fast: size the frame from a timed 8x8 render so it lasts >= ~1 s."""
     sc = G.Scene.cornell(1920, 1080)
-    rd = abi.render_desc(32, 32, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING)
-    check_cancel_then_render(sc, rd, abi.render_desc(2, 2, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING,
-                                                     tile_end=48), delay=0.2)
+    dl = dict(integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING)
+    with G.Renderer(sc) as r:
+        t8 = full_time(r, abi.render_desc(8, 8, **dl))
+    side = 8
+    while side < 128 and t8 * (side / 8) ** 2 < 1.0:
+        side *= 2
+    check_cancel_then_render(sc, abi.render_desc(side, side, **dl),
+                             abi.render_desc(2, 2, tile_end=48, **dl), delay=min(0.1, t8 * (side / 8) ** 2 / 4))
 
 
 def test_cancel_outside_a_render_is_a_no_op():
