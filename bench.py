@@ -405,6 +405,8 @@ def main():
     chain_ms = sum(s.chain_ms for s in stats) / len(stats)
     paths_ms = sum(s.paths_ms for s in stats) / len(stats)
     kernel_kind = int(stats[0].kernel)
+    rays_c = sum(int(s.rays_closest) for s in stats)
+    rays_s = sum(int(s.rays_shadow) for s in stats)
     side = None
     if not args.no_side_mode:
         other = "throughput" if args.mode == "exact" else "exact"
@@ -450,6 +452,13 @@ def main():
                 "kernel": {1: "serial", 2: "wave", 3: "wavefront", 4: "wave_ci"}.get(kernel_kind, "?"),
             },
             "pipeline_ms": {"kernels": kern_ms, "chain": chain_ms, "paths": paths_ms, "merge": merge_ms},
+            # nominal W*H*spp, and the reference's ray segments counted in-kernel
+            # (closest-hit queries of Path.Li's loop + visibility rays; pbrt_gpu_stats.rays_*)
+            "nominal_samples_per_frame": W * H * S * S,
+            "rays": {"closest_per_frame": rays_c / len(stats) * (world if world > 1 else 1),
+                     "shadow_per_frame": rays_s / len(stats) * (world if world > 1 else 1),
+                     "per_s": (rays_c + rays_s) * (world if world > 1 else 1) / elapsed,
+                     "unit": "rays/s", "note": "reference ray segments (rank 0's count x N for N > 1)"},
             "first_frame_ms": first_ms,
             "first_frame_chain_ms": first.chain_ms,
             "roofline": roof,

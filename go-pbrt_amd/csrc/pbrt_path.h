@@ -1286,11 +1286,13 @@ __device__ inline bool estimate_direct_begin(const DevScene& sc, const SI& si, c
 }
 // EstimateDirect (integrator.go:79-195): an occluded shadow ray zeroes Li, so
 // Ld stays spec(0).
+// traced (optional): +1 when the visibility ray is traced (stats.rays_shadow).
 __device__ inline Spec estimate_direct(const DevScene& sc, uint16_t* stack, int& panic, const SI& si, const BSDF& b,
-                                       int li, V2 u_light) {
+                                       int li, V2 u_light, uint64_t* traced = nullptr) {
     Ray sr;
     Spec ld_vis;
     if (!estimate_direct_begin(sc, si, b, li, u_light, sr, ld_vis)) return spec(0);
+    if (traced) ++*traced;
     if (bvh_traverse<true>(sc, sr, nullptr, stack, panic)) return spec(0);
     return ld_vis;
 }
@@ -1300,9 +1302,9 @@ __device__ inline Spec estimate_direct(const DevScene& sc, uint16_t* stack, int&
 // BSDF.SampleF panics (integrator.go:134-139 always runs it); every other BSDF
 // is the shared estimate_direct.
 __device__ inline Spec estimate_direct_x(const DevScene& sc, uint16_t* stack, int& panic, const SI& si, const BSDF& b,
-                                         const BSDFX& x, int li, V2 u_light) {
+                                         const BSDFX& x, int li, V2 u_light, uint64_t* traced = nullptr) {
     if (x.kind != BXDF_KIND_MICROFACET && x.kind != BXDF_KIND_OREN_NAYAR)
-        return estimate_direct(sc, stack, panic, si, b, li, u_light);
+        return estimate_direct(sc, stack, panic, si, b, li, u_light, traced);
     const pbrt_light_desc& L = sc.lights[li];
     const bool is_delta = L.type != PBRT_LIGHT_DIFFUSE_AREA;
     LightSample ls;
@@ -1315,6 +1317,7 @@ __device__ inline Spec estimate_direct_x(const DevScene& sc, uint16_t* stack, in
             const V3 origin = offset_ray_origin(si.p, si.perr, si.n, ls.tp - si.p);
             const V3 target = offset_ray_origin(ls.tp, ls.tperr, ls.tn, origin - ls.tp);
             Ray sr{si.p, target - origin, 1 - 0.0001, si.time};
+            if (traced) ++*traced;
             const bool occluded = bvh_traverse<true>(sc, sr, nullptr, stack, panic);
             if (panic) return spec(0);
             if (!occluded) {
@@ -1403,8 +1406,7 @@ __device__ inline Spec uniform_sample_one_light(const DevScene& sc, Thread& t, c
     }
     V2 ul = get2d(t);
     const V2 us = get2d(t);   // uScattering: only the MIS half reads it
-    t.shadow_rays++;
-    Spec s = estimate_direct_x(sc, t.stack, t.panic, si, b, x, ln, ul);
+    Spec s = estimate_direct_x(sc, t.stack, t.panic, si, b, x, ln, ul, &t.shadow_rays);
     if (fidelity && !t.panic) estimate_direct_mis_ray(sc, t.stack, t.panic, si, b, ln, us);
     if (!t.panic && max_component(s) > 10) t.panic = PBRT_PANIC_LD_GT_10;
     return s;
@@ -1426,9 +1428,9 @@ __device__ __noinline__ Spec path_li(const DevScene& sc, Thread& t, Ray ray, int
         bounces++;
         t.bounce = bounces;
         if (bounces >= max_depth) {   // path.go:66 breaks whether or not the ray hits
+            t.closest_rays++;           // the reference traced it first (path.go:44-45)
             if (fidelity) {
                 SI tmp;
-                t.closest_rays++;
                 (void)bvh_traverse<false>(sc, ray, &tmp, t.stack, t.panic);
             }
             break;
@@ -1541,8 +1543,7 @@ __device__ __noinline__ Spec direct_li(const DevScene& sc, Thread& t, Ray ray, i
                 for (int j = 0; j < sc.n_lights; j++) {
                     V2 ul = get2d(t);
                     const V2 us = get2d(t);
-                    t.shadow_rays++;
-                    acc = acc + estimate_direct_x(sc, t.stack, t.panic, si, b, x, j, ul);
+                    acc = acc + estimate_direct_x(sc, t.stack, t.panic, si, b, x, j, ul, &t.shadow_rays);
                     if (fidelity && !t.panic) estimate_direct_mis_ray(sc, t.stack, t.panic, si, b, j, us);
                     if (t.panic) break;
                 }

@@ -93,6 +93,12 @@ __device__ __forceinline__ V2 c_get2d(Cursor& c, const SpecSampler& s) {
 }
 
 constexpr int kMaxCachedLights = 16;
+// a cached bounce-1 light estimate traced its visibility ray (ray counters;
+// or-ed into the estimate's panic word, whose low 16 bits are the panic kind)
+constexpr int kLdTraced = 0x10000;
+// per-path ray counts (stats.rays_closest / rays_shadow): closest-hit queries
+// in the low 16 bits, visibility rays in the high 16
+constexpr uint32_t kRayClosest = 1u, kRayShadow = 1u << 16;
 
 // Per-pixel bounce-1 state shared by all samples of the pixel (LDS).
 struct PixelCache {
@@ -100,7 +106,7 @@ struct PixelCache {
     BSDF b;
     V3 wo;                            // camera ray direction (path.go:91, #8)
     Spec ld[kMaxCachedLights];        // EstimateDirect(light l, uLight = (0,0))
-    int ld_panic[kMaxCachedLights];   // panic kind of that estimate (incl. Ld > 10)
+    int ld_panic[kMaxCachedLights];   // panic kind of that estimate (incl. Ld > 10) | kLdTraced
     int hit;                          // first hit exists and maxDepth > 1
     int first_panic;                  // panic of the camera-ray traversal
 };
@@ -128,6 +134,7 @@ struct PathState {
     Ray ray;
     int bounces;
     int first;
+    uint32_t rays;   // kRayClosest / kRayShadow counts of the path
 };
 // k_paths_ci's variant: the radiance sum lives in the lane's LDS slot (it is
 // only added to, never read, inside a bounce), freeing its registers for the
@@ -135,6 +142,7 @@ struct PathState {
 struct PathStateLds {
     Spec* L;
     Spec* aux;   // [0] beta0 and [1] ld_vis of a deferred shadow ray, held across the BSDF sample
+    uint32_t* rays;   // the path's ray counts (LDS slot)
     Spec beta;
     Ray ray;
     int bounces;
@@ -142,6 +150,8 @@ struct PathStateLds {
 };
 __device__ __forceinline__ void add_L(PathState& s, Spec v) { s.L = s.L + v; }
 __device__ __forceinline__ void add_L(PathStateLds& s, Spec v) { *s.L = *s.L + v; }
+__device__ __forceinline__ void add_rays(PathState& s, uint32_t v) { s.rays += v; }
+__device__ __forceinline__ void add_rays(PathStateLds& s, uint32_t v) { *s.rays += v; }
 // kWhich: 0 any iteration, 1 only the first (s.first == 1: bounce 1 from the
 // pixel cache, no traversal), 2 only later ones (s.first == 0).
 //
@@ -165,6 +175,7 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
     if (!first) {
         s.bounces++;
         bounce = s.bounces;
+        add_rays(s, kRayClosest);   // the reference's Intersect (path.go:44-45), also at maxDepth
         if (s.bounces >= max_depth) return true;
         const bool hit = bvh_traverse<false, PBRT_PATHS_LB>(sc, s.ray, &isect, stack, panic);
         if (!hit) return true;
@@ -178,6 +189,7 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
         isect = pc.si;
         b = pc.b;
         wo = pc.wo;
+        add_rays(s, kRayClosest);   // the camera ray's closest hit
     }
     bool pending = false, shadow = false;   // a deferred L += beta0 * Ld (with a shadow ray)
     constexpr bool kLdsAux = std::is_same<State, PathStateLds>::value;
@@ -200,8 +212,10 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
             c_get2d(c, ss);
             if (first) {
                 const Spec ld = pc.ld[ln];
-                if (pc.ld_panic[ln]) {
-                    panic = pc.ld_panic[ln];
+                const int lp = pc.ld_panic[ln];
+                if (lp & kLdTraced) add_rays(s, kRayShadow);
+                if (lp & 0xFFFF) {
+                    panic = lp & 0xFFFF;
                     return true;
                 }
                 add_L(s, smul(s.beta, ld));
@@ -240,6 +254,7 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
     if (pending) {
         Spec ld = spec(0);
         if (shadow) {
+            add_rays(s, kRayShadow);
             const bool occluded = bvh_traverse<true, PBRT_PATHS_LB>(sc, sr, nullptr, stack, panic);
             if (panic) return true;
             if (!occluded) {

@@ -298,6 +298,7 @@ struct WaveBufs {
     double* s1d;        // [slot][ppt][ndims * spp]
     uint64_t* memb;     // [slot][ppt][spp]   PCG32 state at sample k's offset
     double* L;          // [slot][ppt][spp][3]
+    uint32_t* rays;     // [slot][ppt][spp]      the sample's reference ray counts (kRayClosest / kRayShadow)
     PanicRec* ppanic;   // [slot][ppt]        first panic of the pixel in sample order
     int32_t* tile_npx;  // [slot]             pixels with records (a panic ends the tile)
     int64_t ppt;        // pixel records per tile slot (tile_size^2)
@@ -462,7 +463,7 @@ __host__ __device__ constexpr size_t paths_group_l_off() {   // per-lane radianc
 }
 template <int P>
 __host__ __device__ constexpr int paths_group_lds(int per) {   // bytes, per wave
-    return (int)(paths_group_l_off<P>() + 3 * kWave * sizeof(Spec) + (size_t)P * per * 8);
+    return (int)(paths_group_l_off<P>() + 3 * kWave * sizeof(Spec) + kWave * 4 + (size_t)P * per * 8);
 }
 // kMB: THROUGHPUT mode, sample k of pixel pi starts from its own stream
 // mb_state(tile, pi, k) instead of the chain's offset state.
@@ -481,7 +482,8 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
     PMeta* meta = (PMeta*)(wlds + paths_group_meta_off<P>());
     Spec* Lslot = (Spec*)(wlds + paths_group_l_off<P>()) + lane;
     Spec* aux = (Spec*)(wlds + paths_group_l_off<P>()) + kWave + 2 * lane;
-    double* s1d = (double*)(wlds + paths_group_l_off<P>() + 3 * kWave * sizeof(Spec));
+    uint32_t* rslot = (uint32_t*)(wlds + paths_group_l_off<P>() + 3 * kWave * sizeof(Spec)) + lane;
+    double* s1d = (double*)(wlds + paths_group_l_off<P>() + 3 * kWave * sizeof(Spec) + kWave * 4);
     if (lane == 0) {
         int cum = 0;
         for (int j = 0; j < P; j++) {
@@ -521,10 +523,11 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
         const int j = lane / nl, l = lane - j * nl;
         if (meta[j].nv > 0 && meta[j].hit && pcs[j].b.n_bxdfs > 0) {
             int pl = 0;
-            Spec ld = estimate_direct(sc, nullptr, pl, pcs[j].si, pcs[j].b, l, V2{0.0, 0.0});
+            uint64_t traced = 0;
+            Spec ld = estimate_direct(sc, nullptr, pl, pcs[j].si, pcs[j].b, l, V2{0.0, 0.0}, &traced);
             if (!pl && max_component(ld) > 10) pl = PBRT_PANIC_LD_GT_10;
             pcs[j].ld[l] = ld;
-            pcs[j].ld_panic[l] = pl;
+            pcs[j].ld_panic[l] = pl | (traced ? kLdTraced : 0);
         }
     }
     wave_sync();
@@ -535,6 +538,7 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
     PathStateLds ps;
     ps.L = Lslot;
     ps.aux = aux;
+    ps.rays = rslot;
     Cursor c;
     int pnc = 0, bnc = 1;
     for (;;) {
@@ -553,6 +557,7 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
                     o[0] = 0.0;
                     o[1] = 0.0;
                     o[2] = 0.0;
+                    wb.rays[rec * n + k] = kRayClosest;   // the camera ray's (missed or maxDepth 1) query
                 } else {
                     w = t;
                     c.rng.state = kMB ? mb_state(meta[j].tile, (uint64_t)(rec % wb.ppt), (uint64_t)k)
@@ -564,6 +569,7 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
                     c.k = k;
                     c.kdep = 0;
                     *ps.L = spec(0);
+                    *ps.rays = 0;
                     ps.beta = spec(1);
                     ps.bounces = 1;
                     ps.first = 1;
@@ -592,6 +598,7 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
                 o[0] = Lp.r;
                 o[1] = Lp.g;
                 o[2] = Lp.b;
+                wb.rays[rec * n + k] = *ps.rays;
                 if (pnc)
                     atomicMin(&pkey[j], ((unsigned long long)k << 32) | ((unsigned long long)(bnc & 0xFFFFFF) << 8) |
                                             (unsigned long long)((pnc + 1) & 0xFF));
@@ -665,7 +672,9 @@ struct alignas(16) PwPath {
     int64_t rec;     // pixel record in the batch
     int32_t k, cur1d, cur2d, kdep;
     int32_t bounces, best, flags, pnc;
-    int32_t bnc, pad0, pad1, pad2;
+    int32_t bnc;
+    uint32_t rays;   // kRayClosest / kRayShadow counts of the path
+    int32_t pad1, pad2;
 };
 constexpr int kPwPending = 1, kPwShadow = 2, kPwDone = 4;
 constexpr int kPwMaxKeys = 64;   // material keys of the sort (more materials share the last)
@@ -711,6 +720,7 @@ __device__ __forceinline__ void pw_finish(const WaveBufs& wb, int n, const PwPat
     o[0] = p.L.r;
     o[1] = p.L.g;
     o[2] = p.L.b;
+    wb.rays[p.rec * n + p.k] = p.rays;
     if (p.pnc)
         atomicMin(&pkey[p.rec], ((unsigned long long)p.k << 32) | ((unsigned long long)(p.bnc & 0xFFFFFF) << 8) |
                                     (unsigned long long)((p.pnc + 1) & 0xFF));
@@ -719,6 +729,7 @@ __device__ __forceinline__ void pw_finish(const WaveBufs& wb, int n, const PwPat
 __device__ __forceinline__ bool pw_next_bounce(PwPath& p, int max_depth) {
     p.bounces++;
     p.bnc = p.bounces;
+    p.rays += kRayClosest;   // the reference's Intersect of this iteration (k_pw_trace, or the maxDepth break)
     return p.bounces < max_depth;
 }
 // the bounce-1 light estimates of the pixel record (global-memory PixelCache)
@@ -742,10 +753,11 @@ __global__ __launch_bounds__(kWave) void k_pw_cache(DevScene sc, WaveBufs wb, in
     const PixelRec& pr = wb.prec[rec0 + r];
     if (!(pr.hit && pr.b.n_bxdfs > 0)) return;
     int pl = 0;
-    const Spec ld = estimate_direct(sc, stack_lds + threadIdx.x, pl, pr.si, pr.b, l, V2{0.0, 0.0});
+    uint64_t traced = 0;
+    const Spec ld = estimate_direct(sc, stack_lds + threadIdx.x, pl, pr.si, pr.b, l, V2{0.0, 0.0}, &traced);
     if (!pl && max_component(ld) > 10) pl = PBRT_PANIC_LD_GT_10;
     ldc[i] = ld;
-    ldp[i] = pl;
+    ldp[i] = pl | (traced ? kLdTraced : 0);
 }
 
 template <bool kMB>
@@ -770,6 +782,7 @@ __global__ __launch_bounds__(kWave) void k_pw_start(DevScene sc, RenderParams rp
     p.L = spec(0);
     p.pnc = 0;
     p.bnc = 1;
+    p.rays = kRayClosest;   // the camera ray's query
     if (!pr.hit) {   // no traced bounce: the sample's radiance is 0
         pw_finish(wb, n, p, pkey);
         return;
@@ -788,6 +801,7 @@ __global__ __launch_bounds__(kWave) void k_pw_start(DevScene sc, RenderParams rp
     s.beta = spec(1);
     s.bounces = 1;
     s.first = 1;
+    s.rays = 0;
     const PwCache pc{pr.si, pr.b, pr.wo, ldc + r * sc.n_lights, ldp + r * sc.n_lights};
     const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, n, rp.ndims};
     int pnc = 0, bnc = 1;
@@ -802,6 +816,7 @@ __global__ __launch_bounds__(kWave) void k_pw_start(DevScene sc, RenderParams rp
     p.kdep = c.kdep;
     p.pnc = pnc;
     p.bnc = bnc;
+    p.rays = s.rays;   // path_step<1> counted the camera ray and its light sample
     if (!done) done = !pw_next_bounce(p, rp.max_depth);
     paths[i] = p;
     if (done)
@@ -965,6 +980,7 @@ __global__ __launch_bounds__(kWave) void k_pw_shadow(DevScene sc, RenderParams r
             if (p.flags & kPwShadow) {
                 int panic = 0;
                 Ray sr = p.sr;
+                p.rays += kRayShadow;
                 const bool occluded = bvh_traverse<true>(sc, sr, nullptr, stack_lds + threadIdx.x, panic);
                 if (panic) {
                     p.pnc = panic;
@@ -1136,6 +1152,28 @@ __global__ void k_panic_reduce(WaveBufs wb, int64_t slot_base, int64_t nslots_ba
 // Bounce 1 of every pixel record of the batch: the camera ray through the
 // pixel corner (pFilm and pLens are (0,0) for every sample), its closest hit
 // and BSDF. The ray time is patched by the chain kernel once StartPixel gives it.
+// stats.rays_closest / rays_shadow of a batch: every valid sample's counts
+// (pixels with records, samples 1 .. nvalid-1), one atomic pair per wave
+__global__ __launch_bounds__(256) void k_ray_count(WaveBufs wb, int64_t nb, int n, Counters* __restrict__ ctr) {
+    unsigned long long cl = 0, sh = 0;
+    const int64_t total = nb * wb.ppt * n;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t rec = i / n, k = i - rec * n, bs = rec / wb.ppt, pi = rec % wb.ppt;
+        if (k < 1 || pi >= wb.tile_npx[bs] || k >= wb.prec[rec].nvalid) continue;
+        const uint32_t v = wb.rays[i];
+        cl += v & 0xFFFFu;
+        sh += v >> 16;
+    }
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+        cl += __shfl_down(cl, off);
+        sh += __shfl_down(sh, off);
+    }
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+        atomicAdd(&ctr->closest_rays, cl);
+        atomicAdd(&ctr->shadow_rays, sh);
+    }
+}
+
 __global__ __launch_bounds__(kWave) void k_wf_primary(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
                                                       int64_t nb) {
     __shared__ uint16_t stack_lds[64 * kStackStride];
@@ -1300,6 +1338,7 @@ __global__ __launch_bounds__(kWave) void k_dl_samples(DevScene sc, RenderParams 
         double* o = wb.L + (rec * n + k) * 3;
         Spec L = spec(0);
         int panic = pr.panic0;
+        uint64_t shadow = 0;   // visibility rays traced (the camera ray's query is counted below)
         if (!panic && pr.hit) {
             Cursor c;
             c.rng.state = wb.memb[rec * n + k];
@@ -1320,14 +1359,14 @@ __global__ __launch_bounds__(kWave) void k_dl_samples(DevScene sc, RenderParams 
                     for (int j = 0; j < nl && !panic; j++) {
                         const V2 ul = c_get2d(c, ss);
                         c_get2d(c, ss);
-                        acc = acc + estimate_direct(sc, stack_lds + threadIdx.x, panic, pr.si, pr.b, j, ul);
+                        acc = acc + estimate_direct(sc, stack_lds + threadIdx.x, panic, pr.si, pr.b, j, ul, &shadow);
                     }
                     L = L + acc;
                 } else {   // UniformSampleOneLight with no distribution (integrator.go:48-77)
                     const int ln = (int)gomath::to_int(gomath::min(c_get1d(c, ss) * (double)nl, (double)(nl - 1)));
                     const V2 ul = c_get2d(c, ss);
                     c_get2d(c, ss);
-                    const Spec s = estimate_direct(sc, stack_lds + threadIdx.x, panic, pr.si, pr.b, ln, ul);
+                    const Spec s = estimate_direct(sc, stack_lds + threadIdx.x, panic, pr.si, pr.b, ln, ul, &shadow);
                     if (!panic && max_component(s) > 10) panic = PBRT_PANIC_LD_GT_10;
                     L = L + s;
                 }
@@ -1337,6 +1376,7 @@ __global__ __launch_bounds__(kWave) void k_dl_samples(DevScene sc, RenderParams 
         o[0] = L.r;
         o[1] = L.g;
         o[2] = L.b;
+        wb.rays[rec * n + k] = kRayClosest + (uint32_t)shadow * kRayShadow;
         if (panic)
             atomicMin((unsigned long long*)&wb.memb[rec * n],
                       ((unsigned long long)k << 32) | (unsigned long long)((panic + 1) & 0xFF));
@@ -2543,7 +2583,7 @@ int wave_buffers(pbrt_gpu_ctx* c) {
     const int64_t ppt = rp.tile_size * rp.tile_size, n = rp.spp, nd = rp.ndims > 0 ? rp.ndims : 1;
     auto al = [](int64_t b) { return (b + 255) & ~int64_t(255); };
     const int64_t per_tile = al(ppt * (int64_t)sizeof(PixelRec)) + al(ppt * nd * n * 8) + al(ppt * n * 8) +
-                             al(ppt * n * 24) + al(ppt * (int64_t)sizeof(PanicRec)) + al(4);
+                             al(ppt * n * 24) + al(ppt * n * 4) + al(ppt * (int64_t)sizeof(PanicRec)) + al(4);
     double gb = 96.0;
     {
         size_t free_b = 0, total_b = 0;
@@ -2573,6 +2613,7 @@ int wave_buffers(pbrt_gpu_ctx* c) {
     wb.s1d = (double*)take(ppt * nd * n * 8);
     wb.memb = (uint64_t*)take(ppt * n * 8);
     wb.L = (double*)take(ppt * n * 24);
+    wb.rays = (uint32_t*)take(ppt * n * 4);
     wb.ppanic = (PanicRec*)take(ppt * (int64_t)sizeof(PanicRec));
     wb.tile_npx = (int32_t*)take(4);
     wb.ppt = ppt;
@@ -2990,6 +3031,11 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                                    c->d_film, rp, c->wb, sb, nb, c->d_films);
                 hipLaunchKernelGGL(k_panic_reduce, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, c->stream, c->wb,
                                    sb, nb, c->d_panics, c->d_ctr);
+                if (rp.spp > 1)
+                    hipLaunchKernelGGL(k_ray_count,
+                                       dim3((unsigned)std::min<int64_t>((nb * c->wb.ppt * rp.spp + 255) / 256,
+                                                                        (int64_t)c->n_simd * 16)),
+                                       dim3(256), 0, c->stream, c->wb, nb, rp.spp, c->d_ctr);
             }
         } else {
             c->last_kernel = PBRT_KERNEL_SERIAL;
@@ -3057,6 +3103,8 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
     st.merge_ms = ms_merge;
     st.kernel = c->last_kernel;
     st.batches = c->n_batches;
+    st.rays_closest = ctr.closest_rays;
+    st.rays_shadow = ctr.shadow_rays;
     for (int b = 0; b < c->n_batches; b++) {
         float a = 0, p = 0;
         (void)hipEventElapsedTime(&a, c->bev[3 * b + 0], c->bev[3 * b + 1]);

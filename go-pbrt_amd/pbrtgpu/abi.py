@@ -239,6 +239,8 @@ class GpuStats(C.Structure):
         ("batches", C.c_int32),
         ("chain_ms", C.c_double),
         ("paths_ms", C.c_double),
+        ("rays_closest", C.c_uint64),
+        ("rays_shadow", C.c_uint64),
     ]
 
 

@@ -254,6 +254,15 @@ typedef struct pbrt_gpu_stats {
     int32_t batches;         /* WAVE/WAVEFRONT: tile batches of the frame         */
     double chain_ms;         /* WAVE/WAVEFRONT: sample-offset chain time, summed  */
     double paths_ms;         /* WAVE/WAVEFRONT: k_paths time (full paths), summed */
+    /* The reference's ray segments for the rendered paths, counted in-kernel
+     * (SURVEY 8(d)): closest-hit queries of Path.Li's loop (path.go:44-45, one per
+     * iteration, incl. the one at bounces == maxDepth; DirectLighting: one per
+     * Li call, directlighting.go:67) and any-hit visibility rays of light
+     * sampling (VisibilityTester.Unoccluded, integrator.go:112-119), on every
+     * kernel. EstimateDirect's BSDF-sampled ray, which always adds 0, is not
+     * counted. Equal to the oracle's counts. */
+    uint64_t rays_closest;
+    uint64_t rays_shadow;
 } pbrt_gpu_stats;
 
 /* ----------------------------------------------------------- ray batches */

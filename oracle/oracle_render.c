@@ -1152,8 +1152,7 @@ static spec estimate_direct(orc_ctx* oc, const si_t* si, const bsdf_t* b, v2 u_s
             ray_t r2;
             r2.o = offset_ray_origin(si->p, si->perr, si->n, wi2);
             r2.d = wi2; r2.tmax = INFINITY; r2.time = si->time;
-            si_t tmp;
-            oc->closest_rays++;
+            si_t tmp;   /* not counted in closest_rays (its result is always 0) */
             orc_bvh_intersect(oc, &r2, &tmp);
         }
     }
@@ -1213,9 +1212,9 @@ static spec path_li(orc_ctx* oc, sampler_t* smp, ray_t ray) {
         bounces++;
         oc->cur_bounce = bounces;
         if (bounces >= rd->max_depth) {          /* path.go:66 (hit or miss)  */
-            if (panic_fidelity(oc)) {            /* traced by path.go:45 first */
+            oc->closest_rays++;                  /* traced by path.go:45 first */
+            if (panic_fidelity(oc)) {
                 si_t tmp;
-                oc->closest_rays++;
                 orc_bvh_intersect(oc, &ray, &tmp);
             }
             break;
