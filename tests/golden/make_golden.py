@@ -6,6 +6,7 @@ no Go toolchain in this image and no render-level goldens of its own (SURVEY
 §4, §8c). Re-run after an intentional oracle change:
     python tests/golden/make_golden.py
 """
+import ctypes as C
 import hashlib
 import json
 import os
@@ -51,6 +52,77 @@ def pcg_vectors():
     return out
 
 
+# SURVEY 8(c)'s build-generated fixtures (round 3): frozen known answers that
+# do not move when the oracle is edited
+TILE_FILMS = {   # 256x256 README frames whose every tile is pinned on its own
+    "readme_256x256_s2x2_path": dict(spp_x=2, spp_y=2),
+    "readme_256x256_s4x4_path": dict(spp_x=4, spp_y=4),
+}
+# config B's frame (1920x1080, Stratified(8,8), Path(10)): the 4x4 tiles whose
+# pixels are x 928..991, y 480..543 -- a 64x64 crop of the headline frame
+CROP_B = dict(w=1920, h=1080, tx0=58, ty0=30, n=4, render=dict(spp_x=8, spp_y=8))
+DRAW_TILES = (0, 4080, 8159)   # per-pixel PCG32 draw counts of these config-B tiles
+N_RAYS = 10000                 # batch-intersect hit records (bvh.go:659-765)
+
+
+def tile_films(name, kw):
+    sc = O.OracleScene.readme(256, 256)
+    rd = abi.render_desc(**kw)
+    rc, film, st = O.render(sc.desc, rd, threads=8)
+    assert rc == 0
+    n = int(O.lib().oracle_num_tiles(C.byref(sc.desc), C.byref(rd)))
+    hashes = []
+    for t in range(n):
+        rc, ft, _ = O.render(sc.desc, abi.render_desc(**dict(kw, tile_begin=t, tile_end=t + 1)), threads=1)
+        assert rc == 0
+        hashes.append(hashlib.sha256(ft.tobytes()).hexdigest())
+    return film, st, hashes
+
+
+def crop_b():
+    c = CROP_B
+    sc = O.OracleScene.readme(c["w"], c["h"])
+    ntx = (c["w"] + 15) // 16
+    acc = None
+    paths = 0
+    for ty in range(c["ty0"], c["ty0"] + c["n"]):
+        t0 = ty * ntx + c["tx0"]
+        rc, f, st = O.render(sc.desc, abi.render_desc(**dict(c["render"], tile_begin=t0, tile_end=t0 + c["n"])),
+                             threads=8)
+        assert rc == 0
+        acc = f if acc is None else acc + f
+        paths += st.paths
+    x0, y0 = c["tx0"] * 16 - 1, c["ty0"] * 16 - 1   # the block's pixels plus the 1-px filter apron
+    win = acc[y0:y0 + 16 * c["n"] + 2, x0:x0 + 16 * c["n"] + 2].copy()
+    return win, paths
+
+
+def draw_counts():
+    sc = O.OracleScene.readme(1920, 1080)
+    rd = abi.render_desc(8, 8)
+    out = {}
+    for t in DRAW_TILES:
+        rc, d = O.tile_draws(sc.desc, rd, t)
+        assert rc == 0
+        out[str(t)] = [int(v) for v in d]
+    return out
+
+
+def hit_records():
+    """10^4 seeded random rays in the README scene: origins in a box around the
+    spheres, directions uniform on the sphere, TMax +Inf or a random finite value."""
+    rng = np.random.default_rng(20261017)
+    o = rng.uniform([-20.0, 0.5, -20.0], [110.0, 60.0, 110.0], size=(N_RAYS, 3))
+    d = rng.normal(size=(N_RAYS, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    tmax = np.where(rng.uniform(size=N_RAYS) < 0.5, np.inf, rng.uniform(1.0, 200.0, size=N_RAYS))
+    rays = np.concatenate([o, d, tmax[:, None]], axis=1)
+    sc = O.OracleScene.readme(64, 64)
+    closest = O.intersect(sc.desc, rays, closest=True)
+    anyhit = O.intersect(sc.desc, rays, closest=False)
+    return rays, closest, anyhit
+
+
 def main():
     commit = subprocess.run(["git", "-C", REPO, "rev-parse", "--short", "HEAD"], capture_output=True,
                             text=True).stdout.strip()
@@ -62,6 +134,22 @@ def main():
                                "scene": CASES[name][0], "w": CASES[name][1], "h": CASES[name][2],
                                "render": {k: (int(v) if isinstance(v, bool) else v) for k, v in CASES[name][3].items()}}
     meta["pcg32_first16"] = pcg_vectors()
+    meta["tile_films"] = {}
+    for name, kw in TILE_FILMS.items():
+        film, st, hashes = tile_films(name, kw)
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), film=film)
+        meta["tile_films"][name] = {"sha256": hashlib.sha256(film.tobytes()).hexdigest(), "paths": int(st.paths),
+                                    "render": kw, "tile_sha256": hashes}
+    win, paths = crop_b()
+    np.savez_compressed(os.path.join(HERE, "readme_1920x1080_s8x8_crop64.npz"), film=win)
+    meta["crop_b"] = dict(CROP_B, sha256=hashlib.sha256(win.tobytes()).hexdigest(), paths=int(paths),
+                          window=[CROP_B["tx0"] * 16 - 1, CROP_B["ty0"] * 16 - 1, 16 * CROP_B["n"] + 2])
+    meta["draw_counts_1920x1080_s8x8"] = draw_counts()
+    rays, closest, anyhit = hit_records()
+    np.savez_compressed(os.path.join(HERE, "readme_hits_1e4.npz"), rays=rays, closest=closest, anyhit=anyhit)
+    meta["hits"] = {"n": N_RAYS, "sha256_closest": hashlib.sha256(closest.tobytes()).hexdigest(),
+                    "sha256_anyhit": hashlib.sha256(anyhit.tobytes()).hexdigest(),
+                    "hit_fraction": float(closest[:, 0].mean())}
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
     print("wrote", len(CASES), "cases")
