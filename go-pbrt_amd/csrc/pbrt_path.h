@@ -63,13 +63,32 @@ struct DevScene {
     const uint32_t* gmasks;
     int n_groups;
     // pbrt_gpu_cancel's flag for the render in flight (fine-grained host memory,
-    // written by the host while kernels run); polled between units of work
+    // written by the host while kernels run), and its device-memory copy that
+    // the first wave to read the host flag set publishes (cleared by the host
+    // before every render); polled between units of work
     const int* cancel;
+    int* cancel_seen;
 };
-// The flag as the whole wave sees it (one system-scope load, lane 0's value).
-__device__ __forceinline__ bool cancel_requested(const DevScene& sc) {
-    const int v = __hip_atomic_load(sc.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+// Is the render cancelled? The device copy is an L2 read; poll_host (a rate
+// the caller bounds: host-memory reads cross PCIe) also reads the host flag and
+// publishes it. The value is the whole wave's (lane 0's).
+__device__ __forceinline__ bool cancel_requested(const DevScene& sc, bool poll_host) {
+    int v = __hip_atomic_load(sc.cancel_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!v && poll_host) {
+        v = __hip_atomic_load(sc.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (v) __hip_atomic_store(sc.cancel_seen, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     return __builtin_amdgcn_readfirstlane(v) != 0;
+}
+// cancel_requested with the host flag read at most once a millisecond per
+// caller (last_host: that caller's wall_clock64 of its last host read; the
+// clock runs at 100 MHz): for loops whose iteration length varies by orders of
+// magnitude (a pixel of Stratified(64,64) vs of (2,2)).
+__device__ __forceinline__ bool cancel_polled(const DevScene& sc, uint64_t& last_host) {
+    const uint64_t now = wall_clock64();
+    const bool host = now - last_host >= 100000;
+    if (host) last_host = now;
+    return cancel_requested(sc, host);
 }
 
 // ---------------------------------------------------------------- PCG32 (rng.go)

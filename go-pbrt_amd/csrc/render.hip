@@ -171,9 +171,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kMinWaves
     const pbrt_camera_desc& cam = *sc.camera;
 
     const bool mb = rp.mode == PBRT_MODE_THROUGHPUT;
+    uint64_t last_host_poll = wall_clock64();
     for (int64_t py = y0; py < y1; py++) {
         for (int64_t px = x0; px < x1; px++) {
-            if (__hip_atomic_load(sc.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;   // pbrt_gpu_cancel
+            if (cancel_polled(sc, last_host_poll)) return;   // pbrt_gpu_cancel
             const uint64_t pi = (uint64_t)((py - y0) * (x1 - x0) + (px - x0));
             if (mb) t.rng.state = mb_state((uint64_t)tile, pi, 0);
             start_pixel(t);
@@ -191,6 +192,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kMinWaves
                 for (int k = 0; k < fp.n; k++)
                     for (int c = 0; c < 3; c++) acc[k][c] = tf[fp.off[k] * 3 + c];
             while (next_sample(t)) {
+                // (a pixel of large spp runs for milliseconds: poll inside it too)
+                if ((t.sample_index & 15) == 0 && cancel_polled(sc, last_host_poll)) return;
                 if (mb) t.rng.state = mb_state((uint64_t)tile, pi, (uint64_t)t.sample_index);
                 V2 u0 = get2d(t);
                 V2 plens = get2d(t);
@@ -637,7 +640,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kPathsWav
     DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr,
     int s1d_lds) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];   // paths_group_lds<P>
-    if (cancel_requested(sc)) return;   // one wave per workgroup
+    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;   // one wave per workgroup
     stage_nodes(sc);
     paths_group<P, kMB>(sc, rp, wb, slot_base, (int64_t)blockIdx.x * P, nrec, ctr, lds, s1d_lds);
 }
@@ -766,7 +769,7 @@ __global__ __launch_bounds__(kWave) void k_pw_start(DevScene sc, RenderParams rp
                                                     const int* __restrict__ ldp, PwPath* __restrict__ paths,
                                                     PwQueues qs, unsigned long long* __restrict__ pkey) {
     const int n = rp.spp;
-    if (cancel_requested(sc)) return;
+    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (n < 2 || i >= nrec * (n - 1)) return;
     const int64_t r = i / (n - 1);
@@ -831,7 +834,7 @@ __global__ __launch_bounds__(kWave) void k_pw_trace(DevScene sc, RenderParams rp
                                                     PwQueues qs, int cin, int n_keys,
                                                     unsigned long long* __restrict__ pkey) {
     __shared__ uint16_t stack_lds[64 * kStackStride];
-    if (cancel_requested(sc)) return;
+    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
     stage_nodes(sc);
     const uint32_t* qin = qs.q[cin];
     const uint32_t nq = qs.cnt[cin];
@@ -877,7 +880,7 @@ __global__ __launch_bounds__(256) void k_pw_scatter(const PwPath* __restrict__ p
 __global__ __launch_bounds__(kWave) void k_pw_shade(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
                                                     PwPath* __restrict__ paths, PwQueues qs, int sorted,
                                                     unsigned long long* __restrict__ pkey) {
-    if (cancel_requested(sc)) return;
+    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
     const uint32_t* qin = sorted ? qs.sorted : qs.q[2];
     const uint32_t nh = qs.cnt[2];
     const int n = rp.spp;
@@ -967,7 +970,7 @@ __global__ __launch_bounds__(kWave) void k_pw_shadow(DevScene sc, RenderParams r
                                                      PwPath* __restrict__ paths, PwQueues qs,
                                                      unsigned long long* __restrict__ pkey) {
     __shared__ uint16_t stack_lds[64 * kStackStride];
-    if (cancel_requested(sc)) return;
+    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
     stage_nodes(sc);
     const uint32_t ns = qs.cnt[1];
     if (blockIdx.x == 0)   // hits and key counts, for the next pass
@@ -1043,7 +1046,7 @@ __global__ __launch_bounds__(kWave) void k_mb_setup(DevScene sc, RenderParams rp
     __shared__ uint16_t stack_lds[64 * kStackStride];
     __shared__ uint64_t sh_state;
     const int lane = threadIdx.x;
-    if (cancel_requested(sc)) return;
+    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
     stage_nodes(sc);
     const int64_t bslot = blockIdx.x / wb.ppt, pi = blockIdx.x % wb.ppt, rec = blockIdx.x;
     if (bslot >= nslots_batch) return;
@@ -1082,7 +1085,10 @@ __global__ __launch_bounds__(kWave) void k_mb_setup(DevScene sc, RenderParams rp
 // One thread per tile-film pixel: the tile film of the serial replay.
 __global__ __launch_bounds__(256) void k_film(const pbrt_film_desc* __restrict__ film_desc, RenderParams rp,
                                               WaveBufs wb, int64_t slot_base, int64_t nslots_batch,
-                                              double* __restrict__ films) {
+                                              double* __restrict__ films, const int* __restrict__ cancel_seen) {
+    // a cancelled render's samples are incomplete: its film is not valid (pbrt_gpu_cancel)
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(cancel_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+        return;
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t per = rp.slot_w * rp.slot_h;
     if (gid >= nslots_batch * per) return;
@@ -1154,7 +1160,10 @@ __global__ void k_panic_reduce(WaveBufs wb, int64_t slot_base, int64_t nslots_ba
 // and BSDF. The ray time is patched by the chain kernel once StartPixel gives it.
 // stats.rays_closest / rays_shadow of a batch: every valid sample's counts
 // (pixels with records, samples 1 .. nvalid-1), one atomic pair per wave
-__global__ __launch_bounds__(256) void k_ray_count(WaveBufs wb, int64_t nb, int n, Counters* __restrict__ ctr) {
+__global__ __launch_bounds__(256) void k_ray_count(WaveBufs wb, int64_t nb, int n, Counters* __restrict__ ctr,
+                                                   const int* __restrict__ cancel_seen) {
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(cancel_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+        return;   // a cancelled render reports no counts
     unsigned long long cl = 0, sh = 0;
     const int64_t total = nb * wb.ppt * n;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -1177,7 +1186,7 @@ __global__ __launch_bounds__(256) void k_ray_count(WaveBufs wb, int64_t nb, int 
 __global__ __launch_bounds__(kWave) void k_wf_primary(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
                                                       int64_t nb) {
     __shared__ uint16_t stack_lds[64 * kStackStride];
-    if (cancel_requested(sc)) return;
+    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
     stage_nodes(sc);
     const int64_t rec = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (rec >= nb * wb.ppt) return;
@@ -1260,7 +1269,7 @@ __global__ __launch_bounds__(kWave) void k_dl_setup(DevScene sc, RenderParams rp
     __shared__ uint64_t sh_state;
     const int64_t bs = blockIdx.x;
     const int lane = threadIdx.x;
-    if (bs >= nb || cancel_requested(sc)) return;
+    if (bs >= nb || cancel_requested(sc, (bs & 63) == 0)) return;
     const PcgJump& J = *jump;
     const int64_t tile = tile_of_slot(rp, slot_base + bs);
     int64_t x0, y0, x1, y1;
@@ -1277,7 +1286,7 @@ __global__ __launch_bounds__(kWave) void k_dl_setup(DevScene sc, RenderParams rp
     uint64_t S = seed.state;
     int64_t used = npx;
     for (int64_t pi = 0; pi < npx; pi++) {
-        if (cancel_requested(sc)) {   // pbrt_gpu_cancel (large spp: a pixel's StartPixel is long)
+        if (cancel_requested(sc, (pi & 15) == 0)) {   // pbrt_gpu_cancel (large spp: a pixel's StartPixel is long)
             used = pi;
             break;
         }
@@ -1319,7 +1328,7 @@ __global__ __launch_bounds__(kWave) void k_dl_setup(DevScene sc, RenderParams rp
 __global__ __launch_bounds__(kWave) void k_dl_samples(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
                                                       int64_t nrec) {
     __shared__ uint16_t stack_lds[64 * kStackStride];
-    if (cancel_requested(sc)) return;
+    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
     stage_nodes(sc);
     const int n = rp.spp;
     if (n < 2) return;
@@ -1328,7 +1337,7 @@ __global__ __launch_bounds__(kWave) void k_dl_samples(DevScene sc, RenderParams 
     const int64_t total = nrec * (n - 1), stride = (int64_t)gridDim.x * blockDim.x;
     int pass = 0;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx - threadIdx.x < total; idx += stride) {
-        if ((++pass & 15) == 0 && cancel_requested(sc)) return;
+        if ((++pass & 15) == 0 && cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
         if (idx >= total) continue;
         const int64_t rec = idx / (n - 1);
         const int k = 1 + (int)(idx - rec * (n - 1));
@@ -1430,7 +1439,7 @@ __global__ __launch_bounds__(kWave) void k_tile_cost(DevScene sc, RenderParams r
                                                      int64_t nb, float* __restrict__ feat,
                                                      uint64_t* __restrict__ keys) {
     __shared__ uint16_t stack_lds[64 * kStackStride];
-    if (cancel_requested(sc)) return;
+    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
     stage_nodes(sc);
     const int64_t bs = blockIdx.x;
     const int lane = threadIdx.x;
@@ -1621,6 +1630,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
     __syncthreads();
 
     uint32_t cancel_poll = 0;   // chain steps since the leader last read the cancel flag
+    uint64_t last_host_poll = t_begin;   // when this workgroup last read the host flag
     // lane trajectory state
     uint32_t off = kNoOff;
     uint64_t st0 = 0;
@@ -1666,8 +1676,13 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
                 // pixel record by k_wf_primary; only the ray time needs StartPixel
                 PixelRec& pr = wb.prec[rec];
                 const int hit0 = pr.hit, panic0 = pr.panic0;
-                if (tid == 0 && cancel_requested(sc))   // pbrt_gpu_cancel: every group of the workgroup ends
-                    for (int q2 = 0; q2 < G; q2++) gs[q2].phase = 2;
+                if (tid == 0) {   // pbrt_gpu_cancel: every group of the workgroup ends
+                    const uint64_t now = wall_clock64();
+                    const bool host = now - last_host_poll >= 100000;   // 1 ms at 100 MHz
+                    if (host) last_host_poll = now;
+                    if (cancel_requested(sc, host))
+                        for (int q2 = 0; q2 < G; q2++) gs[q2].phase = 2;
+                }
                 if (tid == 0 && gs[q].phase == 0) {
                     if (hit0)   // the camera ray's time (Get1D after pFilm, pLens) of the pixel's first traced sample
                         pr.si.time = camera_ray(cam, (double)px, (double)py, time_u, V2{0.0, 0.0}).time;
@@ -1804,7 +1819,12 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
         // ---- (4) each group leader walks its chain through the ring
         if (gl == 0 && sg.phase == 1) {
             CiGroup s = gs[g];
-            if ((++cancel_poll & 127u) == 0 && cancel_requested(sc)) s.phase = 2;   // long pixels (large spp)
+            if ((++cancel_poll & 127u) == 0) {   // long pixels (large spp)
+                const uint64_t now = wall_clock64();
+                const bool host = now - last_host_poll >= 100000;
+                if (host) last_host_poll = now;
+                if (cancel_requested(sc, host)) s.phase = 2;
+            }
             for (; s.phase == 1;) {
                 RingEnt& e = ring[s.head & (R - 1u)];
                 if (e.tag != s.head) break;
@@ -2020,6 +2040,7 @@ struct pbrt_gpu_ctx {
     bool cancel_req = false;
     int* h_cancel = nullptr;   // hipHostMalloc (coherent, mapped)
     int* d_cancel = nullptr;   // its device address
+    int* d_cancel_seen = nullptr;   // device-memory copy the kernels publish (reset per render)
     std::string err;
     std::chrono::steady_clock::time_point t_start;
 };
@@ -2077,6 +2098,7 @@ DevScene dev_scene(const pbrt_gpu_ctx* c, bool with_dist) {
     s.gmasks = c->d_gmasks;
     s.n_groups = c->n_groups;
     s.cancel = c->d_cancel;
+    s.cancel_seen = c->d_cancel_seen;
     return s;
 }
 
@@ -2801,7 +2823,7 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
         (rc = upload(c, &c->d_lights, scene->lights, scene->n_lights)) ||
         (rc = upload(c, &c->d_camera, &scene->camera, 1)) || (rc = upload(c, &c->d_film, &scene->film, 1)) ||
         (rc = upload<pbrt_distribution_desc>(c, &c->d_dist, nullptr, 1)) ||
-        (rc = upload<Counters>(c, &c->d_ctr, nullptr, 1)) ||
+        (rc = upload<Counters>(c, &c->d_ctr, nullptr, 1)) || (rc = upload<int>(c, &c->d_cancel_seen, nullptr, 1)) ||
         (rc = upload<PcgJump>(c, &c->d_jump, &pcg_jump_table(), 1))) {
         pbrt_gpu_destroy(c);
         return rc;
@@ -2848,6 +2870,7 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
     c->film_target = out;
     c->last_heavy = 0;
     HIPCHK(c, hipMemsetAsync(c->d_ctr, 0, sizeof(Counters), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_cancel_seen, 0, sizeof(int), c->stream));
     if (rp.n_slots > 0) HIPCHK(c, hipMemsetAsync(c->d_panics, 0, sizeof(PanicRec) * (size_t)rp.n_slots, c->stream));
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     if (rp.n_slots > 0) {
@@ -3028,14 +3051,14 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                 }
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 2], c->stream));
                 hipLaunchKernelGGL(k_film, dim3((unsigned)((nb * per + 255) / 256)), dim3(256), 0, c->stream,
-                                   c->d_film, rp, c->wb, sb, nb, c->d_films);
+                                   c->d_film, rp, c->wb, sb, nb, c->d_films, c->d_cancel_seen);
                 hipLaunchKernelGGL(k_panic_reduce, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, c->stream, c->wb,
                                    sb, nb, c->d_panics, c->d_ctr);
                 if (rp.spp > 1)
                     hipLaunchKernelGGL(k_ray_count,
                                        dim3((unsigned)std::min<int64_t>((nb * c->wb.ppt * rp.spp + 255) / 256,
                                                                         (int64_t)c->n_simd * 16)),
-                                       dim3(256), 0, c->stream, c->wb, nb, rp.spp, c->d_ctr);
+                                       dim3(256), 0, c->stream, c->wb, nb, rp.spp, c->d_ctr, c->d_cancel_seen);
             }
         } else {
             c->last_kernel = PBRT_KERNEL_SERIAL;
@@ -3264,7 +3287,7 @@ void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
     void* bufs[] = {c->d_shapes, c->d_materials, c->d_prims, c->d_nodes, c->d_order, c->d_lights, c->d_camera, c->d_film,
                     c->d_dist,   c->d_films,     c->d_s1d,   c->d_panics, c->d_ctr,   c->d_out,    c->d_jump,
                     c->d_wave,   c->d_fprims, c->d_ticks, c->d_slot_order, c->d_groups,
-                    c->d_gmasks, c->d_cost,   c->d_cost_keys, c->d_pw};
+                    c->d_gmasks, c->d_cost,   c->d_cost_keys, c->d_pw, c->d_cancel_seen};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     mesh_bvh_free(c->mesh);
