@@ -40,11 +40,13 @@ def parse():
     ap.add_argument("--height", type=int, default=0, help="0 = the config's (1080, or 2160 for E)")
     ap.add_argument("--shard", default="", help="R/N: on ONE GPU, render only tiles t mod N == R, the share of "
                                                 "rank R of an N-GPU job (reported as such)")
-    ap.add_argument("--config", default="B", choices=["B", "C", "D", "E"],
+    ap.add_argument("--config", default="B", choices=["B", "C", "D", "E", "G"],
                     help="BASELINE config: B = README sphere scene, Stratified(8,8), Path(10); "
                          "C = Cornell (SURVEY 8(d)), Stratified(16,16), Path(8); "
                          "D = 999 698-triangle height field (extension), Stratified(8,8), Path(10); "
-                         "E = 9 999 392-triangle height field, 3840x2160, Stratified(32,32), Path(10)")
+                         "E = 9 999 392-triangle height field, 3840x2160, Stratified(32,32), Path(10); "
+                         "G = README scene + server.go's commented-out glass sphere + a mirror, "
+                         "Stratified(8,8), Path(10)")
     ap.add_argument("--spp", type=int, default=0, help="Stratified(spp, spp) (0 = the config's)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "serial", "wave", "wavefront", "wave_ci"])
     ap.add_argument("--tiles-per-wave", type=int, default=0, help="k_chain_ci tiles per wave (0 = library default)")
@@ -133,7 +135,7 @@ def cpu_baseline(args, scene_name, rd_kwargs, W, H, product_scene=None, gpus_per
     import oracle_lib as O
 
     cpu = host_cpu()
-    if scene_name == "heightfield":   # the fixture is data: the oracle renders the product-built descriptor
+    if scene_name in ("heightfield", "readme_glass"):   # scene data: the oracle renders the product-built descriptor
         sc = product_scene
     else:
         sc = (O.OracleScene.readme if scene_name == "readme" else O.OracleScene.cornell)(W, H)
@@ -219,12 +221,18 @@ CONFIGS = {
     "E": dict(scene="heightfield", quads=2236, spp=32, max_depth=10, width=3840, height=2160,
               text="height field 9999392 triangles (device LBVH) + README lights/camera {W}x{H}, "
                    "Stratified({S},{S}) = {T} traced paths/px, Path(maxDepth 10, rr 1, Uniform), tile 16"),
+    # the README scene with server.go:67-91's commented-out glass sphere and a mirror
+    "G": dict(scene="readme_glass", spp=8, max_depth=10,
+              text="README sphere scene + glass sphere (server.go:67-91) + mirror sphere {W}x{H}, "
+                   "Stratified({S},{S}) = {T} traced paths/px, Path(maxDepth 10, rr 1, Uniform), tile 16"),
 }
 
 
 def make_scene(G, cfg, W, H):
     if cfg["scene"] == "readme":
         return G.Scene.readme(W, H)
+    if cfg["scene"] == "readme_glass":
+        return G.Scene.readme_glass(W, H)
     if cfg["scene"] == "cornell":
         return G.Scene.cornell(W, H)
     return G.Scene.heightfield(W, H, quads=cfg["quads"], seed=1)
@@ -439,7 +447,9 @@ def main():
             "dtype": "f64",
             "data": {"readme": "synthetic (the reference's hard-coded README scene; no external data)",
                      "cornell": "synthetic (SURVEY 8(d) Cornell fixture built from reference types)",
-                     "heightfield": "synthetic (procedural height field, seed 1; triangle extension)"}[cfg["scene"]],
+                     "heightfield": "synthetic (procedural height field, seed 1; triangle extension)",
+                     "readme_glass": "synthetic (README scene + server.go's commented-out glass sphere + a mirror)"
+                     }[cfg["scene"]],
             "config": {
                 "workload": cfg["text"].format(W=W, H=H, S=S, T=S * S - 1) + ", "
                             + ("EXACT per-tile RNG" if args.mode == "exact" else "THROUGHPUT per-path RNG"),

@@ -391,6 +391,20 @@ int mesh_bvh_build(const pbrt_scene_desc* s, hipStream_t st, MeshBuild& out, std
         uint64_t* keys = nullptr;
         int* depth = nullptr;
         hipEvent_t e0 = nullptr, e1 = nullptr;
+        // the build's temporaries and events, released on every exit of this
+        // scope (success, or an MB_CHK failure's goto fail)
+        struct Temps {
+            std::vector<void**> bufs;   // the local pointers (nullptr until allocated)
+            hipEvent_t* ev[2];
+            ~Temps() {
+                for (void** b : bufs)
+                    if (*b) (void)hipFree(*b);
+                for (hipEvent_t* e : ev)
+                    if (*e) (void)hipEventDestroy(*e);
+            }
+        } temps{{(void**)&tris, (void**)&gid, (void**)&cen, (void**)&bounds, (void**)&keys, (void**)&cl, (void**)&cr,
+                 (void**)&par, (void**)&rfirst, (void**)&box, (void**)&tc, (void**)&sz, (void**)&flag, (void**)&depth},
+                {&e0, &e1}};
         int npad = 2048;
         while (npad < n) npad <<= 1;
         const unsigned gb = (unsigned)((n + kB - 1) / kB), gpad = (unsigned)(npad / kB);
@@ -458,10 +472,6 @@ int mesh_bvh_build(const pbrt_scene_desc* s, hipStream_t st, MeshBuild& out, std
             out.build_ms = ms;
         }
         out.n_nodes = n_out;
-        (void)hipFree(tris); (void)hipFree(gid); (void)hipFree(cen); (void)hipFree(bounds); (void)hipFree(keys);
-        (void)hipFree(cl); (void)hipFree(cr); (void)hipFree(par); (void)hipFree(rfirst); (void)hipFree(box);
-        (void)hipFree(tc); (void)hipFree(sz); (void)hipFree(flag); (void)hipFree(depth);
-        (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
         return PBRT_OK;
     }
 fail:

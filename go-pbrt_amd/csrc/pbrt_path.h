@@ -1303,6 +1303,35 @@ __device__ inline bool estimate_direct_begin(const DevScene& sc, const SI& si, c
     ld_vis = Ld;
     return true;
 }
+// estimate_direct_begin over a BSDFX (kX wave pipelines): OrenNayar evaluates
+// its own F with the Lambertian Pdf; Lambert, Mirror (F = Pdf = 0: no shadow
+// ray) and smooth glass take the shared begin on `b`.
+__device__ inline bool estimate_direct_begin_x(const DevScene& sc, const SI& si, const BSDF& b, const BSDFX& x, int li,
+                                               V2 u_light, Ray& sr, Spec& ld_vis) {
+    if (x.kind != BXDF_KIND_OREN_NAYAR && x.kind != BXDF_KIND_MICROFACET)
+        return estimate_direct_begin(sc, si, b, li, u_light, sr, ld_vis);
+    const pbrt_light_desc& L = sc.lights[li];
+    const bool is_delta = L.type != PBRT_LIGHT_DIFFUSE_AREA;
+    LightSample ls;
+    sample_li(sc, L, si, u_light, ls);
+    if (!(ls.pdf > 0 && !is_black(ls.Li))) return false;
+    const Spec f = smuls(mf_bsdf_f(b, x, si.wo, ls.wi), absdot(ls.wi, si.sn));
+    const double scat_pdf = mf_bsdf_pdf(b, x, si.wo, ls.wi);
+    if (is_black(f)) return false;
+    const V3 origin = offset_ray_origin(si.p, si.perr, si.n, ls.tp - si.p);
+    const V3 target = offset_ray_origin(ls.tp, ls.tperr, ls.tn, origin - ls.tp);
+    sr = Ray{si.p, target - origin, 1 - 0.0001, si.time};
+    Spec Ld = spec(0);
+    if (is_delta) {
+        Ld = Ld + sdivs(smul(f, ls.Li), ls.pdf);
+    } else {
+        const double fp = 1.0 * ls.pdf, gp = 1.0 * scat_pdf;
+        const double w = (fp * fp) / (fp * fp + gp * gp);
+        Ld = Ld + sdivs(smuls(smul(f, ls.Li), w), ls.pdf);
+    }
+    ld_vis = Ld;
+    return true;
+}
 // EstimateDirect (integrator.go:79-195): an occluded shadow ray zeroes Li, so
 // Ld stays spec(0).
 // traced (optional): +1 when the visibility ray is traced (stats.rays_shadow).

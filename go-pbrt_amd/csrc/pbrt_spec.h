@@ -104,6 +104,7 @@ constexpr uint32_t kRayClosest = 1u, kRayShadow = 1u << 16;
 struct PixelCache {
     SI si;
     BSDF b;
+    BSDFX x;                          // kX pipelines: Mirror / smooth Glass / OrenNayar
     V3 wo;                            // camera ray direction (path.go:91, #8)
     Spec ld[kMaxCachedLights];        // EstimateDirect(light l, uLight = (0,0))
     int ld_panic[kMaxCachedLights];   // panic kind of that estimate (incl. Ld > 10) | kLdTraced
@@ -115,6 +116,7 @@ struct PixelCache {
 struct ChainCache {
     SI si;
     BSDF b;
+    BSDFX x;   // kX pipelines
     V3 wo;
     int hit;
     int pad;
@@ -132,6 +134,7 @@ struct ChainCache {
 struct PathState {
     Spec L, beta;
     Ray ray;
+    double eta_scale;   // Path.Li's etaScale (kX: specular transmission)
     int bounces;
     int first;
     uint32_t rays;   // kRayClosest / kRayShadow counts of the path
@@ -145,6 +148,7 @@ struct PathStateLds {
     uint32_t* rays;   // the path's ray counts (LDS slot)
     Spec beta;
     Ray ray;
+    double eta_scale;
     int bounces;
     int first;
 };
@@ -163,13 +167,18 @@ __device__ __forceinline__ void add_rays(PathStateLds& s, uint32_t v) { *s.rays 
 // dead by then, so the any-hit traversal runs with their registers free (no
 // scratch spills). Every value and every draw is the reference's; a panic of
 // the shadow ray or Ld > 10 ends the path at this bounce, as it would have.
-template <int kWhich = 0, class Cache, class State>
+//
+// kX: scenes with Mirror, smooth Glass or OrenNayar materials (BSDFX,
+// bsdfx_sample_f, Path.Li's etaScale; rough glass stays on the serial kernel).
+// kX = false is the Matte-only code, unchanged.
+template <int kWhich = 0, bool kX = false, class Cache, class State>
 __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, const SpecSampler& ss, Cursor& c,
                                  State& s, int max_depth, double rr_threshold, uint16_t* stack, int& panic,
                                  int& bounce) {
     const bool first = kWhich == 1 ? true : kWhich == 2 ? false : (s.first != 0);
     SI isect;
     BSDF b;
+    BSDFX x;
     V3 wo;
     const int nl = sc.n_lights;
     if (!first) {
@@ -180,7 +189,7 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
         const bool hit = bvh_traverse<false, PBRT_PATHS_LB>(sc, s.ray, &isect, stack, panic);
         if (!hit) return true;
         if (panic) return true;
-        if (compute_bsdf(sc, isect, b) < 0) {
+        if ((kX ? compute_bsdf_x(sc, isect, b, x) : compute_bsdf(sc, isect, b)) < 0) {
             panic = -1;
             return true;
         }
@@ -188,6 +197,7 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
     } else {
         isect = pc.si;
         b = pc.b;
+        if constexpr (kX) x = pc.x;
         wo = pc.wo;
         add_rays(s, kRayClosest);   // the camera ray's closest hit
     }
@@ -197,7 +207,8 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
     Spec ld_vis = spec(0);
     Spec beta0 = s.beta;
     if constexpr (kLdsAux) s.aux[0] = beta0;
-    if (b.n_bxdfs > 0) {   // UniformSampleOneLight (integrator.go:48-77)
+    // NumComponents(BSDFAll &^ BSDFSpecular) > 0: UniformSampleOneLight (integrator.go:48-77)
+    if (kX ? bsdfx_nonspecular(b, x) : b.n_bxdfs > 0) {
         if (nl == 0) {
             add_L(s, smul(s.beta, spec(0)));
         } else {
@@ -221,7 +232,8 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
                 add_L(s, smul(s.beta, ld));
             } else {
                 pending = true;
-                shadow = estimate_direct_begin(sc, isect, b, ln, ul, sr, ld_vis);
+                shadow = kX ? estimate_direct_begin_x(sc, isect, b, x, ln, ul, sr, ld_vis)
+                            : estimate_direct_begin(sc, isect, b, ln, ul, sr, ld_vis);
                 if constexpr (kLdsAux) s.aux[1] = ld_vis;
             }
         }
@@ -232,17 +244,27 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
         V2 u = c_get2d(c, ss);
         V3 wi;
         double pdf;
-        Spec f = bsdf_sample_f(b, wo, u, wi, pdf);
+        int type = 0;
+        Spec f = kX ? bsdfx_sample_f(b, x, wo, u, wi, pdf, type) : bsdf_sample_f(b, wo, u, wi, pdf);
+        if (kX && type == -1) {   // rough glass: the reference's nil dereference (host keeps it off kX)
+            panic = PBRT_PANIC_NIL_DEREF;
+            return true;
+        }
         if (is_black(f) || pdf == 0.0) {
             done = true;
         } else {
             double wp = absdot(wi, isect.sn) / pdf;
             s.beta = smul(s.beta, smuls(f, wp));
+            if (kX && (type & BXDF_SPECULAR) && (type & BXDF_TRANSMISSION)) {   // path.go:106-117
+                const double eta = x.eta;
+                if (dot(wo, isect.n) > 0) s.eta_scale *= eta * eta;
+                else s.eta_scale *= 1 / (eta * eta);
+            }
             s.ray.o = offset_ray_origin(isect.p, isect.perr, isect.n, wi);
             s.ray.d = wi;
             s.ray.tmax = kInf;
             s.ray.time = isect.time;
-            Spec rr = smuls(s.beta, 1.0);
+            Spec rr = smuls(s.beta, kX ? s.eta_scale : 1.0);
             if (max_component(rr) < rr_threshold && s.bounces > 3) {
                 double q = gomath::max(0.05, 1 - max_component(rr));
                 double u1 = c_get1d(c, ss);
@@ -279,10 +301,15 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
 // chain kernel (k_chain_ci) and the cold-frame probe run one per bounce.
 // Returns 0: trace `ray` next; 1: the trajectory ended (D = c.draws);
 // 2: its draw count depends on the sample index (kBadD).
-__device__ inline int traj_scatter(const DevScene& sc, const SI& isect, const BSDF& b, V3 wo, Cursor& c,
-                                   const SpecSampler& ss, Spec& beta, int& bounces, Ray& ray, int max_depth,
-                                   double rr_threshold) {
-    if (b.n_bxdfs > 0 && sc.n_lights > 0) {   // UniformSampleOneLight's draws
+// kX (Mirror / smooth Glass / OrenNayar scenes): the BSDFX `x` and Path.Li's
+// etaScale `eta_scale` (see path_step); a rough-glass sample (the reference
+// panics) returns 2, so the offset is re-run at the chain head and the panic
+// is found by the path stage.
+template <bool kX = false>
+__device__ inline int traj_scatter(const DevScene& sc, const SI& isect, const BSDF& b, const BSDFX& x, V3 wo,
+                                   Cursor& c, const SpecSampler& ss, Spec& beta, double& eta_scale, int& bounces,
+                                   Ray& ray, int max_depth, double rr_threshold) {
+    if ((kX ? bsdfx_nonspecular(b, x) : b.n_bxdfs > 0) && sc.n_lights > 0) {   // UniformSampleOneLight's draws
         c_skip1d(c, ss);
         c_get2d(c, ss);
         c_get2d(c, ss);
@@ -290,15 +317,22 @@ __device__ inline int traj_scatter(const DevScene& sc, const SI& isect, const BS
     V2 u = c_get2d(c, ss);
     V3 wi;
     double pdf;
-    Spec f = bsdf_sample_f(b, wo, u, wi, pdf);
+    int type = 0;
+    Spec f = kX ? bsdfx_sample_f(b, x, wo, u, wi, pdf, type) : bsdf_sample_f(b, wo, u, wi, pdf);
+    if (kX && type == -1) return 2;
     if (is_black(f) || pdf == 0.0) return 1;
     double wp = absdot(wi, isect.sn) / pdf;
     beta = smul(beta, smuls(f, wp));
+    if (kX && (type & BXDF_SPECULAR) && (type & BXDF_TRANSMISSION)) {   // path.go:106-117
+        const double eta = x.eta;
+        if (dot(wo, isect.n) > 0) eta_scale *= eta * eta;
+        else eta_scale *= 1 / (eta * eta);
+    }
     ray.o = offset_ray_origin(isect.p, isect.perr, isect.n, wi);
     ray.d = wi;
     ray.tmax = kInf;
     ray.time = isect.time;
-    Spec rr = smuls(beta, 1.0);
+    Spec rr = smuls(beta, kX ? eta_scale : 1.0);
     if (max_component(rr) < rr_threshold && bounces > 3) {
         double q = gomath::max(0.05, 1 - max_component(rr));
         double u1 = c_get1d(c, ss);

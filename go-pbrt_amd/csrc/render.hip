@@ -290,6 +290,7 @@ __device__ __forceinline__ void stage_nodes(DevScene& sc) {
 struct PixelRec {
     SI si;
     BSDF b;
+    BSDFX x;          // kX pipelines (Mirror / smooth Glass / OrenNayar scenes)
     V3 wo;
     int32_t hit;      // first hit exists and maxDepth > 1
     int32_t nvalid;   // samples 1 .. nvalid-1 have offsets (spp unless a panic cut the chain)
@@ -472,7 +473,7 @@ __host__ __device__ constexpr int paths_group_lds(int per) {   // bytes, per wav
 // mb_state(tile, pi, k) instead of the chain's offset state.
 // s1d_lds: the group's stratified values are staged in LDS (else read from
 // their global records: large spp, e.g. config E's 1024).
-template <int P, bool kMB = false>
+template <int P, bool kMB = false, bool kX = false>
 __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderParams& rp, const WaveBufs& wb, int64_t slot_base,
                             int64_t rec0, int64_t rec_end, Counters* __restrict__ ctr, unsigned char* wlds,
                             int s1d_lds) {
@@ -517,6 +518,7 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
             const PixelRec& pr = wb.prec[rec0 + lane];
             pcs[lane].si = pr.si;
             pcs[lane].b = pr.b;
+            if constexpr (kX) pcs[lane].x = pr.x;
             pcs[lane].wo = pr.wo;
             pcs[lane].hit = pr.hit;
         }
@@ -524,10 +526,11 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
     wave_sync();
     if (nl > 0 && lane < P * nl) {   // bounce-1 light samples, uLight = (0,0); lane = pixel * nl + light
         const int j = lane / nl, l = lane - j * nl;
-        if (meta[j].nv > 0 && meta[j].hit && pcs[j].b.n_bxdfs > 0) {
+        if (meta[j].nv > 0 && meta[j].hit && (kX ? bsdfx_nonspecular(pcs[j].b, pcs[j].x) : pcs[j].b.n_bxdfs > 0)) {
             int pl = 0;
             uint64_t traced = 0;
-            Spec ld = estimate_direct(sc, nullptr, pl, pcs[j].si, pcs[j].b, l, V2{0.0, 0.0}, &traced);
+            Spec ld = kX ? estimate_direct_x(sc, nullptr, pl, pcs[j].si, pcs[j].b, pcs[j].x, l, V2{0.0, 0.0}, &traced)
+                         : estimate_direct(sc, nullptr, pl, pcs[j].si, pcs[j].b, l, V2{0.0, 0.0}, &traced);
             if (!pl && max_component(ld) > 10) pl = PBRT_PANIC_LD_GT_10;
             pcs[j].ld[l] = ld;
             pcs[j].ld_panic[l] = pl | (traced ? kLdTraced : 0);
@@ -574,6 +577,7 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
                     *ps.L = spec(0);
                     *ps.rays = 0;
                     ps.beta = spec(1);
+                    ps.eta_scale = 1.0;
                     ps.bounces = 1;
                     ps.first = 1;
                     pnc = 0;
@@ -592,8 +596,10 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
             // bounce: the cheap first step does not cost the wave an iteration
             const SpecSampler ss{s1d_lds ? s1d + j * per : wb.s1d + (rec0 + j) * wb.s1d_stride, n, ndims};
             bool done = false;
-            if (ps.first) done = path_step<1>(sc, pcs[j], ss, c, ps, rp.max_depth, rp.rr_threshold, nullptr, pnc, bnc);
-            if (!done) done = path_step<2>(sc, pcs[j], ss, c, ps, rp.max_depth, rp.rr_threshold, nullptr, pnc, bnc);
+            if (ps.first)
+                done = path_step<1, kX>(sc, pcs[j], ss, c, ps, rp.max_depth, rp.rr_threshold, nullptr, pnc, bnc);
+            if (!done)
+                done = path_step<2, kX>(sc, pcs[j], ss, c, ps, rp.max_depth, rp.rr_threshold, nullptr, pnc, bnc);
             if (done) {
                 const int64_t rec = rec0 + j;
                 double* o = wb.L + (rec * n + k) * 3;
@@ -635,14 +641,14 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
     wave_sync();   // the LDS block is reused by the wave's next group
 }
 
-template <int P, bool kMB = false>
+template <int P, bool kMB = false, bool kX = false>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kPathsWaves, 8))) void k_paths_ci(
     DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr,
     int s1d_lds) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];   // paths_group_lds<P>
     if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;   // one wave per workgroup
     stage_nodes(sc);
-    paths_group<P, kMB>(sc, rp, wb, slot_base, (int64_t)blockIdx.x * P, nrec, ctr, lds, s1d_lds);
+    paths_group<P, kMB, kX>(sc, rp, wb, slot_base, (int64_t)blockIdx.x * P, nrec, ctr, lds, s1d_lds);
 }
 
 // ------------------------------------------------- path wavefront (k_pw_*)
@@ -802,6 +808,7 @@ __global__ __launch_bounds__(kWave) void k_pw_start(DevScene sc, RenderParams rp
     PathState s;
     s.L = spec(0);
     s.beta = spec(1);
+    s.eta_scale = 1.0;
     s.bounces = 1;
     s.first = 1;
     s.rays = 0;
@@ -1039,6 +1046,7 @@ __global__ void k_pw_panics(RenderParams rp, WaveBufs wb, int64_t slot_base, int
 // (camera ray, first hit, BSDF), written to the PixelRec / s1d buffers the
 // EXACT pipeline fills with k_wf_primary + k_chain_ci. The same arithmetic as
 // the serial kernel's pixel prologue.
+template <bool kX = false>
 __global__ __launch_bounds__(kWave) void k_mb_setup(DevScene sc, RenderParams rp, ChainLayout lay,
                                                     const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
                                                     int64_t nslots_batch) {
@@ -1064,17 +1072,21 @@ __global__ __launch_bounds__(kWave) void k_mb_setup(DevScene sc, RenderParams rp
     int panic0 = 0, hit = 0;
     SI si0;
     BSDF b0;
+    BSDFX bx0;
     b0.n_bxdfs = 0;
+    bx0.kind = BXDF_KIND_LAMBERT;
+    bx0.n = 0;
     Ray ray = camera_ray(*sc.camera, (double)px + 0.0, (double)py + 0.0, s1d[1 < n ? 1 : 0], V2{0.0, 0.0});
     if (n > 1 && 1 < rp.max_depth) {
         hit = bvh_traverse<false>(sc, ray, &si0, stack_lds + lane, panic0) ? 1 : 0;
-        if (!panic0 && hit && compute_bsdf(sc, si0, b0) < 0) panic0 = -1;
+        if (!panic0 && hit && (kX ? compute_bsdf_x(sc, si0, b0, bx0) : compute_bsdf(sc, si0, b0)) < 0) panic0 = -1;
     }
     if (panic0) hit = 0;
     if (lane == 0) {
         PixelRec& pr = wb.prec[rec];
         pr.si = si0;
         pr.b = b0;
+        if constexpr (kX) pr.x = bx0;
         pr.wo = ray.d;
         pr.hit = hit;
         pr.nvalid = n;
@@ -1183,6 +1195,7 @@ __global__ __launch_bounds__(256) void k_ray_count(WaveBufs wb, int64_t nb, int 
     }
 }
 
+template <bool kX = false>
 __global__ __launch_bounds__(kWave) void k_wf_primary(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
                                                       int64_t nb) {
     __shared__ uint16_t stack_lds[64 * kStackStride];
@@ -1198,16 +1211,20 @@ __global__ __launch_bounds__(kWave) void k_wf_primary(DevScene sc, RenderParams 
     int panic0 = 0, hit0 = 0;
     SI si0;
     BSDF b0;
+    BSDFX bx0;
     b0.n_bxdfs = 0;
+    bx0.kind = BXDF_KIND_LAMBERT;
+    bx0.n = 0;
     Ray ray = camera_ray(*sc.camera, (double)px + 0.0, (double)py + 0.0, 0.0, V2{0.0, 0.0});
     // Path.Li traces bounce 1 only below maxDepth (path.go:66); DirectLighting always
     if (rp.spp > 1 && (1 < rp.max_depth || rp.integrator == PBRT_INTEGRATOR_DIRECT_LIGHTING)) {
         hit0 = bvh_traverse<false>(sc, ray, &si0, stack_lds + threadIdx.x, panic0) ? 1 : 0;
-        if (!panic0 && hit0 && compute_bsdf(sc, si0, b0) < 0) panic0 = -1;
+        if (!panic0 && hit0 && (kX ? compute_bsdf_x(sc, si0, b0, bx0) : compute_bsdf(sc, si0, b0)) < 0) panic0 = -1;
     }
     PixelRec& pr = wb.prec[rec];
     pr.si = si0;
     pr.b = b0;
+    if constexpr (kX) pr.x = bx0;
     pr.wo = ray.d;
     pr.hit = panic0 ? 0 : hit0;
     pr.panic0 = panic0;
@@ -1435,6 +1452,7 @@ __global__ void k_dl_panics(RenderParams rp, WaveBufs wb, int64_t slot_base, int
 // (~cost bits << 32 | slot: ascending = heaviest first).
 constexpr int kProbes = 2;
 constexpr double kCostPixel = 150.0;   // one StartPixel ~ this many trajectory bounces of one lane
+template <bool kX = false>
 __global__ __launch_bounds__(kWave) void k_tile_cost(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
                                                      int64_t nb, float* __restrict__ feat,
                                                      uint64_t* __restrict__ keys) {
@@ -1466,16 +1484,20 @@ __global__ __launch_bounds__(kWave) void k_tile_cost(DevScene sc, RenderParams r
         c.k = -1;
         c.kdep = 0;
         Spec beta = spec(1);
+        double eta_scale = 1.0;
         int bounces = 1;
         Ray ray;
-        int r = traj_scatter(sc, pr.si, pr.b, pr.wo, c, ss, beta, bounces, ray, rp.max_depth, rp.rr_threshold);
+        int r = traj_scatter<kX>(sc, pr.si, pr.b, pr.x, pr.wo, c, ss, beta, eta_scale, bounces, ray, rp.max_depth,
+                                 rp.rr_threshold);
         while (r == 0) {
             SI si;
             int panic = 0;
             if (!bvh_traverse<false>(sc, ray, &si, stack_lds + lane, panic) || panic) break;
             BSDF b;
-            if (compute_bsdf(sc, si, b) < 0) break;
-            r = traj_scatter(sc, si, b, ray.d, c, ss, beta, bounces, ray, rp.max_depth, rp.rr_threshold);
+            BSDFX x;
+            if ((kX ? compute_bsdf_x(sc, si, b, x) : compute_bsdf(sc, si, b)) < 0) break;
+            r = traj_scatter<kX>(sc, si, b, x, ray.d, c, ss, beta, eta_scale, bounces, ray, rp.max_depth,
+                                 rp.rr_threshold);
         }
         work += (double)c.draws * (double)bounces;
     }
@@ -1551,7 +1573,7 @@ struct CiGroup {
 // kDepth: traversal stack entries per lane. Trees of <= kLdsNodes (64) nodes
 // are staged in LDS and walk their leaves only (no stack); larger trees walk
 // with the reference's [64] stack (bvh.go:670).
-template <int kW, int kDepth = 32>
+template <int kW, int kDepth = 32, bool kX = false>
 __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT_CI_EU_WAVES, 8))) void k_chain_ci(
     DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
     int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr,
@@ -1643,6 +1665,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
     c.k = -1;
     c.kdep = 0;
     Spec beta = spec(1);
+    double eta_scale = 1.0;
     int bounces = 1;
     Ray ray;
     ray.o = ray.d = V3{0, 0, 0};
@@ -1688,6 +1711,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
                         pr.si.time = camera_ray(cam, (double)px, (double)py, time_u, V2{0.0, 0.0}).time;
                     pcs[q].si = pr.si;
                     pcs[q].b = pr.b;
+                    if constexpr (kX) pcs[q].x = pr.x;
                     pcs[q].wo = pr.wo;
                     pcs[q].hit = hit0;
                     CiGroup& s = gs[q];
@@ -1766,10 +1790,11 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
                 c.k = exact ? sg.kh : -1;
                 c.kdep = 0;
                 beta = spec(1);
+                eta_scale = 1.0;
                 bounces = 1;
                 const ChainCache& pc = pcs[g];
-                const int r = traj_scatter(sc, pc.si, pc.b, pc.wo, c, ss, beta, bounces, ray, rp.max_depth,
-                                           rp.rr_threshold);
+                const int r = traj_scatter<kX>(sc, pc.si, pc.b, pc.x, pc.wo, c, ss, beta, eta_scale, bounces, ray,
+                                               rp.max_depth, rp.rr_threshold);
                 tracing = r == 0;
                 if (r != 0) {
                     RingEnt& e = ring[off & (R - 1u)];
@@ -1796,11 +1821,12 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
                 SI si;
                 prim_si(sc, best, ray, ph, si);
                 BSDF b;
-                if (compute_bsdf(sc, si, b) < 0) {
+                BSDFX x;
+                if ((kX ? compute_bsdf_x(sc, si, b, x) : compute_bsdf(sc, si, b)) < 0) {
                     d = c.k >= 0 ? kBadExactD : kBadSpecD;
                 } else {
-                    const int r = traj_scatter(sc, si, b, ray.d, c, ss, beta, bounces, ray, rp.max_depth,
-                                               rp.rr_threshold);
+                    const int r = traj_scatter<kX>(sc, si, b, x, ray.d, c, ss, beta, eta_scale, bounces, ray,
+                                                   rp.max_depth, rp.rr_threshold);
                     if (r == 1) d = c.draws;
                     else if (r == 2) d = c.k >= 0 ? kBadExactD : kBadSpecD;
                 }
@@ -1946,7 +1972,61 @@ __global__ __launch_bounds__(kWave) void k_intersect(DevScene sc, int64_t n, con
 }  // namespace
 
 // =============================================================== C ABI
+// Experiment knobs (environment), read ONCE when a context is created
+// (pbrt_gpu_create), never per launch; defaults are the measured best.
+struct Knobs {
+    int ci_waves = 0;          // PBRT_CI_WAVES = 1, 2, 4, 8 (0: by tile count)
+    int ci_stride = 0;         // PBRT_CI_STRIDE = 1, 2 (0: 2 at one wave per tile, else 1)
+    int ci_heavy_waves = 4;    // PBRT_CI_HEAVY_WAVES = 4, 8
+    int64_t ci_heavy = -1;     // PBRT_CI_HEAVY = K forces the heavy tile count (tests)
+    bool ci_split = true;      // PBRT_CI_SPLIT=0
+    bool ci_order = true;      // PBRT_CI_ORDER=0
+    bool ci_probe = true;      // PBRT_CI_PROBE=0
+    bool paths_s1d_lds = false;// PBRT_PATHS_S1D=lds
+    int paths_ci = -1;         // PBRT_PATHS_CI = 0, 2, 4, 8 (-1: auto)
+    int paths_wf = -1;         // PBRT_PATHS_WF = 0 / 1 (-1: mesh scenes)
+    bool pw_sort = false;      // PBRT_PW_SORT=1
+    double pw_gb = 24.0;       // PBRT_PW_GB
+    double wave_buffer_gb = 0; // PBRT_WAVE_BUFFER_GB (0: min(96 GB, half the free HBM))
+    int cull_group = 4;        // PBRT_CULL_GROUP: leaves per culling group
+    int cull_min = 2;          // PBRT_CULL_MIN
+    bool cull_groups = true;   // PBRT_CULL_GROUPS=0
+    static Knobs from_env() {
+        Knobs k;
+        auto ival = [](const char* n, int& out) { if (const char* e = getenv(n)) out = atoi(e); };
+        if (const char* e = getenv("PBRT_CI_WAVES")) {
+            const int v = atoi(e);
+            if (v == 1 || v == 2 || v == 4 || v == 8) k.ci_waves = v;
+        }
+        if (const char* e = getenv("PBRT_CI_STRIDE")) {
+            const int v = atoi(e);
+            if (v == 1 || v == 2) k.ci_stride = v;
+        }
+        if (const char* e = getenv("PBRT_CI_HEAVY_WAVES")) k.ci_heavy_waves = atoi(e) == 8 ? 8 : 4;
+        if (const char* e = getenv("PBRT_CI_HEAVY")) k.ci_heavy = (int64_t)atoll(e);
+        if (const char* e = getenv("PBRT_CI_SPLIT")) k.ci_split = atoi(e) != 0;
+        if (const char* e = getenv("PBRT_CI_ORDER")) k.ci_order = atoi(e) != 0;
+        if (const char* e = getenv("PBRT_CI_PROBE")) k.ci_probe = atoi(e) != 0;
+        if (const char* e = getenv("PBRT_PATHS_S1D")) k.paths_s1d_lds = std::strcmp(e, "lds") == 0;
+        if (const char* e = getenv("PBRT_PATHS_CI")) {
+            const int v = atoi(e);
+            if (v == 0 || v == 2 || v == 4 || v == 8) k.paths_ci = v;
+        }
+        if (const char* e = getenv("PBRT_PATHS_WF")) k.paths_wf = atoi(e) == 1 ? 1 : 0;
+        if (const char* e = getenv("PBRT_PW_SORT")) k.pw_sort = atoi(e) == 1;
+        if (const char* e = getenv("PBRT_PW_GB")) k.pw_gb = atof(e) > 0 ? atof(e) : k.pw_gb;
+        if (const char* e = getenv("PBRT_WAVE_BUFFER_GB")) k.wave_buffer_gb = atof(e) > 0 ? atof(e) : 0;
+        if (const char* e = getenv("PBRT_CULL_GROUP")) k.cull_group = std::max(2, atoi(e));
+        if (const char* e = getenv("PBRT_CULL_MIN")) k.cull_min = std::max(0, atoi(e));
+        int cg = 1;
+        ival("PBRT_CULL_GROUPS", cg);
+        k.cull_groups = cg != 0;
+        return k;
+    }
+};
+
 struct pbrt_gpu_ctx {
+    Knobs knobs;
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
@@ -1999,7 +2079,8 @@ struct pbrt_gpu_ctx {
     pbrt_distribution_desc* d_dist = nullptr;
     pbrt_scene_desc host_scene;   // counts + film/camera (pointer fields are not kept)
     std::vector<pbrt_light_desc> host_lights;
-    bool non_matte = false;       // Mirror, Glass or OrenNayar material: serial kernel only
+    bool non_matte = false;       // Mirror, Glass or OrenNayar material: kX wave kernels or the serial kernel
+    bool rough_glass = false;     // a Glass material with roughness: serial kernel only
     // per-render buffers (grown on demand)
     double* d_films = nullptr;
     size_t films_cap = 0;
@@ -2183,7 +2264,7 @@ bool dev_order(const pbrt_scene_desc* s, std::vector<uint32_t>& out) {
 // octant [G + 1] masks over the octant's leaf preorder positions (last: the
 // unconditional leaves). G = 0 (no culling) when the tree is not LDS-staged
 // or the grouping needs more than kMaxCullGroups groups.
-int cull_groups(const pbrt_scene_desc* s, const std::vector<uint32_t>& order, std::vector<double>& boxes,
+int cull_groups(const Knobs& kn, const pbrt_scene_desc* s, const std::vector<uint32_t>& order, std::vector<double>& boxes,
                 std::vector<uint32_t>& masks) {
     boxes.clear();
     masks.clear();
@@ -2206,8 +2287,7 @@ int cull_groups(const pbrt_scene_desc* s, const std::vector<uint32_t>& order, st
     std::vector<std::vector<int>> groups;
     // leaves per group at most: 4 measured best on config B (chain 420 -> 404 ms against 8;
     // 2: 450, 3: 403, 5: 418, 16: 492; profiles/r02/cull_group_ab.json). PBRT_CULL_GROUP overrides.
-    size_t gmax = 4;
-    if (const char* e = getenv("PBRT_CULL_GROUP")) gmax = (size_t)std::max(2, atoi(e));
+    const size_t gmax = (size_t)kn.cull_group;
     std::function<void(std::vector<int>)> split = [&](std::vector<int> g) {
         if (g.size() <= gmax) {
             if (g.size() > 1) groups.push_back(g);
@@ -2229,8 +2309,7 @@ int cull_groups(const pbrt_scene_desc* s, const std::vector<uint32_t>& order, st
     const int G = (int)groups.size();
     // worth it only when the groups can skip a fair share of the leaf tests
     // (README: 21 of 23 leaves grouped; Cornell: 2 of 8, not grouped)
-    int min_frac2 = 2;   // grouped leaves must be at least half of all (PBRT_CULL_MIN=0: any)
-    if (const char* e = getenv("PBRT_CULL_MIN")) min_frac2 = std::max(0, atoi(e));
+    const int min_frac2 = kn.cull_min;   // grouped leaves must be at least half of all (PBRT_CULL_MIN=0: any)
     if (G == 0 || G > kMaxCullGroups || min_frac2 * (int)rest.size() < (int)leaves.size()) return 0;
     boxes.assign((size_t)G * 6, 0.0);
     for (int gi = 0; gi < G; gi++) {
@@ -2327,14 +2406,21 @@ const PcgJump& pcg_jump_table() {
     return J;
 }
 
+int paths_ci_pixels(const pbrt_gpu_ctx* c, const RenderParams& rp);
+bool paths_wf_enabled(const pbrt_gpu_ctx* c);
 // Can the wave-parallel kernels replay this render exactly? (conditions: pbrt_spec.h)
 bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const RenderParams& rp, ChainLayout& L,
                    ChainLayout& Lci) {
     if (rd->flags & PBRT_FLAG_PANIC_FIDELITY) return false;   // the serial kernel traces the extra rays
-    // Mirror and Glass change a path's draw count per bounce (no light sample on
-    // glass) and its direction rule: the serial kernel renders such scenes
-    if (c->non_matte) return false;
     const bool dl = rd->integrator == PBRT_INTEGRATOR_DIRECT_LIGHTING;
+    // Mirror, smooth Glass and OrenNayar: Path renders run the kX instantiations
+    // of the wave pipeline (trajectories and paths over BSDFX, with etaScale),
+    // whose path stage is k_paths_ci; DirectLighting's specular recursion, rough
+    // glass (whose every BSDF sample panics), mesh scenes and renders k_paths_ci
+    // cannot take stay on the serial kernel
+    if (c->non_matte && (dl || c->rough_glass || c->mesh.n_nodes > 0 || paths_wf_enabled(c) ||
+                         paths_ci_pixels(c, rp) < 4 || c->host_scene.n_nodes > kLdsNodes))
+        return false;
     if (dl) {   // k_dl_*: the camera ray must be per pixel (pFilm stratified; pLens stratified or unused)
         if (rd->n_dims < 1 || (rd->n_dims < 2 && c->host_scene.camera.lens_radius > 0)) return false;
     } else if (rd->integrator != PBRT_INTEGRATOR_PATH || rd->n_dims < 3 || rd->max_depth > 2048) {
@@ -2413,10 +2499,7 @@ ChainLayout ci_layout(const ChainLayout& base, int w, int G, unsigned& lds_bytes
 // launch cannot keep every wave slot busy (2 waves/SIMD) a tile gets 2 or 4
 // waves. PBRT_CI_WAVES (1, 2, 4) overrides.
 int ci_waves(const pbrt_gpu_ctx* c, int64_t nb) {
-    if (const char* e = getenv("PBRT_CI_WAVES")) {
-        const int v = atoi(e);
-        if (v == 1 || v == 2 || v == 4 || v == 8) return v;
-    }
+    if (c->knobs.ci_waves) return c->non_matte ? std::min(c->knobs.ci_waves, 4) : c->knobs.ci_waves;
     if (c->tiles_per_wave > 1) return 1;
     // measured on config B shards (tools/shard_sim.py): 8160 tiles -> 1,
     // 4080 -> 2, 2040 and 1020 -> 4
@@ -2437,38 +2520,20 @@ int ci_waves(const pbrt_gpu_ctx* c, int64_t nb) {
 // and the rest 1 wave each in a concurrent one (1/4- and 1/2-frame shards:
 // 387 -> 305 ms and 524 -> 472 ms per rank). PBRT_CI_SPLIT=0 disables it;
 // PBRT_CI_HEAVY=K forces the heavy count (tests).
-bool ci_split_enabled() {
-    const char* e = getenv("PBRT_CI_SPLIT");
-    return !(e && atoi(e) == 0);
-}
-int64_t ci_heavy_override() {
-    const char* e = getenv("PBRT_CI_HEAVY");
-    return e ? (int64_t)atoll(e) : -1;
-}
+bool ci_split_enabled(const pbrt_gpu_ctx* c) { return c->knobs.ci_split; }
+int64_t ci_heavy_override(const pbrt_gpu_ctx* c) { return c->knobs.ci_heavy; }
 // k_chain_ci candidate stride: 2 issues candidates at the chain head's parity
 // only (dropped when an odd draw count flips it), 1 at every offset (twice
 // the candidates, none dropped). PBRT_CI_STRIDE = 1 / 2 overrides.
-int ci_stride(int w) {
-    if (const char* e = getenv("PBRT_CI_STRIDE")) {
-        const int v = atoi(e);
-        if (v == 1 || v == 2) return v;
-    }
+int ci_stride(const pbrt_gpu_ctx* c, int w) {
+    if (c->knobs.ci_stride) return c->knobs.ci_stride;
     return w > 1 ? 1 : 2;
 }
 // PBRT_CI_HEAVY_WAVES = 4 (default) or 8: waves per heavy tile of the split
-int ci_heavy_waves() {
-    const char* e = getenv("PBRT_CI_HEAVY_WAVES");
-    return (e && atoi(e) == 8) ? 8 : 4;
-}
-bool ci_order_enabled() {
-    const char* e = getenv("PBRT_CI_ORDER");
-    return !(e && atoi(e) == 0);
-}
+int ci_heavy_waves(const pbrt_gpu_ctx* c) { return c->non_matte ? 4 : c->knobs.ci_heavy_waves; }
+bool ci_order_enabled(const pbrt_gpu_ctx* c) { return c->knobs.ci_order; }
 // PBRT_CI_PROBE=0: a fresh context's first frame runs in launch order (no k_tile_cost)
-bool ci_probe_enabled() {
-    const char* e = getenv("PBRT_CI_PROBE");
-    return !(e && atoi(e) == 0);
-}
+bool ci_probe_enabled(const pbrt_gpu_ctx* c) { return c->knobs.ci_probe; }
 uint64_t schedule_key(const RenderParams& rp, int kw) {
     const int64_t v[] = {rp.film_min_x, rp.film_min_y, rp.film_w,   rp.film_h,    rp.tile_size, rp.tile_begin,
                          rp.tile_stride, rp.n_slots,   rp.spp,      rp.ndims,     rp.jitter,    rp.max_depth,
@@ -2487,18 +2552,14 @@ uint64_t schedule_key(const RenderParams& rp, int kw) {
 // Off by default: read from their global records (L2-resident; config B
 // 111.0 -> 109.9 ms EXACT, 136.0 -> 134.8 ms THROUGHPUT against LDS staging).
 // PBRT_PATHS_S1D=lds stages them where they fit (experiments).
-bool paths_ci_s1d_lds(const RenderParams& rp, int P) {
-    const char* e = getenv("PBRT_PATHS_S1D");
-    return e && std::strcmp(e, "lds") == 0 && (int64_t)P * rp.ndims * rp.spp * 8 <= 16 * 1024;
+bool paths_ci_s1d_lds(const pbrt_gpu_ctx* c, const RenderParams& rp, int P) {
+    return c->knobs.paths_s1d_lds && (int64_t)P * rp.ndims * rp.spp * 8 <= 16 * 1024;
 }
 int paths_ci_pixels(const pbrt_gpu_ctx* c, const RenderParams& rp) {
     int pp = 4;
     bool forced = false;
-    if (const char* e = getenv("PBRT_PATHS_CI")) {
-        const int v = atoi(e);
-        if (v == 0) return 0;
-        if (v == 2 || v == 4 || v == 8) pp = v, forced = true;
-    }
+    if (c->knobs.paths_ci == 0) return 0;
+    if (c->knobs.paths_ci > 0) pp = c->knobs.paths_ci, forced = true;
     auto fits = [&](int p) {
         return c->host_scene.n_nodes <= kLdsNodes && p * c->host_scene.n_lights <= kWave;
     };
@@ -2519,18 +2580,16 @@ int paths_ci_pixels(const pbrt_gpu_ctx* c, const RenderParams& rp) {
 // between trace and shade: a loss on every scene measured (B 212 -> 245 ms: a
 // few matte materials leave no shading divergence to remove), so off by default.
 bool paths_wf_enabled(const pbrt_gpu_ctx* c) {
-    if (const char* e = getenv("PBRT_PATHS_WF")) return atoi(e) == 1;
+    if (c->knobs.paths_wf >= 0) return c->knobs.paths_wf == 1;
     return c->mesh.n_nodes > 0;
 }
 int paths_wavefront(pbrt_gpu_ctx* c, const DevScene& sc, int64_t sb, int64_t nb) {
     const RenderParams& rp = c->rp;
     const int64_t nrec = nb * c->wb.ppt, per = rp.spp - 1;
     const int nl = sc.n_lights;
-    const char* se = getenv("PBRT_PW_SORT");
-    const int sort = (se && atoi(se) == 1) ? 1 : 0;
+    const int sort = c->knobs.pw_sort ? 1 : 0;
     const int n_keys = std::max(1, std::min(c->host_scene.n_materials, kPwMaxKeys));
-    double gb = 24.0;
-    if (const char* e = getenv("PBRT_PW_GB")) gb = atof(e) > 0 ? atof(e) : gb;
+    const double gb = c->knobs.pw_gb;
     const int64_t per_path = (int64_t)sizeof(PwPath) + 4 * 4;   // record + 4 queue slots
     int64_t chunk = per > 0 ? std::max<int64_t>(1, (int64_t)(gb * 1073741824.0) / (per_path * per)) : nrec;
     chunk = std::min(chunk, nrec);
@@ -2612,7 +2671,7 @@ int wave_buffers(pbrt_gpu_ctx* c) {
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
             gb = std::min(gb, 0.5 * (double)(free_b + c->wave_cap) / 1073741824.0);
     }
-    if (const char* e = getenv("PBRT_WAVE_BUFFER_GB")) gb = atof(e) > 0 ? atof(e) : gb;
+    if (c->knobs.wave_buffer_gb > 0) gb = c->knobs.wave_buffer_gb;
     int64_t batch = (int64_t)(gb * 1073741824.0) / per_tile;
     if (batch < 1) batch = 1;
     if (batch > rp.n_slots) batch = rp.n_slots > 0 ? rp.n_slots : 1;
@@ -2754,6 +2813,7 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
     int rc = validate_scene(scene);
     if (rc != PBRT_OK) return rc;
     auto* c = new pbrt_gpu_ctx();
+    c->knobs = Knobs::from_env();
     c->device = (opts && opts->device >= 0) ? opts->device : -1;
     if (opts && opts->lanes_per_wave > 0 && opts->lanes_per_wave <= 64) {
         c->lanes_per_wave = opts->lanes_per_wave;
@@ -2791,6 +2851,10 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
     for (int i = 0; i < scene->n_materials; i++)   // Mirror, Glass or OrenNayar (Matte with sigma != 0)
         c->non_matte |= scene->materials[i].type != PBRT_MAT_MATTE ||
                         !(std::min(std::max(scene->materials[i].sigma, 0.0), 90.0) == 0);
+    c->rough_glass = false;
+    for (int i = 0; i < scene->n_materials; i++)
+        c->rough_glass |= scene->materials[i].type == PBRT_MAT_GLASS &&
+                          !(scene->materials[i].u_roughness == 0 && scene->materials[i].v_roughness == 0);
     c->h_node_prims.resize((size_t)scene->n_nodes);
     for (int i = 0; i < scene->n_nodes; i++) c->h_node_prims[i] = scene->nodes[i].n_prims;
     c->host_scene.shapes = nullptr;
@@ -2831,9 +2895,8 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
     {   // leaf culling groups of the LDS-staged walk
         std::vector<double> gb;
         std::vector<uint32_t> gm;
-        c->n_groups = cull_groups(scene, order, gb, gm);
-        if (const char* e = getenv("PBRT_CULL_GROUPS"))   // 0: test every leaf (A/B)
-            if (atoi(e) == 0) c->n_groups = 0;
+        c->n_groups = cull_groups(c->knobs, scene, order, gb, gm);
+        if (!c->knobs.cull_groups) c->n_groups = 0;   // PBRT_CULL_GROUPS=0: test every leaf (A/B)
         if (c->n_groups > 0 && ((rc = upload(c, &c->d_groups, gb.data(), gb.size())) ||
                                 (rc = upload(c, &c->d_gmasks, gm.data(), gm.size())))) {
             pbrt_gpu_destroy(c);
@@ -2879,6 +2942,7 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
             c->last_kernel = c->use_dl ? PBRT_KERNEL_WAVE_DL
                              : rp.mode == PBRT_MODE_THROUGHPUT ? PBRT_KERNEL_WAVE : PBRT_KERNEL_WAVE_CI;
             const bool lds_nodes = c->host_scene.n_nodes <= kLdsNodes;
+            const bool kx = c->non_matte;   // Mirror / smooth Glass / OrenNayar: the kX instantiations
             const int64_t per = rp.slot_w * rp.slot_h;
             c->n_batches = (int)((rp.n_slots + c->wave_batch - 1) / c->wave_batch);
             while ((int)c->bev.size() < 3 * c->n_batches) {
@@ -2891,7 +2955,7 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 0], c->stream));
                 const int G = c->tiles_per_wave;
                 if (c->use_dl) {
-                    hipLaunchKernelGGL(k_wf_primary, dim3((unsigned)((nb * c->wb.ppt + kWave - 1) / kWave)),
+                    hipLaunchKernelGGL(k_wf_primary<false>, dim3((unsigned)((nb * c->wb.ppt + kWave - 1) / kWave)),
                                        dim3(kWave), 0, c->stream, with_slot(sc, 1), rp, c->wb, sb, nb);
                     unsigned lds = 0;
                     const ChainLayout lw = ci_layout(c->lay_ci, 1, 1, lds);
@@ -2900,13 +2964,14 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                 } else if (rp.mode == PBRT_MODE_THROUGHPUT) {
                     // no offset chain: every sample's stream is known up front
                 } else {
-                    hipLaunchKernelGGL(k_wf_primary, dim3((unsigned)((nb * c->wb.ppt + kWave - 1) / kWave)),
+                    hipLaunchKernelGGL(kx ? k_wf_primary<true> : k_wf_primary<false>,
+                                       dim3((unsigned)((nb * c->wb.ppt + kWave - 1) / kWave)),
                                        dim3(kWave), 0, c->stream, with_slot(sc, 1), rp, c->wb, sb, nb);
                     const int kw = ci_waves(c, nb);
                     const uint32_t* order = nullptr;
                     bool learned = false;   // order from the last frame's measured chain times
                     uint32_t* ticks = nullptr;
-                    if ((kw > 1 || G == 1) && c->n_batches == 1 && ci_order_enabled()) {
+                    if ((kw > 1 || G == 1) && c->n_batches == 1 && ci_order_enabled(c)) {
                         if (c->ticks_cap < nb) {
                             if (c->d_ticks) (void)hipFree(c->d_ticks);
                             if (c->d_slot_order) (void)hipFree(c->d_slot_order);
@@ -2924,7 +2989,7 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                             learned = true;
                         }
                         c->probed = false;
-                        if (!order && ci_probe_enabled() && nb <= (int64_t)1 << 24) {
+                        if (!order && ci_probe_enabled(c) && nb <= (int64_t)1 << 24) {
                             // no measured order for this configuration yet: estimate it
                             int64_t npad = 2048;
                             while (npad < nb) npad <<= 1;
@@ -2939,7 +3004,8 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                                 c->cost_cap = npad;
                             }
                             HIPCHK(c, hipMemsetAsync(c->d_cost_keys, 0xFF, sizeof(uint64_t) * (size_t)npad, c->stream));
-                            hipLaunchKernelGGL(k_tile_cost, dim3((unsigned)nb), dim3(kWave), 0, c->stream, with_slot(sc, 0),
+                            hipLaunchKernelGGL(kx ? k_tile_cost<true> : k_tile_cost<false>, dim3((unsigned)nb),
+                                               dim3(kWave), 0, c->stream, with_slot(sc, 0),
                                                rp, c->wb, sb, nb, c->d_cost, c->d_cost_keys);
                             bitonic_sort_u64(c->d_cost_keys, (uint32_t)npad, c->stream);
                             hipLaunchKernelGGL(k_order_of_keys, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0,
@@ -2959,22 +3025,24 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                             const int ring = w * kCiRingBytes / (int)sizeof(RingEnt);
                             unsigned lds = 0;
                             const ChainLayout lw = ci_layout(c->lay_ci, w, 1, lds);
-                            auto kern = w == 2   ? (lds_nodes ? k_chain_ci<2> : k_chain_ci<2, 64>)
-                                        : w == 4 ? (lds_nodes ? k_chain_ci<4> : k_chain_ci<4, 64>)
-                                                 : (lds_nodes ? k_chain_ci<8> : k_chain_ci<8, 64>);
+                            // kX: LDS-staged trees only, at most 4 waves per tile (wave_eligible, ci_waves)
+                            auto kern = kx ? (w == 2 ? k_chain_ci<2, 32, true> : k_chain_ci<4, 32, true>)
+                                           : (w == 2   ? (lds_nodes ? k_chain_ci<2> : k_chain_ci<2, 64>)
+                                              : w == 4 ? (lds_nodes ? k_chain_ci<4> : k_chain_ci<4, 64>)
+                                                       : (lds_nodes ? k_chain_ci<8> : k_chain_ci<8, 64>));
                             hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3(kWave * w), lds, st, with_slot(sc, 2), rp, lw,
                                                c->d_jump, c->wb, sb, nb, kWave * w, ring, c->d_ctr, ord, ticks,
-                                               ci_stride(w));
+                                               ci_stride(c, w));
                         } else {
                             const int Gc = std::min(G, kCiMaxGroups);
                             const int ring = kCiRingBytes / (int)sizeof(RingEnt) / Gc;
                             unsigned lds = 0;
                             const ChainLayout lw = ci_layout(c->lay_ci, 1, Gc, lds);
-                            auto kern1 = lds_nodes ? k_chain_ci<1> : k_chain_ci<1, 64>;
+                            auto kern1 = kx ? k_chain_ci<1, 32, true> : (lds_nodes ? k_chain_ci<1> : k_chain_ci<1, 64>);
                             hipLaunchKernelGGL(kern1, dim3((unsigned)((n + Gc - 1) / Gc)), dim3(kWave),
                                                lds, st, with_slot(sc, 2), rp, lw, c->d_jump, c->wb, sb,
                                                nb, kWave / Gc, ring, c->d_ctr, Gc == 1 ? ord : nullptr,
-                                               Gc == 1 ? ticks : nullptr, ci_stride(1));
+                                               Gc == 1 ? ticks : nullptr, ci_stride(c, 1));
                         }
                     };
                     // the heaviest tiles of the last frame get 4 waves each; they are
@@ -2984,19 +3052,19 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                     // tile, the most efficient per lane)
                     // measured wins at 1/2 and 1/4 shards (nb > n_simd); a loss at 1/8
                     // (1020 tiles: 294 -> 307 ms), so smaller launches never split
-                    int64_t heavy = (learned && kw > 1 && G == 1 && nb > c->n_simd && ci_split_enabled())
+                    int64_t heavy = (learned && kw > 1 && G == 1 && nb > c->n_simd && ci_split_enabled(c))
                                         ? std::min<int64_t>(c->heavy_k, nb) : 0;
-                    if (ci_heavy_override() >= 0 && learned && G == 1)   // tests and experiments force the split
-                        heavy = std::min<int64_t>(ci_heavy_override(), nb);
+                    if (ci_heavy_override(c) >= 0 && learned && G == 1)   // tests and experiments force the split
+                        heavy = std::min<int64_t>(ci_heavy_override(c), nb);
                     if (heavy >= nb) heavy = 0;   // nothing left for the light launch: one launch at kw
                     c->last_heavy = heavy;
                     if (ticks) {   // label every slot with the waves it actually runs at
                         c->h_slot_kw.assign((size_t)nb, (uint8_t)(heavy > 0 ? 1 : kw));
-                        for (int64_t i = 0; i < heavy; i++) c->h_slot_kw[c->h_slot_order[(size_t)i]] = (uint8_t)ci_heavy_waves();
+                        for (int64_t i = 0; i < heavy; i++) c->h_slot_kw[c->h_slot_order[(size_t)i]] = (uint8_t)ci_heavy_waves(c);
                     }
                     if (heavy > 0) {
                         HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
-                        launch_ci(ci_heavy_waves(), heavy, order, c->stream);
+                        launch_ci(ci_heavy_waves(c), heavy, order, c->stream);
                         HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
                         launch_ci(1, nb - heavy, order + heavy, c->stream2);
                         HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
@@ -3019,19 +3087,21 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                     // the path wavefront: mesh scenes, and whatever k_paths_ci cannot
                     // take (a tree beyond LDS, more than 64 / P lights)
                     if (rp.mode == PBRT_MODE_THROUGHPUT)
-                        hipLaunchKernelGGL(k_mb_setup, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
+                        hipLaunchKernelGGL(k_mb_setup<false>, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
                                            (unsigned)c->lay.total, c->stream, with_slot(sc, 4), rp, c->lay, c->d_jump,
                                            c->wb, sb, nb);
                     const int rcp = paths_wavefront(c, with_slot(sc, rp.mode == PBRT_MODE_THROUGHPUT ? 5 : 3), sb, nb);
                     if (rcp != PBRT_OK) return rcp;
                 } else if (rp.mode == PBRT_MODE_THROUGHPUT && paths_ci_pixels(c, rp) > 0) {
                     // setup (StartPixel + bounce 1 per pixel), then lane-refill paths
-                    hipLaunchKernelGGL(k_mb_setup, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
-                                       (unsigned)c->lay.total, c->stream, with_slot(sc, 4), rp, c->lay, c->d_jump, c->wb, sb, nb);
+                    hipLaunchKernelGGL(kx ? k_mb_setup<true> : k_mb_setup<false>, dim3((unsigned)(nb * c->wb.ppt)),
+                                       dim3(kWave), (unsigned)c->lay.total, c->stream, with_slot(sc, 4), rp, c->lay,
+                                       c->d_jump, c->wb, sb, nb);
                     const int pp = paths_ci_pixels(c, rp);
                     const int per = rp.ndims * rp.spp;
-                    auto kern = pp == 8 ? k_paths_ci<8, true> : pp == 2 ? k_paths_ci<2, true> : k_paths_ci<4, true>;
-                    const int sl = paths_ci_s1d_lds(rp, pp) ? 1 : 0;
+                    auto kern = kx ? (pp == 8 ? k_paths_ci<8, true, true> : k_paths_ci<4, true, true>)
+                                   : (pp == 8 ? k_paths_ci<8, true> : pp == 2 ? k_paths_ci<2, true> : k_paths_ci<4, true>);
+                    const int sl = paths_ci_s1d_lds(c, rp, pp) ? 1 : 0;
                     const int lds = pp == 8 ? paths_group_lds<8>(sl * per) : pp == 2 ? paths_group_lds<2>(sl * per)
                                                                                      : paths_group_lds<4>(sl * per);
                     hipLaunchKernelGGL(kern, dim3((unsigned)((nb * c->wb.ppt + pp - 1) / pp)), dim3(kWave),
@@ -3041,8 +3111,9 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                 else {
                     const int pp = paths_ci_pixels(c, rp);
                     const int per = rp.ndims * rp.spp;
-                    auto kern = pp == 8 ? k_paths_ci<8> : pp == 2 ? k_paths_ci<2> : k_paths_ci<4>;
-                    const int sl = paths_ci_s1d_lds(rp, pp) ? 1 : 0;
+                    auto kern = kx ? (pp == 8 ? k_paths_ci<8, false, true> : k_paths_ci<4, false, true>)
+                                   : (pp == 8 ? k_paths_ci<8> : pp == 2 ? k_paths_ci<2> : k_paths_ci<4>);
+                    const int sl = paths_ci_s1d_lds(c, rp, pp) ? 1 : 0;
                     const int lds = pp == 8 ? paths_group_lds<8>(sl * per) : pp == 2 ? paths_group_lds<2>(sl * per)
                                                                                      : paths_group_lds<4>(sl * per);
                     hipLaunchKernelGGL(kern, dim3((unsigned)((nb * c->wb.ppt + pp - 1) / pp)), dim3(kWave),
@@ -3158,7 +3229,7 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
         int64_t k = 0;
         while (k < (int64_t)t.size() && cost[c->h_slot_order[(size_t)k]] > thr) k++;
         c->heavy_k = std::min<int64_t>(k, c->n_simd / 4);   // at most a quarter of the wave slots
-        if (ci_heavy_override() >= 0) c->heavy_k = ci_heavy_override();
+        if (ci_heavy_override(c) >= 0) c->heavy_k = ci_heavy_override(c);
         c->order_key = c->ticks_key;
     }
     if (ctr.any_panic) {

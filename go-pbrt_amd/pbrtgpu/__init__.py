@@ -202,6 +202,25 @@ class Scene:
         return s
 
     @classmethod
+    def readme_glass(cls, w, h, special="glass", mirror=True):
+        """internal/render/server.go:67-91 (commented out): the README scene plus
+        a sphere of radius 5 at (50, 2.5, 50) of NewGlass(Kr = Kt = 0.5, index
+        1.5) -- the commented code attaches the checkerboard `m`, the glass it
+        defines is what image.png shows. special = "black": that sphere a black
+        Matte instead. mirror: a Mirror (Kr 0.9) sphere beside it at (35, 5, 45).
+        Built (BVH, 2 primitives per node as server.go:162)."""
+        s = cls.readme(w, h)
+        m = s.add_glass() if special == "glass" else s.add_matte((0.0, 0.0, 0.0))
+        spheres = [((50, 2.5, 50), m)]
+        if mirror:
+            spheres.append(((35, 5.0, 45), s.add_mirror()))
+        for (pos, mat) in spheres:
+            sph = s.add_sphere(translate(0, 0, 0), 5.0)
+            s.add_primitive(sph, mat, translate(*pos))
+        s.build(2)
+        return s
+
+    @classmethod
     def heightfield(cls, w, h, quads=707, seed=1, spheres=False):
         """BASELINE config D (quads 707: 999 698 triangles) / E (2236): the
         height-field extension scene (include/pbrt_scene.h)."""

@@ -25,6 +25,12 @@ Quirks restated (and therefore tested here):
   own quirks (D's alphaX*alphaY, MicrofacetTransmission.F's inverted hemisphere
   test, its unset TransportMode) are restated.
 
+Path renders of these scenes (smooth glass, mirror, OrenNayar; n_dims >= 3)
+run on the wave pipeline's kX instantiations (k_wf_primary / k_chain_ci /
+k_paths_ci / k_mb_setup over BSDFX, with Path.Li's etaScale); everything else
+(n_dims < 3, DirectLighting's specular recursion, rough glass) on the serial
+kernel. Both are checked bit for bit against the oracle.
+
 No reference test covers these materials and there is no Go toolchain here:
 device-vs-oracle parity is bit-exact but "parity unpinned" against Go itself.
 The oracle's FrDielectric is pinned by closed forms below.
@@ -109,21 +115,9 @@ def test_oracle_direct_lighting_mirror_is_black_matte():
 
 
 def readme_glass_scene(w=96, h=64, special="glass", mirror=False):
-    """internal/render/server.go:67-91 (commented out): the README scene plus a
-    sphere of radius 5 at (50, 2.5, 50) made of NewGlass(Kr = Kt = 0.5, index 1.5)
-    -- the commented code attaches the checkerboard `m`, the glass it defines is
-    what image.png shows. special = "black": that sphere a black Matte instead.
-    mirror: a Mirror sphere beside it at (35, 5, 45)."""
-    sc = G.Scene.readme(w, h)
-    m = sc.add_glass() if special == "glass" else sc.add_matte((0.0, 0.0, 0.0))
-    spheres = [((50, 2.5, 50), m)]
-    if mirror:
-        spheres.append(((35, 5.0, 45), sc.add_mirror()))
-    for (pos, mat) in spheres:
-        sph = sc.add_sphere(G.translate(0, 0, 0), 5.0)
-        sc.add_primitive(sph, mat, G.translate(*pos))
-    sc.build(2)
-    return sc
+    """internal/render/server.go:67-91's commented-out glass sphere added to the
+    README scene (pbrtgpu.Scene.readme_glass; bench.py config G)."""
+    return G.Scene.readme_glass(w, h, special=special, mirror=mirror)
 
 
 @pytest.mark.parametrize("strategy", [abi.PBRT_DL_UNIFORM_SAMPLE_ALL, abi.PBRT_DL_UNIFORM_SAMPLE_ONE])
@@ -191,9 +185,16 @@ def test_material_desc_layout():
 
 
 # ------------------------------------------------------------------ GPU tests
+def path_kernel(nd, mode):
+    """The kernel a Path render of a Mirror/Glass/OrenNayar scene runs on."""
+    if nd < 3:
+        return abi.PBRT_KERNEL_SERIAL
+    return abi.PBRT_KERNEL_WAVE_CI if mode == abi.PBRT_MODE_EXACT else abi.PBRT_KERNEL_WAVE
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", [abi.PBRT_MODE_EXACT, abi.PBRT_MODE_THROUGHPUT])
-@pytest.mark.parametrize("spp,nd,depth", [(3, 4, 6), (2, 2, 8), (4, 0, 5)])
+@pytest.mark.parametrize("spp,nd,depth", [(3, 4, 6), (2, 2, 8), (4, 0, 5), (4, 5, 10), (2, 3, 2)])
 def test_device_materials_bitexact_vs_oracle(mode, spp, nd, depth):
     sc = material_scene()
     rd = abi.render_desc(spp, spp, n_dims=nd, max_depth=depth, mode=mode)
@@ -201,8 +202,45 @@ def test_device_materials_bitexact_vs_oracle(mode, spp, nd, depth):
     assert rc == 0
     with G.Renderer(sc) as r:
         film, st = r.render(rd)
-    assert st.kernel == abi.PBRT_KERNEL_SERIAL
+    assert st.kernel == path_kernel(nd, mode)
     assert np.array_equal(bits(film), bits(of))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ci_waves", ["1", "2", "4", "8"])
+def test_device_materials_chain_waves_vs_oracle(monkeypatch, ci_waves):
+    """k_chain_ci<kW, 32, kX> for every waves-per-tile count, and the serial
+    kernel on the same render: all bit-identical to the oracle."""
+    monkeypatch.setenv("PBRT_CI_WAVES", ci_waves)
+    sc = material_scene(w=48, h=40)
+    rd = abi.render_desc(4, 4, max_depth=8)
+    rc, of, _ = O.render(sc.desc, rd, threads=8)
+    assert rc == 0
+    with G.Renderer(sc) as r:
+        film, st = r.render(rd)
+        film2, _ = r.render(rd)   # the second frame runs in the measured tile order
+    assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
+    assert np.array_equal(bits(film), bits(of)) and np.array_equal(bits(film2), bits(of))
+    with G.Renderer(sc, kernel="serial") as r:
+        fs, sts = r.render(rd)
+    assert sts.kernel == abi.PBRT_KERNEL_SERIAL and np.array_equal(bits(fs), bits(of))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [abi.PBRT_MODE_EXACT, abi.PBRT_MODE_THROUGHPUT])
+def test_device_materials_stats_match_oracle(mode):
+    """Path counts and the in-kernel ray counters of the kX pipeline equal the
+    oracle's (glass bounces sample no light: fewer shadow rays per bounce)."""
+    sc = material_scene(w=40, h=32)
+    rd = abi.render_desc(3, 3, max_depth=7, mode=mode)
+    rc, of, ost = O.render(sc.desc, rd, threads=8)
+    assert rc == 0
+    with G.Renderer(sc) as r:
+        film, st = r.render(rd)
+    assert st.kernel == path_kernel(4, mode)
+    assert np.array_equal(bits(film), bits(of))
+    assert st.paths_traced == ost.paths
+    assert (st.rays_closest, st.rays_shadow) == (ost.closest_rays, ost.shadow_rays)
 
 
 @pytest.mark.gpu
@@ -298,23 +336,41 @@ def test_device_oren_nayar_vs_oracle(integrator, mode, sigma):
     assert rc == 0
     with G.Renderer(sc) as r:
         film, st = r.render(rd)
-    assert st.kernel == abi.PBRT_KERNEL_SERIAL
+    expect = path_kernel(4, mode) if integrator == abi.PBRT_INTEGRATOR_PATH else abi.PBRT_KERNEL_SERIAL
+    assert st.kernel == expect
     assert np.array_equal(bits(film), bits(of))
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", [abi.PBRT_MODE_EXACT, abi.PBRT_MODE_THROUGHPUT])
-def test_device_readme_scene_with_the_commented_out_glass_sphere(mode):
+@pytest.mark.parametrize("kernel", ["auto", "serial"])
+def test_device_readme_scene_with_the_commented_out_glass_sphere(mode, kernel):
     """internal/render/server.go:67-91 (commented out): a glass sphere of radius 5
     at (50, 2.5, 50) with Kr = Kt = 0.5 and index 1.5, added to the README scene;
-    plus a mirror sphere beside it. Rendered on the serial kernel, bit-exact."""
+    plus a mirror sphere beside it. The wave pipeline (kX) and the serial
+    kernel, both bit-exact."""
     sc = readme_glass_scene(mirror=True)
     rd = abi.render_desc(2, 2, mode=mode)
     rc, of, _ = O.render(sc.desc, rd, threads=8)
     assert rc == 0
+    with G.Renderer(sc, kernel=kernel) as r:
+        film, st = r.render(rd)
+    assert st.kernel == (path_kernel(4, mode) if kernel == "auto" else abi.PBRT_KERNEL_SERIAL)
+    assert np.array_equal(bits(film), bits(of))
+
+
+@pytest.mark.gpu
+def test_device_readme_glass_scene_at_8x8_spp_bitexact():
+    """The README scene with server.go's glass sphere and a mirror at config B's
+    sampler (Stratified(8,8), Path(10)) on a 256x160 film: the kX chain (one wave
+    per tile and the default) and paths, every tile bit-identical."""
+    sc = readme_glass_scene(256, 160, mirror=True)
+    rd = abi.render_desc(8, 8)
+    rc, of, ost = O.render(sc.desc, rd, threads=8)
+    assert rc == 0
     with G.Renderer(sc) as r:
         film, st = r.render(rd)
-    assert st.kernel == abi.PBRT_KERNEL_SERIAL
+    assert st.kernel == abi.PBRT_KERNEL_WAVE_CI and st.paths_traced == ost.paths
     assert np.array_equal(bits(film), bits(of))
 
 
@@ -347,3 +403,60 @@ def test_device_direct_lighting_through_glass_depth_limit():
         with pytest.raises(G.PbrtError) as ei:
             r.render(abi.render_desc(2, 2, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING, max_depth=65))
     assert ei.value.code == abi.PBRT_E_UNSUPPORTED
+
+
+def mesh_material_scene(material, w=40, h=32):
+    """A small triangle mesh (a tilted 4x4-quad grid) made of `material`
+    ("glass" | "mirror" | "oren"), over the checker floor, beside a matte
+    sphere; include/pbrt_gpu.h lets a mesh take any material."""
+    s = G.Scene()
+    chk = s.add_checker((0.2, 0, 0), (0, 0, 0.2), 0, 0, (1, 1, 1), (0.18, 0.18, 0.18))
+    s.add_primitive(s.add_disk(G.rotate(0, 90), 0.0, 100.0), chk)
+    m = {"glass": lambda: s.add_glass(), "mirror": lambda: s.add_mirror(),
+         "oren": lambda: s.add_matte((0.5, 0.6, 0.4), sigma=30.0)}[material]()
+    n = 4
+    xs = np.linspace(-3.0, 3.0, n + 1)
+    p = np.array([(x, 1.0 + 0.4 * x + 0.3 * z, z) for z in xs for x in xs], dtype=np.float32)
+    idx = []
+    for j in range(n):
+        for i in range(n):
+            a, b, c, d = j * (n + 1) + i, j * (n + 1) + i + 1, (j + 1) * (n + 1) + i, (j + 1) * (n + 1) + i + 1
+            idx += [(a, b, d), (a, d, c)]
+    s.add_mesh(p, np.array(idx, dtype=np.int32), m)
+    s.add_primitive(s.add_sphere(G.translate(0, 0, 0), 1.5), s.add_matte((0.6, 0.1, 0.1)), G.translate(0, 1.5, -4))
+    s.add_point_light(G.translate(-6, 10, 8), (60, 60, 60))
+    s.add_area_light((6, 6, 6), s.add_sphere(G.translate(0, 9, 2), 0.75))
+    s.set_film(w, h)
+    s.set_camera(G.look_at((0, 7, 12), (0, 1.5, 0), (0, 1, 0)), fov=55)
+    return s.build(max_prims_in_node=1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("material", ["glass", "mirror", "oren"])
+@pytest.mark.parametrize("mode", [abi.PBRT_MODE_EXACT, abi.PBRT_MODE_THROUGHPUT])
+def test_device_mesh_with_specular_material_vs_oracle(material, mode):
+    """A triangle mesh of Glass / Mirror / OrenNayar: mesh scenes with such a
+    material render on the serial kernel (the kX wave pipeline takes analytic
+    scenes only), bit-exact against the oracle, which resolves the mesh's
+    material the same way (oracle_render.c)."""
+    sc = mesh_material_scene(material)
+    rd = abi.render_desc(3, 3, max_depth=6, mode=mode)
+    rc, of, _ = O.render(sc.desc, rd, threads=8)
+    assert rc == 0 and np.isfinite(of).all()
+    with G.Renderer(sc) as r:
+        film, st = r.render(rd)
+    assert st.kernel == abi.PBRT_KERNEL_SERIAL
+    assert np.array_equal(bits(film), bits(of))
+
+
+def test_oracle_mesh_material_changes_the_image():
+    """The mesh's material is honoured by the oracle: a glass or mirror mesh
+    renders differently from an OrenNayar one."""
+    rd = abi.render_desc(2, 2, max_depth=5)
+    films = {}
+    for m in ("glass", "mirror", "oren"):
+        sc = mesh_material_scene(m)
+        rc, films[m], _ = O.render(sc.desc, rd, threads=8)
+        assert rc == 0
+    assert not np.array_equal(films["glass"], films["mirror"])
+    assert not np.array_equal(films["glass"], films["oren"])
