@@ -683,7 +683,7 @@ struct alignas(16) PwPath {
     int32_t bounces, best, flags, pnc;
     int32_t bnc;
     uint32_t rays;   // kRayClosest / kRayShadow counts of the path
-    int32_t pad1, pad2;
+    double eta;      // Path.Li's etaScale (kX)
 };
 constexpr int kPwPending = 1, kPwShadow = 2, kPwDone = 4;
 constexpr int kPwMaxKeys = 64;   // material keys of the sort (more materials share the last)
@@ -745,11 +745,13 @@ __device__ __forceinline__ bool pw_next_bounce(PwPath& p, int max_depth) {
 struct PwCache {
     SI si;
     BSDF b;
+    BSDFX x;
     V3 wo;
     const Spec* ld;
     const int* ld_panic;
 };
 
+template <bool kX = false>
 __global__ __launch_bounds__(kWave) void k_pw_cache(DevScene sc, WaveBufs wb, int64_t rec0, int64_t nrec,
                                                     Spec* __restrict__ ldc, int* __restrict__ ldp) {
     __shared__ uint16_t stack_lds[64 * kStackStride];
@@ -760,16 +762,17 @@ __global__ __launch_bounds__(kWave) void k_pw_cache(DevScene sc, WaveBufs wb, in
     const int64_t r = i / nl;
     const int l = (int)(i - r * nl);
     const PixelRec& pr = wb.prec[rec0 + r];
-    if (!(pr.hit && pr.b.n_bxdfs > 0)) return;
+    if (!(pr.hit && (kX ? bsdfx_nonspecular(pr.b, pr.x) : pr.b.n_bxdfs > 0))) return;
     int pl = 0;
     uint64_t traced = 0;
-    const Spec ld = estimate_direct(sc, stack_lds + threadIdx.x, pl, pr.si, pr.b, l, V2{0.0, 0.0}, &traced);
+    const Spec ld = kX ? estimate_direct_x(sc, stack_lds + threadIdx.x, pl, pr.si, pr.b, pr.x, l, V2{0.0, 0.0}, &traced)
+                       : estimate_direct(sc, stack_lds + threadIdx.x, pl, pr.si, pr.b, l, V2{0.0, 0.0}, &traced);
     if (!pl && max_component(ld) > 10) pl = PBRT_PANIC_LD_GT_10;
     ldc[i] = ld;
     ldp[i] = pl | (traced ? kLdTraced : 0);
 }
 
-template <bool kMB>
+template <bool kMB, bool kX = false>
 __global__ __launch_bounds__(kWave) void k_pw_start(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
                                                     int64_t rec0, int64_t nrec, const Spec* __restrict__ ldc,
                                                     const int* __restrict__ ldp, PwPath* __restrict__ paths,
@@ -812,12 +815,13 @@ __global__ __launch_bounds__(kWave) void k_pw_start(DevScene sc, RenderParams rp
     s.bounces = 1;
     s.first = 1;
     s.rays = 0;
-    const PwCache pc{pr.si, pr.b, pr.wo, ldc + r * sc.n_lights, ldp + r * sc.n_lights};
+    const PwCache pc{pr.si, pr.b, pr.x, pr.wo, ldc + r * sc.n_lights, ldp + r * sc.n_lights};
     const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, n, rp.ndims};
     int pnc = 0, bnc = 1;
-    bool done = path_step<1>(sc, pc, ss, c, s, rp.max_depth, rp.rr_threshold, nullptr, pnc, bnc);
+    bool done = path_step<1, kX>(sc, pc, ss, c, s, rp.max_depth, rp.rr_threshold, nullptr, pnc, bnc);
     p.L = s.L;
     p.beta = s.beta;
+    p.eta = s.eta_scale;
     p.ray = s.ray;
     p.bounces = s.bounces;
     p.rng = c.rng.state;
@@ -884,6 +888,7 @@ __global__ __launch_bounds__(256) void k_pw_scatter(const PwPath* __restrict__ p
     }
 }
 
+template <bool kX = false>
 __global__ __launch_bounds__(kWave) void k_pw_shade(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
                                                     PwPath* __restrict__ paths, PwQueues qs, int sorted,
                                                     unsigned long long* __restrict__ pkey) {
@@ -898,7 +903,8 @@ __global__ __launch_bounds__(kWave) void k_pw_shade(DevScene sc, RenderParams rp
         SI isect;
         prim_si(sc, p.best, p.ray, p.ph, isect);
         BSDF b;
-        if (compute_bsdf(sc, isect, b) < 0) {
+        BSDFX x;
+        if ((kX ? compute_bsdf_x(sc, isect, b, x) : compute_bsdf(sc, isect, b)) < 0) {
             p.pnc = -1;
             pw_finish(wb, n, p, pkey);
             continue;
@@ -918,7 +924,7 @@ __global__ __launch_bounds__(kWave) void k_pw_shade(DevScene sc, RenderParams rp
         int flags = 0;
         const Spec beta0 = p.beta;
         const int nl = sc.n_lights;
-        if (b.n_bxdfs > 0) {   // UniformSampleOneLight (integrator.go:48-77)
+        if (kX ? bsdfx_nonspecular(b, x) : b.n_bxdfs > 0) {   // UniformSampleOneLight (integrator.go:48-77)
             if (nl == 0) {
                 p.L = p.L + smul(p.beta, spec(0));
             } else {
@@ -934,7 +940,9 @@ __global__ __launch_bounds__(kWave) void k_pw_shade(DevScene sc, RenderParams rp
                 flags |= kPwPending;
                 Ray sr;
                 Spec ld_vis = spec(0);
-                if (estimate_direct_begin(sc, isect, b, ln, ul, sr, ld_vis)) flags |= kPwShadow;
+                if (kX ? estimate_direct_begin_x(sc, isect, b, x, ln, ul, sr, ld_vis)
+                       : estimate_direct_begin(sc, isect, b, ln, ul, sr, ld_vis))
+                    flags |= kPwShadow;
                 p.sr = sr;
                 p.ld = ld_vis;
             }
@@ -943,17 +951,28 @@ __global__ __launch_bounds__(kWave) void k_pw_shade(DevScene sc, RenderParams rp
             V2 u = c_get2d(c, ss);
             V3 wi;
             double pdf;
-            Spec f = bsdf_sample_f(b, wo, u, wi, pdf);
+            int type = 0;
+            Spec f = kX ? bsdfx_sample_f(b, x, wo, u, wi, pdf, type) : bsdf_sample_f(b, wo, u, wi, pdf);
+            if (kX && type == -1) {   // rough glass: the reference's nil dereference (never routed here)
+                p.pnc = PBRT_PANIC_NIL_DEREF;
+                pw_finish(wb, n, p, pkey);
+                continue;
+            }
             if (is_black(f) || pdf == 0.0) {
                 flags |= kPwDone;
             } else {
                 double wp = absdot(wi, isect.sn) / pdf;
                 p.beta = smul(p.beta, smuls(f, wp));
+                if (kX && (type & BXDF_SPECULAR) && (type & BXDF_TRANSMISSION)) {   // path.go:106-117
+                    const double eta = x.eta;
+                    if (dot(wo, isect.n) > 0) p.eta *= eta * eta;
+                    else p.eta *= 1 / (eta * eta);
+                }
                 p.ray.o = offset_ray_origin(isect.p, isect.perr, isect.n, wi);
                 p.ray.d = wi;
                 p.ray.tmax = kInf;
                 p.ray.time = isect.time;
-                Spec rr = smuls(p.beta, 1.0);
+                Spec rr = smuls(p.beta, kX ? p.eta : 1.0);
                 if (max_component(rr) < rp.rr_threshold && p.bounces > 3) {
                     double q = gomath::max(0.05, 1 - max_component(rr));
                     double u1 = c_get1d(c, ss);
@@ -2414,12 +2433,12 @@ bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Rend
     if (rd->flags & PBRT_FLAG_PANIC_FIDELITY) return false;   // the serial kernel traces the extra rays
     const bool dl = rd->integrator == PBRT_INTEGRATOR_DIRECT_LIGHTING;
     // Mirror, smooth Glass and OrenNayar: Path renders run the kX instantiations
-    // of the wave pipeline (trajectories and paths over BSDFX, with etaScale),
-    // whose path stage is k_paths_ci; DirectLighting's specular recursion, rough
-    // glass (whose every BSDF sample panics), mesh scenes and renders k_paths_ci
-    // cannot take stay on the serial kernel
-    if (c->non_matte && (dl || c->rough_glass || c->mesh.n_nodes > 0 || paths_wf_enabled(c) ||
-                         paths_ci_pixels(c, rp) < 4 || c->host_scene.n_nodes > kLdsNodes))
+    // of the wave pipeline (trajectories and paths over BSDFX, with etaScale):
+    // k_chain_ci for LDS-staged trees, then k_paths_ci (P = 4, 8) or the path
+    // wavefront (mesh scenes); DirectLighting's specular recursion, rough glass
+    // (whose every BSDF sample panics) and larger trees stay on the serial kernel
+    if (c->non_matte && (dl || c->rough_glass || c->host_scene.n_nodes > kLdsNodes ||
+                         (!paths_wf_enabled(c) && paths_ci_pixels(c, rp) > 0 && paths_ci_pixels(c, rp) < 4)))
         return false;
     if (dl) {   // k_dl_*: the camera ray must be per pixel (pFilm stratified; pLens stratified or unused)
         if (rd->n_dims < 1 || (rd->n_dims < 2 && c->host_scene.camera.lens_radius > 0)) return false;
@@ -2625,14 +2644,17 @@ int paths_wavefront(pbrt_gpu_ctx* c, const DevScene& sc, int64_t sb, int64_t nb)
     const unsigned G = (unsigned)std::max<int64_t>(64, (int64_t)c->n_simd * 8);   // grid-stride blocks
     HIPCHK(c, hipMemsetAsync(pkey, 0xFF, (size_t)nrec * 8, c->stream));
     const bool mb = rp.mode == PBRT_MODE_THROUGHPUT;
+    const bool kx = c->non_matte;   // Mirror / smooth Glass / OrenNayar: the kX instantiations
     for (int64_t r0 = 0; r0 < nrec; r0 += chunk) {
         const int64_t nr = std::min(chunk, nrec - r0);
         if (per > 0) {
             HIPCHK(c, hipMemsetAsync(qs.cnt, 0, (size_t)ncnt * 4, c->stream));
             if (nl > 0)
-                hipLaunchKernelGGL(k_pw_cache, dim3((unsigned)((nr * nl + kWave - 1) / kWave)), dim3(kWave), 0,
+                hipLaunchKernelGGL(kx ? k_pw_cache<true> : k_pw_cache<false>,
+                                   dim3((unsigned)((nr * nl + kWave - 1) / kWave)), dim3(kWave), 0,
                                    c->stream, sc, c->wb, r0, nr, ldc, ldp);
-            auto start = mb ? k_pw_start<true> : k_pw_start<false>;
+            auto start = kx ? (mb ? k_pw_start<true, true> : k_pw_start<false, true>)
+                            : (mb ? k_pw_start<true> : k_pw_start<false>);
             hipLaunchKernelGGL(start, dim3((unsigned)((nr * per + kWave - 1) / kWave)), dim3(kWave), 0, c->stream,
                                sc, rp, c->wb, sb, r0, nr, ldc, ldp, paths, qs, pkey);
             for (int pass = 0; pass + 1 < rp.max_depth; pass++) {
@@ -2642,7 +2664,8 @@ int paths_wavefront(pbrt_gpu_ctx* c, const DevScene& sc, int64_t sb, int64_t nb)
                     hipLaunchKernelGGL(k_pw_scan, dim3(1), dim3(1), 0, c->stream, qs, n_keys);
                     hipLaunchKernelGGL(k_pw_scatter, dim3(G / 4), dim3(256), 0, c->stream, paths, qs);
                 }
-                hipLaunchKernelGGL(k_pw_shade, dim3(G), dim3(kWave), 0, c->stream, sc, rp, c->wb, sb, paths, qs,
+                hipLaunchKernelGGL(kx ? k_pw_shade<true> : k_pw_shade<false>, dim3(G), dim3(kWave), 0, c->stream, sc,
+                                   rp, c->wb, sb, paths, qs,
                                    sort && n_keys > 1 ? 1 : 0, pkey);
                 hipLaunchKernelGGL(k_pw_shadow, dim3(G), dim3(kWave), 0, c->stream, sc, rp, c->wb, paths, qs, pkey);
             }

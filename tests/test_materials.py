@@ -434,18 +434,43 @@ def mesh_material_scene(material, w=40, h=32):
 @pytest.mark.gpu
 @pytest.mark.parametrize("material", ["glass", "mirror", "oren"])
 @pytest.mark.parametrize("mode", [abi.PBRT_MODE_EXACT, abi.PBRT_MODE_THROUGHPUT])
-def test_device_mesh_with_specular_material_vs_oracle(material, mode):
-    """A triangle mesh of Glass / Mirror / OrenNayar: mesh scenes with such a
-    material render on the serial kernel (the kX wave pipeline takes analytic
-    scenes only), bit-exact against the oracle, which resolves the mesh's
-    material the same way (oracle_render.c)."""
+def test_device_mesh_with_specular_material_vs_oracle(monkeypatch, material, mode):
+    """A triangle mesh of Glass / Mirror / OrenNayar: the kX chain and the kX
+    path wavefront (k_pw_*, the path stage of mesh scenes), unsorted and
+    material-sorted, and the serial kernel, all bit-exact against the oracle,
+    which resolves the mesh's material the same way (oracle_render.c)."""
     sc = mesh_material_scene(material)
     rd = abi.render_desc(3, 3, max_depth=6, mode=mode)
     rc, of, _ = O.render(sc.desc, rd, threads=8)
     assert rc == 0 and np.isfinite(of).all()
-    with G.Renderer(sc) as r:
+    for sort in ("0", "1"):
+        monkeypatch.setenv("PBRT_PW_SORT", sort)
+        with G.Renderer(sc) as r:
+            film, st = r.render(rd)
+        assert st.kernel == path_kernel(4, mode)
+        assert np.array_equal(bits(film), bits(of))
+    with G.Renderer(sc, kernel="serial") as r:
         film, st = r.render(rd)
     assert st.kernel == abi.PBRT_KERNEL_SERIAL
+    assert np.array_equal(bits(film), bits(of))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [abi.PBRT_MODE_EXACT, abi.PBRT_MODE_THROUGHPUT])
+@pytest.mark.parametrize("sort", ["0", "1"])
+def test_device_glass_scene_on_the_path_wavefront(monkeypatch, mode, sort):
+    """The README + glass + mirror scene with the path stage forced onto the kX
+    path wavefront (PBRT_PATHS_WF=1), unsorted and sorted by material between
+    trace and shade: bit-exact against the oracle."""
+    monkeypatch.setenv("PBRT_PATHS_WF", "1")
+    monkeypatch.setenv("PBRT_PW_SORT", sort)
+    sc = readme_glass_scene(mirror=True)
+    rd = abi.render_desc(3, 3, mode=mode)
+    rc, of, _ = O.render(sc.desc, rd, threads=8)
+    assert rc == 0
+    with G.Renderer(sc) as r:
+        film, st = r.render(rd)
+    assert st.kernel == path_kernel(4, mode)
     assert np.array_equal(bits(film), bits(of))
 
 
