@@ -312,6 +312,7 @@ struct ChainLayout {   // byte offsets into the chain / setup kernels' dynamic L
     int s1d, other, sbuf, dbuf, vbuf, total;
     int ring;      // k_chain_ci: offset ring after the StartPixel staging (no sbuf / dbuf)
     int staging;   // k_chain_ci: bytes of the StartPixel staging (s1d, other, vbuf)
+    int pcs;       // k_chain_ci: the lane groups' bounce-1 ChainCache records (ci_layout)
 };
 #ifndef PBRT_CI_RING_KB
 #define PBRT_CI_RING_KB 4
@@ -1592,7 +1593,7 @@ struct CiGroup {
 // kDepth: traversal stack entries per lane. Trees of <= kLdsNodes (64) nodes
 // are staged in LDS and walk their leaves only (no stack); larger trees walk
 // with the reference's [64] stack (bvh.go:670).
-template <int kW, int kDepth = 32, bool kX = false>
+template <int kW, int kDepth = 0, bool kX = false>
 __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT_CI_EU_WAVES, 8))) void k_chain_ci(
     DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
     int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr,
@@ -1601,8 +1602,8 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
     const uint64_t t_begin = wall_clock64();
     const uint32_t cs = cstride == 1 ? 1u : 2u;   // candidate offsets head + cs * j
     constexpr int kT = kWave * kW;   // threads per workgroup (stack stride)
-    __shared__ uint16_t stack_lds[kDepth * kT];
-    __shared__ ChainCache pcs[kCiMaxGroups];
+    // kDepth 0: an LDS-staged tree, walked without a stack (no stack array)
+    __shared__ uint16_t stack_lds[kDepth > 0 ? kDepth * kT : 1];
     __shared__ CiGroup gs[kCiMaxGroups];
     __shared__ uint64_t sh_state;
     __shared__ int wcnt[kW];
@@ -1624,6 +1625,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
     uint16_t* other = (uint16_t*)(lds + lay.other);
     uint32_t* vbuf = (uint32_t*)(lds + lay.vbuf);
     RingEnt* ring = (RingEnt*)(lds + lay.ring) + (size_t)g * R;
+    ChainCache* pcs = (ChainCache*)(lds + lay.pcs);
     uint16_t* stack = stack_lds + tid;
     const int n = rp.spp, ndims = rp.ndims;
     const pbrt_camera_desc& cam = *sc.camera;
@@ -2509,6 +2511,9 @@ ChainLayout ci_layout(const ChainLayout& base, int w, int G, unsigned& lds_bytes
     } else {
         lds_bytes = (unsigned)(base.total + (w - 1) * kCiRingBytes);
     }
+    // then one ChainCache per lane group (only the groups in use: G, not kCiMaxGroups)
+    l.pcs = (int)((lds_bytes + 15u) & ~15u);
+    lds_bytes = (unsigned)l.pcs + (unsigned)(G * sizeof(ChainCache));
     l.total = (int)lds_bytes;
     return l;
 }
@@ -3049,7 +3054,7 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                             unsigned lds = 0;
                             const ChainLayout lw = ci_layout(c->lay_ci, w, 1, lds);
                             // kX: LDS-staged trees only, at most 4 waves per tile (wave_eligible, ci_waves)
-                            auto kern = kx ? (w == 2 ? k_chain_ci<2, 32, true> : k_chain_ci<4, 32, true>)
+                            auto kern = kx ? (w == 2 ? k_chain_ci<2, 0, true> : k_chain_ci<4, 0, true>)
                                            : (w == 2   ? (lds_nodes ? k_chain_ci<2> : k_chain_ci<2, 64>)
                                               : w == 4 ? (lds_nodes ? k_chain_ci<4> : k_chain_ci<4, 64>)
                                                        : (lds_nodes ? k_chain_ci<8> : k_chain_ci<8, 64>));
@@ -3061,7 +3066,7 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                             const int ring = kCiRingBytes / (int)sizeof(RingEnt) / Gc;
                             unsigned lds = 0;
                             const ChainLayout lw = ci_layout(c->lay_ci, 1, Gc, lds);
-                            auto kern1 = kx ? k_chain_ci<1, 32, true> : (lds_nodes ? k_chain_ci<1> : k_chain_ci<1, 64>);
+                            auto kern1 = kx ? k_chain_ci<1, 0, true> : (lds_nodes ? k_chain_ci<1> : k_chain_ci<1, 64>);
                             hipLaunchKernelGGL(kern1, dim3((unsigned)((n + Gc - 1) / Gc)), dim3(kWave),
                                                lds, st, with_slot(sc, 2), rp, lw, c->d_jump, c->wb, sb,
                                                nb, kWave / Gc, ring, c->d_ctr, Gc == 1 ? ord : nullptr,
