@@ -21,6 +21,26 @@ def demangle_short(sym):
     return name
 
 
+_cache = {}
+
+
+def resolve(txt, name):
+    """Value of `.set name, expr`, where expr may be max(...) over numbers and
+    other symbols (kernels that call out-of-line device functions)."""
+    if name in _cache:
+        return _cache[name]
+    m = re.search(r"^\s+\.set " + re.escape(name) + r", (.+)$", txt, re.M)
+    val = 0
+    if m:
+        expr = m.group(1)
+        nums = [int(x) for x in re.findall(r"(?<![\w.])(\d+)(?![\w.])", expr)]
+        refs = re.findall(r"([A-Za-z_.$][\w.$]*\.(?:num_vgpr|num_agpr|numbered_sgpr))", expr)
+        vals = nums + [resolve(txt, r) for r in refs if r != name]
+        val = max(vals) if vals else 0
+    _cache[name] = val
+    return val
+
+
 def main():
     path = sys.argv[1]
     filt = sys.argv[2:]
@@ -34,12 +54,11 @@ def main():
         def field(k):
             f = re.search(r"\.amdhsa_" + k + r"\s+(\S+)", body)
             return f.group(1) if f else None
-        sets = dict(re.findall(re.escape(sym) + r"\.(\w+), (\S+)", txt))
-        vg = int(sets.get("num_vgpr", 0))
-        ag = int(sets.get("num_agpr", 0))
+        vg = resolve(txt, sym + ".num_vgpr")
+        ag = resolve(txt, sym + ".num_agpr")
         total = ((vg + 7) // 8) * 8 + ((ag + 7) // 8) * 8 if ag else vg
         out[name] = {
-            "arch_vgpr": vg, "acc_vgpr": ag, "sgpr": int(sets.get("numbered_sgpr", 0)),
+            "arch_vgpr": vg, "acc_vgpr": ag, "sgpr": resolve(txt, sym + ".numbered_sgpr"),
             "scratch_bytes_per_lane": int(field("private_segment_fixed_size") or 0),
             "lds_static_bytes": int(field("group_segment_fixed_size") or 0),
             "waves_per_simd_by_registers": min(8, 512 // max(total, 1)) if total else 8,
