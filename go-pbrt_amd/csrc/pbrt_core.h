@@ -204,12 +204,24 @@ GO_HD EF ef_mul(EF a, EF b, int& panic) {
 }
 // MulScalar(s) = Mul(New(s, 0)) (efloat.go:86-88)
 GO_HD EF ef_muls(EF a, double s, int& panic) { return ef_mul(a, ef_new(s, 0.0, panic), panic); }
+// efloat.go Div. When b's interval excludes 0 the extreme quotients are known
+// from the signs alone: correctly rounded division is monotone in each operand,
+// so min/max over the four rounded quotients are the rounded quotients of the
+// analytic extremes (ties and the sign of a zero vanish in NextFloatDown/Up).
+// Two divisions instead of four; an interval with a zero end keeps the
+// four-quotient form (its Inf/NaN reaches Check as in Go).
 GO_HD EF ef_div(EF a, EF b, int& panic) {
     EF r;
     r.v = a.v / b.v;
     if (b.lo < 0 && b.hi > 0) {
         r.lo = -kInf;
         r.hi = kInf;
+    } else if (b.lo > 0) {
+        r.lo = gomath::next_down(a.lo / (a.lo >= 0 ? b.hi : b.lo));
+        r.hi = gomath::next_up(a.hi / (a.hi >= 0 ? b.lo : b.hi));
+    } else if (b.hi < 0) {
+        r.lo = gomath::next_down(a.hi / (a.hi >= 0 ? b.hi : b.lo));
+        r.hi = gomath::next_up(a.lo / (a.lo >= 0 ? b.lo : b.hi));
     } else {
         double d0 = a.lo / b.lo, d1 = a.hi / b.lo, d2 = a.lo / b.hi, d3 = a.hi / b.hi;
         r.lo = gomath::next_down(gomath::min(gomath::min(d0, d1), gomath::min(d2, d3)));
