@@ -3115,7 +3115,7 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                     // the path wavefront: mesh scenes, and whatever k_paths_ci cannot
                     // take (a tree beyond LDS, more than 64 / P lights)
                     if (rp.mode == PBRT_MODE_THROUGHPUT)
-                        hipLaunchKernelGGL(k_mb_setup<false>, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
+                        hipLaunchKernelGGL(kx ? k_mb_setup<true> : k_mb_setup<false>, dim3((unsigned)(nb * c->wb.ppt)), dim3(kWave),
                                            (unsigned)c->lay.total, c->stream, with_slot(sc, 4), rp, c->lay, c->d_jump,
                                            c->wb, sb, nb);
                     const int rcp = paths_wavefront(c, with_slot(sc, rp.mode == PBRT_MODE_THROUGHPUT ? 5 : 3), sb, nb);
