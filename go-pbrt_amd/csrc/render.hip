@@ -2009,6 +2009,7 @@ struct Knobs {
     bool pw_sort = false;      // PBRT_PW_SORT=1
     double pw_gb = 24.0;       // PBRT_PW_GB
     double wave_buffer_gb = 0; // PBRT_WAVE_BUFFER_GB (0: min(96 GB, half the free HBM))
+    int64_t ci_exclusive = 0;  // PBRT_CI_EXCLUSIVE = K: a shard's K heaviest tiles get a CU each (LDS pad)
     int cull_group = 4;        // PBRT_CULL_GROUP: leaves per culling group
     int cull_min = 2;          // PBRT_CULL_MIN
     bool cull_groups = true;   // PBRT_CULL_GROUPS=0
@@ -2026,6 +2027,7 @@ struct Knobs {
         if (const char* e = getenv("PBRT_CI_HEAVY_WAVES")) k.ci_heavy_waves = atoi(e) == 8 ? 8 : 4;
         if (const char* e = getenv("PBRT_CI_HEAVY")) k.ci_heavy = (int64_t)atoll(e);
         if (const char* e = getenv("PBRT_CI_SPLIT")) k.ci_split = atoi(e) != 0;
+        if (const char* e = getenv("PBRT_CI_EXCLUSIVE")) k.ci_exclusive = std::max<int64_t>(0, (int64_t)atoll(e));
         if (const char* e = getenv("PBRT_CI_ORDER")) k.ci_order = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_PROBE")) k.ci_probe = atoi(e) != 0;
         if (const char* e = getenv("PBRT_PATHS_S1D")) k.paths_s1d_lds = std::strcmp(e, "lds") == 0;
@@ -2079,6 +2081,7 @@ struct pbrt_gpu_ctx {
     std::vector<hipEvent_t> bev;       // per batch: before the chain, after the chain, after the paths
     int n_batches = 0;
     int n_simd = 1024;                 // SIMDs of the device (4 per CU)
+    size_t lds_per_block = 65536;      // the device's LDS limit per workgroup (sharedMemPerBlock)
     WaveBufs wb{};
     bool use_ci = false;   // the Path chain stage (k_chain_ci)
     bool use_dl = false;   // DirectLighting on k_dl_setup / k_dl_samples
@@ -2866,8 +2869,10 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
     }
     {
         hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)
+        if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0) {
             c->n_simd = 4 * prop.multiProcessorCount;
+            c->lds_per_block = prop.sharedMemPerBlock;
+        }
     }
     std::vector<uint32_t> order;
     if (!dev_order(scene, order)) {
@@ -3048,11 +3053,18 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                         c->ticks_n = nb;
                     }
                     // one launch of n workgroups, workgroup b on slot ord[b] (identity if null)
-                    auto launch_ci = [&](int w, int64_t n, const uint32_t* ord, hipStream_t st) {
+                    // excl: pad the dynamic LDS so that no other chain workgroup fits
+                    // beside one of these on a CU (a heavy tile's waves issue alone)
+                    auto launch_ci = [&](int w, int64_t n, const uint32_t* ord, hipStream_t st, bool excl = false) {
                         if (w > 1) {   // one tile per workgroup of w waves; the ring grows with the lanes
                             const int ring = w * kCiRingBytes / (int)sizeof(RingEnt);
                             unsigned lds = 0;
                             const ChainLayout lw = ci_layout(c->lay_ci, w, 1, lds);
+                            if (excl) {
+                                // half the CU's LDS (160 KB on gfx950) plus a bit, within the per-workgroup limit
+                                const size_t want = 84 * 1024;
+                                if (c->lds_per_block >= want + 16 * 1024) lds = std::max<unsigned>(lds, (unsigned)want);
+                            }
                             // kX: LDS-staged trees only, at most 4 waves per tile (wave_eligible, ci_waves)
                             auto kern = kx ? (w == 2 ? k_chain_ci<2, 0, true> : k_chain_ci<4, 0, true>)
                                            : (w == 2   ? (lds_nodes ? k_chain_ci<2> : k_chain_ci<2, 64>)
@@ -3082,6 +3094,12 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                     // (1020 tiles: 294 -> 307 ms), so smaller launches never split
                     int64_t heavy = (learned && kw > 1 && G == 1 && nb > c->n_simd && ci_split_enabled(c))
                                         ? std::min<int64_t>(c->heavy_k, nb) : 0;
+                    // PBRT_CI_EXCLUSIVE = K (experiment): the K heaviest tiles of a shard run first with
+                    // a CU each; the rest at kw waves beside them on the second stream
+                    int64_t excl = (learned && kw > 1 && G == 1 && c->knobs.ci_exclusive > 0)
+                                       ? std::min<int64_t>({c->knobs.ci_exclusive, nb - 1, (int64_t)c->n_simd / 8})
+                                       : 0;
+                    if (excl > 0) heavy = 0;
                     if (ci_heavy_override(c) >= 0 && learned && G == 1)   // tests and experiments force the split
                         heavy = std::min<int64_t>(ci_heavy_override(c), nb);
                     if (heavy >= nb) heavy = 0;   // nothing left for the light launch: one launch at kw
@@ -3090,7 +3108,14 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
                         c->h_slot_kw.assign((size_t)nb, (uint8_t)(heavy > 0 ? 1 : kw));
                         for (int64_t i = 0; i < heavy; i++) c->h_slot_kw[c->h_slot_order[(size_t)i]] = (uint8_t)ci_heavy_waves(c);
                     }
-                    if (heavy > 0) {
+                    if (excl > 0) {
+                        HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
+                        launch_ci(kw, excl, order, c->stream, true);
+                        HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
+                        launch_ci(kw, nb - excl, order + excl, c->stream2);
+                        HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
+                        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+                    } else if (heavy > 0) {
                         HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
                         launch_ci(ci_heavy_waves(c), heavy, order, c->stream);
                         HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
