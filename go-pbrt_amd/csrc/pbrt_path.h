@@ -68,6 +68,7 @@ struct DevScene {
     // before every render); polled between units of work
     const int* cancel;
     int* cancel_seen;
+    int dense_ok;   // k_chain_ci may use bvh_walk_dense (one primitive per leaf, groups, no meshes)
 };
 // Is the render cancelled? The device copy is an L2 read; poll_host (a rate
 // the caller bounds: host-memory reads cross PCIe) also reads the host flag and
@@ -777,6 +778,249 @@ __device__ inline bool bvh_traverse(const DevScene& sc, Ray& ray, SI* si, uint16
     if (!kAny && best >= 0) prim_si(sc, best, ray, best_ph, *si);
     STEP_T(if (!kAny) tt.mark(7);)
     return hit;
+}
+
+// ------------------------------------------- dense closest hit (k_chain_ci)
+// The closest-hit walk of an LDS-staged tree with culling groups and one
+// primitive per leaf, for a whole wave at once. The per-lane walk
+// (bvh_walk_analytic) runs a wave's leaf tests one per lane per iteration, so
+// a wave pays for its lane with the most candidate leaves (the leaf tests are
+// 89% of a closest-hit traversal, profiles/r03/phase_steptime_B.txt). Here:
+//  1. each lane finds its candidate leaves: the culling groups' members whose
+//     own box it enters with its initial TMax (a superset of what it will test);
+//  2. the wave computes every (lane, candidate) primitive test, 64 pairs per
+//     round, lane-dense: the part of Sphere/Disk.Intersect that does not read
+//     TMax (EFloat quadratic, clipping of both roots, its panics);
+//  3. each lane replays its own candidates in its octant's leaf preorder: the
+//     leaf box with the current TMax (as the reference tests it), then the
+//     TMax comparisons of Intersect (sphere.go:103-131, disk.go:72-95).
+// Every test the reference runs is decided by the same values and comparisons
+// in the same order; tests it never runs (a box that fails at the current TMax)
+// only had their TMax-free part computed, and their panics are ignored. The
+// result (best, TMax, hit point) is the per-lane walk's.
+struct DensePair {
+    double a, b, c, d, e, f;   // sphere: t0 lo/v/hi, t1 lo/v/hi; disk: a = t
+    uint32_t flags;            // kDp*
+    int32_t panic;
+};
+constexpr uint32_t kDpMiss = 1, kDpClip0 = 2, kDpClip1 = 4, kDpDisk = 8;
+constexpr int kDenseScratch = 64 * (int)sizeof(DensePair) + 2 * 64 * 4;   // LDS bytes per wave
+__device__ __forceinline__ void dense_wave_sync() {   // the wave's LDS writes are visible to the wave
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+// the k-th set bit of m (k < popcount(m))
+__device__ __forceinline__ int nth_bit(uint32_t m, int k) {
+    for (int i = 0; i < k; i++) m &= m - 1;
+    return __builtin_ctz(m);
+}
+__device__ __forceinline__ bool sphere_clipped(const pbrt_shape_desc& s, V3 ph) {
+    return (s.z_min > -s.radius && ph.z < s.z_min) || (s.z_max < s.radius && ph.z > s.z_max) ||
+           phi_beyond(ph.y, ph.x, s.phi_max);
+}
+__device__ __forceinline__ V3 sphere_point(const pbrt_shape_desc& s, const Ray& ray, double t) {   // sphere.go:111-114
+    V3 ph = ray.o + muls(ray.d, t);
+    ph = muls(ph, s.radius / dist(ph, V3{0, 0, 0}));
+    if (ph.x == 0.0 && ph.y == 0.0) ph.x = 1e-5 * s.radius;
+    return ph;
+}
+// the TMax-free part of prim pi's test against world ray r
+__device__ inline void dense_pair(const DevScene& sc, int pi, const Ray& r, DensePair& o) {
+    const DevPrim& p = sc.fprims[pi];
+    Ray ray = r;
+    if (p.kind == PBRT_PRIM_TRANSFORMED) ray = xf_ray(p.prim_to_world.m_inv, r, nullptr, nullptr);
+    const pbrt_shape_desc& s = p.shape;
+    V3 oerr, derr;
+    const Ray ro = xf_ray(s.object_to_world.m_inv, ray, &oerr, &derr);
+    o.flags = 0;
+    o.panic = 0;
+    o.a = o.b = o.c = o.d = o.e = o.f = 0;
+    if (s.type != PBRT_SHAPE_SPHERE) {   // disk.go:72-95 without the TMax test
+        o.flags = kDpDisk;
+        if (ro.d.z == 0) {
+            o.flags |= kDpMiss;
+            return;
+        }
+        const double ts = (s.height - ro.o.z) / ro.d.z;
+        o.a = ts;
+        const V3 ph = ro.o + muls(ro.d, ts);
+        const double d2 = ph.x * ph.x + ph.y * ph.y;
+        if (d2 > s.radius * s.radius || d2 < s.inner_radius * s.inner_radius || phi_beyond(ph.y, ph.x, s.phi_max))
+            o.flags |= kDpMiss;
+        return;
+    }
+    // sphere_hit up to its first TMax comparison
+    {
+        const double av = (ro.d.x * ro.d.x + ro.d.y * ro.d.y) + ro.d.z * ro.d.z;
+        const double bv = ((ro.d.x * ro.o.x + ro.d.y * ro.o.y) + ro.d.z * ro.o.z) * 2.0;
+        const double cv = ((ro.o.x * ro.o.x + ro.o.y * ro.o.y) + ro.o.z * ro.o.z) - s.radius * s.radius;
+        const double disc = bv * bv - 4. * av * cv;
+        const double big = 1e100;
+        const bool moderate =
+            gomath::abs(ro.o.x) < big && gomath::abs(ro.o.y) < big && gomath::abs(ro.o.z) < big &&
+            gomath::abs(ro.d.x) < big && gomath::abs(ro.d.y) < big && gomath::abs(ro.d.z) < big &&
+            gomath::abs(oerr.x) < big && gomath::abs(oerr.y) < big && gomath::abs(oerr.z) < big &&
+            gomath::abs(derr.x) < big && gomath::abs(derr.y) < big && gomath::abs(derr.z) < big &&
+            gomath::abs(s.radius) < big;
+#ifndef PBRT_NO_EARLY_MISS
+        if (disc < 0 && moderate) {
+            o.flags = kDpMiss;
+            return;
+        }
+#endif
+    }
+    int panic = 0;
+    EF ox = ef_new(ro.o.x, oerr.x, panic), oy = ef_new(ro.o.y, oerr.y, panic), oz = ef_new(ro.o.z, oerr.z, panic);
+    EF dx = ef_new(ro.d.x, derr.x, panic), dy = ef_new(ro.d.y, derr.y, panic), dz = ef_new(ro.d.z, derr.z, panic);
+    EF a = ef_add(ef_add(ef_mul(dx, dx, panic), ef_mul(dy, dy, panic), panic), ef_mul(dz, dz, panic), panic);
+    EF b = ef_muls(ef_add(ef_add(ef_mul(dx, ox, panic), ef_mul(dy, oy, panic), panic), ef_mul(dz, oz, panic), panic),
+                   2.0, panic);
+    EF c0 = ef_add(ef_add(ef_mul(ox, ox, panic), ef_mul(oy, oy, panic), panic), ef_mul(oz, oz, panic), panic);
+    EF c = ef_sub(c0, ef_muls(ef_new(s.radius, 0, panic), s.radius, panic), panic);
+    EF t0, t1;
+    const bool q = ef_quadratic(a, b, c, t0, t1, panic);
+    o.panic = panic;
+    if (panic) return;
+    if (!q) {
+        o.flags = kDpMiss;
+        return;
+    }
+    o.a = t0.lo; o.b = t0.v; o.c = t0.hi;
+    o.d = t1.lo; o.e = t1.v; o.f = t1.hi;
+    if (s.z_min > -s.radius || s.z_max < s.radius || s.phi_max < 2 * gomath::kPi) {   // a partial sphere
+        if (sphere_clipped(s, sphere_point(s, ro, t0.v))) o.flags |= kDpClip0;
+        if (sphere_clipped(s, sphere_point(s, ro, t1.v))) o.flags |= kDpClip1;
+    }
+}
+// sphere.go:103-131 / disk.go:72-74 given the TMax-free part: hit and its t
+__device__ __forceinline__ bool dense_accept(const DensePair& r, double tmax, double& t) {
+    if (r.flags & kDpMiss) return false;
+    if (r.flags & kDpDisk) {
+        if (r.a <= 0 || r.a >= tmax) return false;
+        t = r.a;
+        return true;
+    }
+    if (r.c > tmax || r.d <= 0) return false;   // t0.hi > tMax || t1.lo <= 0
+    bool used_t1 = false;
+    double lo = r.a, hi = r.c, v = r.b;
+    if (lo <= 0) {
+        used_t1 = true;
+        lo = r.d; v = r.e; hi = r.f;
+        if (hi > tmax) return false;
+    }
+    if (used_t1 ? (r.flags & kDpClip1) : (r.flags & kDpClip0)) {
+        if (used_t1) return false;
+        if (r.f > tmax) return false;
+        if (r.flags & kDpClip1) return false;
+        v = r.e;
+    }
+    (void)lo;
+    t = v;
+    return true;
+}
+// the object-space hit point of prim pi at t (what sphere_hit / disk_hit leave in ph)
+__device__ inline V3 dense_hit_point(const DevScene& sc, int pi, const Ray& r, double t) {
+    const DevPrim& p = sc.fprims[pi];
+    Ray ray = r;
+    if (p.kind == PBRT_PRIM_TRANSFORMED) ray = xf_ray(p.prim_to_world.m_inv, r, nullptr, nullptr);
+    const Ray ro = xf_ray(p.shape.object_to_world.m_inv, ray, nullptr, nullptr);
+    if (p.shape.type == PBRT_SHAPE_SPHERE) return sphere_point(p.shape, ro, t);
+    return ro.o + muls(ro.d, t);
+}
+// Whole-wave closest hit (see above). Every lane of the wave calls it (active:
+// the lane has a ray); scratch: kDenseScratch bytes of LDS for this wave.
+// Preconditions (uniform, checked by the caller): LDS-staged nodes, culling
+// groups, one primitive per leaf, no triangle meshes.
+__device__ inline bool bvh_walk_dense(const DevScene& sc, Ray& ray, bool active, int& panic, int& best, V3& best_ph,
+                                      unsigned char* scratch) {
+    DensePair* res = (DensePair*)scratch;
+    int* incl = (int*)(scratch + 64 * sizeof(DensePair));
+    uint32_t* masks = (uint32_t*)(incl + 64);
+    const int lane = threadIdx.x & 63;
+    best = -1;
+    const V3 inv{1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z};
+    const int nx = inv.x < 0, ny = inv.y < 0, nz = inv.z < 0;
+    const int oct = nx | (ny << 1) | (nz << 2);
+    const uint16_t* leaves = g_leaf_lds + oct * kLdsNodes;
+    const int ng = sc.n_groups;
+    uint32_t m = 0;
+    if (active) {
+        const uint32_t* gm = g_gmask_lds + oct * (kMaxCullGroups + 1);
+        uint32_t cand = gm[ng];
+        for (int g = 0; g < ng; g++) {
+            NodeView gv;
+#pragma unroll
+            for (int k = 0; k < 6; k++) gv.b[k] = g_grp_lds[g * 6 + k];
+            if (node_hit(gv, ray, inv, nx, ny, nz)) cand |= gm[g];
+        }
+        while (cand) {   // each candidate leaf's own box with the initial TMax
+            const int j = __builtin_ctz(cand);
+            cand &= cand - 1;
+            if (node_hit(load_node(sc, leaves[j]), ray, inv, nx, ny, nz)) m |= 1u << j;
+        }
+    }
+    const int n = __builtin_popcount(m);
+    int S = n;   // inclusive prefix sum of the lanes' pair counts
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(S, o);
+        if (lane >= o) S += v;
+    }
+    const int T = __shfl(S, 63);
+    const int S0 = S - n;
+    incl[lane] = S;
+    masks[lane] = m;
+    dense_wave_sync();
+    double tmax = ray.tmax;
+    bool live = active;
+    uint32_t rem = m;   // my candidates not replayed yet (positions in my leaf preorder)
+    for (int base = 0; base < T; base += 64) {
+        // 2. pair base + lane: its owner lane (the first whose inclusive sum exceeds it)
+        const int p = base + lane;
+        int own = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1)   // own = #{l : incl[l] <= p} (incl is non-decreasing)
+            if (incl[own + step - 1] <= p) own += step;
+        const int ownc = own > 63 ? 63 : own;
+        Ray r;
+        r.o.x = __shfl(ray.o.x, ownc); r.o.y = __shfl(ray.o.y, ownc); r.o.z = __shfl(ray.o.z, ownc);
+        r.d.x = __shfl(ray.d.x, ownc); r.d.y = __shfl(ray.d.y, ownc); r.d.z = __shfl(ray.d.z, ownc);
+        r.tmax = kInf;
+        r.time = 0;
+        const int ooct = __shfl(oct, ownc);
+        if (p < T) {
+            const int k = p - (incl[ownc] - __builtin_popcount(masks[ownc]));
+            const int j = nth_bit(masks[ownc], k);
+            const int pi = (int)load_node(sc, g_leaf_lds[ooct * kLdsNodes + j]).offset;
+            dense_pair(sc, pi, r, res[lane]);
+        }
+        dense_wave_sync();
+        // 3. my pairs of this round, in my leaf preorder
+        const int lo = S0 > base ? S0 : base, hi = S < base + 64 ? S : base + 64;
+        for (int q = lo; live && q < hi; q++) {
+            const int j = __builtin_ctz(rem);
+            rem &= rem - 1;
+            const NodeView nv = load_node(sc, leaves[j]);
+            Ray rt = ray;
+            rt.tmax = tmax;
+            if (!node_hit(nv, rt, inv, nx, ny, nz)) continue;   // the reference does not test this leaf
+            const DensePair& rr = res[q - base];
+            if (rr.panic) {
+                panic = rr.panic;
+                live = false;
+                break;
+            }
+            double t;
+            if (dense_accept(rr, tmax, t)) {
+                tmax = t;
+                best = (int)nv.offset;
+            }
+        }
+        dense_wave_sync();   // res is rewritten by the next round
+    }
+    ray.tmax = tmax;
+    if (best >= 0) best_ph = dense_hit_point(sc, best, ray, tmax);
+    return best >= 0;
 }
 
 // ----------------------------------------------------------------- material

@@ -1604,6 +1604,8 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
     constexpr int kT = kWave * kW;   // threads per workgroup (stack stride)
     // kDepth 0: an LDS-staged tree, walked without a stack (no stack array)
     __shared__ uint16_t stack_lds[kDepth > 0 ? kDepth * kT : 1];
+    // bvh_walk_dense's per-wave scratch (LDS-staged trees only)
+    __shared__ __attribute__((aligned(16))) unsigned char dense_lds[kDepth > 0 ? 16 : kW * kDenseScratch];
     __shared__ CiGroup gs[kCiMaxGroups];
     __shared__ uint64_t sh_state;
     __shared__ int wcnt[kW];
@@ -1828,10 +1830,13 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
         }
         mark(1);
         // ---- (3) one bounce of every live trajectory
+        // the whole wave walks together (dense leaf tests) where the tree allows
+        const bool dense = kDepth == 0 && sc.dense_ok && sc.use_lds_nodes;
+        int panic = 0, best = -1;
+        V3 ph{0, 0, 0};
+        if (dense) bvh_walk_dense(sc, ray, tracing, panic, best, ph, dense_lds + (size_t)wv * kDenseScratch);
         if (tracing) {
-            int panic = 0, best;
-            V3 ph;
-            bvh_walk<false, kT, PBRT_CHAIN_LB>(sc, ray, stack, panic, best, ph);
+            if (!dense) bvh_walk<false, kT, PBRT_CHAIN_LB>(sc, ray, stack, panic, best, ph);
             mark(2);
             uint32_t d = kNoOff;
             if (panic) {
@@ -2010,6 +2015,7 @@ struct Knobs {
     double pw_gb = 24.0;       // PBRT_PW_GB
     double wave_buffer_gb = 0; // PBRT_WAVE_BUFFER_GB (0: min(96 GB, half the free HBM))
     int64_t ci_exclusive = 0;  // PBRT_CI_EXCLUSIVE = K: a shard's K heaviest tiles get a CU each (LDS pad)
+    bool ci_dense = true;      // PBRT_CI_DENSE=0: k_chain_ci's per-lane closest-hit walk instead of bvh_walk_dense
     int cull_group = 4;        // PBRT_CULL_GROUP: leaves per culling group
     int cull_min = 2;          // PBRT_CULL_MIN
     bool cull_groups = true;   // PBRT_CULL_GROUPS=0
@@ -2027,6 +2033,7 @@ struct Knobs {
         if (const char* e = getenv("PBRT_CI_HEAVY_WAVES")) k.ci_heavy_waves = atoi(e) == 8 ? 8 : 4;
         if (const char* e = getenv("PBRT_CI_HEAVY")) k.ci_heavy = (int64_t)atoll(e);
         if (const char* e = getenv("PBRT_CI_SPLIT")) k.ci_split = atoi(e) != 0;
+        if (const char* e = getenv("PBRT_CI_DENSE")) k.ci_dense = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_EXCLUSIVE")) k.ci_exclusive = std::max<int64_t>(0, (int64_t)atoll(e));
         if (const char* e = getenv("PBRT_CI_ORDER")) k.ci_order = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_PROBE")) k.ci_probe = atoi(e) != 0;
@@ -2204,6 +2211,9 @@ DevScene dev_scene(const pbrt_gpu_ctx* c, bool with_dist) {
     s.n_groups = c->n_groups;
     s.cancel = c->d_cancel;
     s.cancel_seen = c->d_cancel_seen;
+    // bvh_walk_dense: culling groups over a tree of one primitive per leaf, no meshes
+    s.dense_ok = c->knobs.ci_dense && s.n_groups > 0 && s.n_leaves == s.n_prims && s.mesh.n_nodes == 0 &&
+                 s.n_nodes <= kLdsNodes;
     return s;
 }
 
