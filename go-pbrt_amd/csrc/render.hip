@@ -2015,7 +2015,7 @@ struct Knobs {
     double pw_gb = 24.0;       // PBRT_PW_GB
     double wave_buffer_gb = 0; // PBRT_WAVE_BUFFER_GB (0: min(96 GB, half the free HBM))
     int64_t ci_exclusive = 0;  // PBRT_CI_EXCLUSIVE = K: a shard's K heaviest tiles get a CU each (LDS pad)
-    bool ci_dense = true;      // PBRT_CI_DENSE=0: k_chain_ci's per-lane closest-hit walk instead of bvh_walk_dense
+    bool ci_dense = false;     // PBRT_CI_DENSE=1: k_chain_ci's closest hit by bvh_walk_dense (bit-exact; slower on B)
     int cull_group = 4;        // PBRT_CULL_GROUP: leaves per culling group
     int cull_min = 2;          // PBRT_CULL_MIN
     bool cull_groups = true;   // PBRT_CULL_GROUPS=0
