@@ -29,11 +29,17 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=8)
     ap.add_argument("--threads", type=int, default=os.cpu_count())
-    ap.add_argument("--scene", default="readme", choices=["readme", "cornell"])
+    ap.add_argument("--scene", default="readme", choices=["readme", "cornell", "readme_glass"],
+                    help="readme_glass: bench.py config G (the README scene + server.go's glass sphere "
+                         "+ a mirror), built by the product's scene builder (scene data only)")
     ap.add_argument("--max-depth", type=int, default=10)
     ap.add_argument("--tile-stride", type=int, default=1)
     a = ap.parse_args()
-    sc = getattr(O.OracleScene, a.scene)(a.width, a.height)
+    if a.scene == "readme_glass":
+        import pbrtgpu as G
+        sc = G.Scene.readme_glass(a.width, a.height)
+    else:
+        sc = getattr(O.OracleScene, a.scene)(a.width, a.height)
     rd = abi.render_desc(a.spp, a.spp, max_depth=a.max_depth, tile_begin=0, tile_stride=a.tile_stride)
     t = time.time()
     rc, film, st = O.render(sc.desc, rd, threads=a.threads, flops=True)
