@@ -1604,8 +1604,10 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
     constexpr int kT = kWave * kW;   // threads per workgroup (stack stride)
     // kDepth 0: an LDS-staged tree, walked without a stack (no stack array)
     __shared__ uint16_t stack_lds[kDepth > 0 ? kDepth * kT : 1];
+#ifdef PBRT_CI_DENSE_WALK
     // bvh_walk_dense's per-wave scratch (LDS-staged trees only)
     __shared__ __attribute__((aligned(16))) unsigned char dense_lds[kDepth > 0 ? 16 : kW * kDenseScratch];
+#endif
     __shared__ CiGroup gs[kCiMaxGroups];
     __shared__ uint64_t sh_state;
     __shared__ int wcnt[kW];
@@ -1830,13 +1832,19 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
         }
         mark(1);
         // ---- (3) one bounce of every live trajectory
-        // the whole wave walks together (dense leaf tests) where the tree allows
+#ifdef PBRT_CI_DENSE_WALK   // experiment build: the whole wave walks together (dense leaf tests)
         const bool dense = kDepth == 0 && sc.dense_ok && sc.use_lds_nodes;
         int panic = 0, best = -1;
         V3 ph{0, 0, 0};
         if (dense) bvh_walk_dense(sc, ray, tracing, panic, best, ph, dense_lds + (size_t)wv * kDenseScratch);
         if (tracing) {
             if (!dense) bvh_walk<false, kT, PBRT_CHAIN_LB>(sc, ray, stack, panic, best, ph);
+#else
+        if (tracing) {
+            int panic = 0, best;
+            V3 ph;
+            bvh_walk<false, kT, PBRT_CHAIN_LB>(sc, ray, stack, panic, best, ph);
+#endif
             mark(2);
             uint32_t d = kNoOff;
             if (panic) {
@@ -2015,7 +2023,8 @@ struct Knobs {
     double pw_gb = 24.0;       // PBRT_PW_GB
     double wave_buffer_gb = 0; // PBRT_WAVE_BUFFER_GB (0: min(96 GB, half the free HBM))
     int64_t ci_exclusive = 0;  // PBRT_CI_EXCLUSIVE = K: a shard's K heaviest tiles get a CU each (LDS pad)
-    bool ci_dense = false;     // PBRT_CI_DENSE=1: k_chain_ci's closest hit by bvh_walk_dense (bit-exact; slower on B)
+    bool ci_dense = false;     // PBRT_CI_DENSE=1 (builds with -DPBRT_CI_DENSE_WALK): k_chain_ci's closest hit by
+                               // bvh_walk_dense (bit-exact; slower on B)
     int cull_group = 4;        // PBRT_CULL_GROUP: leaves per culling group
     int cull_min = 2;          // PBRT_CULL_MIN
     bool cull_groups = true;   // PBRT_CULL_GROUPS=0
