@@ -93,8 +93,10 @@ enum { PBRT_MAT_MATTE = 0, PBRT_MAT_MIRROR = 1, PBRT_MAT_GLASS = 2 };
  * smooth glass (both roughnesses 0) is one FresnelSpecular lobe; rough glass is
  * MicrofacetReflection + MicrofacetTransmission over TrowbridgeReitz(u, v)
  * (microfacet.go, reflection.go:670-835), whose sampling panics in the reference
- * (PBRT_PANIC_NIL_DEREF). The serial kernel renders scenes holding a Mirror or
- * Glass material. */
+ * (PBRT_PANIC_NIL_DEREF). Path renders of Mirror, smooth Glass and OrenNayar
+ * scenes run on the wave pipeline (its kX instantiations, LDS-sized trees);
+ * rough glass, DirectLighting through these materials and panic fidelity run
+ * on the serial kernel. */
 typedef struct pbrt_material_desc {
     int32_t kd_type;
     int32_t type;                  /* PBRT_MAT_* (0 = Matte)                  */
@@ -293,7 +295,8 @@ typedef struct pbrt_gpu_opts {
  *             (any render; the only one for n_dims < 3 Path renders,
  *             zero-pdf lights, filter radius >= 1.5 and PBRT_FLAG_PANIC_FIDELITY);
  *  WAVE_CI    the wave pipeline (Path integrator, n_dims >= 3, every light
- *             pdf > 0, filter radius < 1.5): per-pixel shared bounce 1, the
+ *             pdf > 0, filter radius < 1.5, no rough glass; Mirror / smooth
+ *             Glass / OrenNayar on trees of <= 64 nodes): per-pixel shared bounce 1, the
  *             tile's path offsets found by a continuous-issue chain of
  *             speculative trajectories + jump-ahead (k_chain_ci), then the
  *             samples as full paths (k_paths_ci, or the per-bounce path
