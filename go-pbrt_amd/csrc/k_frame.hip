@@ -1,0 +1,447 @@
+// k_frame.hip — bounce-1 records, DirectLighting, tile cost probe, film kernels, batch intersect
+#pragma clang fp contract(off)
+
+#include "render_common.h"
+
+namespace pbrtk {
+
+// One thread per tile-film pixel: the tile film of the serial replay.
+__global__ __launch_bounds__(256) void k_film(const pbrt_film_desc* __restrict__ film_desc, RenderParams rp,
+                                              WaveBufs wb, int64_t slot_base, int64_t nslots_batch,
+                                              double* __restrict__ films, const int* __restrict__ cancel_seen) {
+    // a cancelled render's samples are incomplete: its film is not valid (pbrt_gpu_cancel)
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(cancel_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+        return;
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per = rp.slot_w * rp.slot_h;
+    if (gid >= nslots_batch * per) return;
+    const int64_t bslot = gid / per, fi = gid % per;
+    const int64_t slot = slot_base + bslot;
+    const pbrt_film_desc& film = *film_desc;
+    int64_t x0, y0, x1, y1, px0, py0, px1, py1;
+    tile_bounds(rp, tile_of_slot(rp, slot), x0, y0, x1, y1);
+    film_tile_bounds(film, x0, y0, x1, y1, px0, py0, px1, py1);
+    const int64_t tw = px1 - px0;
+    if (fi >= tw * (py1 - py0)) return;
+    const int64_t fx = px0 + fi % tw, fy = py0 + fi / tw;
+    const int n = rp.spp;
+    const int64_t npx = wb.tile_npx[bslot];
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+    // pixels whose footprint can reach (fx, fy): |p - f| < radius + 1, in row-major order
+    for (int64_t py = fy - 2; py <= fy + 2; py++) {
+        if (py < y0 || py >= y1) continue;
+        for (int64_t px = fx - 2; px <= fx + 2; px++) {
+            if (px < x0 || px >= x1) continue;
+            const int64_t pi = (py - y0) * (x1 - x0) + (px - x0);
+            if (pi >= npx) continue;
+            Footprint fp;
+            int64_t p0x, p0y, p1x, p1y;
+            footprint(film, (double)px + 0.0, (double)py + 0.0, px0, py0, px1, py1, fp, p0x, p0y, p1x, p1y);
+            const int64_t want = fi;
+            int f = -1;
+            for (int q = 0; q < fp.n; q++)
+                if (fp.off[q] == want) f = q;
+            if (f < 0) continue;
+            const double w = fp.w[f];
+            const int64_t rec = bslot * wb.ppt + pi;
+            const int nv = wb.prec[rec].nvalid;
+            const double* Lp = wb.L + rec * n * 3;
+            for (int k = 1; k < nv; k++) {
+                Spec Ls{Lp[k * 3 + 0], Lp[k * 3 + 1], Lp[k * 3 + 2]};
+                if (has_nans(Ls)) Ls = spec(0.1);   // integrator.go:256-262
+                if (0.0 > film.max_sample_luminance) Ls = smuls(Ls, film.max_sample_luminance / 0.0);
+                a0 += Ls.r * w;
+                a1 += Ls.g * w;
+                a2 += Ls.b * w;
+            }
+        }
+    }
+    double* tf = films + slot * per * 3 + fi * 3;
+    tf[0] = a0;
+    tf[1] = a1;
+    tf[2] = a2;
+}
+
+// First panic of each tile slot in pixel order -> panics[slot].
+__global__ void k_panic_reduce(WaveBufs wb, int64_t slot_base, int64_t nslots_batch, PanicRec* __restrict__ panics,
+                               Counters* __restrict__ ctr) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nslots_batch) return;
+    const int npx = wb.tile_npx[b];
+    for (int p = 0; p < npx; p++) {
+        const PanicRec& r = wb.ppanic[b * wb.ppt + p];
+        if (r.kind) {
+            panics[slot_base + b] = r;
+            atomicExch(&ctr->any_panic, 1);
+            return;
+        }
+    }
+}
+
+// Bounce 1 of every pixel record of the batch: the camera ray through the
+// pixel corner (pFilm and pLens are (0,0) for every sample), its closest hit
+// and BSDF. The ray time is patched by the chain kernel once StartPixel gives it.
+// stats.rays_closest / rays_shadow of a batch: every valid sample's counts
+// (pixels with records, samples 1 .. nvalid-1), one atomic pair per wave
+__global__ __launch_bounds__(256) void k_ray_count(WaveBufs wb, int64_t nb, int n, Counters* __restrict__ ctr,
+                                                   const int* __restrict__ cancel_seen) {
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(cancel_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+        return;   // a cancelled render reports no counts
+    unsigned long long cl = 0, sh = 0;
+    const int64_t total = nb * wb.ppt * n;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t rec = i / n, k = i - rec * n, bs = rec / wb.ppt, pi = rec % wb.ppt;
+        if (k < 1 || pi >= wb.tile_npx[bs] || k >= wb.prec[rec].nvalid) continue;
+        const uint32_t v = wb.rays[i];
+        cl += v & 0xFFFFu;
+        sh += v >> 16;
+    }
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+        cl += __shfl_down(cl, off);
+        sh += __shfl_down(sh, off);
+    }
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+        atomicAdd(&ctr->closest_rays, cl);
+        atomicAdd(&ctr->shadow_rays, sh);
+    }
+}
+
+template <bool kX = false>
+__global__ __launch_bounds__(kWave) void k_wf_primary(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
+                                                      int64_t nb) {
+    __shared__ uint16_t stack_lds[64 * kStackStride];
+    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
+    stage_nodes(sc);
+    const int64_t rec = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (rec >= nb * wb.ppt) return;
+    const int64_t bs = rec / wb.ppt, pi = rec % wb.ppt;
+    int64_t x0, y0, x1, y1;
+    tile_bounds(rp, tile_of_slot(rp, slot_base + bs), x0, y0, x1, y1);
+    if (pi >= (x1 - x0) * (y1 - y0)) return;
+    const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
+    int panic0 = 0, hit0 = 0;
+    SI si0;
+    BSDF b0;
+    BSDFX bx0;
+    b0.n_bxdfs = 0;
+    bx0.kind = BXDF_KIND_LAMBERT;
+    bx0.n = 0;
+    Ray ray = camera_ray(*sc.camera, (double)px + 0.0, (double)py + 0.0, 0.0, V2{0.0, 0.0});
+    // Path.Li traces bounce 1 only below maxDepth (path.go:66); DirectLighting always
+    if (rp.spp > 1 && (1 < rp.max_depth || rp.integrator == PBRT_INTEGRATOR_DIRECT_LIGHTING)) {
+        hit0 = bvh_traverse<false>(sc, ray, &si0, stack_lds + threadIdx.x, panic0) ? 1 : 0;
+        if (!panic0 && hit0 && (kX ? compute_bsdf_x(sc, si0, b0, bx0) : compute_bsdf(sc, si0, b0)) < 0) panic0 = -1;
+    }
+    PixelRec& pr = wb.prec[rec];
+    pr.si = si0;
+    pr.b = b0;
+    if constexpr (kX) pr.x = bx0;
+    pr.wo = ray.d;
+    pr.hit = panic0 ? 0 : hit0;
+    pr.panic0 = panic0;
+    pr.nvalid = rp.spp;
+}
+
+// One wave per tile slot: the tile's pixels in order. Leaves each pixel's
+// stratified values in wb.s1d, the PCG32 state of each of its samples in
+// wb.memb (slot 0 of a pixel: its panic key, reset here), and the pixels
+// with records in wb.tile_npx (a camera-ray panic ends the tile, as in
+// k_chain_ci). THROUGHPUT mode: each pixel and sample on its own stream.
+__global__ __launch_bounds__(kWave) void k_dl_setup(DevScene sc, RenderParams rp, ChainLayout lay,
+                                                    const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
+                                                    int64_t nb) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ uint64_t sh_state;
+    const int64_t bs = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (bs >= nb || cancel_requested(sc, (bs & 63) == 0)) return;
+    const PcgJump& J = *jump;
+    const int64_t tile = tile_of_slot(rp, slot_base + bs);
+    int64_t x0, y0, x1, y1;
+    tile_bounds(rp, tile, x0, y0, x1, y1);
+    const int64_t npx = (x1 - x0) * (y1 - y0);
+    const uint64_t inc = pcg_inc_of((uint64_t)tile);
+    const bool mb = rp.mode == PBRT_MODE_THROUGHPUT;
+    const int n = rp.spp;
+    double* s1d = lay.s1d >= 0 ? (double*)(lds + lay.s1d) : nullptr;
+    uint16_t* other = (uint16_t*)(lds + lay.other);
+    uint32_t* vbuf = (uint32_t*)(lds + lay.vbuf);
+    Pcg seed;
+    pcg_seed(seed, (uint64_t)tile);   // Sampler.Clone(tile), integrator.go:318,328
+    uint64_t S = seed.state;
+    int64_t used = npx;
+    for (int64_t pi = 0; pi < npx; pi++) {
+        if (cancel_requested(sc, (pi & 15) == 0)) {   // pbrt_gpu_cancel (large spp: a pixel's StartPixel is long)
+            used = pi;
+            break;
+        }
+        const int64_t rec = bs * wb.ppt + pi;
+        double* gs1d = wb.s1d + rec * wb.s1d_stride;
+        double* sp = s1d ? s1d : gs1d;
+        const uint64_t S1 =
+            start_pixel_wave(rp, J, mb ? mb_state((uint64_t)tile, (uint64_t)pi, 0) : S, inc, sp, other, vbuf, &sh_state);
+        if (s1d)
+            for (int idx = lane; idx < rp.ndims * n; idx += kWave) gs1d[idx] = s1d[idx];
+        PixelRec& pr = wb.prec[rec];
+        const int hit = pr.hit, panic0 = pr.panic0;
+        const uint64_t D = dl_draws(rp, hit, sc.n_lights);
+        uint64_t* mst = wb.memb + rec * n;
+        for (int k = 1 + lane; k < n; k += kWave)
+            mst[k] = mb ? mb_state((uint64_t)tile, (uint64_t)pi, (uint64_t)k) : pcg_advance(J, S1, inc, (uint64_t)(k - 1) * D);
+        if (lane == 0) {
+            mst[0] = ~0ULL;
+            if (hit) {   // the camera ray's time (Get1D, dim 0) of the pixel's first traced sample
+                const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
+                pr.si.time = camera_ray(*sc.camera, (double)px, (double)py, sp[1 < n ? 1 : 0], V2{0.0, 0.0}).time;
+            }
+            pr.nvalid = n;
+        }
+        __syncthreads();   // the StartPixel staging is reused by the next pixel
+        if (panic0) {      // its first traced sample panics at bounce 1: the tile ends here
+            used = pi + 1;
+            break;
+        }
+        S = pcg_advance(J, S1, inc, (uint64_t)(n - 1) * D);
+    }
+    if (lane == 0) wb.tile_npx[bs] = (int32_t)used;
+}
+
+// One lane per (pixel record, traced sample): DirectLighting.Li at depth 0
+// from the pixel's bounce-1 record, with the sample's own PCG32 state.
+// Radiance to wb.L; a panic lowers the pixel's key (sample << 32 | kind + 1)
+// in wb.memb[rec * spp + 0] (the first panic in sample order wins).
+__global__ __launch_bounds__(kWave) void k_dl_samples(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
+                                                      int64_t nrec) {
+    __shared__ uint16_t stack_lds[64 * kStackStride];
+    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
+    stage_nodes(sc);
+    const int n = rp.spp;
+    if (n < 2) return;
+    // grid-stride over every (pixel record, sample): a bounded grid, so a cancel
+    // (polled every 16 passes) ends the kernel quickly at any spp
+    const int64_t total = nrec * (n - 1), stride = (int64_t)gridDim.x * blockDim.x;
+    int pass = 0;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx - threadIdx.x < total; idx += stride) {
+        if ((++pass & 15) == 0 && cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
+        if (idx >= total) continue;
+        const int64_t rec = idx / (n - 1);
+        const int k = 1 + (int)(idx - rec * (n - 1));
+        const int64_t bs = rec / wb.ppt, pi = rec % wb.ppt;
+        if (pi >= wb.tile_npx[bs]) continue;
+        const PixelRec& pr = wb.prec[rec];
+        double* o = wb.L + (rec * n + k) * 3;
+        Spec L = spec(0);
+        int panic = pr.panic0;
+        uint64_t shadow = 0;   // visibility rays traced (the camera ray's query is counted below)
+        if (!panic && pr.hit) {
+            Cursor c;
+            c.rng.state = wb.memb[rec * n + k];
+            c.rng.inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + bs));
+            c.draws = 0;
+            c.cur1d = c.cur2d = 0;
+            c.k = k;
+            c.kdep = 0;
+            const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, n, rp.ndims};
+            c_get2d(c, ss);   // camera: pFilm, pLens, time
+            c_get2d(c, ss);
+            c_get1d(c, ss);
+            L = L + spec(0);   // si.Le(si.Wo): no primitive carries an area light
+            const int nl = sc.n_lights;
+            if (nl > 0) {
+                if (rp.dl_strategy == PBRT_DL_UNIFORM_SAMPLE_ALL) {   // integrator.go:23-46
+                    Spec acc = spec(0);
+                    for (int j = 0; j < nl && !panic; j++) {
+                        const V2 ul = c_get2d(c, ss);
+                        c_get2d(c, ss);
+                        acc = acc + estimate_direct(sc, stack_lds + threadIdx.x, panic, pr.si, pr.b, j, ul, &shadow);
+                    }
+                    L = L + acc;
+                } else {   // UniformSampleOneLight with no distribution (integrator.go:48-77)
+                    const int ln = (int)gomath::to_int(gomath::min(c_get1d(c, ss) * (double)nl, (double)(nl - 1)));
+                    const V2 ul = c_get2d(c, ss);
+                    c_get2d(c, ss);
+                    const Spec s = estimate_direct(sc, stack_lds + threadIdx.x, panic, pr.si, pr.b, ln, ul, &shadow);
+                    if (!panic && max_component(s) > 10) panic = PBRT_PANIC_LD_GT_10;
+                    L = L + s;
+                }
+            }
+            // SpecularReflect / SpecularTransmit: black for a Lambertian-only BSDF
+        }
+        o[0] = L.r;
+        o[1] = L.g;
+        o[2] = L.b;
+        wb.rays[rec * n + k] = kRayClosest + (uint32_t)shadow * kRayShadow;
+        if (panic)
+            atomicMin((unsigned long long*)&wb.memb[rec * n],
+                      ((unsigned long long)k << 32) | (unsigned long long)((panic + 1) & 0xFF));
+
+    }
+}
+
+// Per pixel record: its first panic (sample order) -> wb.ppanic, and the
+// traced-path counters of pixels that finish (as paths_group counts them).
+__global__ void k_dl_panics(RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr) {
+    const int64_t rec = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (rec >= nrec) return;
+    const int64_t bs = rec / wb.ppt, pi = rec % wb.ppt;
+    if (pi >= wb.tile_npx[bs]) return;
+    int64_t x0, y0, x1, y1;
+    tile_bounds(rp, tile_of_slot(rp, slot_base + bs), x0, y0, x1, y1);
+    PanicRec p{0, 0, 0, 0, x0 + pi % (x1 - x0), y0 + pi / (x1 - x0)};
+    const uint64_t key = rp.spp >= 2 ? wb.memb[rec * rp.spp] : ~0ULL;
+    if (wb.prec[rec].panic0) {
+        p.kind = wb.prec[rec].panic0;
+        p.sample = 1;
+        p.bounce = 1;
+    } else if (key != ~0ULL) {
+        p.kind = (int)(key & 0xFF) - 1;
+        p.sample = (int)(key >> 32);
+        p.bounce = 1;
+    }
+    wb.ppanic[rec] = p;
+    if (!p.kind && rp.spp > 1) {
+        atomicAdd(&ctr->paths, (unsigned long long)(rp.spp - 1));
+        atomicAdd(&ctr->camera_samples, (unsigned long long)(rp.spp - 1));
+    }
+}
+
+template <bool kX = false>
+__global__ __launch_bounds__(kWave) void k_tile_cost(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
+                                                     int64_t nb, float* __restrict__ feat,
+                                                     uint64_t* __restrict__ keys) {
+    __shared__ uint16_t stack_lds[64 * kStackStride];
+    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
+    stage_nodes(sc);
+    const int64_t bs = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (bs >= nb) return;
+    const int64_t tile = tile_of_slot(rp, slot_base + bs);
+    int64_t x0, y0, x1, y1;
+    tile_bounds(rp, tile, x0, y0, x1, y1);
+    const int64_t npx = (x1 - x0) * (y1 - y0);
+    const uint64_t inc = pcg_inc_of((uint64_t)tile);
+    const SpecSampler ss{nullptr, rp.spp, rp.ndims};   // k < 0: stratified values are never read
+    double work = 0;
+    int hits = 0;
+    for (int64_t it = lane; it < npx * kProbes; it += kWave) {
+        const int64_t pi = it / kProbes;
+        const PixelRec& pr = wb.prec[bs * wb.ppt + pi];
+        if (!pr.hit) continue;
+        hits += (it % kProbes) == 0;
+        Cursor c;
+        c.rng.state = mb_state((uint64_t)tile, (uint64_t)pi, 0x70726f6265ULL + (uint64_t)(it % kProbes));
+        c.rng.inc = inc;
+        c.draws = 0;
+        c.cur1d = 1;
+        c.cur2d = 2;
+        c.k = -1;
+        c.kdep = 0;
+        Spec beta = spec(1);
+        double eta_scale = 1.0;
+        int bounces = 1;
+        Ray ray;
+        int r = traj_scatter<kX>(sc, pr.si, pr.b, pr.x, pr.wo, c, ss, beta, eta_scale, bounces, ray, rp.max_depth,
+                                 rp.rr_threshold);
+        while (r == 0) {
+            SI si;
+            int panic = 0;
+            if (!bvh_traverse<false>(sc, ray, &si, stack_lds + lane, panic) || panic) break;
+            BSDF b;
+            BSDFX x;
+            if ((kX ? compute_bsdf_x(sc, si, b, x) : compute_bsdf(sc, si, b)) < 0) break;
+            r = traj_scatter<kX>(sc, si, b, x, ray.d, c, ss, beta, eta_scale, bounces, ray, rp.max_depth,
+                                 rp.rr_threshold);
+        }
+        work += (double)c.draws * (double)bounces;
+    }
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        work += __shfl_xor(work, o);
+        hits += __shfl_xor(hits, o);
+    }
+    if (lane == 0) {
+        const double w = work / kProbes * (double)(rp.spp - 1);
+        const float cost = (float)(w + kCostPixel * (double)npx);
+        feat[4 * bs + 0] = (float)w;
+        feat[4 * bs + 1] = (float)hits;
+        feat[4 * bs + 2] = (float)npx;
+        feat[4 * bs + 3] = cost;
+        keys[bs] = ((uint64_t)~__float_as_uint(cost) << 32) | (uint64_t)bs;
+    }
+}
+
+__global__ void k_order_of_keys(const uint64_t* __restrict__ keys, int64_t nb, uint32_t* __restrict__ order) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nb) order[i] = (uint32_t)keys[i];
+}
+
+// ---------------------------------------------------------- merge kernel
+// Film.MergeFilmTile (film.go:115-132) in tile-index order. A film pixel is
+// covered by at most the 3x3 tiles around its own (filter radius < tile size).
+__global__ __launch_bounds__(256) void k_merge_film(const pbrt_film_desc* __restrict__ film_desc, RenderParams rp,
+                                                    const double* __restrict__ films, double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rp.film_w * rp.film_h) return;
+    const pbrt_film_desc& f = *film_desc;
+    const int64_t x = rp.film_min_x + i % rp.film_w, y = rp.film_min_y + i / rp.film_w;
+    const int64_t tx = (x - rp.film_min_x) / rp.tile_size, ty = (y - rp.film_min_y) / rp.tile_size;
+    double v0 = 0, v1 = 0, v2 = 0;
+    for (int64_t dy = -1; dy <= 1; dy++) {
+        for (int64_t dx = -1; dx <= 1; dx++) {
+            int64_t cx = tx + dx, cy = ty + dy;
+            if (cx < 0 || cy < 0 || cx >= rp.ntx || cy >= rp.nty) continue;
+            int64_t tile = cy * rp.ntx + cx;
+            if (tile < rp.tile_begin || (tile - rp.tile_begin) % rp.tile_stride != 0) continue;
+            int64_t slot = (tile - rp.tile_begin) / rp.tile_stride;
+            if (slot >= rp.n_slots) continue;
+            int64_t x0, y0, x1, y1, px0, py0, px1, py1;
+            tile_bounds(rp, tile, x0, y0, x1, y1);
+            film_tile_bounds(f, x0, y0, x1, y1, px0, py0, px1, py1);
+            if (x < px0 || x >= px1 || y < py0 || y >= py1) continue;
+            const double* c = films + slot * (rp.slot_w * rp.slot_h * 3) + ((x - px0) + (y - py0) * (px1 - px0)) * 3;
+            // spectrum.go:35-41 RGBToXYZ
+            v0 += 0.412453 * c[0] + 0.357580 * c[1] + 0.180423 * c[2];
+            v1 += 0.212671 * c[0] + 0.715160 * c[1] + 0.072169 * c[2];
+            v2 += 0.019334 * c[0] + 0.119193 * c[1] + 0.950227 * c[2];
+        }
+    }
+    out[i * 3 + 0] = v0;
+    out[i * 3 + 1] = v1;
+    out[i * 3 + 2] = v2;
+}
+
+// ------------------------------------------------------- batch intersect
+__global__ __launch_bounds__(kWave) void k_intersect(DevScene sc, int64_t n, const double* __restrict__ rays,
+                                                     double* __restrict__ out, int any_hit) {
+    __shared__ uint16_t stack_lds[64 * kStackStride];
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double* q = rays + 7 * i;
+    Ray r{V3{q[0], q[1], q[2]}, V3{q[3], q[4], q[5]}, q[6], 0};
+    int panic = 0;
+    if (any_hit) {
+        bool h = bvh_traverse<true>(sc, r, nullptr, stack_lds + threadIdx.x, panic);
+        out[i] = panic ? gomath::nan() : (h ? 1.0 : 0.0);
+        return;
+    }
+    SI si;
+    si.p = si.n = V3{0, 0, 0};
+    si.prim = -1;
+    bool h = bvh_traverse<false>(sc, r, &si, stack_lds + threadIdx.x, panic);
+    double* o = out + 9 * i;
+    if (panic) {
+        for (int k = 0; k < 9; k++) o[k] = gomath::nan();
+        return;
+    }
+    o[0] = h ? 1.0 : 0.0;
+    o[1] = r.tmax;
+    o[2] = h ? (double)si.prim : -1.0;
+    o[3] = si.p.x; o[4] = si.p.y; o[5] = si.p.z;
+    o[6] = si.n.x; o[7] = si.n.y; o[8] = si.n.z;
+}
+
+template __global__ void k_wf_primary<false>(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nb);
+template __global__ void k_wf_primary<true>(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nb);
+template __global__ void k_tile_cost<false>(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nb, float* __restrict__ feat, uint64_t* __restrict__ keys);
+template __global__ void k_tile_cost<true>(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nb, float* __restrict__ feat, uint64_t* __restrict__ keys);
+
+}  // namespace pbrtk

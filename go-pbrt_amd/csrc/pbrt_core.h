@@ -209,17 +209,20 @@ GO_HD EF ef_muls(EF a, double s, int& panic) { return ef_mul(a, ef_new(s, 0.0, p
 // so min/max over the four rounded quotients are the rounded quotients of the
 // analytic extremes (ties and the sign of a zero vanish in NextFloatDown/Up).
 // Two divisions instead of four; an interval with a zero end keeps the
-// four-quotient form (its Inf/NaN reaches Check as in Go).
+// four-quotient form (its Inf/NaN reaches Check as in Go), and so does any
+// operand with a non-finite bound (Go's Min/Max see NaN quotients there).
 GO_HD EF ef_div(EF a, EF b, int& panic) {
     EF r;
     r.v = a.v / b.v;
+    const bool finite = gomath::abs(a.lo) < kInf && gomath::abs(a.hi) < kInf && gomath::abs(b.lo) < kInf &&
+                        gomath::abs(b.hi) < kInf;
     if (b.lo < 0 && b.hi > 0) {
         r.lo = -kInf;
         r.hi = kInf;
-    } else if (b.lo > 0) {
+    } else if (finite && b.lo > 0) {
         r.lo = gomath::next_down(a.lo / (a.lo >= 0 ? b.hi : b.lo));
         r.hi = gomath::next_up(a.hi / (a.hi >= 0 ? b.lo : b.hi));
-    } else if (b.hi < 0) {
+    } else if (finite && b.hi < 0) {
         r.lo = gomath::next_down(a.hi / (a.hi >= 0 ? b.hi : b.lo));
         r.hi = gomath::next_up(a.lo / (a.lo >= 0 ? b.lo : b.hi));
     } else {

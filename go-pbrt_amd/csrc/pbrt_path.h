@@ -18,6 +18,7 @@
 
 #include "pbrt_core.h"
 #include "pbrt_mesh.h"
+#include "sphere_filter.h"
 
 namespace pbrt {
 
@@ -269,56 +270,47 @@ __device__ __forceinline__ bool phi_beyond(double y, double x, double phi_max) {
 // `ray` is already in object space (shape_hit), oerr/derr its transform errors.
 __device__ inline bool sphere_hit(const pbrt_shape_desc& s, const Ray& ray, V3 oerr, V3 derr, double& t_hit, V3& ph,
                                   int& panic) {
-    // Early miss: the EFloat values are plain float64 arithmetic on the values
-    // (efloat.go Add/Mul), so the quadratic's discriminant below is computed
-    // here bit for bit without the interval bounds; when it is negative
-    // efloat/math.go:38-40 returns false. With every operand finite and below
-    // 1e100 no Check() (efloat.go:102-111) can panic on the way there, so the
-    // reference returns that same miss.
-    {
-        const double av = (ray.d.x * ray.d.x + ray.d.y * ray.d.y) + ray.d.z * ray.d.z;
-        const double bv = ((ray.d.x * ray.o.x + ray.d.y * ray.o.y) + ray.d.z * ray.o.z) * 2.0;
-        const double cv = ((ray.o.x * ray.o.x + ray.o.y * ray.o.y) + ray.o.z * ray.o.z) - s.radius * s.radius;
-        const double disc = bv * bv - 4. * av * cv;
-        const double big = 1e100;
-        const bool moderate =
-            gomath::abs(ray.o.x) < big && gomath::abs(ray.o.y) < big && gomath::abs(ray.o.z) < big &&
-            gomath::abs(ray.d.x) < big && gomath::abs(ray.d.y) < big && gomath::abs(ray.d.z) < big &&
-            gomath::abs(oerr.x) < big && gomath::abs(oerr.y) < big && gomath::abs(oerr.z) < big &&
-            gomath::abs(derr.x) < big && gomath::abs(derr.y) < big && gomath::abs(derr.z) < big &&
-            gomath::abs(s.radius) < big;
-#ifndef PBRT_NO_EARLY_MISS
-        if (disc < 0 && moderate) return false;
-#else
-        (void)disc; (void)moderate;
-#endif
+    // Value-first decisions (sphere_filter.h): the reference's
+    // bound comparisons decided from the EFloat values and a proven radius, so
+    // the intervals below are evaluated only when the filter cannot decide
+    // (a near-tie with TMax or 0, a near-zero divisor, extreme magnitudes).
+    sf_roots rt;
+    const int fr = sphere_roots_filter(ray.o.x, ray.o.y, ray.o.z, ray.d.x, ray.d.y, ray.d.z, oerr.x, oerr.y, oerr.z,
+                                       derr.x, derr.y, derr.z, s.radius, ray.tmax, &rt);
+    if (fr == 0) return false;
+    if (fr < 0) {
+        EF ox = ef_new(ray.o.x, oerr.x, panic), oy = ef_new(ray.o.y, oerr.y, panic), oz = ef_new(ray.o.z, oerr.z, panic);
+        EF dx = ef_new(ray.d.x, derr.x, panic), dy = ef_new(ray.d.y, derr.y, panic), dz = ef_new(ray.d.z, derr.z, panic);
+        EF a = ef_add(ef_add(ef_mul(dx, dx, panic), ef_mul(dy, dy, panic), panic), ef_mul(dz, dz, panic), panic);
+        EF b = ef_muls(ef_add(ef_add(ef_mul(dx, ox, panic), ef_mul(dy, oy, panic), panic), ef_mul(dz, oz, panic), panic),
+                       2.0, panic);
+        EF c0 = ef_add(ef_add(ef_mul(ox, ox, panic), ef_mul(oy, oy, panic), panic), ef_mul(oz, oz, panic), panic);
+        EF c = ef_sub(c0, ef_muls(ef_new(s.radius, 0, panic), s.radius, panic), panic);
+        EF t0, t1;
+        if (!ef_quadratic(a, b, c, t0, t1, panic)) return false;
+        if (t0.hi > ray.tmax || t1.lo <= 0) return false;
+        rt.t0v = t0.v;
+        rt.t1v = t1.v;
+        rt.t0lo_le0 = t0.lo <= 0;
+        rt.t1hi_gt = t1.hi > ray.tmax;
     }
-    EF ox = ef_new(ray.o.x, oerr.x, panic), oy = ef_new(ray.o.y, oerr.y, panic), oz = ef_new(ray.o.z, oerr.z, panic);
-    EF dx = ef_new(ray.d.x, derr.x, panic), dy = ef_new(ray.d.y, derr.y, panic), dz = ef_new(ray.d.z, derr.z, panic);
-    EF a = ef_add(ef_add(ef_mul(dx, dx, panic), ef_mul(dy, dy, panic), panic), ef_mul(dz, dz, panic), panic);
-    EF b = ef_muls(ef_add(ef_add(ef_mul(dx, ox, panic), ef_mul(dy, oy, panic), panic), ef_mul(dz, oz, panic), panic),
-                   2.0, panic);
-    EF c0 = ef_add(ef_add(ef_mul(ox, ox, panic), ef_mul(oy, oy, panic), panic), ef_mul(oz, oz, panic), panic);
-    EF c = ef_sub(c0, ef_muls(ef_new(s.radius, 0, panic), s.radius, panic), panic);
-    EF t0, t1;
-    if (!ef_quadratic(a, b, c, t0, t1, panic)) return false;
-    if (t0.hi > ray.tmax || t1.lo <= 0) return false;
-    EF ts = t0;
+    // sphere.go:87-131 on the decided comparisons
+    double tsv = rt.t0v;
     bool used_t1 = false;
-    if (ts.lo <= 0) {
-        ts = t1;
+    if (rt.t0lo_le0) {
+        tsv = rt.t1v;
         used_t1 = true;
-        if (ts.hi > ray.tmax) return false;
+        if (rt.t1hi_gt) return false;
     }
-    ph = ray.o + muls(ray.d, ts.v);
+    ph = ray.o + muls(ray.d, tsv);
     ph = muls(ph, s.radius / dist(ph, V3{0, 0, 0}));
     if (ph.x == 0.0 && ph.y == 0.0) ph.x = 1e-5 * s.radius;
     if ((s.z_min > -s.radius && ph.z < s.z_min) || (s.z_max < s.radius && ph.z > s.z_max) ||
         phi_beyond(ph.y, ph.x, s.phi_max)) {
         if (used_t1) return false;
-        if (t1.hi > ray.tmax) return false;
-        ts = t1;
-        ph = ray.o + muls(ray.d, ts.v);
+        if (rt.t1hi_gt) return false;
+        tsv = rt.t1v;
+        ph = ray.o + muls(ray.d, tsv);
         ph = muls(ph, s.radius / dist(ph, V3{0, 0, 0}));
         if (ph.x == 0.0 && ph.y == 0.0) ph.x = 1e-5 * s.radius;
         // sphere.go:127 shadows phi (`:=`): the new phi is only tested here
@@ -326,7 +318,7 @@ __device__ inline bool sphere_hit(const pbrt_shape_desc& s, const Ray& ray, V3 o
             phi_beyond(ph.y, ph.x, s.phi_max))
             return false;
     }
-    t_hit = ts.v;
+    t_hit = tsv;
     return true;
 }
 // Sphere.Intersect, interaction part (sphere.go:133-186); ray in object space.

@@ -1,6 +1,8 @@
-// render.hip — MI355X (gfx950) kernels and the C ABI of include/pbrt_gpu.h.
+// render.hip — host side of the MI355X (gfx950) library: scene upload, launch
+// planning and the C ABI of include/pbrt_gpu.h.
 //
-// Kernels
+// Kernels (each family in its own translation unit, k_*.hip; declarations in
+// render_kernels.h, shared types and helpers in render_common.h)
 //   k_render_exact   EXACT mode: one lane per 16-px tile. The lane replays the
 //                    tile's PCG32 stream exactly as pbrt.Render's worker does
 //                    (integrator.go:228-289, 311-340): pixel loop, Stratified
@@ -35,1975 +37,11 @@
 #include "../../include/pbrt_gpu.h"
 #include "../../include/pbrt_scene.h"
 #include "mesh_bvh.h"
-#include "pbrt_spec.h"
+#include "render_kernels.h"
 
 using namespace pbrt;
+using namespace pbrtk;
 
-namespace {
-
-constexpr int kWave = 64;
-
-struct RenderParams {
-    int64_t film_min_x, film_min_y, film_w, film_h;   // CroppedPixelBounds
-    int64_t tile_size, ntx, nty;
-    int64_t tile_begin, tile_stride, n_slots;
-    int64_t slot_w, slot_h;                            // max tile-film extent
-    int32_t spp, xs, ys, ndims, jitter;
-    int32_t integrator, max_depth, dl_strategy;
-    double rr_threshold;
-    int32_t lanes_per_wave;
-    int32_t flags;   // pbrt_render_desc.flags
-    int32_t sp_events, sp_draws, sp_serial;   // wave kernel StartPixel: events, raw draws buffered
-    int32_t mode;                             // PBRT_MODE_EXACT / _THROUGHPUT
-};
-
-struct PanicRec {
-    int32_t kind;
-    int32_t sample;
-    int32_t bounce;
-    int32_t pad;
-    int64_t px, py;
-};
-
-struct Counters {
-    unsigned long long paths, camera_samples, closest_rays, shadow_rays;
-    int32_t any_panic;
-    int32_t pad;
-    // wave kernel diagnostics (pbrt_gpu_counters): speculation windows, and
-    // lane-0 clock64 cycles in StartPixel / bounce 1 / chain / full paths / film add
-    unsigned long long windows, phase[8];
-    unsigned long long dhist[64];   // k_chain_ci diagnostics: on-chain draw counts D (bin D/2, last bin >= 126)
-};
-constexpr int kNumCounters = 6 + 8 + 64;
-
-__device__ __forceinline__ void tile_bounds(const RenderParams& rp, int64_t tile, int64_t& x0, int64_t& y0,
-                                            int64_t& x1, int64_t& y1) {
-    // integrator.go:316-325
-    int64_t tx = tile % rp.ntx, ty = tile / rp.ntx;
-    x0 = rp.film_min_x + tx * rp.tile_size;
-    x1 = gomath::to_int(gomath::min((double)(x0 + rp.tile_size), (double)(rp.film_min_x + rp.film_w)));
-    y0 = rp.film_min_y + ty * rp.tile_size;
-    y1 = gomath::to_int(gomath::min((double)(y0 + rp.tile_size), (double)(rp.film_min_y + rp.film_h)));
-}
-// Film.GetFilmTile (film.go:106-113)
-__device__ __host__ __forceinline__ void film_tile_bounds(const pbrt_film_desc& f, int64_t x0, int64_t y0, int64_t x1,
-                                                          int64_t y1, int64_t& px0, int64_t& py0, int64_t& px1,
-                                                          int64_t& py1) {
-    int64_t p0x = gomath::to_int(gomath::ceil(((double)x0 - 0.5) - f.filter_radius_x));
-    int64_t p0y = gomath::to_int(gomath::ceil(((double)y0 - 0.5) - f.filter_radius_y));
-    int64_t p1x = gomath::to_int(gomath::floor(((double)x1 - 0.5) + f.filter_radius_x)) + 1;
-    int64_t p1y = gomath::to_int(gomath::floor(((double)y1 - 0.5) + f.filter_radius_y)) + 1;
-    px0 = gomath::to_int(gomath::max((double)f.crop_min_x, (double)p0x));
-    py0 = gomath::to_int(gomath::max((double)f.crop_min_y, (double)p0y));
-    px1 = gomath::to_int(gomath::min((double)f.crop_max_x, (double)p1x));
-    py1 = gomath::to_int(gomath::min((double)f.crop_max_y, (double)p1y));
-}
-
-// Footprint of one sample on the tile film (film.go:211-248). pFilm is the
-// pixel corner for every sample of a pixel (2D stratified dims are (0,0), #3),
-// so the footprint and the filter weights are per pixel.
-struct Footprint {
-    int n;               // number of film pixels touched (<= 4 in the register path)
-    int64_t off[4];      // offsets (in pixels) into the tile film slot
-    double w[4];         // sampleWeight * filterWeight
-};
-__device__ inline int footprint(const pbrt_film_desc& f, double pfx, double pfy, int64_t px0, int64_t py0,
-                                int64_t px1, int64_t py1, Footprint& fp, int64_t& p0x, int64_t& p0y, int64_t& p1x,
-                                int64_t& p1y) {
-    double dx = pfx - 0.5, dy = pfy - 0.5;
-    double p0fx = gomath::ceil(dx - f.filter_radius_x), p0fy = gomath::ceil(dy - f.filter_radius_y);
-    double p1fx = gomath::floor(dx + f.filter_radius_x) + 1, p1fy = gomath::floor(dy + f.filter_radius_y) + 1;
-    p0x = gomath::to_int(gomath::max(p0fx, (double)px0));
-    p0y = gomath::to_int(gomath::max(p0fy, (double)py0));
-    p1x = gomath::to_int(gomath::min(p1fx, (double)px1));
-    p1y = gomath::to_int(gomath::min(p1fy, (double)py1));
-    int64_t nx = p1x - p0x, ny = p1y - p0y;
-    if (nx <= 0 || ny <= 0) { fp.n = 0; return 0; }
-    if (nx * ny > 4) return -1;
-    const double ifx = 1.0 / f.filter_radius_x, ify = 1.0 / f.filter_radius_y;
-    int64_t tw = px1 - px0;
-    int k = 0;
-    for (int64_t y = p0y; y < p1y; y++) {
-        int iy = (int)gomath::to_int(gomath::min(gomath::floor(gomath::abs(((double)y - dy) * ify * 16.0)), 16.0 - 1));
-        for (int64_t x = p0x; x < p1x; x++) {
-            int ix =
-                (int)gomath::to_int(gomath::min(gomath::floor(gomath::abs(((double)x - dx) * ifx * 16.0)), 16.0 - 1));
-            fp.off[k] = (x - px0) + (y - py0) * tw;
-            fp.w[k] = 1.0 * f.filter_table[iy * 16 + ix];
-            k++;
-        }
-    }
-    fp.n = k;
-    return 0;
-}
-
-// ----------------------------------------------------------- EXACT kernel
-// One lane per tile; `lanes_per_wave` lanes of each 64-lane workgroup work
-// (fewer busy lanes per wave = less divergence, more waves per SIMD).
-template <int kMinWaves>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kMinWaves, 8))) void k_render_exact(DevScene sc, RenderParams rp, double* __restrict__ films,
-                                                        double* __restrict__ s1d_scratch, PanicRec* __restrict__ panics,
-                                                        Counters* __restrict__ ctr) {
-    __shared__ uint16_t stack_lds[64 * kStackStride];
-    const int lane = threadIdx.x;
-    if (lane >= rp.lanes_per_wave) return;
-    const int64_t slot = (int64_t)blockIdx.x * rp.lanes_per_wave + lane;
-    if (slot >= rp.n_slots) return;
-    const int64_t tile = rp.tile_begin + slot * rp.tile_stride;
-    const pbrt_film_desc& film = *sc.film;
-
-    int64_t x0, y0, x1, y1, px0, py0, px1, py1;
-    tile_bounds(rp, tile, x0, y0, x1, y1);
-    film_tile_bounds(film, x0, y0, x1, y1, px0, py0, px1, py1);
-    double* tf = films + slot * (rp.slot_w * rp.slot_h * 3);
-    const int64_t npx = (px1 - px0) * (py1 - py0);
-    for (int64_t i = 0; i < npx * 3; i++) tf[i] = 0.0;
-
-    Thread t;
-    t.spp = rp.spp; t.ndims = rp.ndims; t.xs = rp.xs; t.ys = rp.ys; t.jitter = rp.jitter;
-    t.s1d = s1d_scratch + slot * (int64_t)(rp.ndims * rp.spp);
-    t.stack = stack_lds + lane;
-    t.panic = 0;
-    t.bounce = 0;
-    t.closest_rays = t.shadow_rays = 0;
-    pcg_seed(t.rng, (uint64_t)tile);   // Sampler.Clone(seed = tile index), integrator.go:318,328
-    unsigned long long paths = 0;
-    const pbrt_camera_desc& cam = *sc.camera;
-
-    const bool mb = rp.mode == PBRT_MODE_THROUGHPUT;
-    uint64_t last_host_poll = wall_clock64();
-    for (int64_t py = y0; py < y1; py++) {
-        for (int64_t px = x0; px < x1; px++) {
-            if (cancel_polled(sc, last_host_poll)) return;   // pbrt_gpu_cancel
-            const uint64_t pi = (uint64_t)((py - y0) * (x1 - x0) + (px - x0));
-            if (mb) t.rng.state = mb_state((uint64_t)tile, pi, 0);
-            start_pixel(t);
-            // camera sample: pFilm = pixel + Get2D() == pixel corner; pLens = Get2D() = (0,0)
-            const double fx = (double)px + 0.0, fy = (double)py + 0.0;
-            Footprint fp;
-            int64_t p0x, p0y, p1x, p1y;
-            // With n_dims >= 1 the camera's Get2D is stratified 2D dim 0 == (0,0) for every
-            // sample, so pFilm is the pixel corner and the footprint is per pixel; with
-            // n_dims == 0 it comes from the RNG and the footprint is per sample.
-            const bool reg = rp.ndims >= 1 &&
-                             footprint(film, fx, fy, px0, py0, px1, py1, fp, p0x, p0y, p1x, p1y) == 0;
-            double acc[4][3];
-            if (reg)
-                for (int k = 0; k < fp.n; k++)
-                    for (int c = 0; c < 3; c++) acc[k][c] = tf[fp.off[k] * 3 + c];
-            while (next_sample(t)) {
-                // (a pixel of large spp runs for milliseconds: poll inside it too)
-                if ((t.sample_index & 15) == 0 && cancel_polled(sc, last_host_poll)) return;
-                if (mb) t.rng.state = mb_state((uint64_t)tile, pi, (uint64_t)t.sample_index);
-                V2 u0 = get2d(t);
-                V2 plens = get2d(t);
-                double tu = get1d(t);
-                Ray ray = camera_ray(cam, (double)px + u0.x, (double)py + u0.y, tu, plens);
-                const bool fid = (rp.flags & PBRT_FLAG_PANIC_FIDELITY) != 0;
-                Spec L = (rp.integrator == PBRT_INTEGRATOR_PATH)
-                             ? path_li(sc, t, ray, rp.max_depth, rp.rr_threshold, fid)
-                             : direct_li(sc, t, ray, rp.max_depth, rp.dl_strategy, fid);
-                paths++;
-                if (t.panic) {
-                    PanicRec pr;
-                    pr.kind = t.panic;
-                    pr.sample = t.sample_index;
-                    pr.bounce = t.bounce;
-                    pr.pad = 0;
-                    pr.px = px;
-                    pr.py = py;
-                    panics[slot] = pr;
-                    atomicExch(&ctr->any_panic, 1);
-                    return;
-                }
-                if (has_nans(L)) L = spec(0.1);   // integrator.go:256-262
-                if (0.0 > film.max_sample_luminance) L = smuls(L, film.max_sample_luminance / 0.0);   // L.Y() == 0
-                if (reg) {
-                    for (int k = 0; k < fp.n; k++) {
-                        Spec a = smuls(L, fp.w[k]);
-                        acc[k][0] += a.r; acc[k][1] += a.g; acc[k][2] += a.b;
-                    }
-                } else {
-                    // general footprint: FilmTile.AddSample straight into the slot
-                    const double sfx = (double)px + u0.x, sfy = (double)py + u0.y;
-                    double dx = sfx - 0.5, dy = sfy - 0.5;
-                    p0x = gomath::to_int(gomath::max(gomath::ceil(dx - film.filter_radius_x), (double)px0));
-                    p0y = gomath::to_int(gomath::max(gomath::ceil(dy - film.filter_radius_y), (double)py0));
-                    p1x = gomath::to_int(gomath::min(gomath::floor(dx + film.filter_radius_x) + 1, (double)px1));
-                    p1y = gomath::to_int(gomath::min(gomath::floor(dy + film.filter_radius_y) + 1, (double)py1));
-                    const double ifx = 1.0 / film.filter_radius_x, ify = 1.0 / film.filter_radius_y;
-                    int64_t tw = px1 - px0;
-                    for (int64_t y = p0y; y < p1y; y++) {
-                        int iy = (int)gomath::to_int(
-                            gomath::min(gomath::floor(gomath::abs(((double)y - dy) * ify * 16.0)), 16.0 - 1));
-                        for (int64_t x = p0x; x < p1x; x++) {
-                            int ix = (int)gomath::to_int(
-                                gomath::min(gomath::floor(gomath::abs(((double)x - dx) * ifx * 16.0)), 16.0 - 1));
-                            Spec a = smuls(L, 1.0 * film.filter_table[iy * 16 + ix]);
-                            double* p = tf + ((x - px0) + (y - py0) * tw) * 3;
-                            p[0] += a.r; p[1] += a.g; p[2] += a.b;
-                        }
-                    }
-                }
-            }
-            if (reg)
-                for (int k = 0; k < fp.n; k++)
-                    for (int c = 0; c < 3; c++) tf[fp.off[k] * 3 + c] = acc[k][c];
-        }
-    }
-    atomicAdd(&ctr->paths, paths);
-    atomicAdd(&ctr->camera_samples, paths);
-    atomicAdd(&ctr->closest_rays, (unsigned long long)t.closest_rays);
-    atomicAdd(&ctr->shadow_rays, (unsigned long long)t.shadow_rays);
-}
-
-// ------------------------------------------------------ EXACT, wave-parallel
-// The kernels that replace the serial tile replay (see pbrt_spec.h for why
-// the results are the same bits):
-//   k_chain_ci  per tile: StartPixel (lane-parallel, pcg_bounded rejections
-//               resolved), then speculative trajectories at RNG offsets until
-//               every sample's offset is known; writes the stratified values
-//               and each sample's RNG state. The only serial dependency of the
-//               reference (the per-tile PCG32 stream) lives here.
-//   k_paths_ci  the samples as full paths (bounce-1 EstimateDirect per light
-//               cached per pixel); writes L per sample and the pixel's first
-//               panic. k_pw_*: the same as per-bounce compacted queues.
-//   k_film      one thread per tile-film pixel: FilmTile.AddSample
-//               contributions summed in the reference's order (pixels
-//               row-major, samples in order), the serial replay's sums.
-__device__ __forceinline__ void stage_nodes(DevScene& sc) {
-    if (sc.n_nodes > kLdsNodes) return;
-    for (int i = threadIdx.x; i < sc.n_nodes; i += blockDim.x) g_nodes_lds[i] = sc.nodes[i];
-    for (int i = threadIdx.x; i < 8 * sc.n_nodes; i += blockDim.x) {
-        const int oct = i / sc.n_nodes, j = i - oct * sc.n_nodes;
-        if (j < sc.n_leaves) g_leaf_lds[oct * kLdsNodes + j] = (uint16_t)sc.order[8 * sc.n_nodes + i];
-    }
-    for (int i = threadIdx.x; i < sc.n_groups * 6; i += blockDim.x) g_grp_lds[i] = sc.groups[i];
-    for (int i = threadIdx.x; i < 8 * (sc.n_groups + 1) && sc.n_groups > 0; i += blockDim.x) {
-        const int oct = i / (sc.n_groups + 1), g = i - oct * (sc.n_groups + 1);
-        g_gmask_lds[oct * (kMaxCullGroups + 1) + g] = sc.gmasks[i];
-    }
-    __syncthreads();
-    sc.use_lds_nodes = 1;
-}
-
-struct PixelRec {
-    SI si;
-    BSDF b;
-    BSDFX x;          // kX pipelines (Mirror / smooth Glass / OrenNayar scenes)
-    V3 wo;
-    int32_t hit;      // first hit exists and maxDepth > 1
-    int32_t nvalid;   // samples 1 .. nvalid-1 have offsets (spp unless a panic cut the chain)
-    int32_t panic0;   // the camera ray's traversal panics (kind), else 0
-    int32_t pad;
-};
-struct WaveBufs {
-    PixelRec* prec;     // [slot][ppt]
-    double* s1d;        // [slot][ppt][ndims * spp]
-    uint64_t* memb;     // [slot][ppt][spp]   PCG32 state at sample k's offset
-    double* L;          // [slot][ppt][spp][3]
-    uint32_t* rays;     // [slot][ppt][spp]      the sample's reference ray counts (kRayClosest / kRayShadow)
-    PanicRec* ppanic;   // [slot][ppt]        first panic of the pixel in sample order
-    int32_t* tile_npx;  // [slot]             pixels with records (a panic ends the tile)
-    int64_t ppt;        // pixel records per tile slot (tile_size^2)
-    int64_t s1d_stride; // ndims * spp
-};
-struct ChainLayout {   // byte offsets into the chain / setup kernels' dynamic LDS block
-    int s1d, other, sbuf, dbuf, vbuf, total;
-    int ring;      // k_chain_ci: offset ring after the StartPixel staging (no sbuf / dbuf)
-    int staging;   // k_chain_ci: bytes of the StartPixel staging (s1d, other, vbuf)
-    int pcs;       // k_chain_ci: the lane groups' bounce-1 ChainCache records (ci_layout)
-};
-#ifndef PBRT_CI_RING_KB
-#define PBRT_CI_RING_KB 4
-#endif
-constexpr int kCiRingBytes = PBRT_CI_RING_KB * 1024;   // k_chain_ci offset ring (all lane groups of a wave)
-constexpr int kCiMaxGroups = 4;          // k_chain_ci lane groups (tiles) per wave
-
-__device__ __forceinline__ double pcg_float_of(uint32_t v) {
-    return gomath::min(gomath::kOneMinusEpsilon, (double)v * 2.3283064365386963e-10);
-}
-__device__ __forceinline__ int64_t tile_of_slot(const RenderParams& rp, int64_t slot) {
-    return rp.tile_begin + slot * rp.tile_stride;
-}
-__device__ __forceinline__ uint64_t pcg_inc_of(uint64_t seed) { return (seed << 1) | 1; }   // rng.go:28-34
-
-// Stratified.StartPixel (stratified.go:21-48) for one pixel. Every thread of
-// the workgroup calls it (it holds the block's barriers); the first wave does
-// the work. The shuffled 1D values are left in s1d (LDS); returns the PCG32
-// state after the pixel's draws.
-__shared__ int g_sp_overflow;
-__device__ uint64_t start_pixel_wave(const RenderParams& rp, const PcgJump& J, uint64_t S, uint64_t inc, double* s1d,
-                                     uint16_t* other, uint32_t* vbuf, uint64_t* sh_state) {
-    const int lane = threadIdx.x;
-    const bool w0 = lane < kWave;
-    const int n = rp.spp, ndims = rp.ndims;
-    const double inv_n = 1.0 / (double)n;
-    const int s1 = rp.jitter ? 2 * n : n, s2 = rp.jitter ? 3 * n : n;   // StartPixel draws per 1D / 2D dim
-    // StartPixel (stratified.go:21-48). The pixel's draws form a fixed
-    // list of E events (jitter floats and pcg_bounded picks,
-    // sampling.go:101-145). A pick retries on v < 2^32 mod b, which
-    // the reference's (rot+1)&31 output rotation makes common (v < 4
-    // has probability ~1/64), so event e lands on draw e + R(e),
-    // R(e) = rejections before it. Lanes fill the raw stream by
-    // jump-ahead, then resolve R chunk by chunk: one ballot per
-    // rejection shifts every later event by one draw.
-    bool serial_sp = rp.sp_serial != 0;
-    if (!serial_sp) {
-        const int E = rp.sp_events, V = rp.sp_draws;
-        if (w0) {
-            uint64_t st = pcg_advance(J, S, inc, (uint64_t)lane);
-            for (int t = lane; t < V; t += kWave) {
-                vbuf[t] = pcg_output(st);
-                st = J.a[6] * st + inc * J.b[6];   // +64 draws
-            }
-        }
-        __syncthreads();
-        int R = 0;
-        bool overflow = false;
-        for (int cb = 0; w0 && cb < E; cb += kWave) {
-            const int e = cb + lane;
-            int kind = 0, slt = 0, i = 0;   // 0 none, 1 1D float, 2 1D pick, 3 2D pick
-            if (e < E) {
-                if (e < ndims * s1) {
-                    const int d = e / s1, qq = e - d * s1;
-                    if (rp.jitter && qq < n) { kind = 1; slt = d * n + qq; }
-                    else { kind = 2; i = qq - (rp.jitter ? n : 0); slt = d * n + i; }
-                } else {
-                    const int e2 = e - ndims * s1, d = e2 / s2, qq = e2 - d * s2;
-                    if (!(rp.jitter && qq < 2 * n)) { kind = 3; i = qq - (rp.jitter ? 2 * n : 0); }
-                }
-            }
-            const uint32_t b = (uint32_t)(n - i);
-            const uint32_t thr = kind >= 2 ? (~b + 1u) % b : 0u;
-            int local = 0;
-            for (;;) {
-                const int t = e + R + local;
-                const bool out = kind != 0 && t >= V;
-                const bool bad = !out && kind >= 2 && vbuf[t] < thr;
-                if (__any(out)) { overflow = true; break; }
-                const unsigned long long m = __ballot(bad);
-                if (m == 0) break;
-                const int first = __ffsll((long long)m) - 1;
-                if (lane >= first) local++;
-            }
-            if (overflow) break;
-            const uint32_t v = kind != 0 ? vbuf[e + R + local] : 0u;
-            if (kind == 1)
-                s1d[slt] = gomath::min(((double)(slt % n) + pcg_float_of(v)) * inv_n, gomath::kOneMinusEpsilon);
-            else if (kind == 2)
-                other[slt] = (uint16_t)(i + (int)(v % b));
-            R += __shfl(local, kWave - 1);
-        }
-        if (lane == 0) g_sp_overflow = overflow;
-        __syncthreads();
-        serial_sp = g_sp_overflow != 0;
-        if (!serial_sp) {
-            if (!rp.jitter && w0)
-                for (int idx = lane; idx < ndims * n; idx += kWave)
-                    s1d[idx] = gomath::min(((double)(idx % n) + 0.5) * inv_n, gomath::kOneMinusEpsilon);
-            __syncthreads();
-            if (lane < ndims) {
-                double* samp = s1d + lane * n;
-                const uint16_t* oth = other + lane * n;
-                for (int k = 0; k < n; k++) {
-                    const int o = oth[k];
-                    double a = samp[k];
-                    samp[k] = samp[o];
-                    samp[o] = a;
-                }
-            }
-            if (lane == 0) *sh_state = pcg_advance(J, S, inc, (uint64_t)(E + R));
-        }
-    }
-    if (serial_sp || (rp.flags & PBRT_FLAG_SERIAL_START_PIXEL)) {
-        if (lane == 0) {   // serial replay (huge sample counts, or forced)
-            Thread t;
-            t.rng.state = S;
-            t.rng.inc = inc;
-            t.spp = n; t.ndims = ndims; t.xs = rp.xs; t.ys = rp.ys; t.jitter = rp.jitter;
-            t.s1d = s1d;
-            start_pixel(t);
-            *sh_state = t.rng.state;
-        }
-    }
-    __syncthreads();
-    return *sh_state;
-}
-
-#ifndef PBRT_PATHS_WAVES
-#define PBRT_PATHS_WAVES 2
-#endif
-constexpr int kPathsWaves = PBRT_PATHS_WAVES;   // k_paths_ci waves/SIMD (build option)
-
-// k_paths_ci: full paths with lane refill. One pixel's samples per wave would
-// make a wave last as long as its longest path (~4x the mean). Here a wave
-// owns P pixel records and treats their samples as one
-// work list: a lane whose path ends writes its radiance and takes the next
-// (pixel, sample) at once, so the wave only waits for its longest path at
-// the end of the P pixels. Every path runs the same arithmetic as
-// Path.Li (path_step), from the offset the chain found, so L per
-// (pixel, sample) is bit-identical; k_film sums them in sample order as
-// before. Requires LDS-staged nodes (no traversal stack) and P * n_lights <= 64.
-//
-// paths_group is the per-wave body, synchronised within the wave only (a
-// fused variant that ran it inside k_chain_ci after each tile's chain was
-// bit-exact but slower: 1000 vs 874 ms, the chain kernel spilled). Its LDS:
-// PixelCache[P], then P panic keys, then the P pixels' stratified values.
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
-struct PMeta {   // per pixel of a paths_group: PCG increment, tile, nvalid, hit, first work index
-    uint64_t inc, tile;
-    int32_t nv, hit, cum, pad;
-};
-template <int P>
-__host__ __device__ constexpr size_t paths_group_meta_off() {
-    return (P * sizeof(PixelCache) + P * 8 + 15) & ~(size_t)15;
-}
-template <int P>
-__host__ __device__ constexpr size_t paths_group_l_off() {   // per-lane radiance sums (PathStateLds)
-    return paths_group_meta_off<P>() + (P + 1) * sizeof(PMeta);
-}
-template <int P>
-__host__ __device__ constexpr int paths_group_lds(int per) {   // bytes, per wave
-    return (int)(paths_group_l_off<P>() + 3 * kWave * sizeof(Spec) + kWave * 4 + (size_t)P * per * 8);
-}
-// kMB: THROUGHPUT mode, sample k of pixel pi starts from its own stream
-// mb_state(tile, pi, k) instead of the chain's offset state.
-// s1d_lds: the group's stratified values are staged in LDS (else read from
-// their global records: large spp, e.g. config E's 1024).
-template <int P, bool kMB = false, bool kX = false>
-__device__ __forceinline__ void paths_group(const DevScene& sc, const RenderParams& rp, const WaveBufs& wb, int64_t slot_base,
-                            int64_t rec0, int64_t rec_end, Counters* __restrict__ ctr, unsigned char* wlds,
-                            int s1d_lds) {
-    const int lane = threadIdx.x & (kWave - 1);
-    const int n = rp.spp, ndims = rp.ndims, nl = sc.n_lights;
-    const int per = ndims * n;
-    PixelCache* pcs = (PixelCache*)wlds;
-    unsigned long long* pkey = (unsigned long long*)(wlds + P * sizeof(PixelCache));
-    // per-pixel metadata lives in LDS (not in per-lane register arrays)
-    PMeta* meta = (PMeta*)(wlds + paths_group_meta_off<P>());
-    Spec* Lslot = (Spec*)(wlds + paths_group_l_off<P>()) + lane;
-    Spec* aux = (Spec*)(wlds + paths_group_l_off<P>()) + kWave + 2 * lane;
-    uint32_t* rslot = (uint32_t*)(wlds + paths_group_l_off<P>() + 3 * kWave * sizeof(Spec)) + lane;
-    double* s1d = (double*)(wlds + paths_group_l_off<P>() + 3 * kWave * sizeof(Spec) + kWave * 4);
-    if (lane == 0) {
-        int cum = 0;
-        for (int j = 0; j < P; j++) {
-            const int64_t rec = rec0 + j;
-            PMeta m{0, 0, 0, 0, cum, 0};
-            if (rec < rec_end) {
-                const int64_t bslot = rec / wb.ppt, pi = rec % wb.ppt;
-                if (pi < wb.tile_npx[bslot]) {
-                    m.nv = wb.prec[rec].nvalid;
-                    m.hit = wb.prec[rec].hit;
-                    m.tile = (uint64_t)tile_of_slot(rp, slot_base + bslot);
-                    m.inc = pcg_inc_of(m.tile);
-                }
-            }
-            meta[j] = m;
-            cum += m.nv > 1 ? m.nv - 1 : 0;
-        }
-        meta[P].cum = cum;
-    }
-    wave_sync();
-    for (int idx = lane; s1d_lds && idx < P * per; idx += kWave) {
-        const int j = idx / per;
-        if (meta[j].nv > 0) s1d[idx] = wb.s1d[(rec0 + j) * wb.s1d_stride + (idx - j * per)];
-    }
-    if (lane < P) {
-        pkey[lane] = ~0ULL;
-        if (meta[lane].nv > 0) {
-            const PixelRec& pr = wb.prec[rec0 + lane];
-            pcs[lane].si = pr.si;
-            pcs[lane].b = pr.b;
-            if constexpr (kX) pcs[lane].x = pr.x;
-            pcs[lane].wo = pr.wo;
-            pcs[lane].hit = pr.hit;
-        }
-    }
-    wave_sync();
-    if (nl > 0 && lane < P * nl) {   // bounce-1 light samples, uLight = (0,0); lane = pixel * nl + light
-        const int j = lane / nl, l = lane - j * nl;
-        if (meta[j].nv > 0 && meta[j].hit && (kX ? bsdfx_nonspecular(pcs[j].b, pcs[j].x) : pcs[j].b.n_bxdfs > 0)) {
-            int pl = 0;
-            uint64_t traced = 0;
-            Spec ld = kX ? estimate_direct_x(sc, nullptr, pl, pcs[j].si, pcs[j].b, pcs[j].x, l, V2{0.0, 0.0}, &traced)
-                         : estimate_direct(sc, nullptr, pl, pcs[j].si, pcs[j].b, l, V2{0.0, 0.0}, &traced);
-            if (!pl && max_component(ld) > 10) pl = PBRT_PANIC_LD_GT_10;
-            pcs[j].ld[l] = ld;
-            pcs[j].ld_panic[l] = pl | (traced ? kLdTraced : 0);
-        }
-    }
-    wave_sync();
-    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
-    const int T = meta[P].cum;
-    int base = 0;
-    int w = -1, j = 0, k = 0;
-    PathStateLds ps;
-    ps.L = Lslot;
-    ps.aux = aux;
-    ps.rays = rslot;
-    Cursor c;
-    int pnc = 0, bnc = 1;
-    for (;;) {
-        const bool idle = w < 0;
-        const unsigned long long m = __ballot(idle);
-        if (idle) {
-            const int t = base + __popcll(m & lt_mask);
-            if (t < T) {
-                j = 0;
-#pragma unroll
-                for (int q = 1; q < P; q++) j += t >= meta[q].cum ? 1 : 0;
-                k = 1 + (t - meta[j].cum);
-                const int64_t rec = rec0 + j;
-                if (!meta[j].hit) {   // no traced bounce: the sample's radiance is 0
-                    double* o = wb.L + (rec * n + k) * 3;
-                    o[0] = 0.0;
-                    o[1] = 0.0;
-                    o[2] = 0.0;
-                    wb.rays[rec * n + k] = kRayClosest;   // the camera ray's (missed or maxDepth 1) query
-                } else {
-                    w = t;
-                    c.rng.state = kMB ? mb_state(meta[j].tile, (uint64_t)(rec % wb.ppt), (uint64_t)k)
-                                      : wb.memb[rec * n + k];
-                    c.rng.inc = meta[j].inc;
-                    c.draws = 0;
-                    c.cur1d = 1;   // camera: Get2D pFilm, Get2D pLens, Get1D time (stratified)
-                    c.cur2d = 2;
-                    c.k = k;
-                    c.kdep = 0;
-                    *ps.L = spec(0);
-                    *ps.rays = 0;
-                    ps.beta = spec(1);
-                    ps.eta_scale = 1.0;
-                    ps.bounces = 1;
-                    ps.first = 1;
-                    pnc = 0;
-                    bnc = 1;
-                }
-            }
-        }
-        base += __popcll(m);
-        if (!__any(w >= 0)) {
-            if (base >= T) break;
-            continue;
-        }
-        if (w >= 0) {
-            // a path taken this iteration runs its bounce 1 from the pixel cache
-            // (no traversal) and then, with every other live path, one traced
-            // bounce: the cheap first step does not cost the wave an iteration
-            const SpecSampler ss{s1d_lds ? s1d + j * per : wb.s1d + (rec0 + j) * wb.s1d_stride, n, ndims};
-            bool done = false;
-            if (ps.first)
-                done = path_step<1, kX>(sc, pcs[j], ss, c, ps, rp.max_depth, rp.rr_threshold, nullptr, pnc, bnc);
-            if (!done)
-                done = path_step<2, kX>(sc, pcs[j], ss, c, ps, rp.max_depth, rp.rr_threshold, nullptr, pnc, bnc);
-            if (done) {
-                const int64_t rec = rec0 + j;
-                double* o = wb.L + (rec * n + k) * 3;
-                const Spec Lp = *ps.L;
-                o[0] = Lp.r;
-                o[1] = Lp.g;
-                o[2] = Lp.b;
-                wb.rays[rec * n + k] = *ps.rays;
-                if (pnc)
-                    atomicMin(&pkey[j], ((unsigned long long)k << 32) | ((unsigned long long)(bnc & 0xFFFFFF) << 8) |
-                                            (unsigned long long)((pnc + 1) & 0xFF));
-                w = -1;
-            }
-        }
-    }
-    wave_sync();
-    if (lane < P && meta[lane].nv > 0) {
-        const int64_t rec = rec0 + lane;
-        const int64_t bslot = rec / wb.ppt, pi = rec % wb.ppt;
-        int64_t x0, y0, x1, y1;
-        tile_bounds(rp, tile_of_slot(rp, slot_base + bslot), x0, y0, x1, y1);
-        PanicRec p{0, 0, 0, 0, x0 + pi % (x1 - x0), y0 + pi / (x1 - x0)};
-        const int panic0 = wb.prec[rec].panic0;
-        if (panic0) {
-            p.kind = panic0;
-            p.sample = 1;
-            p.bounce = 1;
-        } else if (pkey[lane] != ~0ULL) {
-            p.kind = (int)(pkey[lane] & 0xFF) - 1;
-            p.bounce = (int)((pkey[lane] >> 8) & 0xFFFFFF);
-            p.sample = (int)(pkey[lane] >> 32);
-        }
-        wb.ppanic[rec] = p;
-        if (!p.kind && meta[lane].nv > 1) {
-            atomicAdd(&ctr->paths, (unsigned long long)(meta[lane].nv - 1));
-            atomicAdd(&ctr->camera_samples, (unsigned long long)(meta[lane].nv - 1));
-        }
-    }
-    wave_sync();   // the LDS block is reused by the wave's next group
-}
-
-template <int P, bool kMB = false, bool kX = false>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kPathsWaves, 8))) void k_paths_ci(
-    DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr,
-    int s1d_lds) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];   // paths_group_lds<P>
-    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;   // one wave per workgroup
-    stage_nodes(sc);
-    paths_group<P, kMB, kX>(sc, rp, wb, slot_base, (int64_t)blockIdx.x * P, nrec, ctr, lds, s1d_lds);
-}
-
-// ------------------------------------------------- path wavefront (k_pw_*)
-// The full-path stage (k_paths_ci's work: every (pixel, sample) path from its
-// RNG state, with light sampling) as per-bounce launches over queues of live
-// paths, compacted every bounce and, between the closest-hit trace and the
-// shading, counting-sorted by the hit's material (SURVEY §8 north_star: "rays
-// compacted and sorted by material between bounces"):
-//   k_pw_cache   bounce-1 EstimateDirect per (pixel, light), uLight = (0,0)
-//   k_pw_start   per path: bounce 1 from the pixel record (path_step<1>),
-//                then the next bounce's depth test -> trace queue or done
-//   k_pw_trace   closest hit of every queued ray; a miss or a panic ends the
-//                path, a hit goes to the hit queue with its material key
-//   k_pw_count / k_pw_scan / k_pw_scatter   counting sort of the hit queue
-//   k_pw_shade   interaction, BSDF, light-sample draws up to the shadow ray,
-//                BSDF sample, throughput and Russian roulette
-//   k_pw_shadow  the deferred shadow ray, L += beta0 * Ld, then the depth
-//                test -> trace queue or done
-//   k_pw_panics  per pixel record: its first panic (sample order) + counters
-// Each step is path_step<2>'s code split at its two traversals, in its order,
-// so L per (pixel, sample) is bit-identical to k_paths_ci's. Grid-stride
-// kernels read the queue lengths on the device (no host round trip).
-struct alignas(16) PwPath {
-    Ray ray;         // next closest-hit ray (tmax: after the walk, for prim_si)
-    Spec L, beta;
-    Ray sr;          // deferred shadow ray
-    Spec beta0, ld;  // its throughput and unoccluded Ld
-    V3 ph;           // object-space hit point of the closest hit
-    uint64_t rng;    // PCG32 state (the increment is the tile's)
-    int64_t rec;     // pixel record in the batch
-    int32_t k, cur1d, cur2d, kdep;
-    int32_t bounces, best, flags, pnc;
-    int32_t bnc;
-    uint32_t rays;   // kRayClosest / kRayShadow counts of the path
-    double eta;      // Path.Li's etaScale (kX)
-};
-constexpr int kPwPending = 1, kPwShadow = 2, kPwDone = 4;
-constexpr int kPwMaxKeys = 64;   // material keys of the sort (more materials share the last)
-struct PwQueues {
-    uint32_t* q[3];          // trace queue (current / next) and the hit queue, path ids
-    uint32_t* sorted;        // hit queue in material order
-    uint32_t* cnt;           // [0] trace, [1] next trace, [2] hits, [3..3+kPwMaxKeys) key counts, then offsets
-    int64_t cap;
-};
-__device__ __forceinline__ uint32_t pw_push(uint32_t* cnt, uint32_t* q, uint32_t v) {
-    const unsigned long long m = __ballot(1);
-    const int lead = __ffsll((long long)m) - 1, lane = threadIdx.x & (kWave - 1);
-    uint32_t base = 0;
-    if (lane == lead) base = atomicAdd(cnt, (uint32_t)__popcll(m));
-    base = __shfl(base, lead);
-    const uint32_t pos = base + (uint32_t)__popcll(m & ((1ULL << lane) - 1ULL));
-    q[pos] = v;
-    return pos;
-}
-// atomicAdd(&ctr[key], 1) for every active lane, aggregated per distinct key
-// of the wave (few materials: a handful of atomics per wave instead of one per
-// lane on the same few addresses); returns the lane's old-count position
-__device__ __forceinline__ uint32_t pw_add_by_key(uint32_t* ctr, int key) {
-    const int lane = threadIdx.x & (kWave - 1);
-    uint32_t pos = 0;
-    unsigned long long todo = __ballot(1);
-    for (;;) {
-        const int lead = __ffsll((long long)todo) - 1;
-        const int k0 = __shfl(key, lead);
-        const unsigned long long m = __ballot(key == k0) & todo;
-        uint32_t base = 0;
-        if (lane == lead) base = atomicAdd(&ctr[k0], (uint32_t)__popcll(m));
-        base = __shfl(base, lead);
-        if (key == k0 && ((todo >> lane) & 1ULL)) pos = base + (uint32_t)__popcll(m & ((1ULL << lane) - 1ULL));
-        todo &= ~m;
-        if (!todo) break;
-    }
-    return pos;
-}
-// a finished path: its radiance, and its panic into the pixel's key
-__device__ __forceinline__ void pw_finish(const WaveBufs& wb, int n, const PwPath& p, unsigned long long* pkey) {
-    double* o = wb.L + (p.rec * n + p.k) * 3;
-    o[0] = p.L.r;
-    o[1] = p.L.g;
-    o[2] = p.L.b;
-    wb.rays[p.rec * n + p.k] = p.rays;
-    if (p.pnc)
-        atomicMin(&pkey[p.rec], ((unsigned long long)p.k << 32) | ((unsigned long long)(p.bnc & 0xFFFFFF) << 8) |
-                                    (unsigned long long)((p.pnc + 1) & 0xFF));
-}
-// path_step's loop-top depth test; false: the path is done
-__device__ __forceinline__ bool pw_next_bounce(PwPath& p, int max_depth) {
-    p.bounces++;
-    p.bnc = p.bounces;
-    p.rays += kRayClosest;   // the reference's Intersect of this iteration (k_pw_trace, or the maxDepth break)
-    return p.bounces < max_depth;
-}
-// the bounce-1 light estimates of the pixel record (global-memory PixelCache)
-struct PwCache {
-    SI si;
-    BSDF b;
-    BSDFX x;
-    V3 wo;
-    const Spec* ld;
-    const int* ld_panic;
-};
-
-template <bool kX = false>
-__global__ __launch_bounds__(kWave) void k_pw_cache(DevScene sc, WaveBufs wb, int64_t rec0, int64_t nrec,
-                                                    Spec* __restrict__ ldc, int* __restrict__ ldp) {
-    __shared__ uint16_t stack_lds[64 * kStackStride];
-    stage_nodes(sc);
-    const int nl = sc.n_lights;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nrec * nl) return;
-    const int64_t r = i / nl;
-    const int l = (int)(i - r * nl);
-    const PixelRec& pr = wb.prec[rec0 + r];
-    if (!(pr.hit && (kX ? bsdfx_nonspecular(pr.b, pr.x) : pr.b.n_bxdfs > 0))) return;
-    int pl = 0;
-    uint64_t traced = 0;
-    const Spec ld = kX ? estimate_direct_x(sc, stack_lds + threadIdx.x, pl, pr.si, pr.b, pr.x, l, V2{0.0, 0.0}, &traced)
-                       : estimate_direct(sc, stack_lds + threadIdx.x, pl, pr.si, pr.b, l, V2{0.0, 0.0}, &traced);
-    if (!pl && max_component(ld) > 10) pl = PBRT_PANIC_LD_GT_10;
-    ldc[i] = ld;
-    ldp[i] = pl | (traced ? kLdTraced : 0);
-}
-
-template <bool kMB, bool kX = false>
-__global__ __launch_bounds__(kWave) void k_pw_start(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
-                                                    int64_t rec0, int64_t nrec, const Spec* __restrict__ ldc,
-                                                    const int* __restrict__ ldp, PwPath* __restrict__ paths,
-                                                    PwQueues qs, unsigned long long* __restrict__ pkey) {
-    const int n = rp.spp;
-    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (n < 2 || i >= nrec * (n - 1)) return;
-    const int64_t r = i / (n - 1);
-    const int k = 1 + (int)(i - r * (n - 1));
-    const int64_t rec = rec0 + r, bs = rec / wb.ppt, pi = rec % wb.ppt;
-    if (k == 1) pkey[rec] = ~0ULL;
-    if (pi >= wb.tile_npx[bs]) return;
-    const PixelRec& pr = wb.prec[rec];
-    if (k >= pr.nvalid) return;
-    PwPath p;
-    p.rec = rec;
-    p.k = k;
-    p.L = spec(0);
-    p.pnc = 0;
-    p.bnc = 1;
-    p.rays = kRayClosest;   // the camera ray's query
-    if (!pr.hit) {   // no traced bounce: the sample's radiance is 0
-        pw_finish(wb, n, p, pkey);
-        return;
-    }
-    const uint64_t tile = (uint64_t)tile_of_slot(rp, slot_base + bs);
-    Cursor c;
-    c.rng.state = kMB ? mb_state(tile, (uint64_t)pi, (uint64_t)k) : wb.memb[rec * n + k];
-    c.rng.inc = pcg_inc_of(tile);
-    c.draws = 0;
-    c.cur1d = 1;   // camera: Get2D pFilm, Get2D pLens, Get1D time (stratified)
-    c.cur2d = 2;
-    c.k = k;
-    c.kdep = 0;
-    PathState s;
-    s.L = spec(0);
-    s.beta = spec(1);
-    s.eta_scale = 1.0;
-    s.bounces = 1;
-    s.first = 1;
-    s.rays = 0;
-    const PwCache pc{pr.si, pr.b, pr.x, pr.wo, ldc + r * sc.n_lights, ldp + r * sc.n_lights};
-    const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, n, rp.ndims};
-    int pnc = 0, bnc = 1;
-    bool done = path_step<1, kX>(sc, pc, ss, c, s, rp.max_depth, rp.rr_threshold, nullptr, pnc, bnc);
-    p.L = s.L;
-    p.beta = s.beta;
-    p.eta = s.eta_scale;
-    p.ray = s.ray;
-    p.bounces = s.bounces;
-    p.rng = c.rng.state;
-    p.cur1d = c.cur1d;
-    p.cur2d = c.cur2d;
-    p.kdep = c.kdep;
-    p.pnc = pnc;
-    p.bnc = bnc;
-    p.rays = s.rays;   // path_step<1> counted the camera ray and its light sample
-    if (!done) done = !pw_next_bounce(p, rp.max_depth);
-    paths[i] = p;
-    if (done)
-        pw_finish(wb, n, p, pkey);
-    else
-        pw_push(&qs.cnt[0], qs.q[0], (uint32_t)i);
-}
-
-// in: trace queue `qin` (count cnt[cin]); out: hits (cnt[2], qs.q[2]) with
-// their material key counted in cnt[3 + key]
-__global__ __launch_bounds__(kWave) void k_pw_trace(DevScene sc, RenderParams rp, WaveBufs wb, PwPath* __restrict__ paths,
-                                                    PwQueues qs, int cin, int n_keys,
-                                                    unsigned long long* __restrict__ pkey) {
-    __shared__ uint16_t stack_lds[64 * kStackStride];
-    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
-    stage_nodes(sc);
-    const uint32_t* qin = qs.q[cin];
-    const uint32_t nq = qs.cnt[cin];
-    if (blockIdx.x == 0 && threadIdx.x == 0) qs.cnt[1] = 0;   // k_pw_shade's output, consumed after this pass's shadow step
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nq; t += gridDim.x * blockDim.x) {
-        const uint32_t id = qin[t];
-        PwPath& p = paths[id];
-        Ray ray = p.ray;
-        int panic = 0, best;
-        V3 ph{0, 0, 0};
-        const bool hit = bvh_walk<false>(sc, ray, stack_lds + threadIdx.x, panic, best, ph);
-        if (!hit || panic) {   // path_step: a miss or a traversal panic ends the path
-            if (panic) p.pnc = panic;
-            pw_finish(wb, rp.spp, p, pkey);
-            continue;
-        }
-        p.ray.tmax = ray.tmax;
-        p.best = best;
-        p.ph = ph;
-        int key = best < sc.n_prims ? sc.prims[best].material : sc.mesh.mesh_mat[tri_mesh(sc, best - sc.n_prims)];
-        key = min(max(key, 0), n_keys - 1);
-        p.flags = key;
-        pw_push(&qs.cnt[2], qs.q[2], id);
-        if (n_keys > 1) (void)pw_add_by_key(qs.cnt + 3, key);
-    }
-}
-// exclusive scan of the key counts into offsets (one thread; n_keys <= 64)
-__global__ void k_pw_scan(PwQueues qs, int n_keys) {
-    uint32_t acc = 0;
-    for (int k = 0; k < n_keys; k++) {
-        qs.cnt[3 + kPwMaxKeys + k] = acc;
-        acc += qs.cnt[3 + k];
-    }
-}
-__global__ __launch_bounds__(256) void k_pw_scatter(const PwPath* __restrict__ paths, PwQueues qs) {
-    const uint32_t nh = qs.cnt[2];
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nh; t += gridDim.x * blockDim.x) {
-        const uint32_t id = qs.q[2][t];
-        qs.sorted[pw_add_by_key(qs.cnt + 3 + kPwMaxKeys, paths[id].flags)] = id;
-    }
-}
-
-template <bool kX = false>
-__global__ __launch_bounds__(kWave) void k_pw_shade(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
-                                                    PwPath* __restrict__ paths, PwQueues qs, int sorted,
-                                                    unsigned long long* __restrict__ pkey) {
-    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
-    const uint32_t* qin = sorted ? qs.sorted : qs.q[2];
-    const uint32_t nh = qs.cnt[2];
-    const int n = rp.spp;
-    if (blockIdx.x == 0 && threadIdx.x == 0) qs.cnt[0] = 0;   // k_pw_shadow's output (this pass's trace has read it)
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nh; t += gridDim.x * blockDim.x) {
-        const uint32_t id = qin[t];
-        PwPath& p = paths[id];
-        SI isect;
-        prim_si(sc, p.best, p.ray, p.ph, isect);
-        BSDF b;
-        BSDFX x;
-        if ((kX ? compute_bsdf_x(sc, isect, b, x) : compute_bsdf(sc, isect, b)) < 0) {
-            p.pnc = -1;
-            pw_finish(wb, n, p, pkey);
-            continue;
-        }
-        const V3 wo = p.ray.d;
-        const int64_t bs = p.rec / wb.ppt;
-        Cursor c;
-        c.rng.state = p.rng;
-        c.rng.inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + bs));
-        c.draws = 0;
-        c.cur1d = p.cur1d;
-        c.cur2d = p.cur2d;
-        c.k = p.k;
-        c.kdep = p.kdep;
-        const SpecSampler ss{wb.s1d + p.rec * wb.s1d_stride, n, rp.ndims};
-        // path_step<2> after its closest-hit traversal (pbrt_spec.h)
-        int flags = 0;
-        const Spec beta0 = p.beta;
-        const int nl = sc.n_lights;
-        if (kX ? bsdfx_nonspecular(b, x) : b.n_bxdfs > 0) {   // UniformSampleOneLight (integrator.go:48-77)
-            if (nl == 0) {
-                p.L = p.L + smul(p.beta, spec(0));
-            } else {
-                int ln;
-                if (sc.dist) {
-                    double lpdf;
-                    ln = sample_discrete(*sc.dist, c_get1d(c, ss), lpdf);
-                } else {
-                    ln = (int)gomath::to_int(gomath::min(c_get1d(c, ss) * (double)nl, (double)(nl - 1)));
-                }
-                V2 ul = c_get2d(c, ss);
-                c_get2d(c, ss);
-                flags |= kPwPending;
-                Ray sr;
-                Spec ld_vis = spec(0);
-                if (kX ? estimate_direct_begin_x(sc, isect, b, x, ln, ul, sr, ld_vis)
-                       : estimate_direct_begin(sc, isect, b, ln, ul, sr, ld_vis))
-                    flags |= kPwShadow;
-                p.sr = sr;
-                p.ld = ld_vis;
-            }
-        }
-        {
-            V2 u = c_get2d(c, ss);
-            V3 wi;
-            double pdf;
-            int type = 0;
-            Spec f = kX ? bsdfx_sample_f(b, x, wo, u, wi, pdf, type) : bsdf_sample_f(b, wo, u, wi, pdf);
-            if (kX && type == -1) {   // rough glass: the reference's nil dereference (never routed here)
-                p.pnc = PBRT_PANIC_NIL_DEREF;
-                pw_finish(wb, n, p, pkey);
-                continue;
-            }
-            if (is_black(f) || pdf == 0.0) {
-                flags |= kPwDone;
-            } else {
-                double wp = absdot(wi, isect.sn) / pdf;
-                p.beta = smul(p.beta, smuls(f, wp));
-                if (kX && (type & BXDF_SPECULAR) && (type & BXDF_TRANSMISSION)) {   // path.go:106-117
-                    const double eta = x.eta;
-                    if (dot(wo, isect.n) > 0) p.eta *= eta * eta;
-                    else p.eta *= 1 / (eta * eta);
-                }
-                p.ray.o = offset_ray_origin(isect.p, isect.perr, isect.n, wi);
-                p.ray.d = wi;
-                p.ray.tmax = kInf;
-                p.ray.time = isect.time;
-                Spec rr = smuls(p.beta, kX ? p.eta : 1.0);
-                if (max_component(rr) < rp.rr_threshold && p.bounces > 3) {
-                    double q = gomath::max(0.05, 1 - max_component(rr));
-                    double u1 = c_get1d(c, ss);
-                    if (c.kdep || u1 < q) flags |= kPwDone;
-                    else p.beta = sdivs(p.beta, 1 - q);
-                }
-            }
-        }
-        p.beta0 = beta0;
-        p.rng = c.rng.state;
-        p.cur1d = c.cur1d;
-        p.cur2d = c.cur2d;
-        p.kdep = c.kdep;
-        p.flags = flags;
-        pw_push(&qs.cnt[1], qs.q[1], id);   // every shaded path passes the shadow step
-    }
-}
-
-// in: the shaded paths (cnt[1], q[1]); out: the next trace queue (cnt[0], q[0])
-__global__ __launch_bounds__(kWave) void k_pw_shadow(DevScene sc, RenderParams rp, WaveBufs wb,
-                                                     PwPath* __restrict__ paths, PwQueues qs,
-                                                     unsigned long long* __restrict__ pkey) {
-    __shared__ uint16_t stack_lds[64 * kStackStride];
-    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
-    stage_nodes(sc);
-    const uint32_t ns = qs.cnt[1];
-    if (blockIdx.x == 0)   // hits and key counts, for the next pass
-        for (int i = threadIdx.x; i < 1 + kPwMaxKeys; i += blockDim.x) qs.cnt[2 + i] = 0;
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < ns; t += gridDim.x * blockDim.x) {
-        const uint32_t id = qs.q[1][t];
-        PwPath& p = paths[id];
-        if (p.flags & kPwPending) {
-            Spec ld = spec(0);
-            if (p.flags & kPwShadow) {
-                int panic = 0;
-                Ray sr = p.sr;
-                p.rays += kRayShadow;
-                const bool occluded = bvh_traverse<true>(sc, sr, nullptr, stack_lds + threadIdx.x, panic);
-                if (panic) {
-                    p.pnc = panic;
-                    pw_finish(wb, rp.spp, p, pkey);
-                    continue;
-                }
-                if (!occluded) ld = p.ld;
-            }
-            if (max_component(ld) > 10) {
-                p.pnc = PBRT_PANIC_LD_GT_10;
-                pw_finish(wb, rp.spp, p, pkey);
-                continue;
-            }
-            p.L = p.L + smul(p.beta0, ld);
-        }
-        if ((p.flags & kPwDone) || !pw_next_bounce(p, rp.max_depth))
-            pw_finish(wb, rp.spp, p, pkey);
-        else
-            pw_push(&qs.cnt[0], qs.q[0], id);
-    }
-}
-
-// per pixel record: paths_group's epilogue (first panic in sample order, counters)
-__global__ void k_pw_panics(RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t rec0, int64_t nrec,
-                            const unsigned long long* __restrict__ pkey, Counters* __restrict__ ctr) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nrec) return;
-    const int64_t rec = rec0 + r, bs = rec / wb.ppt, pi = rec % wb.ppt;
-    if (pi >= wb.tile_npx[bs]) return;
-    int64_t x0, y0, x1, y1;
-    tile_bounds(rp, tile_of_slot(rp, slot_base + bs), x0, y0, x1, y1);
-    PanicRec p{0, 0, 0, 0, x0 + pi % (x1 - x0), y0 + pi / (x1 - x0)};
-    const PixelRec& pr = wb.prec[rec];
-    const unsigned long long key = rp.spp >= 2 ? pkey[rec] : ~0ULL;
-    if (pr.panic0) {
-        p.kind = pr.panic0;
-        p.sample = 1;
-        p.bounce = 1;
-    } else if (key != ~0ULL) {
-        p.kind = (int)(key & 0xFF) - 1;
-        p.bounce = (int)((key >> 8) & 0xFFFFFF);
-        p.sample = (int)(key >> 32);
-    }
-    wb.ppanic[rec] = p;
-    if (!p.kind && pr.nvalid > 1) {
-        atomicAdd(&ctr->paths, (unsigned long long)(pr.nvalid - 1));
-        atomicAdd(&ctr->camera_samples, (unsigned long long)(pr.nvalid - 1));
-    }
-}
-
-// THROUGHPUT mode setup for k_paths_ci<P, true>, one wave per pixel record:
-// StartPixel on the pixel's own stream mb_state(tile, pi, 0) and bounce 1
-// (camera ray, first hit, BSDF), written to the PixelRec / s1d buffers the
-// EXACT pipeline fills with k_wf_primary + k_chain_ci. The same arithmetic as
-// the serial kernel's pixel prologue.
-template <bool kX = false>
-__global__ __launch_bounds__(kWave) void k_mb_setup(DevScene sc, RenderParams rp, ChainLayout lay,
-                                                    const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
-                                                    int64_t nslots_batch) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    __shared__ uint16_t stack_lds[64 * kStackStride];
-    __shared__ uint64_t sh_state;
-    const int lane = threadIdx.x;
-    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
-    stage_nodes(sc);
-    const int64_t bslot = blockIdx.x / wb.ppt, pi = blockIdx.x % wb.ppt, rec = blockIdx.x;
-    if (bslot >= nslots_batch) return;
-    const int64_t tile = tile_of_slot(rp, slot_base + bslot);
-    int64_t x0, y0, x1, y1;
-    tile_bounds(rp, tile, x0, y0, x1, y1);
-    if (pi == 0 && lane == 0) wb.tile_npx[bslot] = (int32_t)((x1 - x0) * (y1 - y0));
-    if (pi >= (x1 - x0) * (y1 - y0)) return;
-    const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
-    const int n = rp.spp;
-    double* s1d = (double*)(lds + lay.s1d);
-    (void)start_pixel_wave(rp, *jump, mb_state((uint64_t)tile, (uint64_t)pi, 0), pcg_inc_of((uint64_t)tile), s1d,
-                           (uint16_t*)(lds + lay.other), (uint32_t*)(lds + lay.vbuf), &sh_state);
-    for (int idx = lane; idx < rp.ndims * n; idx += kWave) wb.s1d[rec * wb.s1d_stride + idx] = s1d[idx];
-    int panic0 = 0, hit = 0;
-    SI si0;
-    BSDF b0;
-    BSDFX bx0;
-    b0.n_bxdfs = 0;
-    bx0.kind = BXDF_KIND_LAMBERT;
-    bx0.n = 0;
-    Ray ray = camera_ray(*sc.camera, (double)px + 0.0, (double)py + 0.0, s1d[1 < n ? 1 : 0], V2{0.0, 0.0});
-    if (n > 1 && 1 < rp.max_depth) {
-        hit = bvh_traverse<false>(sc, ray, &si0, stack_lds + lane, panic0) ? 1 : 0;
-        if (!panic0 && hit && (kX ? compute_bsdf_x(sc, si0, b0, bx0) : compute_bsdf(sc, si0, b0)) < 0) panic0 = -1;
-    }
-    if (panic0) hit = 0;
-    if (lane == 0) {
-        PixelRec& pr = wb.prec[rec];
-        pr.si = si0;
-        pr.b = b0;
-        if constexpr (kX) pr.x = bx0;
-        pr.wo = ray.d;
-        pr.hit = hit;
-        pr.nvalid = n;
-        pr.panic0 = panic0;
-    }
-}
-
-// One thread per tile-film pixel: the tile film of the serial replay.
-__global__ __launch_bounds__(256) void k_film(const pbrt_film_desc* __restrict__ film_desc, RenderParams rp,
-                                              WaveBufs wb, int64_t slot_base, int64_t nslots_batch,
-                                              double* __restrict__ films, const int* __restrict__ cancel_seen) {
-    // a cancelled render's samples are incomplete: its film is not valid (pbrt_gpu_cancel)
-    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(cancel_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
-        return;
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t per = rp.slot_w * rp.slot_h;
-    if (gid >= nslots_batch * per) return;
-    const int64_t bslot = gid / per, fi = gid % per;
-    const int64_t slot = slot_base + bslot;
-    const pbrt_film_desc& film = *film_desc;
-    int64_t x0, y0, x1, y1, px0, py0, px1, py1;
-    tile_bounds(rp, tile_of_slot(rp, slot), x0, y0, x1, y1);
-    film_tile_bounds(film, x0, y0, x1, y1, px0, py0, px1, py1);
-    const int64_t tw = px1 - px0;
-    if (fi >= tw * (py1 - py0)) return;
-    const int64_t fx = px0 + fi % tw, fy = py0 + fi / tw;
-    const int n = rp.spp;
-    const int64_t npx = wb.tile_npx[bslot];
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-    // pixels whose footprint can reach (fx, fy): |p - f| < radius + 1, in row-major order
-    for (int64_t py = fy - 2; py <= fy + 2; py++) {
-        if (py < y0 || py >= y1) continue;
-        for (int64_t px = fx - 2; px <= fx + 2; px++) {
-            if (px < x0 || px >= x1) continue;
-            const int64_t pi = (py - y0) * (x1 - x0) + (px - x0);
-            if (pi >= npx) continue;
-            Footprint fp;
-            int64_t p0x, p0y, p1x, p1y;
-            footprint(film, (double)px + 0.0, (double)py + 0.0, px0, py0, px1, py1, fp, p0x, p0y, p1x, p1y);
-            const int64_t want = fi;
-            int f = -1;
-            for (int q = 0; q < fp.n; q++)
-                if (fp.off[q] == want) f = q;
-            if (f < 0) continue;
-            const double w = fp.w[f];
-            const int64_t rec = bslot * wb.ppt + pi;
-            const int nv = wb.prec[rec].nvalid;
-            const double* Lp = wb.L + rec * n * 3;
-            for (int k = 1; k < nv; k++) {
-                Spec Ls{Lp[k * 3 + 0], Lp[k * 3 + 1], Lp[k * 3 + 2]};
-                if (has_nans(Ls)) Ls = spec(0.1);   // integrator.go:256-262
-                if (0.0 > film.max_sample_luminance) Ls = smuls(Ls, film.max_sample_luminance / 0.0);
-                a0 += Ls.r * w;
-                a1 += Ls.g * w;
-                a2 += Ls.b * w;
-            }
-        }
-    }
-    double* tf = films + slot * per * 3 + fi * 3;
-    tf[0] = a0;
-    tf[1] = a1;
-    tf[2] = a2;
-}
-
-// First panic of each tile slot in pixel order -> panics[slot].
-__global__ void k_panic_reduce(WaveBufs wb, int64_t slot_base, int64_t nslots_batch, PanicRec* __restrict__ panics,
-                               Counters* __restrict__ ctr) {
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nslots_batch) return;
-    const int npx = wb.tile_npx[b];
-    for (int p = 0; p < npx; p++) {
-        const PanicRec& r = wb.ppanic[b * wb.ppt + p];
-        if (r.kind) {
-            panics[slot_base + b] = r;
-            atomicExch(&ctr->any_panic, 1);
-            return;
-        }
-    }
-}
-
-// Bounce 1 of every pixel record of the batch: the camera ray through the
-// pixel corner (pFilm and pLens are (0,0) for every sample), its closest hit
-// and BSDF. The ray time is patched by the chain kernel once StartPixel gives it.
-// stats.rays_closest / rays_shadow of a batch: every valid sample's counts
-// (pixels with records, samples 1 .. nvalid-1), one atomic pair per wave
-__global__ __launch_bounds__(256) void k_ray_count(WaveBufs wb, int64_t nb, int n, Counters* __restrict__ ctr,
-                                                   const int* __restrict__ cancel_seen) {
-    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(cancel_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
-        return;   // a cancelled render reports no counts
-    unsigned long long cl = 0, sh = 0;
-    const int64_t total = nb * wb.ppt * n;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t rec = i / n, k = i - rec * n, bs = rec / wb.ppt, pi = rec % wb.ppt;
-        if (k < 1 || pi >= wb.tile_npx[bs] || k >= wb.prec[rec].nvalid) continue;
-        const uint32_t v = wb.rays[i];
-        cl += v & 0xFFFFu;
-        sh += v >> 16;
-    }
-    for (int off = kWave / 2; off > 0; off >>= 1) {
-        cl += __shfl_down(cl, off);
-        sh += __shfl_down(sh, off);
-    }
-    if ((threadIdx.x & (kWave - 1)) == 0) {
-        atomicAdd(&ctr->closest_rays, cl);
-        atomicAdd(&ctr->shadow_rays, sh);
-    }
-}
-
-template <bool kX = false>
-__global__ __launch_bounds__(kWave) void k_wf_primary(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
-                                                      int64_t nb) {
-    __shared__ uint16_t stack_lds[64 * kStackStride];
-    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
-    stage_nodes(sc);
-    const int64_t rec = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (rec >= nb * wb.ppt) return;
-    const int64_t bs = rec / wb.ppt, pi = rec % wb.ppt;
-    int64_t x0, y0, x1, y1;
-    tile_bounds(rp, tile_of_slot(rp, slot_base + bs), x0, y0, x1, y1);
-    if (pi >= (x1 - x0) * (y1 - y0)) return;
-    const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
-    int panic0 = 0, hit0 = 0;
-    SI si0;
-    BSDF b0;
-    BSDFX bx0;
-    b0.n_bxdfs = 0;
-    bx0.kind = BXDF_KIND_LAMBERT;
-    bx0.n = 0;
-    Ray ray = camera_ray(*sc.camera, (double)px + 0.0, (double)py + 0.0, 0.0, V2{0.0, 0.0});
-    // Path.Li traces bounce 1 only below maxDepth (path.go:66); DirectLighting always
-    if (rp.spp > 1 && (1 < rp.max_depth || rp.integrator == PBRT_INTEGRATOR_DIRECT_LIGHTING)) {
-        hit0 = bvh_traverse<false>(sc, ray, &si0, stack_lds + threadIdx.x, panic0) ? 1 : 0;
-        if (!panic0 && hit0 && (kX ? compute_bsdf_x(sc, si0, b0, bx0) : compute_bsdf(sc, si0, b0)) < 0) panic0 = -1;
-    }
-    PixelRec& pr = wb.prec[rec];
-    pr.si = si0;
-    pr.b = b0;
-    if constexpr (kX) pr.x = bx0;
-    pr.wo = ray.d;
-    pr.hit = panic0 ? 0 : hit0;
-    pr.panic0 = panic0;
-    pr.nvalid = rp.spp;
-}
-
-// ------------------------------------------- DirectLighting, wave-parallel
-// DirectLighting.Li (directlighting.go:62-104) has no chain problem: with
-// n_dims >= 1 (and n_dims >= 2 or a pinhole camera) every sample of a pixel
-// traces the same camera ray, so hit or miss -- the only thing the number of
-// PCG32 draws of a sample depends on -- is per pixel, and sample k of the
-// pixel starts at the state after StartPixel advanced by (k - 1) * D.
-// k_dl_setup replays the tile's pixels in order (StartPixel, then jump-ahead
-// over the pixel's samples); k_dl_samples runs every (pixel, sample) at once.
-//
-// Draws of one DirectLighting sample (pixel.go:60-80 counters): the camera's
-// Get2D pFilm, Get2D pLens, Get1D time (camera.go via integrator.go:240-255),
-// then on a hit UniformSampleAllLights' two Get2D per light (clones carry no
-// sample arrays, #23) or UniformSampleOneLight's Get1D + 2 Get2D, then the two
-// Get2D of SpecularReflect / SpecularTransmit when maxDepth > 1.
-__device__ __forceinline__ uint32_t dl_draws(const RenderParams& rp, int hit, int n_lights) {
-    int c1 = 0, c2 = 0;
-    uint32_t d = 0;
-    auto g1 = [&]() { if (c1 < rp.ndims) c1++; else d += 1; };
-    auto g2 = [&]() { if (c2 < rp.ndims) c2++; else d += 2; };
-    g2();
-    g2();
-    g1();
-    if (hit) {
-        if (n_lights > 0) {
-            if (rp.dl_strategy == PBRT_DL_UNIFORM_SAMPLE_ALL) {
-                for (int j = 0; j < n_lights; j++) {
-                    g2();
-                    g2();
-                }
-            } else {
-                g1();
-                g2();
-                g2();
-            }
-        }
-        if (1 < rp.max_depth) {
-            g2();
-            g2();
-        }
-    }
-    return d;
-}
-
-// One wave per tile slot: the tile's pixels in order. Leaves each pixel's
-// stratified values in wb.s1d, the PCG32 state of each of its samples in
-// wb.memb (slot 0 of a pixel: its panic key, reset here), and the pixels
-// with records in wb.tile_npx (a camera-ray panic ends the tile, as in
-// k_chain_ci). THROUGHPUT mode: each pixel and sample on its own stream.
-__global__ __launch_bounds__(kWave) void k_dl_setup(DevScene sc, RenderParams rp, ChainLayout lay,
-                                                    const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
-                                                    int64_t nb) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    __shared__ uint64_t sh_state;
-    const int64_t bs = blockIdx.x;
-    const int lane = threadIdx.x;
-    if (bs >= nb || cancel_requested(sc, (bs & 63) == 0)) return;
-    const PcgJump& J = *jump;
-    const int64_t tile = tile_of_slot(rp, slot_base + bs);
-    int64_t x0, y0, x1, y1;
-    tile_bounds(rp, tile, x0, y0, x1, y1);
-    const int64_t npx = (x1 - x0) * (y1 - y0);
-    const uint64_t inc = pcg_inc_of((uint64_t)tile);
-    const bool mb = rp.mode == PBRT_MODE_THROUGHPUT;
-    const int n = rp.spp;
-    double* s1d = lay.s1d >= 0 ? (double*)(lds + lay.s1d) : nullptr;
-    uint16_t* other = (uint16_t*)(lds + lay.other);
-    uint32_t* vbuf = (uint32_t*)(lds + lay.vbuf);
-    Pcg seed;
-    pcg_seed(seed, (uint64_t)tile);   // Sampler.Clone(tile), integrator.go:318,328
-    uint64_t S = seed.state;
-    int64_t used = npx;
-    for (int64_t pi = 0; pi < npx; pi++) {
-        if (cancel_requested(sc, (pi & 15) == 0)) {   // pbrt_gpu_cancel (large spp: a pixel's StartPixel is long)
-            used = pi;
-            break;
-        }
-        const int64_t rec = bs * wb.ppt + pi;
-        double* gs1d = wb.s1d + rec * wb.s1d_stride;
-        double* sp = s1d ? s1d : gs1d;
-        const uint64_t S1 =
-            start_pixel_wave(rp, J, mb ? mb_state((uint64_t)tile, (uint64_t)pi, 0) : S, inc, sp, other, vbuf, &sh_state);
-        if (s1d)
-            for (int idx = lane; idx < rp.ndims * n; idx += kWave) gs1d[idx] = s1d[idx];
-        PixelRec& pr = wb.prec[rec];
-        const int hit = pr.hit, panic0 = pr.panic0;
-        const uint64_t D = dl_draws(rp, hit, sc.n_lights);
-        uint64_t* mst = wb.memb + rec * n;
-        for (int k = 1 + lane; k < n; k += kWave)
-            mst[k] = mb ? mb_state((uint64_t)tile, (uint64_t)pi, (uint64_t)k) : pcg_advance(J, S1, inc, (uint64_t)(k - 1) * D);
-        if (lane == 0) {
-            mst[0] = ~0ULL;
-            if (hit) {   // the camera ray's time (Get1D, dim 0) of the pixel's first traced sample
-                const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
-                pr.si.time = camera_ray(*sc.camera, (double)px, (double)py, sp[1 < n ? 1 : 0], V2{0.0, 0.0}).time;
-            }
-            pr.nvalid = n;
-        }
-        __syncthreads();   // the StartPixel staging is reused by the next pixel
-        if (panic0) {      // its first traced sample panics at bounce 1: the tile ends here
-            used = pi + 1;
-            break;
-        }
-        S = pcg_advance(J, S1, inc, (uint64_t)(n - 1) * D);
-    }
-    if (lane == 0) wb.tile_npx[bs] = (int32_t)used;
-}
-
-// One lane per (pixel record, traced sample): DirectLighting.Li at depth 0
-// from the pixel's bounce-1 record, with the sample's own PCG32 state.
-// Radiance to wb.L; a panic lowers the pixel's key (sample << 32 | kind + 1)
-// in wb.memb[rec * spp + 0] (the first panic in sample order wins).
-__global__ __launch_bounds__(kWave) void k_dl_samples(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
-                                                      int64_t nrec) {
-    __shared__ uint16_t stack_lds[64 * kStackStride];
-    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
-    stage_nodes(sc);
-    const int n = rp.spp;
-    if (n < 2) return;
-    // grid-stride over every (pixel record, sample): a bounded grid, so a cancel
-    // (polled every 16 passes) ends the kernel quickly at any spp
-    const int64_t total = nrec * (n - 1), stride = (int64_t)gridDim.x * blockDim.x;
-    int pass = 0;
-    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx - threadIdx.x < total; idx += stride) {
-        if ((++pass & 15) == 0 && cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
-        if (idx >= total) continue;
-        const int64_t rec = idx / (n - 1);
-        const int k = 1 + (int)(idx - rec * (n - 1));
-        const int64_t bs = rec / wb.ppt, pi = rec % wb.ppt;
-        if (pi >= wb.tile_npx[bs]) continue;
-        const PixelRec& pr = wb.prec[rec];
-        double* o = wb.L + (rec * n + k) * 3;
-        Spec L = spec(0);
-        int panic = pr.panic0;
-        uint64_t shadow = 0;   // visibility rays traced (the camera ray's query is counted below)
-        if (!panic && pr.hit) {
-            Cursor c;
-            c.rng.state = wb.memb[rec * n + k];
-            c.rng.inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + bs));
-            c.draws = 0;
-            c.cur1d = c.cur2d = 0;
-            c.k = k;
-            c.kdep = 0;
-            const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, n, rp.ndims};
-            c_get2d(c, ss);   // camera: pFilm, pLens, time
-            c_get2d(c, ss);
-            c_get1d(c, ss);
-            L = L + spec(0);   // si.Le(si.Wo): no primitive carries an area light
-            const int nl = sc.n_lights;
-            if (nl > 0) {
-                if (rp.dl_strategy == PBRT_DL_UNIFORM_SAMPLE_ALL) {   // integrator.go:23-46
-                    Spec acc = spec(0);
-                    for (int j = 0; j < nl && !panic; j++) {
-                        const V2 ul = c_get2d(c, ss);
-                        c_get2d(c, ss);
-                        acc = acc + estimate_direct(sc, stack_lds + threadIdx.x, panic, pr.si, pr.b, j, ul, &shadow);
-                    }
-                    L = L + acc;
-                } else {   // UniformSampleOneLight with no distribution (integrator.go:48-77)
-                    const int ln = (int)gomath::to_int(gomath::min(c_get1d(c, ss) * (double)nl, (double)(nl - 1)));
-                    const V2 ul = c_get2d(c, ss);
-                    c_get2d(c, ss);
-                    const Spec s = estimate_direct(sc, stack_lds + threadIdx.x, panic, pr.si, pr.b, ln, ul, &shadow);
-                    if (!panic && max_component(s) > 10) panic = PBRT_PANIC_LD_GT_10;
-                    L = L + s;
-                }
-            }
-            // SpecularReflect / SpecularTransmit: black for a Lambertian-only BSDF
-        }
-        o[0] = L.r;
-        o[1] = L.g;
-        o[2] = L.b;
-        wb.rays[rec * n + k] = kRayClosest + (uint32_t)shadow * kRayShadow;
-        if (panic)
-            atomicMin((unsigned long long*)&wb.memb[rec * n],
-                      ((unsigned long long)k << 32) | (unsigned long long)((panic + 1) & 0xFF));
-
-    }
-}
-
-// Per pixel record: its first panic (sample order) -> wb.ppanic, and the
-// traced-path counters of pixels that finish (as paths_group counts them).
-__global__ void k_dl_panics(RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr) {
-    const int64_t rec = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (rec >= nrec) return;
-    const int64_t bs = rec / wb.ppt, pi = rec % wb.ppt;
-    if (pi >= wb.tile_npx[bs]) return;
-    int64_t x0, y0, x1, y1;
-    tile_bounds(rp, tile_of_slot(rp, slot_base + bs), x0, y0, x1, y1);
-    PanicRec p{0, 0, 0, 0, x0 + pi % (x1 - x0), y0 + pi / (x1 - x0)};
-    const uint64_t key = rp.spp >= 2 ? wb.memb[rec * rp.spp] : ~0ULL;
-    if (wb.prec[rec].panic0) {
-        p.kind = wb.prec[rec].panic0;
-        p.sample = 1;
-        p.bounce = 1;
-    } else if (key != ~0ULL) {
-        p.kind = (int)(key & 0xFF) - 1;
-        p.sample = (int)(key >> 32);
-        p.bounce = 1;
-    }
-    wb.ppanic[rec] = p;
-    if (!p.kind && rp.spp > 1) {
-        atomicAdd(&ctr->paths, (unsigned long long)(rp.spp - 1));
-        atomicAdd(&ctr->camera_samples, (unsigned long long)(rp.spp - 1));
-    }
-}
-
-// Cold-frame schedule of k_chain_ci. Workgroups start in launch order, so a
-// heavy tile launched late stretches the frame; a context that has rendered
-// this configuration before orders its tiles by their measured chain times
-// (heaviest first). A fresh context (internal/render/server.go builds one per
-// RPC) estimates them instead: one wave per tile slot runs kProbes trajectories
-// per pixel from the pixel's bounce-1 record (k_wf_primary) at pseudo-random
-// PCG32 states, exactly the work a chain candidate does (traj_scatter), and
-// prices the slot as
-//   cost = traced_spp * mean(D * bounces) summed over the hit pixels   (chain lane-bounces)
-//        + kCostPixel * pixels                                         (StartPixel)
-// Only the launch order depends on it, never a result. Writes the features
-// (feat[4 * slot]: work, hit pixels, pixels, cost) and the sort key
-// (~cost bits << 32 | slot: ascending = heaviest first).
-constexpr int kProbes = 2;
-constexpr double kCostPixel = 150.0;   // one StartPixel ~ this many trajectory bounces of one lane
-template <bool kX = false>
-__global__ __launch_bounds__(kWave) void k_tile_cost(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
-                                                     int64_t nb, float* __restrict__ feat,
-                                                     uint64_t* __restrict__ keys) {
-    __shared__ uint16_t stack_lds[64 * kStackStride];
-    if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
-    stage_nodes(sc);
-    const int64_t bs = blockIdx.x;
-    const int lane = threadIdx.x;
-    if (bs >= nb) return;
-    const int64_t tile = tile_of_slot(rp, slot_base + bs);
-    int64_t x0, y0, x1, y1;
-    tile_bounds(rp, tile, x0, y0, x1, y1);
-    const int64_t npx = (x1 - x0) * (y1 - y0);
-    const uint64_t inc = pcg_inc_of((uint64_t)tile);
-    const SpecSampler ss{nullptr, rp.spp, rp.ndims};   // k < 0: stratified values are never read
-    double work = 0;
-    int hits = 0;
-    for (int64_t it = lane; it < npx * kProbes; it += kWave) {
-        const int64_t pi = it / kProbes;
-        const PixelRec& pr = wb.prec[bs * wb.ppt + pi];
-        if (!pr.hit) continue;
-        hits += (it % kProbes) == 0;
-        Cursor c;
-        c.rng.state = mb_state((uint64_t)tile, (uint64_t)pi, 0x70726f6265ULL + (uint64_t)(it % kProbes));
-        c.rng.inc = inc;
-        c.draws = 0;
-        c.cur1d = 1;
-        c.cur2d = 2;
-        c.k = -1;
-        c.kdep = 0;
-        Spec beta = spec(1);
-        double eta_scale = 1.0;
-        int bounces = 1;
-        Ray ray;
-        int r = traj_scatter<kX>(sc, pr.si, pr.b, pr.x, pr.wo, c, ss, beta, eta_scale, bounces, ray, rp.max_depth,
-                                 rp.rr_threshold);
-        while (r == 0) {
-            SI si;
-            int panic = 0;
-            if (!bvh_traverse<false>(sc, ray, &si, stack_lds + lane, panic) || panic) break;
-            BSDF b;
-            BSDFX x;
-            if ((kX ? compute_bsdf_x(sc, si, b, x) : compute_bsdf(sc, si, b)) < 0) break;
-            r = traj_scatter<kX>(sc, si, b, x, ray.d, c, ss, beta, eta_scale, bounces, ray, rp.max_depth,
-                                 rp.rr_threshold);
-        }
-        work += (double)c.draws * (double)bounces;
-    }
-    for (int o = kWave / 2; o > 0; o >>= 1) {
-        work += __shfl_xor(work, o);
-        hits += __shfl_xor(hits, o);
-    }
-    if (lane == 0) {
-        const double w = work / kProbes * (double)(rp.spp - 1);
-        const float cost = (float)(w + kCostPixel * (double)npx);
-        feat[4 * bs + 0] = (float)w;
-        feat[4 * bs + 1] = (float)hits;
-        feat[4 * bs + 2] = (float)npx;
-        feat[4 * bs + 3] = cost;
-        keys[bs] = ((uint64_t)~__float_as_uint(cost) << 32) | (uint64_t)bs;
-    }
-}
-__global__ void k_order_of_keys(const uint64_t* __restrict__ keys, int64_t nb, uint32_t* __restrict__ order) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nb) order[i] = (uint32_t)keys[i];
-}
-
-// ------------------------------------------- continuous-issue offset chain
-// k_chain_ci replaced round 1's fixed 64-candidate windows: a window lasts as
-// long as its longest trajectory (~6.5 bounces for a 2.25-bounce mean), so
-// most lanes idle through most of it. Here a lane that finishes a
-// trajectory, or whose candidate the chain has jumped over, takes the next
-// unissued offset at once: every bounce step keeps every lane busy, and
-// candidates left behind by the chain are dropped mid-trajectory.
-//
-// Per lane group (L = 64 / G lanes = one tile): a ring of resolved offsets
-// {offset, D, PCG state} in LDS; the group leader walks the exact chain
-// head -> head + D(head) through it after every step. Offsets are relative
-// to the pixel's first sample (the state after StartPixel). Candidates are
-// issued at head + even offsets; when D is odd the parity of the chain flips
-// and the group's in-flight candidates are dropped. A speculative result
-// that is not usable at the head (a panic or a draw count that depends on
-// the sample index) is re-run there with the sample index known; an exact
-// panic ends the tile at that sample. Bit-identical to the
-// serial replay: only the schedule changes.
-#ifndef PBRT_CI_EU_WAVES
-#define PBRT_CI_EU_WAVES 2   // k_chain_ci waves/SIMD (build option)
-#endif
-#ifndef PBRT_CHAIN_LB
-#define PBRT_CHAIN_LB 1   // leaf boxes per scan iteration in k_chain_ci's traversal (build option)
-#endif
-constexpr uint32_t kNoOff = 0xFFFFFFFFu;
-constexpr uint32_t kBadSpecD = 0xFFFFFFFEu;   // speculative lane could not resolve D
-constexpr uint32_t kBadExactD = 0xFFFFFFFDu;  // the exact head's trajectory panics
-struct RingEnt {
-    uint32_t tag;   // offset this entry resolves (kNoOff: empty)
-    uint32_t d;     // its draw count D, or kBadSpecD / kBadExactD
-    uint64_t st;    // PCG32 state at the offset
-};
-struct CiGroup {
-    uint64_t S;     // PCG32 state at the current pixel's first sample (offset 0)
-    int64_t pi;     // current pixel (row-major index in the tile)
-    int64_t npx;    // pixels of the tile
-    uint32_t head;  // offset of sample kh
-    uint32_t nxt;   // next offset to issue (same parity as head)
-    int kh;         // next sample without an offset
-    int phase;      // 0 needs a pixel, 1 resolving offsets, 2 tile finished
-    int reissue;    // the head must be re-run with its sample index known
-    int pad;
-};
-
-//
-// kW > 1: one tile per workgroup of kW waves (lanes_per_tile = 64 * kW). The
-// tile's chain then advances kW times as many candidates per step, which cuts
-// the slowest tile's latency, the frame's critical path when tiles are few
-// per GPU (a multi-GPU shard). Idle lanes are ranked across the waves through
-// LDS; StartPixel runs on the first wave.
-// kDepth: traversal stack entries per lane. Trees of <= kLdsNodes (64) nodes
-// are staged in LDS and walk their leaves only (no stack); larger trees walk
-// with the reference's [64] stack (bvh.go:670).
-template <int kW, int kDepth = 0, bool kX = false>
-__global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT_CI_EU_WAVES, 8))) void k_chain_ci(
-    DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
-    int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr,
-    const uint32_t* __restrict__ order, uint32_t* __restrict__ ticks, int cstride) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const uint64_t t_begin = wall_clock64();
-    const uint32_t cs = cstride == 1 ? 1u : 2u;   // candidate offsets head + cs * j
-    constexpr int kT = kWave * kW;   // threads per workgroup (stack stride)
-    // kDepth 0: an LDS-staged tree, walked without a stack (no stack array)
-    __shared__ uint16_t stack_lds[kDepth > 0 ? kDepth * kT : 1];
-#ifdef PBRT_CI_DENSE_WALK
-    // bvh_walk_dense's per-wave scratch (LDS-staged trees only)
-    __shared__ __attribute__((aligned(16))) unsigned char dense_lds[kDepth > 0 ? 16 : kW * kDenseScratch];
-#endif
-    __shared__ CiGroup gs[kCiMaxGroups];
-    __shared__ uint64_t sh_state;
-    __shared__ int wcnt[kW];
-#ifdef PBRT_CI_DIAG
-    __shared__ uint32_t dh[64];   // on-chain D histogram of the block (diagnostics)
-#endif
-    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
-    stage_nodes(sc);
-    const int L = kW > 1 ? kT : lanes_per_tile, G = kW > 1 ? 1 : kWave / L;
-    const int g = kW > 1 ? 0 : lane / L, gl = kW > 1 ? tid : lane - g * L;
-    // workgroup -> tile slot: heaviest-first order from the previous frame
-    // (one tile per workgroup only), else the identity
-    const int64_t blk = order ? (int64_t)order[blockIdx.x] : (int64_t)blockIdx.x;
-    const uint32_t R = (uint32_t)ring_size;   // a power of two (host: 256 / G or 256 * kW entries)
-    const PcgJump& J = *jump;
-    // StartPixel's values: staged in LDS, or (lay.s1d < 0: large spp, serial
-    // StartPixel) written by it straight to the pixel's global record
-    double* s1d = lay.s1d >= 0 ? (double*)(lds + lay.s1d) : nullptr;
-    uint16_t* other = (uint16_t*)(lds + lay.other);
-    uint32_t* vbuf = (uint32_t*)(lds + lay.vbuf);
-    RingEnt* ring = (RingEnt*)(lds + lay.ring) + (size_t)g * R;
-    ChainCache* pcs = (ChainCache*)(lds + lay.pcs);
-    uint16_t* stack = stack_lds + tid;
-    const int n = rp.spp, ndims = rp.ndims;
-    const pbrt_camera_desc& cam = *sc.camera;
-    const unsigned long long gmask = L >= 64 ? ~0ULL : (((1ULL << (L & 63)) - 1ULL) << (g * L));
-    const unsigned long long lt_mask = (1ULL << lane) - 1ULL;
-    const int64_t bs = blk * G + g;
-    const uint64_t inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + (bs < nslots_batch ? bs : 0)));
-#ifdef PBRT_CI_DIAG   // diagnostics build (make diag): steps, lane-0 phase clocks, on-chain D histogram
-    unsigned long long steps = 0;
-    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    long long tprev = clock64();
-    auto mark = [&](int k) {
-        long long now = clock64();
-        ph[k] += (unsigned long long)(now - tprev);
-        tprev = now;
-    };
-    if (tid < 64) dh[tid] = 0;
-#define CI_DIAG(x) x
-#else
-    auto mark = [](int) {};
-#define CI_DIAG(x)
-#endif
-    if (tid < G) {
-        const int64_t b = blk * G + tid;
-        CiGroup& s = gs[tid];
-        s.pi = 0;
-        s.kh = 1;
-        s.head = s.nxt = 0;
-        s.reissue = 0;
-        if (b < nslots_batch) {
-            int64_t x0, y0, x1, y1;
-            tile_bounds(rp, tile_of_slot(rp, slot_base + b), x0, y0, x1, y1);
-            Pcg seed;
-            pcg_seed(seed, (uint64_t)tile_of_slot(rp, slot_base + b));   // Sampler.Clone(tile), integrator.go:318,328
-            s.S = seed.state;
-            s.npx = (x1 - x0) * (y1 - y0);
-            s.phase = s.npx > 0 ? 0 : 2;
-            wb.tile_npx[b] = 0;
-        } else {
-            s.S = 0;
-            s.npx = 0;
-            s.phase = 2;
-        }
-    }
-    __syncthreads();
-
-    uint32_t cancel_poll = 0;   // chain steps since the leader last read the cancel flag
-    uint64_t last_host_poll = t_begin;   // when this workgroup last read the host flag
-    // lane trajectory state
-    uint32_t off = kNoOff;
-    uint64_t st0 = 0;
-    bool tracing = false;
-    Cursor c;
-    c.rng.state = 0;
-    c.rng.inc = inc;
-    c.draws = 0;
-    c.cur1d = c.cur2d = 0;
-    c.k = -1;
-    c.kdep = 0;
-    Spec beta = spec(1);
-    double eta_scale = 1.0;
-    int bounces = 1;
-    Ray ray;
-    ray.o = ray.d = V3{0, 0, 0};
-    ray.tmax = kInf;
-    ray.time = 0;
-
-    for (;;) {
-        // ---- (1) groups that need a pixel: StartPixel + bounce 1, one group at a time
-        for (int q = 0; q < G; q++) {
-            while (gs[q].phase == 0) {
-                const int64_t bq = blk * G + q;
-                const int64_t tile = tile_of_slot(rp, slot_base + bq);
-                const uint64_t incq = pcg_inc_of((uint64_t)tile);
-                const int64_t pi = gs[q].pi;
-                const int64_t rec = bq * wb.ppt + pi;
-                int64_t x0, y0, x1, y1;
-                tile_bounds(rp, tile, x0, y0, x1, y1);
-                const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
-                double* gs1d = wb.s1d + rec * wb.s1d_stride;
-                double* sp = s1d ? s1d : gs1d;
-                const uint64_t S1 = start_pixel_wave(rp, J, gs[q].S, incq, sp, other, vbuf, &sh_state);
-                if (s1d)
-                    for (int idx = tid; idx < ndims * n; idx += kT) gs1d[idx] = s1d[idx];
-                // the first traced sample's camera time value (read before the ring
-                // clear: with one tile per workgroup the StartPixel staging aliases the ring)
-                const double time_u = sp[1 < n ? 1 : 0];
-                __syncthreads();
-                RingEnt* rq = (RingEnt*)(lds + lay.ring) + (size_t)q * R;
-                for (uint32_t i = (uint32_t)tid; i < R; i += kT) rq[i].tag = kNoOff;
-                // bounce 1 (camera ray, first hit, BSDF) was computed for every
-                // pixel record by k_wf_primary; only the ray time needs StartPixel
-                PixelRec& pr = wb.prec[rec];
-                const int hit0 = pr.hit, panic0 = pr.panic0;
-                if (tid == 0) {   // pbrt_gpu_cancel: every group of the workgroup ends
-                    const uint64_t now = wall_clock64();
-                    const bool host = now - last_host_poll >= 100000;   // 1 ms at 100 MHz
-                    if (host) last_host_poll = now;
-                    if (cancel_requested(sc, host))
-                        for (int q2 = 0; q2 < G; q2++) gs[q2].phase = 2;
-                }
-                if (tid == 0 && gs[q].phase == 0) {
-                    if (hit0)   // the camera ray's time (Get1D after pFilm, pLens) of the pixel's first traced sample
-                        pr.si.time = camera_ray(cam, (double)px, (double)py, time_u, V2{0.0, 0.0}).time;
-                    pcs[q].si = pr.si;
-                    pcs[q].b = pr.b;
-                    if constexpr (kX) pcs[q].x = pr.x;
-                    pcs[q].wo = pr.wo;
-                    pcs[q].hit = hit0;
-                    CiGroup& s = gs[q];
-                    s.S = S1;
-                    s.head = s.nxt = 0;
-                    s.kh = 1;
-                    s.reissue = 0;
-                    wb.tile_npx[bq] = (int32_t)(pi + 1);
-                    if (panic0) {   // the first traced sample panics at bounce 1: the tile ends here
-                        s.phase = 2;
-                    } else if (hit0) {
-                        s.phase = 1;
-                    } else {   // no traced bounce: every sample is black and draws nothing
-                        s.pi = pi + 1;
-                        s.phase = s.pi < s.npx ? 0 : 2;
-                    }
-                }
-                __syncthreads();
-            }
-        }
-        mark(0);
-        bool any_chain = false;
-        for (int q = 0; q < G; q++) any_chain |= gs[q].phase == 1;
-        if (!any_chain) break;
-        CI_DIAG(steps++;)
-
-        // ---- (2) idle lanes take the next offsets of their group
-        const CiGroup sg = gs[g];
-        const int64_t rec = bs * wb.ppt + sg.pi;
-        const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, n, ndims};
-        {
-            const bool idle = sg.phase == 1 && off == kNoOff;
-            const unsigned long long m = __ballot(idle) & gmask;
-            int nidle = __popcll(m);
-            int rank = __popcll(m & lt_mask);
-            if (kW > 1) {   // rank the idle lanes across the tile's waves
-                if (lane == 0) wcnt[wv] = nidle;
-                __syncthreads();
-                int before = 0, tot = 0;
-                for (int w = 0; w < kW; w++) {
-                    const int cw = wcnt[w];
-                    before += w < wv ? cw : 0;
-                    tot += cw;
-                }
-                rank += before;
-                nidle = tot;
-            }
-            const int re = (sg.reissue && nidle > 0) ? 1 : 0;
-            const uint32_t nx0 = sg.nxt;
-            // offsets < head + R keep the ring collision-free
-            const int avail = nx0 < sg.head + R ? (int)((sg.head + R - nx0 + cs - 1) / cs) : 0;
-            const int nspec = min(nidle - re, avail);
-            uint32_t o = kNoOff;
-            bool exact = false;
-            if (idle) {
-                if (re && rank == 0) {
-                    o = sg.head;
-                    exact = true;
-                } else {
-                    rank -= re;
-                    if (rank < nspec) o = nx0 + cs * (uint32_t)rank;
-                }
-            }
-            if (gl == 0 && sg.phase == 1) {
-                gs[g].nxt = nx0 + cs * (uint32_t)max(nspec, 0);
-                CI_DIAG(ph[5] += (unsigned long long)(max(nspec, 0) + re);)   // candidate trajectories issued
-                if (re) gs[g].reissue = 0;
-            }
-            if (o != kNoOff) {
-                off = o;
-                st0 = pcg_advance(J, sg.S, inc, (uint64_t)o);
-                c.rng.state = st0;
-                c.draws = 0;
-                c.cur1d = 1;   // camera: Get2D pFilm, Get2D pLens, Get1D time (stratified)
-                c.cur2d = 2;
-                c.k = exact ? sg.kh : -1;
-                c.kdep = 0;
-                beta = spec(1);
-                eta_scale = 1.0;
-                bounces = 1;
-                const ChainCache& pc = pcs[g];
-                const int r = traj_scatter<kX>(sc, pc.si, pc.b, pc.x, pc.wo, c, ss, beta, eta_scale, bounces, ray,
-                                               rp.max_depth, rp.rr_threshold);
-                tracing = r == 0;
-                if (r != 0) {
-                    RingEnt& e = ring[off & (R - 1u)];
-                    e.st = st0;
-                    e.d = r == 1 ? c.draws : (c.k >= 0 ? kBadExactD : kBadSpecD);
-                    e.tag = off;
-                    off = kNoOff;
-                }
-            }
-        }
-        mark(1);
-        // ---- (3) one bounce of every live trajectory
-#ifdef PBRT_CI_DENSE_WALK   // experiment build: the whole wave walks together (dense leaf tests)
-        const bool dense = kDepth == 0 && sc.dense_ok && sc.use_lds_nodes;
-        int panic = 0, best = -1;
-        V3 ph{0, 0, 0};
-        if (dense) bvh_walk_dense(sc, ray, tracing, panic, best, ph, dense_lds + (size_t)wv * kDenseScratch);
-        if (tracing) {
-            if (!dense) bvh_walk<false, kT, PBRT_CHAIN_LB>(sc, ray, stack, panic, best, ph);
-#else
-        if (tracing) {
-            int panic = 0, best;
-            V3 ph;
-            bvh_walk<false, kT, PBRT_CHAIN_LB>(sc, ray, stack, panic, best, ph);
-#endif
-            mark(2);
-            uint32_t d = kNoOff;
-            if (panic) {
-                d = c.k >= 0 ? kBadExactD : kBadSpecD;
-            } else if (best < 0) {
-                d = c.draws;
-            } else {
-                SI si;
-                prim_si(sc, best, ray, ph, si);
-                BSDF b;
-                BSDFX x;
-                if ((kX ? compute_bsdf_x(sc, si, b, x) : compute_bsdf(sc, si, b)) < 0) {
-                    d = c.k >= 0 ? kBadExactD : kBadSpecD;
-                } else {
-                    const int r = traj_scatter<kX>(sc, si, b, x, ray.d, c, ss, beta, eta_scale, bounces, ray,
-                                                   rp.max_depth, rp.rr_threshold);
-                    if (r == 1) d = c.draws;
-                    else if (r == 2) d = c.k >= 0 ? kBadExactD : kBadSpecD;
-                }
-            }
-            if (d != kNoOff) {
-                RingEnt& e = ring[off & (R - 1u)];
-                e.st = st0;
-                e.d = d;
-                e.tag = off;
-                off = kNoOff;
-                tracing = false;
-            }
-        }
-        mark(3);
-        __syncthreads();
-        // ---- (4) each group leader walks its chain through the ring
-        if (gl == 0 && sg.phase == 1) {
-            CiGroup s = gs[g];
-            if ((++cancel_poll & 127u) == 0) {   // long pixels (large spp)
-                const uint64_t now = wall_clock64();
-                const bool host = now - last_host_poll >= 100000;
-                if (host) last_host_poll = now;
-                if (cancel_requested(sc, host)) s.phase = 2;
-            }
-            for (; s.phase == 1;) {
-                RingEnt& e = ring[s.head & (R - 1u)];
-                if (e.tag != s.head) break;
-                const uint32_t d = e.d;
-                if (d == kBadSpecD) {   // re-run the head with its sample index known
-                    e.tag = kNoOff;
-                    s.reissue = 1;
-                    break;
-                }
-                wb.memb[rec * n + s.kh] = e.st;
-                if (d == kBadExactD) {   // the exact head's trajectory panics: the tile ends at this sample
-                    wb.prec[rec].nvalid = s.kh + 1;
-                    s.phase = 2;
-                    break;
-                }
-                CI_DIAG(atomicAdd(&dh[min(d / 2u, 63u)], 1u);)
-                s.kh++;
-                s.head += d;
-                if (s.kh >= n) {   // every sample of the pixel has its offset; the next StartPixel starts here
-                    s.S = pcg_advance(J, s.S, inc, (uint64_t)s.head);
-                    s.pi++;
-                    s.phase = s.pi < s.npx ? 0 : 2;
-                    break;
-                }
-            }
-            if (s.nxt < s.head || (cs == 2u && ((s.nxt ^ s.head) & 1u))) s.nxt = s.head;
-            gs[g] = s;
-        }
-        __syncthreads();
-        // ---- (5) drop candidates the chain has left behind
-        if (off != kNoOff) {
-            const CiGroup s2 = gs[g];
-            if (s2.phase != 1 || off < s2.head || (cs == 2u && ((off ^ s2.head) & 1u)) || s2.pi != sg.pi) {
-                off = kNoOff;
-                tracing = false;
-            }
-        }
-        mark(4);
-    }
-#ifdef PBRT_CI_DIAG
-    __syncthreads();
-    if (tid < 64 && dh[tid]) atomicAdd(&ctr->dhist[tid], (unsigned long long)dh[tid]);
-    if (tid == 0) {
-        atomicAdd(&ctr->windows, steps);
-        for (int k = 0; k < 8; k++) atomicAdd(&ctr->phase[k], ph[k]);
-    }
-#endif
-#undef CI_DIAG
-    if (tid == 0) {
-        if (ticks && G == 1 && bs < nslots_batch) ticks[bs] = (uint32_t)min(wall_clock64() - t_begin, (uint64_t)0xFFFFFFFFu);
-    }
-}
-
-// ---------------------------------------------------------- merge kernel
-// Film.MergeFilmTile (film.go:115-132) in tile-index order. A film pixel is
-// covered by at most the 3x3 tiles around its own (filter radius < tile size).
-__global__ __launch_bounds__(256) void k_merge_film(const pbrt_film_desc* __restrict__ film_desc, RenderParams rp,
-                                                    const double* __restrict__ films, double* __restrict__ out) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= rp.film_w * rp.film_h) return;
-    const pbrt_film_desc& f = *film_desc;
-    const int64_t x = rp.film_min_x + i % rp.film_w, y = rp.film_min_y + i / rp.film_w;
-    const int64_t tx = (x - rp.film_min_x) / rp.tile_size, ty = (y - rp.film_min_y) / rp.tile_size;
-    double v0 = 0, v1 = 0, v2 = 0;
-    for (int64_t dy = -1; dy <= 1; dy++) {
-        for (int64_t dx = -1; dx <= 1; dx++) {
-            int64_t cx = tx + dx, cy = ty + dy;
-            if (cx < 0 || cy < 0 || cx >= rp.ntx || cy >= rp.nty) continue;
-            int64_t tile = cy * rp.ntx + cx;
-            if (tile < rp.tile_begin || (tile - rp.tile_begin) % rp.tile_stride != 0) continue;
-            int64_t slot = (tile - rp.tile_begin) / rp.tile_stride;
-            if (slot >= rp.n_slots) continue;
-            int64_t x0, y0, x1, y1, px0, py0, px1, py1;
-            tile_bounds(rp, tile, x0, y0, x1, y1);
-            film_tile_bounds(f, x0, y0, x1, y1, px0, py0, px1, py1);
-            if (x < px0 || x >= px1 || y < py0 || y >= py1) continue;
-            const double* c = films + slot * (rp.slot_w * rp.slot_h * 3) + ((x - px0) + (y - py0) * (px1 - px0)) * 3;
-            // spectrum.go:35-41 RGBToXYZ
-            v0 += 0.412453 * c[0] + 0.357580 * c[1] + 0.180423 * c[2];
-            v1 += 0.212671 * c[0] + 0.715160 * c[1] + 0.072169 * c[2];
-            v2 += 0.019334 * c[0] + 0.119193 * c[1] + 0.950227 * c[2];
-        }
-    }
-    out[i * 3 + 0] = v0;
-    out[i * 3 + 1] = v1;
-    out[i * 3 + 2] = v2;
-}
-
-// ------------------------------------------------------- batch intersect
-__global__ __launch_bounds__(kWave) void k_intersect(DevScene sc, int64_t n, const double* __restrict__ rays,
-                                                     double* __restrict__ out, int any_hit) {
-    __shared__ uint16_t stack_lds[64 * kStackStride];
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const double* q = rays + 7 * i;
-    Ray r{V3{q[0], q[1], q[2]}, V3{q[3], q[4], q[5]}, q[6], 0};
-    int panic = 0;
-    if (any_hit) {
-        bool h = bvh_traverse<true>(sc, r, nullptr, stack_lds + threadIdx.x, panic);
-        out[i] = panic ? gomath::nan() : (h ? 1.0 : 0.0);
-        return;
-    }
-    SI si;
-    si.p = si.n = V3{0, 0, 0};
-    si.prim = -1;
-    bool h = bvh_traverse<false>(sc, r, &si, stack_lds + threadIdx.x, panic);
-    double* o = out + 9 * i;
-    if (panic) {
-        for (int k = 0; k < 9; k++) o[k] = gomath::nan();
-        return;
-    }
-    o[0] = h ? 1.0 : 0.0;
-    o[1] = r.tmax;
-    o[2] = h ? (double)si.prim : -1.0;
-    o[3] = si.p.x; o[4] = si.p.y; o[5] = si.p.z;
-    o[6] = si.n.x; o[7] = si.n.y; o[8] = si.n.z;
-}
-
-}  // namespace
 
 // =============================================================== C ABI
 // Experiment knobs (environment), read ONCE when a context is created

@@ -1,0 +1,41 @@
+#!/bin/bash
+# One GPU session on the MI355X box: the named steps in order, each under its own
+# time limit, chained so that the first failure ends the session. Outputs land in
+# gpurun_out/<tag>/ (merged back by gpurun).
+#   tools/gpu_session.sh <tag> <step> [<step> ...]
+# steps:
+#   tests                 the whole GPU suite
+#   tests=<expr>          GPU tests selected with pytest -k <expr>
+#   bench=<cfg>[,args]    bench.py --config <cfg> (no CPU baseline, no side mode);
+#                         extra bench args after commas, e.g. bench=C,--steps,1
+#   benchfull=<cfg>       bench.py --config <cfg> with its CPU baseline and side mode
+#   profile=<cfg>         tools/profile_round.sh for that config
+#   smoke                 __graft_entry__.smoke()
+set -o pipefail
+TAG=$1
+shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+for step in "$@"; do
+  case "$step" in
+  tests)
+    timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo "tests failed"; tail -30 $OUT/pytest.log; exit 1; } ;;
+  tests=*)
+    timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -k "${step#tests=}" > $OUT/pytest_k.log 2>&1 || { echo "tests failed"; tail -30 $OUT/pytest_k.log; exit 1; } ;;
+  bench=*)
+    spec=${step#bench=}; cfg=${spec%%,*}; extra=""
+    [[ "$spec" == *,* ]] && extra=$(echo "${spec#*,}" | tr ',' ' ')
+    timeout -k 10 500 python bench.py --config $cfg --no-cpu-baseline --no-side-mode $extra > $OUT/bench_$cfg.json 2> $OUT/bench_$cfg.err || { echo "bench $cfg failed"; tail -20 $OUT/bench_$cfg.err; exit 1; } ;;
+  benchfull=*)
+    cfg=${step#benchfull=}
+    timeout -k 10 600 python bench.py --config $cfg > $OUT/benchfull_$cfg.json 2> $OUT/benchfull_$cfg.err || { echo "bench $cfg failed"; tail -20 $OUT/benchfull_$cfg.err; exit 1; } ;;
+  profile=*)
+    cfg=${step#profile=}
+    bash tools/profile_round.sh ${TAG}/prof_$cfg --config $cfg || { echo "profile $cfg failed"; exit 1; } ;;
+  smoke)
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $OUT/smoke.log; exit 1; } ;;
+  *) echo "unknown step $step"; exit 2 ;;
+  esac
+  echo "$step done"
+done
