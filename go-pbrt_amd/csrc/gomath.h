@@ -11,10 +11,15 @@
 #pragma once
 #pragma clang fp contract(off)
 
-#include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
 #define GO_HD __host__ __device__ __forceinline__
+#else
+// plain C++ (host-only checks of the product headers, tests/xf_fast_check.cpp)
+#define GO_HD inline
+#endif
 // Go's trig routines are long polynomial sequences; GO_TRIG lets a build keep
 // one out-of-line copy of each instead of inlining them at every call site.
 #ifndef GO_TRIG

@@ -378,9 +378,13 @@ __global__ void k_order_of_keys(const uint64_t* __restrict__ keys, int64_t nb, u
 // Film.MergeFilmTile (film.go:115-132) in tile-index order. A film pixel is
 // covered by at most the 3x3 tiles around its own (filter radius < tile size).
 __global__ __launch_bounds__(256) void k_merge_film(const pbrt_film_desc* __restrict__ film_desc, RenderParams rp,
-                                                    const double* __restrict__ films, double* __restrict__ out) {
+                                                    const double* __restrict__ films, double* __restrict__ out,
+                                                    const int* __restrict__ cancel_seen) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= rp.film_w * rp.film_h) return;
+    // a cancelled frame's tile films are partial (or the previous frame's):
+    // leave the caller's buffer as it is (pbrt_gpu.h: undefined after a cancel)
+    if (__atomic_load_n(cancel_seen, __ATOMIC_RELAXED)) return;
     const pbrt_film_desc& f = *film_desc;
     const int64_t x = rp.film_min_x + i % rp.film_w, y = rp.film_min_y + i / rp.film_w;
     const int64_t tx = (x - rp.film_min_x) / rp.tile_size, ty = (y - rp.film_min_y) / rp.tile_size;

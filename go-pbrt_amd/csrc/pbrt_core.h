@@ -136,6 +136,66 @@ GO_HD Ray xf_ray(const pbrt_matrix4x4& M, const Ray& r, V3* oerr, V3* derr) {
     return out;
 }
 
+// Value-only TransformRay (transform.go:279-300) for a hit test.
+// TransformRay pushes the transformed origin along d by
+// dt = (|d'| . oError) / |d'|^2; oError = gamma(3) * (...) and gamma(3) is
+// 3 * MachineEpsilon, a denormal. With every |m_ij| <= 1e10,
+// |p_i|, |d'_i| <= 1e50 and |d'|^2 >= 1e-20, |oError_i| <= 6e-263 and each
+// component of the push is <= 2e-142, below a quarter ulp of any |o'_i| >=
+// 1e-100: o' + push rounds back to o'. So where these hold the origin is
+// M*p, the direction M*d, and both error vectors are below 1e-150 with
+// oError's sign irrelevant (|o'| >= 1e-100) -- all sphere_roots_filter needs
+// (DESIGN.md 3.6). Classes (xf_fast_kind, host):
+//   kXfIdentity:    M = I; M*p = p, M*d = d when no component is 0
+//                   (the matrix product adds signed zeros, which only matter
+//                   for zero components -- those take the exact path);
+//   kXfTranslation: M*p = p + t (the three 1*p_i and 0*p_j products are
+//                   exact; t_i + p_i is the one rounding), M*d = d;
+//   kXfAffine:      last row (0,0,0,1), |m_ij| <= 1e10: the product as
+//                   xf_point / xf_vector compute it, without the errors;
+//   kXfSlow:        anything else: always the exact path.
+constexpr int kXfIdentity = 0, kXfTranslation = 1, kXfAffine = 2, kXfSlow = 3;
+GO_HD bool xf_fast(int kind, const pbrt_matrix4x4& M, V3& o, V3& d) {
+    if (kind == kXfSlow) return false;
+    const double big = 1e50;
+    bool ok = gomath::abs(o.x) <= big && gomath::abs(o.y) <= big && gomath::abs(o.z) <= big;
+    if (kind == kXfAffine) {
+        const double(*m)[4] = M.m;
+        const V3 p = o, v = d;
+        o = V3{m[0][0] * p.x + m[0][1] * p.y + m[0][2] * p.z + m[0][3],
+               m[1][0] * p.x + m[1][1] * p.y + m[1][2] * p.z + m[1][3],
+               m[2][0] * p.x + m[2][1] * p.y + m[2][2] * p.z + m[2][3]};
+        d = xf_vector(M, v);
+    } else {
+        // no zero direction component (signed-zero sums), and d' = d
+        ok = ok && d.x != 0 && d.y != 0 && d.z != 0;
+        if (kind == kXfTranslation) o = V3{o.x + M.m[0][3], o.y + M.m[1][3], o.z + M.m[2][3]};
+    }
+    const double l2 = len2(d), small = 1e-100;
+    return ok && gomath::abs(d.x) <= big && gomath::abs(d.y) <= big && gomath::abs(d.z) <= big && l2 >= 1e-20 &&
+           gomath::abs(o.x) >= small && gomath::abs(o.y) >= small && gomath::abs(o.z) >= small;
+}
+// Host: the xf_fast class of a world->object matrix.
+inline int xf_fast_kind(const pbrt_matrix4x4& M) {
+    const double(*m)[4] = M.m;
+    if (m[3][0] != 0 || m[3][1] != 0 || m[3][2] != 0 || m[3][3] != 1) return kXfSlow;
+    bool lin_identity = true, small = true;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 4; j++) {
+            const double v = m[i][j];
+            if (!(v >= -1e10 && v <= 1e10)) small = false;
+            if (j < 3 && __builtin_bit_cast(uint64_t, v) != __builtin_bit_cast(uint64_t, i == j ? 1.0 : 0.0))
+                lin_identity = false;
+        }
+    if (!small) return kXfSlow;
+    if (lin_identity) {
+        // the identity test of the translation column is on values: +-0 both give p + 0 = p for p != 0
+        if (m[0][3] == 0 && m[1][3] == 0 && m[2][3] == 0) return kXfIdentity;
+        return kXfTranslation;
+    }
+    return kXfAffine;
+}
+
 // ray.go:57-74
 GO_HD V3 offset_ray_origin(V3 p, V3 perr, V3 n, V3 w) {
     double d = dot(vabs(n), perr) * 1024.0;

@@ -268,33 +268,30 @@ __device__ __forceinline__ bool phi_beyond(double y, double x, double phi_max) {
 // Sphere.Intersect / IntersectP, hit part (sphere.go:64-131). world->object
 // = the swap of object_to_world (Transform.Inverse, transform.go:175-177).
 // `ray` is already in object space (shape_hit), oerr/derr its transform errors.
-__device__ inline bool sphere_hit(const pbrt_shape_desc& s, const Ray& ray, V3 oerr, V3 derr, double& t_hit, V3& ph,
-                                  int& panic) {
-    // Value-first decisions (sphere_filter.h): the reference's
-    // bound comparisons decided from the EFloat values and a proven radius, so
-    // the intervals below are evaluated only when the filter cannot decide
-    // (a near-tie with TMax or 0, a near-zero divisor, extreme magnitudes).
-    sf_roots rt;
-    const int fr = sphere_roots_filter(ray.o.x, ray.o.y, ray.o.z, ray.d.x, ray.d.y, ray.d.z, oerr.x, oerr.y, oerr.z,
-                                       derr.x, derr.y, derr.z, s.radius, ray.tmax, &rt);
-    if (fr == 0) return false;
-    if (fr < 0) {
-        EF ox = ef_new(ray.o.x, oerr.x, panic), oy = ef_new(ray.o.y, oerr.y, panic), oz = ef_new(ray.o.z, oerr.z, panic);
-        EF dx = ef_new(ray.d.x, derr.x, panic), dy = ef_new(ray.d.y, derr.y, panic), dz = ef_new(ray.d.z, derr.z, panic);
-        EF a = ef_add(ef_add(ef_mul(dx, dx, panic), ef_mul(dy, dy, panic), panic), ef_mul(dz, dz, panic), panic);
-        EF b = ef_muls(ef_add(ef_add(ef_mul(dx, ox, panic), ef_mul(dy, oy, panic), panic), ef_mul(dz, oz, panic), panic),
-                       2.0, panic);
-        EF c0 = ef_add(ef_add(ef_mul(ox, ox, panic), ef_mul(oy, oy, panic), panic), ef_mul(oz, oz, panic), panic);
-        EF c = ef_sub(c0, ef_muls(ef_new(s.radius, 0, panic), s.radius, panic), panic);
-        EF t0, t1;
-        if (!ef_quadratic(a, b, c, t0, t1, panic)) return false;
-        if (t0.hi > ray.tmax || t1.lo <= 0) return false;
-        rt.t0v = t0.v;
-        rt.t1v = t1.v;
-        rt.t0lo_le0 = t0.lo <= 0;
-        rt.t1hi_gt = t1.hi > ray.tmax;
-    }
-    // sphere.go:87-131 on the decided comparisons
+// The EFloat path of Sphere.Intersect up to its bound comparisons
+// (sphere.go:64-92): fills rt, or returns false where the reference does.
+__device__ inline bool sphere_roots_exact(const pbrt_shape_desc& s, const Ray& ray, V3 oerr, V3 derr, sf_roots& rt,
+                                          int& panic) {
+    EF ox = ef_new(ray.o.x, oerr.x, panic), oy = ef_new(ray.o.y, oerr.y, panic), oz = ef_new(ray.o.z, oerr.z, panic);
+    EF dx = ef_new(ray.d.x, derr.x, panic), dy = ef_new(ray.d.y, derr.y, panic), dz = ef_new(ray.d.z, derr.z, panic);
+    EF a = ef_add(ef_add(ef_mul(dx, dx, panic), ef_mul(dy, dy, panic), panic), ef_mul(dz, dz, panic), panic);
+    EF b = ef_muls(ef_add(ef_add(ef_mul(dx, ox, panic), ef_mul(dy, oy, panic), panic), ef_mul(dz, oz, panic), panic),
+                   2.0, panic);
+    EF c0 = ef_add(ef_add(ef_mul(ox, ox, panic), ef_mul(oy, oy, panic), panic), ef_mul(oz, oz, panic), panic);
+    EF c = ef_sub(c0, ef_muls(ef_new(s.radius, 0, panic), s.radius, panic), panic);
+    EF t0, t1;
+    if (!ef_quadratic(a, b, c, t0, t1, panic)) return false;
+    if (t0.hi > ray.tmax || t1.lo <= 0) return false;
+    rt.t0v = t0.v;
+    rt.t1v = t1.v;
+    rt.t0lo_le0 = t0.lo <= 0;
+    rt.t1hi_gt = t1.hi > ray.tmax;
+    return true;
+}
+// sphere.go:87-131 on the decided comparisons: the root, the refined hit point
+// and the partial-sphere clipping
+__device__ inline bool sphere_accept(const pbrt_shape_desc& s, const Ray& ray, const sf_roots& rt, double& t_hit,
+                                     V3& ph) {
     double tsv = rt.t0v;
     bool used_t1 = false;
     if (rt.t0lo_le0) {
@@ -320,6 +317,22 @@ __device__ inline bool sphere_hit(const pbrt_shape_desc& s, const Ray& ray, V3 o
     }
     t_hit = tsv;
     return true;
+}
+// Sphere.Intersect / IntersectP, hit part (sphere.go:64-131). world->object
+// = the swap of object_to_world (Transform.Inverse, transform.go:175-177).
+// `ray` is already in object space (shape_hit), oerr/derr its transform errors.
+// Value-first decisions (sphere_filter.h): the reference's
+// bound comparisons decided from the EFloat values and a proven radius; the
+// intervals are evaluated only when the filter cannot decide (a near-tie with
+// TMax or 0, a near-zero divisor, extreme magnitudes).
+__device__ inline bool sphere_hit(const pbrt_shape_desc& s, const Ray& ray, V3 oerr, V3 derr, double& t_hit, V3& ph,
+                                  int& panic) {
+    sf_roots rt;
+    const int fr = sphere_roots_filter(ray.o.x, ray.o.y, ray.o.z, ray.d.x, ray.d.y, ray.d.z, oerr.x, oerr.y, oerr.z,
+                                       derr.x, derr.y, derr.z, s.radius, ray.tmax, &rt);
+    if (fr == 0) return false;
+    if (fr < 0 && !sphere_roots_exact(s, ray, oerr, derr, rt, panic)) return false;
+    return sphere_accept(s, ray, rt, t_hit, ph);
 }
 // Sphere.Intersect, interaction part (sphere.go:133-186); ray in object space.
 // Only dpdu, dpdv of the parametric representation feed the outputs.
@@ -377,17 +390,37 @@ __device__ inline void shape_si(const pbrt_shape_desc& s, const Ray& r, V3 ph, S
 
 // A primitive with a copy of its shape: a leaf test reads one record (one
 // dependent memory level) instead of primitive -> shape.
+// fast: the value-only TransformRay class (xf_fast) of the primitive's
+// world->primitive transform (bits 0-7) and of the shape's world->object
+// transform (bits 8-15), set on the host by xf_fast_kind.
 struct alignas(16) DevPrim {
     pbrt_shape_desc shape;
     pbrt_transform prim_to_world;   // TransformedPrimitive only
-    int32_t kind, material, prim_identity, pad;
+    int32_t kind, material, prim_identity, fast;
 };
 
 // Shape test without the SurfaceInteraction: the hit parameter and point.
+// The object-space ray comes from xf_fast where it applies (both transforms of
+// a TransformedPrimitive's shape); otherwise, and when the
+// sphere filter cannot decide, from the exact TransformRay with its errors.
 __device__ inline bool prim_hit_t(const DevScene& sc, int pi, const Ray& r, double& t_hit, V3& ph, int& panic) {
     const DevPrim& p = sc.fprims[pi];
+    const bool xformed = p.kind == PBRT_PRIM_TRANSFORMED;
+    {
+        Ray ro = r;
+        bool fast = !xformed || xf_fast(p.fast & 0xff, p.prim_to_world.m_inv, ro.o, ro.d);
+        fast = fast && xf_fast((p.fast >> 8) & 0xff, p.shape.object_to_world.m_inv, ro.o, ro.d);
+        if (fast) {
+            if (p.shape.type != PBRT_SHAPE_SPHERE) return disk_hit(p.shape, ro, t_hit, ph);
+            sf_roots rt;
+            const int fr = sphere_roots_filter(ro.o.x, ro.o.y, ro.o.z, ro.d.x, ro.d.y, ro.d.z, 0, 0, 0, 0, 0, 0,
+                                               p.shape.radius, ro.tmax, &rt);
+            if (fr == 0) return false;
+            if (fr > 0) return sphere_accept(p.shape, ro, rt, t_hit, ph);
+        }
+    }
     Ray ray = r;
-    if (p.kind == PBRT_PRIM_TRANSFORMED) ray = xf_ray(p.prim_to_world.m_inv, r, nullptr, nullptr);
+    if (xformed) ray = xf_ray(p.prim_to_world.m_inv, r, nullptr, nullptr);
     return shape_hit(p.shape, ray, t_hit, ph, panic);
 }
 

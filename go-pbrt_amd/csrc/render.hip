@@ -427,6 +427,7 @@ std::vector<DevPrim> dev_prims(const pbrt_scene_desc* s) {
         v[i].kind = p.kind;
         v[i].material = p.material;
         v[i].prim_identity = is_identity(p.prim_to_world.m) ? 1 : 0;
+        v[i].fast = xf_fast_kind(p.prim_to_world.m_inv) | xf_fast_kind(v[i].shape.object_to_world.m_inv) << 8;
     }
     return v;
 }
@@ -1006,18 +1007,35 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
     return PBRT_OK;
 }
 
+namespace {
+int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_device);
+}
+
 int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_device) {
     if (!c) return PBRT_E_INVALID;
-    HIPCHK(c, hipSetDevice(c->device));
-    c->t_start = std::chrono::steady_clock::now();
-    int rc = prepare(c, rd);
-    if (rc != PBRT_OK) return rc;
-    {   // this render is the one pbrt_gpu_cancel now cancels
+    {   // from here on this render is the one pbrt_gpu_cancel cancels: a cancel
+        // that lands while prepare() sizes and allocates the buffers is kept
         std::lock_guard<std::mutex> lk(c->cancel_mu);
         c->in_flight = true;
         c->cancel_req = false;
         __atomic_store_n(c->h_cancel, 0, __ATOMIC_SEQ_CST);
     }
+    const int rc = render_enqueue(c, rd, film_device);
+    if (rc != PBRT_OK) {   // nothing was launched (or the launch failed): no render is in flight
+        std::lock_guard<std::mutex> lk(c->cancel_mu);
+        c->in_flight = false;
+        c->cancel_req = false;
+        __atomic_store_n(c->h_cancel, 0, __ATOMIC_SEQ_CST);
+    }
+    return rc;
+}
+
+namespace {
+int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_device) {
+    HIPCHK(c, hipSetDevice(c->device));
+    c->t_start = std::chrono::steady_clock::now();
+    int rc = prepare(c, rd);
+    if (rc != PBRT_OK) return rc;
     const RenderParams& rp = c->rp;
     double* out = film_device ? film_device : c->d_out;
     c->film_target = out;
@@ -1257,12 +1275,13 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     int64_t npx = rp.film_w * rp.film_h;
     hipLaunchKernelGGL(k_merge_film, dim3((unsigned)((npx + 255) / 256)), dim3(256), 0, c->stream, c->d_film, rp,
-                       c->d_films, out);
+                       c->d_films, out, c->d_cancel_seen);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev2, c->stream));
     c->rendered = true;
     return PBRT_OK;
 }
+}  // namespace
 
 int pbrt_gpu_render_async(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
     return pbrt_gpu_render_async_into(c, rd, nullptr);

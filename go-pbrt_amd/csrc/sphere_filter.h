@@ -15,7 +15,8 @@
  *   - every bound satisfies Low <= Value <= High (rounding is monotone, next_down
  *     / next_up move outward), so Value > TMax implies High > TMax and
  *     Value <= 0 implies Low <= 0: those rejects are exact;
- *   - with |o|,|d|,r <= 1e50, errors <= 1e-150, r, a, |q| >= 1e-20 and
+ *   - with |o|,|d|,r <= 1e50, |errors| <= 1e-150 (direction errors >= 0, an
+ *     origin error < 0 only where |o_i| >= 1e-100), r, a, |q| >= 1e-20 and
  *     |q| > 2 R_q, every bound is finite and a, q exclude zero, so no Check fails;
  *   - a running-error bound over the op sequence gives R_q <= 17.5 eps M_q,
  *     R(q/a) <= 31 eps M_q/a, R(c/q) <= (15 eps + 17.5 eps M_q/|q|) M_c/(|q| - R_q)
@@ -55,21 +56,28 @@ SF_HD int sphere_roots_filter(double ox, double oy, double oz, double dx, double
     const double bv = ((dx * ox + dy * oy) + dz * oz) * 2.0;
     const double cv = ((ox * ox + oy * oy) + oz * oz) - radius * radius;
     const double disc = bv * bv - 4. * av * cv;
+    const double V = 1e-100;
+    /* New(v, err) keeps Low <= v <= High for err >= 0, and for err < 0 where
+     * |err| is below half an ulp of v: the origin errors can be negative
+     * (TransformPoint's signed |m[i][1]| * p.Y term); the
+     * direction errors are sums of |.| products. (A NaN fails every test.) */
+    const int sgn_ok = (oex >= 0 || sf_abs(ox) >= V) && (oey >= 0 || sf_abs(oy) >= V) &&
+                       (oez >= 0 || sf_abs(oz) >= V) && dex >= 0 && dey >= 0 && dez >= 0;
     if (disc < 0) {
         /* efloat/math.go:38-40 returns false; with every operand finite and
-         * below 1e100 no Check() before it can panic */
+         * below 1e100 (and errors of |.| <= 1e100 as above) no Check() before it
+         * can panic */
         const double big = 1e100;
         const int moderate = sf_abs(ox) < big && sf_abs(oy) < big && sf_abs(oz) < big && sf_abs(dx) < big &&
-                             sf_abs(dy) < big && sf_abs(dz) < big && sf_abs(oex) < big && sf_abs(oey) < big &&
-                             sf_abs(oez) < big && sf_abs(dex) < big && sf_abs(dey) < big && sf_abs(dez) < big &&
+                             sf_abs(dy) < big && sf_abs(dz) < big && sf_abs(oex) <= 1e-150 &&
+                             sf_abs(oey) <= 1e-150 && sf_abs(oez) <= 1e-150 && dex < big && dey < big && dez < big &&
                              sf_abs(radius) < big;
-        return moderate ? 0 : -1;
+        return moderate && sgn_ok ? 0 : -1;
     }
     const double B = 1e50, E = 1e-150, S = 1e-20;
-    /* the errors are sums of |.| products (TransformRay): >= 0 or NaN, and a NaN fails <= */
-    const int g1 = sf_abs(ox) <= B && sf_abs(oy) <= B && sf_abs(oz) <= B && sf_abs(dx) <= B && sf_abs(dy) <= B &&
-                   sf_abs(dz) <= B && oex <= E && oey <= E && oez <= E && dex <= E && dey <= E && dez <= E &&
-                   sf_abs(radius) <= B && sf_abs(radius) >= S;
+    const int g1 = sgn_ok && sf_abs(ox) <= B && sf_abs(oy) <= B && sf_abs(oz) <= B && sf_abs(dx) <= B &&
+                   sf_abs(dy) <= B && sf_abs(dz) <= B && sf_abs(oex) <= E && sf_abs(oey) <= E && sf_abs(oez) <= E &&
+                   dex <= E && dey <= E && dez <= E && sf_abs(radius) <= B && sf_abs(radius) >= S;
     if (!g1) return -1;
     const double rd = __builtin_sqrt(disc);
     const double qv = (bv < 0 ? bv - rd : bv + rd) * -0.5;

@@ -354,7 +354,8 @@ int pbrt_gpu_intersect_p(pbrt_gpu_ctx* ctx, const pbrt_ray_soa* rays, size_t n,
  * entry until its pbrt_gpu_synchronize returns): the kernels poll a flag between
  * units of work (a pixel's chain, every 128 chain steps, a workgroup of paths),
  * so the frame stops within milliseconds and its synchronize returns
- * PBRT_E_CANCELLED (the film is then not valid). Like the reference's
+ * PBRT_E_CANCELLED (the caller's film buffer is then left undefined: the final
+ * merge is skipped when the kernels saw the cancel). Like the reference's
  * errgroup, which stops issuing tiles once ctx is done (integrator.go:332-335),
  * it ends that render only: the flag is cleared when the render ends, so the
  * next render on the context runs normally. With no render in flight it does

@@ -395,31 +395,55 @@ func (b *BVH) device() error {
 	return b.err
 }
 
-// raySoA packs rays into the C SoA (pbrt_ray_soa); the slices stay alive in the
-// returned holder for the duration of the cgo call.
-type raySoA struct {
-	o, d [3][]float64
-	tmax []float64
-	soa  C.pbrt_ray_soa
+// cArena is one C allocation holding a batch's SoA arrays. cgo forbids passing
+// C a Go value that points at Go memory (pbrt_ray_soa / pbrt_hit_soa hold the
+// array pointers: with cgocheck=1 the call panics "cgo argument has Go pointer
+// to unpinned Go pointer"), so the arrays live in C memory and the structs
+// passed to C hold only C pointers. Slices over the C memory are made with the
+// fixed-size-array idiom (no unsafe.Slice: go-pbrt builds with Go 1.11).
+type cArena struct {
+	base unsafe.Pointer
+	off  uintptr
 }
 
-func packRays(rays []*pbrt.Ray) *raySoA {
+func newArena(bytes int) *cArena {
+	if bytes < 8 {
+		bytes = 8
+	}
+	return &cArena{base: C.malloc(C.size_t(bytes))}
+}
+
+func (a *cArena) take(bytes int) unsafe.Pointer {
+	p := unsafe.Pointer(uintptr(a.base) + a.off)
+	a.off += (uintptr(bytes) + 7) &^ 7
+	return p
+}
+
+func (a *cArena) f64(n int) []float64 { return (*[1 << 28]float64)(a.take(8 * n))[:n:n] }
+func (a *cArena) i32(n int) []int32   { return (*[1 << 29]int32)(a.take(4 * n))[:n:n] }
+func (a *cArena) u8(n int) []uint8    { return (*[1 << 30]uint8)(a.take(n))[:n:n] }
+func (a *cArena) free()               { C.free(a.base) }
+
+func cdp(s []float64) *C.double { return (*C.double)(unsafe.Pointer(&s[0])) }
+
+// packRays copies the rays into a pbrt_ray_soa whose arrays are in arena a.
+func packRays(a *cArena, rays []*pbrt.Ray) C.pbrt_ray_soa {
 	n := len(rays)
-	h := &raySoA{tmax: make([]float64, n)}
+	var o, d [3][]float64
 	for k := 0; k < 3; k++ {
-		h.o[k] = make([]float64, n)
-		h.d[k] = make([]float64, n)
+		o[k], d[k] = a.f64(n), a.f64(n)
 	}
+	tmax := a.f64(n)
 	for i, r := range rays {
-		h.o[0][i], h.o[1][i], h.o[2][i] = r.Origin.X, r.Origin.Y, r.Origin.Z
-		h.d[0][i], h.d[1][i], h.d[2][i] = r.Direction.X, r.Direction.Y, r.Direction.Z
-		h.tmax[i] = r.TMax
+		o[0][i], o[1][i], o[2][i] = r.Origin.X, r.Origin.Y, r.Origin.Z
+		d[0][i], d[1][i], d[2][i] = r.Direction.X, r.Direction.Y, r.Direction.Z
+		tmax[i] = r.TMax
 	}
-	dp := func(s []float64) *C.double { return (*C.double)(unsafe.Pointer(&s[0])) }
-	h.soa.ox, h.soa.oy, h.soa.oz = dp(h.o[0]), dp(h.o[1]), dp(h.o[2])
-	h.soa.dx, h.soa.dy, h.soa.dz = dp(h.d[0]), dp(h.d[1]), dp(h.d[2])
-	h.soa.tmax = dp(h.tmax)
-	return h
+	var soa C.pbrt_ray_soa
+	soa.ox, soa.oy, soa.oz = cdp(o[0]), cdp(o[1]), cdp(o[2])
+	soa.dx, soa.dy, soa.dz = cdp(d[0]), cdp(d[1]), cdp(d[2])
+	soa.tmax = cdp(tmax)
+	return soa
 }
 
 // IntersectBatch is BVH.Intersect (bvh.go:659-712) for every ray; like the
@@ -435,23 +459,22 @@ func (b *BVH) IntersectBatch(rays []*pbrt.Ray, hits []Hit) error {
 	if err := b.device(); err != nil {
 		return err
 	}
-	h := packRays(rays)
-	hit := make([]uint8, n)
-	tmax := make([]float64, n)
-	prim := make([]int32, n)
+	// rays: 7 doubles; hits: 7 doubles, an int32 and a byte per ray (+ alignment)
+	a := newArena(n*(14*8+4+1) + 16*8)
+	defer a.free()
+	soa := packRays(a, rays)
+	hit, tmax, prim := a.u8(n), a.f64(n), a.i32(n)
 	var p, nn [3][]float64
 	for k := 0; k < 3; k++ {
-		p[k] = make([]float64, n)
-		nn[k] = make([]float64, n)
+		p[k], nn[k] = a.f64(n), a.f64(n)
 	}
-	dp := func(s []float64) *C.double { return (*C.double)(unsafe.Pointer(&s[0])) }
 	var hs C.pbrt_hit_soa
 	hs.hit = (*C.uint8_t)(unsafe.Pointer(&hit[0]))
-	hs.t_max = dp(tmax)
+	hs.t_max = cdp(tmax)
 	hs.prim = (*C.int32_t)(unsafe.Pointer(&prim[0]))
-	hs.px, hs.py, hs.pz = dp(p[0]), dp(p[1]), dp(p[2])
-	hs.nx, hs.ny, hs.nz = dp(nn[0]), dp(nn[1]), dp(nn[2])
-	if rc := C.pbrt_gpu_intersect(b.renderer.ctx, &h.soa, C.size_t(n), &hs); rc != C.PBRT_OK {
+	hs.px, hs.py, hs.pz = cdp(p[0]), cdp(p[1]), cdp(p[2])
+	hs.nx, hs.ny, hs.nz = cdp(nn[0]), cdp(nn[1]), cdp(nn[2])
+	if rc := C.pbrt_gpu_intersect(b.renderer.ctx, &soa, C.size_t(n), &hs); rc != C.PBRT_OK {
 		return fmt.Errorf("pbrt_gpu_intersect: %s", C.GoString(C.pbrt_gpu_last_error(b.renderer.ctx)))
 	}
 	for i := 0; i < n; i++ {
@@ -478,9 +501,11 @@ func (b *BVH) IntersectPBatch(rays []*pbrt.Ray, occluded []bool) error {
 	if err := b.device(); err != nil {
 		return err
 	}
-	h := packRays(rays)
-	occ := make([]uint8, n)
-	if rc := C.pbrt_gpu_intersect_p(b.renderer.ctx, &h.soa, C.size_t(n), (*C.uint8_t)(unsafe.Pointer(&occ[0]))); rc != C.PBRT_OK {
+	a := newArena(n*(7*8+1) + 8*8)
+	defer a.free()
+	soa := packRays(a, rays)
+	occ := a.u8(n)
+	if rc := C.pbrt_gpu_intersect_p(b.renderer.ctx, &soa, C.size_t(n), (*C.uint8_t)(unsafe.Pointer(&occ[0]))); rc != C.PBRT_OK {
 		return fmt.Errorf("pbrt_gpu_intersect_p: %s", C.GoString(C.pbrt_gpu_last_error(b.renderer.ctx)))
 	}
 	for i := 0; i < n; i++ {

@@ -224,9 +224,13 @@ func (r *Renderer) RenderFrame(ctx context.Context, rd *C.pbrt_render_desc, film
 	}
 	// pbrt_gpu_cancel acts on the render in flight only: a cancel that lands
 	// before the render starts or after it ends is a no-op (include/pbrt_gpu.h)
+	// The watcher is joined before RenderFrame returns: a cancel racing the end
+	// of the render must not reach pbrt_gpu_cancel after the caller's Close
+	// (pbrt_gpu_destroy frees the context the cancel locks).
 	done := make(chan struct{})
-	defer close(done)
+	exited := make(chan struct{})
 	go func() {
+		defer close(exited)
 		select {
 		case <-ctx.Done():
 			C.pbrt_gpu_cancel(r.ctx)
@@ -235,8 +239,15 @@ func (r *Renderer) RenderFrame(ctx context.Context, rd *C.pbrt_render_desc, film
 	}()
 	var st C.pbrt_gpu_stats
 	rc := C.pbrt_gpu_render(r.ctx, rd, (*C.double)(unsafe.Pointer(&film[0])), &st)
+	close(done)
+	<-exited
 	switch rc {
 	case C.PBRT_OK:
+		// a cancel that landed before the render was in flight is not seen by
+		// the device; the frame completed, but the caller asked to stop
+		if err := ctx.Err(); err != nil {
+			return err
+		}
 		return nil
 	case C.PBRT_E_CANCELLED:
 		if err := ctx.Err(); err != nil {

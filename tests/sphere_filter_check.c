@@ -107,6 +107,14 @@ static int family(const char* name, int kind, long n) {
             for (int i = 0; i < 3; i++) c.d[i] *= m;
             small_errors(&c);
         }
+        if (kind == 7) { /* negative origin errors (TransformPoint's signed p.Y term) and zero/denormal origins */
+            for (int i = 0; i < 3; i++) {
+                c.oe[i] = -(double)(nextu() % 6) * 4.9406564584124654e-324;
+                int z = (int)(nextu() % 4);
+                if (z == 0) c.o[i] = 0.0;
+                else if (z == 1) c.o[i] = (double)(nextu() % 4) * 4.9406564584124654e-324;
+            }
+        }
         c.tmax = INFINITY;
         /* TMax near the roots' values: exact ties and a few ulps either side */
         sf_roots pre;
@@ -155,5 +163,6 @@ int main(int argc, char** argv) {
     rc |= family("big_errors", 4, n / 4);
     rc |= family("extreme_scale", 5, n / 4);
     rc |= family("odd_direction", 6, n / 4);
+    rc |= family("negative_origin_error", 7, n / 4);
     return rc;
 }

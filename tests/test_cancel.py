@@ -28,10 +28,11 @@ def full_time(r, rd):
     return time.time() - t0
 
 
-def check_cancel_then_render(sc, rd, small_rd, delay=0.4, bound=0.25):
+def check_cancel_then_render(sc, rd, small_rd, kernel, delay=0.4, bound=0.25):
     """Enqueue the frame (render_async returns with the render in flight), cancel
     it from another thread after `delay`, and require synchronize to return
-    PBRT_E_CANCELLED within `bound` seconds of the cancel."""
+    PBRT_E_CANCELLED within `bound` seconds of the cancel, from the kernel
+    family `kernel` (pbrt_gpu_stats.kernel of the cancelled render)."""
     with G.Renderer(sc) as r:
         G.lib().pbrt_gpu_cancel(r.h)   # nothing in flight: a no-op
         r.render_async(rd)
@@ -48,6 +49,7 @@ def check_cancel_then_render(sc, rd, small_rd, delay=0.4, bound=0.25):
         t_done = time.time()
         timer.join()
         assert ei.value.code == abi.PBRT_E_CANCELLED
+        assert ei.value.stats is not None and ei.value.stats.kernel == kernel
         dt = t_done - t_cancel[0]
         assert dt < bound, f"the frame ran {dt:.3f} s past the cancel"
         # the cancel died with its render: the next one is exact
@@ -61,23 +63,22 @@ def test_cancel_config_c_chain_then_render_again():
     """config C (Cornell, 1080p, Stratified(16,16), Path(8)): ~10 s of k_chain_ci."""
     sc = G.Scene.cornell(1920, 1080)
     check_cancel_then_render(sc, abi.render_desc(16, 16, max_depth=8),
-                             abi.render_desc(2, 2, max_depth=8, tile_end=48))
+                             abi.render_desc(2, 2, max_depth=8, tile_end=48), abi.PBRT_KERNEL_WAVE_CI)
 
 
 def test_cancel_throughput_mode_paths():
     sc = G.Scene.cornell(1920, 1080)
     check_cancel_then_render(sc, abi.render_desc(32, 32, max_depth=8, mode=abi.PBRT_MODE_THROUGHPUT),
-                             abi.render_desc(2, 2, max_depth=8, tile_end=48), delay=0.3)
+                             abi.render_desc(2, 2, max_depth=8, tile_end=48), abi.PBRT_KERNEL_WAVE, delay=0.3)
 
 
 def test_cancel_serial_kernel():
-    """A scene holding glass renders on the serial kernel (one lane per tile)."""
+    """Stratified with n_dims = 2 (< 3: the bounce-1 light sample is not per
+    pixel) renders on the serial kernel (one lane per tile), whose pixels poll
+    the flag by wall clock."""
     sc = G.Scene.readme(1920, 1080)
-    glass = sc.add_glass()
-    sph = sc.add_sphere(G.translate(0, 0, 0), 5.0)
-    sc.add_primitive(sph, glass, G.translate(50, 2.5, 50))
-    sc.build(2)
-    check_cancel_then_render(sc, abi.render_desc(8, 8), abi.render_desc(2, 2, tile_end=32), delay=0.3)
+    check_cancel_then_render(sc, abi.render_desc(8, 8, n_dims=2), abi.render_desc(2, 2, n_dims=2, tile_end=32),
+                             abi.PBRT_KERNEL_SERIAL, delay=0.3)
 
 
 def test_cancel_direct_lighting_wave():
@@ -90,7 +91,8 @@ def test_cancel_direct_lighting_wave():
     while side < 128 and t8 * (side / 8) ** 2 < 1.0:
         side *= 2
     check_cancel_then_render(sc, abi.render_desc(side, side, **dl),
-                             abi.render_desc(2, 2, tile_end=48, **dl), delay=min(0.1, t8 * (side / 8) ** 2 / 4))
+                             abi.render_desc(2, 2, tile_end=48, **dl), abi.PBRT_KERNEL_WAVE_DL,
+                             delay=min(0.1, t8 * (side / 8) ** 2 / 4))
 
 
 def test_cancel_outside_a_render_is_a_no_op():

@@ -19,7 +19,7 @@ PATCHES = os.path.join(REPO, "integration", "go", "patches")
 REFERENCE = "/root/reference"
 # cgo pseudo-identifiers and C scalar types, not ABI names
 CGO_BUILTINS = {"GoString", "CString", "GoBytes", "int", "int32_t", "int64_t", "uint8_t", "double", "size_t",
-                "uint64_t", "float", "char", "int32_t"}
+                "uint64_t", "float", "char", "int32_t", "malloc", "free"}
 
 
 def shim_parts():
@@ -98,3 +98,21 @@ def test_patches_apply_to_the_reference(tmp_path):
     assert "+\tif fr, ok := s.(FrameRenderer); ok {" in hook and "+func RenderTiles(" in hook
     server = open(os.path.join(PATCHES, pats[1])).read()
     assert "+\tdli := rec.NewPath(10, camera, sampler, pixelBounds, 1, pbrt.Uniform, 0)" in server
+
+
+def test_batch_arrays_live_in_c_memory():
+    """cgo forbids passing C a Go value that points at Go memory:
+    pbrt_ray_soa / pbrt_hit_soa hold array pointers, so the batch methods build
+    their arrays in one C.malloc'd arena, and the render watcher goroutine is
+    joined before RenderFrame returns (no pbrt_gpu_cancel after Close)."""
+    src = open(os.path.join(SHIM_DIR, "dropin.go")).read()
+    for m in ("IntersectBatch", "IntersectPBatch"):
+        body = src[src.index(f"func (b *BVH) {m}("):]
+        body = body[:body.index("\n}\n")]
+        assert "newArena(" in body and "defer a.free()" in body, m
+        assert "make([]" not in body, m   # no Go-allocated array reaches the SoA structs
+    assert "C.malloc(" in src and "C.free(" in src
+    shim = open(os.path.join(SHIM_DIR, "pbrtgpu.go")).read()
+    rf = shim[shim.index("func (r *Renderer) RenderFrame("):]
+    rf = rf[:rf.index("\n}\n")]
+    assert "<-exited" in rf and rf.index("close(done)") < rf.index("<-exited") < rf.index("switch rc")

@@ -7,7 +7,8 @@ decided case must match the interval arithmetic bit for bit (roots' values,
 t0.Low <= 0, t1.High > TMax) and must not skip a Check() panic. Families:
 random rays, rays aimed at grazing angles, origins on the surface (b and c
 near 0, where the oracle panics), TMax a few ulps from either root, input
-errors above the guard, extreme scales and unnormalised directions.
+errors above the guard, extreme scales, unnormalised directions, and negative
+origin errors at zero / denormal origins (New panics there).
 """
 import os
 import re
@@ -27,7 +28,8 @@ def test_sphere_filter_agrees_with_oracle_intervals(tmp_path):
     for line in r.stdout.splitlines():
         name = line.split()[0]
         fams[name] = {k: int(v) for k, v in re.findall(r"(\w+)=(\d+)", line)}
-    assert set(fams) == {"random", "aimed", "on_surface", "tmax_any", "big_errors", "extreme_scale", "odd_direction"}
+    assert set(fams) == {"random", "aimed", "on_surface", "tmax_any", "big_errors", "extreme_scale", "odd_direction",
+                         "negative_origin_error"}
     for f in fams.values():
         assert f["bad"] == 0
     # both verdicts are exercised, and the oracle's panics are all left undecided
@@ -35,3 +37,27 @@ def test_sphere_filter_agrees_with_oracle_intervals(tmp_path):
     assert fams["on_surface"]["oracle_panics"] > 0
     # errors above 1e-150 are never accepted on values
     assert fams["big_errors"]["decided1"] == 0
+    # New(0, err < 0) panics in Go (Low > High): those cases stay undecided
+    assert fams["negative_origin_error"]["oracle_panics"] > 0
+
+
+def test_value_only_transform_ray_matches_exact(tmp_path):
+    """xf_fast (value-only TransformRay) against the exact
+    xf_ray (transform.go:279-300) on identity / translation (incl. Go's -0
+    inverse translation) / rotation / affine / projective matrices and origins
+    and directions with +-0, denormal and tiny components: bit-identical o, d
+    wherever xf_fast accepts, and error vectors inside the filter's guard."""
+    exe = tmp_path / "xfc"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Werror",
+                    "-Wno-unknown-pragmas", "-o", str(exe), os.path.join(REPO, "tests", "xf_fast_check.cpp")],
+                   check=True)
+    r = subprocess.run([str(exe), "100000"], capture_output=True, text=True)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stderr
+    fams = {line.split()[0]: {k: int(v) for k, v in re.findall(r"(\w+)=(\d+)", line)}
+            for line in r.stdout.splitlines()}
+    assert set(fams) == {"identity", "translation", "rotation", "affine", "slow"}
+    for name, f in fams.items():
+        assert f["bad"] == 0, name
+        if name != "slow":
+            assert f["fast"] > 1000, name
