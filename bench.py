@@ -27,7 +27,10 @@ sys.path.insert(0, os.path.join(REPO, "go-pbrt_amd"))
 
 METRIC = ("Mpaths/s (samples×pixels/s) at 1920×1080, 64 spp; 1/2/4/8-GPU scaling + HBM GB/s vs "
           "roofline")
-FP64_PEAK_TFLOPS = 78.6     # MI355X fp64 vector peak (datasheet); the path is fp64-VALU bound
+FP64_PEAK_TFLOPS = 78.6     # MI355X fp64 vector peak (datasheet, an FMA = 2 FLOP); the path is fp64-VALU bound
+# the parity build forbids contraction (-ffp-contract=off: Go evaluates a*b+c as
+# two rounded ops), so the attainable add/mul issue rate is half the FMA peak
+FP64_PEAK_NOFMA_TFLOPS = FP64_PEAK_TFLOPS / 2
 HBM_PEAK_GBS = 8000.0
 
 
@@ -40,21 +43,22 @@ def parse():
     ap.add_argument("--height", type=int, default=0, help="0 = the config's (1080, or 2160 for E)")
     ap.add_argument("--shard", default="", help="R/N: on ONE GPU, render only tiles t mod N == R, the share of "
                                                 "rank R of an N-GPU job (reported as such)")
-    ap.add_argument("--config", default="B", choices=["B", "C", "D", "E", "G"],
+    ap.add_argument("--config", default="B", choices=["B", "C", "D", "E", "G", "H", "F", "N"],
                     help="BASELINE config: B = README sphere scene, Stratified(8,8), Path(10); "
                          "C = Cornell (SURVEY 8(d)), Stratified(16,16), Path(8); "
                          "D = 999 698-triangle height field (extension), Stratified(8,8), Path(10); "
                          "E = 9 999 392-triangle height field, 3840x2160, Stratified(32,32), Path(10); "
                          "G = README scene + server.go's commented-out glass sphere + a mirror, "
-                         "Stratified(8,8), Path(10)")
+                         "Stratified(8,8), Path(10); serial-kernel cases: H = DirectLighting(10) through "
+                         "server.go's glass sphere, F = B with BoxFilter radius 1.5, N = B with 2 sampled dims")
     ap.add_argument("--spp", type=int, default=0, help="Stratified(spp, spp) (0 = the config's)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "serial", "wave", "wavefront", "wave_ci"])
     ap.add_argument("--tiles-per-wave", type=int, default=0, help="k_chain_ci tiles per wave (0 = library default)")
     ap.add_argument("--occupancy", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=30.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="threads of the CPU baseline's per-GPU timing (0 = nproc / 8: the host's share per "
-                         "GPU of an 8-GPU node); a second timing always uses every host core")
+                    help="threads of the CPU baseline (0 = nproc / 8, the host's share per GPU of an 8-GPU node, "
+                         "capped by the CPUs this process may use)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="exact", choices=["exact", "throughput"],
                     help="mode of the headline line (exact = the reference's per-tile RNG, bit-exact)")
@@ -125,24 +129,40 @@ def cpu_rate(sc, rd_kwargs, threads, seconds):
     return paths / dt / 1e6, f"{what}: {paths} paths in {dt:.2f} s on {threads} threads"
 
 
+def effective_cpus(cpu):
+    """CPUs this process can actually run on: the affinity mask, capped by the
+    cgroup's CPU quota (cgroup v2 cpu.max) when there is one."""
+    eff = cpu["affinity"]
+    if cpu["cgroup_cpus"]:
+        eff = min(eff, max(1, int(cpu["cgroup_cpus"])))
+    return eff
+
+
 def cpu_baseline(args, scene_name, rd_kwargs, W, H, product_scene=None, gpus_per_host=8):
     """The oracle (C restatement of the Go path, oracle/) on the same frame's
-    tiles, on this box's host cores, timed twice (one worker per
-    host core): on the per-GPU share of the host (nproc / 8 threads: the node
-    has 8 GPUs) and on every host core (nproc threads). `value` is the share;
-    `whole_host` the other. The cgroup quota, if any, caps what either can use."""
+    tiles, on this box's host CPUs (one worker per host core).
+
+    The threads are the per-GPU share of the node (nproc / 8: the node has 8
+    GPUs), capped by what this process may use (min of the affinity mask and
+    the cgroup quota). Where the cap binds, the per-GPU share cannot be timed
+    here: the line says so and adds a linear extrapolation (labelled as one).
+    When the box grants more CPUs than the share, a second timing on all of
+    them is added under `all_granted`."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib as O
 
     cpu = host_cpu()
-    if scene_name in ("heightfield", "readme_glass"):   # scene data: the oracle renders the product-built descriptor
+    eff = effective_cpus(cpu)
+    if scene_name in ("heightfield", "readme_glass", "readme_glass1", "readme_filter15"):
+        # scene data: the oracle renders the product-built descriptor
         sc = product_scene
     else:
         sc = (O.OracleScene.readme if scene_name == "readme" else O.OracleScene.cornell)(W, H)
-    share = args.cpu_threads or max(1, cpu["nproc"] // gpus_per_host)
-    whole = cpu["nproc"]
+    node_share = max(1, cpu["nproc"] // gpus_per_host)
+    share = args.cpu_threads or min(node_share, eff)
     budget = args.cpu_seconds / 2
     v_share, s_share = cpu_rate(sc, rd_kwargs, share, budget)
+    capped = share < node_share
     out = {
         "value": v_share,
         "unit": "Mpaths/s",
@@ -151,16 +171,25 @@ def cpu_baseline(args, scene_name, rd_kwargs, W, H, product_scene=None, gpus_per
         "nproc": cpu["nproc"],
         "affinity": cpu["affinity"],
         "cgroup_cpus": cpu["cgroup_cpus"],
+        "effective_cpus": eff,
         "cpu_model": cpu["cpu_model"],
         "per_core": v_share / share,
-        "sample": f"{s_share} (the per-GPU share of the host: nproc {cpu['nproc']} / {gpus_per_host} GPUs); "
-                  "oracle/ C restatement of the Go path, which has no Go per-op heap allocation, so it is "
-                  "expected to be faster than go-pbrt",
+        "sample": f"{s_share}; "
+                  + (f"the node's per-GPU share is nproc {cpu['nproc']} / {gpus_per_host} GPUs = {node_share} CPUs, "
+                     f"but this box grants {eff} (affinity {cpu['affinity']}, cgroup quota {cpu['cgroup_cpus']}): "
+                     f"timed on all {share} granted CPUs" if capped else
+                     f"the per-GPU share of the host: nproc {cpu['nproc']} / {gpus_per_host} GPUs")
+                  + "; oracle/ C restatement of the Go path, which has no Go per-op heap allocation, so it is "
+                    "expected to be faster than go-pbrt",
     }
-    if whole != share:
-        v_whole, s_whole = cpu_rate(sc, rd_kwargs, whole, budget)
-        out["whole_host"] = {"value": v_whole, "unit": "Mpaths/s", "cores": whole, "per_core": v_whole / whole,
-                             "sample": s_whole + " (every host core, SURVEY 8(d))"}
+    if capped:
+        out["per_gpu_share"] = {"cpus": node_share, "value_extrapolated": v_share / share * node_share,
+                                "note": f"linear extrapolation of the {share}-CPU timing to the node's per-GPU "
+                                        f"share ({node_share} CPUs); not measured"}
+    elif eff > share:
+        v_all, s_all = cpu_rate(sc, rd_kwargs, eff, budget)
+        out["all_granted"] = {"value": v_all, "unit": "Mpaths/s", "cores": eff, "per_core": v_all / eff,
+                              "sample": s_all + f" (all {eff} CPUs this box grants)"}
     return out
 
 
@@ -188,20 +217,36 @@ def roofline(scene_name, W, H, S, paths_per_launch, kernel_kind, kern_ms, chain_
     else:
         algo, name, ms = total, "k_render_exact", kern_ms
     achieved = algo / (ms / 1e3) / 1e12
-    traffic = (pmc.get(name) or {}).get("hbm_bytes_per_launch")
-    frame_bytes = sum(v.get("hbm_bytes_per_launch", 0) for v in pmc.values() if isinstance(v, dict))
     return {"bound": "fp64-valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+            "frac": achieved / FP64_PEAK_TFLOPS,
+            # the add/mul peak the no-contraction parity build can reach
+            "peak_nofma": FP64_PEAK_NOFMA_TFLOPS, "frac_nofma": achieved / FP64_PEAK_NOFMA_TFLOPS,
             "kernel": name, "kernel_ms": ms, "flops_per_launch": algo,
-            # the north_star's "HBM GB/s vs peak": PMC bytes (profiles/pmc_*.json, same command under
-            # rocprofv3) over this run's kernel time, for the dominant kernel and the whole frame
-            "hbm": {"kernel_gbs": traffic / (ms / 1e3) / 1e9 if traffic else None,
-                    "frame_gbs": frame_bytes / (kern_ms / 1e3) / 1e9 if frame_bytes else None,
-                    "peak_gbs": HBM_PEAK_GBS,
-                    "kernel_frac": traffic / (ms / 1e3) / 1e9 / HBM_PEAK_GBS if traffic else None},
+            "flops_source": f"profiles/flops_{scene_name}_{W}x{H}_s{S}x{S}.json",
+            **pmc_fields(pmc, name, ms, kern_ms),
             "pipeline": {"kernels_ms": kern_ms, "k_paths_ms": paths_ms, "merge_ms": merge_ms,
                          "achieved_tflops": total / (kern_ms / 1e3) / 1e12,
                          "flops_per_path": fl["flops_per_path"]}}
+
+
+def pmc_fields(pmc, name, ms, frame_ms):
+    """`traffic` and the north_star's "HBM GB/s vs peak" from the PMC passes
+    (profiles/pmc_*.json: rocprofv3 FETCH_SIZE / WRITE_SIZE runs of the same
+    bench command, tools/pmc_traffic.py), named by the library build they
+    measured: `traffic_same_build` says whether that is the build running now."""
+    traffic = (pmc.get(name) or {}).get("hbm_bytes_per_launch")
+    frame_bytes = sum(v.get("hbm_bytes_per_launch", 0) for v in pmc.values() if isinstance(v, dict))
+    pmc_build = pmc.get("build_id")
+    return {"traffic": traffic,
+            "traffic_source": pmc.get("source"), "traffic_build_id": pmc_build,
+            "traffic_same_build": bool(pmc_build) and pmc_build == BUILD_ID,
+            "hbm": {"kernel_gbs": traffic / (ms / 1e3) / 1e9 if traffic else None,
+                    "frame_gbs": frame_bytes / (frame_ms / 1e3) / 1e9 if frame_bytes else None,
+                    "peak_gbs": HBM_PEAK_GBS,
+                    "kernel_frac": traffic / (ms / 1e3) / 1e9 / HBM_PEAK_GBS if traffic else None}}
+
+
+BUILD_ID = None   # pbrt_gpu_build_id() of the loaded library (set in main)
 
 
 CONFIGS = {
@@ -225,6 +270,20 @@ CONFIGS = {
     "G": dict(scene="readme_glass", spp=8, max_depth=10,
               text="README sphere scene + glass sphere (server.go:67-91) + mirror sphere {W}x{H}, "
                    "Stratified({S},{S}) = {T} traced paths/px, Path(maxDepth 10, rr 1, Uniform), tile 16"),
+    # The reference behaviours that run on the serial kernel, at 1080p:
+    # H: server.go:160's commented-out DirectLighting(UniformSampleAll, 10) with the
+    #    commented-out glass sphere (server.go:67-94)
+    "H": dict(scene="readme_glass1", spp=8, max_depth=10, integrator="direct",
+              text="README sphere scene + glass sphere (server.go:67-94) {W}x{H}, Stratified({S},{S}) = {T} traced "
+                   "samples/px, DirectLighting(UniformSampleAll, maxDepth 10), tile 16"),
+    # F: config B with a BoxFilter of radius 1.5 (film.go:211-248: 4-9 film pixels per sample)
+    "F": dict(scene="readme_filter15", spp=8, max_depth=10,
+              text="README sphere scene {W}x{H}, BoxFilter radius 1.5, Stratified({S},{S}) = {T} traced paths/px, "
+                   "Path(maxDepth 10, rr 1, Uniform), tile 16"),
+    # N: config B with Stratified(8, 8, false, 2): two sampled dimensions (stratified.go:12-19)
+    "N": dict(scene="readme", spp=8, max_depth=10, n_dims=2,
+              text="README sphere scene {W}x{H}, Stratified({S},{S}) with 2 sampled dimensions = {T} traced "
+                   "paths/px, Path(maxDepth 10, rr 1, Uniform), tile 16"),
 }
 
 
@@ -233,6 +292,12 @@ def make_scene(G, cfg, W, H):
         return G.Scene.readme(W, H)
     if cfg["scene"] == "readme_glass":
         return G.Scene.readme_glass(W, H)
+    if cfg["scene"] == "readme_glass1":
+        return G.Scene.readme_glass(W, H, mirror=False)
+    if cfg["scene"] == "readme_filter15":
+        s = G.Scene.readme(W, H)
+        s.set_film(W, H, filter_radius=(1.5, 1.5))
+        return s.build(2)
     if cfg["scene"] == "cornell":
         return G.Scene.cornell(W, H)
     return G.Scene.heightfield(W, H, quads=cfg["quads"], seed=1)
@@ -256,9 +321,9 @@ def mesh_roofline(cfg, W, H, S, mode, stats_ms, paths):
         return None
     frame_bytes = k["bytes_per_path"] * paths
     achieved = frame_bytes / (ms / 1e3) / 1e9
-    traffic = (pmc.get(name.replace("_mb", "")) or {}).get("hbm_bytes_per_launch")
+    pf = pmc_fields(pmc, name.replace("_mb", ""), ms, stats_ms["kernels"])
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": name, "kernel_ms": ms,
+            "frac": achieved / HBM_PEAK_GBS, **pf, "kernel": name, "kernel_ms": ms,
             "bytes_per_launch": frame_bytes, "bytes_per_path": k["bytes_per_path"],
             "per_walk": {q: {"nodes": k[q]["nodes_per_walk"], "triangles": k[q]["triangles_per_walk"]}
                          for q in ("closest", "any") if q in k},
@@ -370,6 +435,8 @@ def main():
 
     import pbrtgpu as G
 
+    global BUILD_ID
+    BUILD_ID = G.build_id()
     cfg = CONFIGS[args.config]
     W, H = args.width or cfg.get("width", 1920), args.height or cfg.get("height", 1080)
     shard_r, shard_n = rank, world
@@ -379,6 +446,10 @@ def main():
         shard_r, shard_n = (int(x) for x in args.shard.split("/"))
     S = args.spp or cfg["spp"]
     rd_kwargs = dict(spp_x=S, spp_y=S, max_depth=cfg["max_depth"])
+    if cfg.get("integrator") == "direct":
+        rd_kwargs["integrator"] = G.abi.PBRT_INTEGRATOR_DIRECT_LIGHTING
+    if "n_dims" in cfg:
+        rd_kwargs["n_dims"] = cfg["n_dims"]
     scene = make_scene(G, cfg, W, H)
     # the renderer (and its two HIP streams) before RCCL's own streams, so the
     # heavy/light chain launches get hardware queues of their own
@@ -427,7 +498,9 @@ def main():
 
     if rank == 0:
         value = paths_total / elapsed / 1e6
-        if cfg["scene"] == "heightfield":
+        if cfg.get("integrator") or "n_dims" in cfg or cfg["scene"] == "readme_filter15":
+            roof = None   # no algorithmic-FLOP count of these variants (profiles/flops_* are B, C, G)
+        elif cfg["scene"] == "heightfield":
             roof = mesh_roofline(cfg, W, H, S, args.mode, {"chain": chain_ms, "paths": paths_ms, "kernels": kern_ms},
                                  paths_local / len(stats))
         else:
@@ -448,7 +521,9 @@ def main():
             "data": {"readme": "synthetic (the reference's hard-coded README scene; no external data)",
                      "cornell": "synthetic (SURVEY 8(d) Cornell fixture built from reference types)",
                      "heightfield": "synthetic (procedural height field, seed 1; triangle extension)",
-                     "readme_glass": "synthetic (README scene + server.go's commented-out glass sphere + a mirror)"
+                     "readme_glass": "synthetic (README scene + server.go's commented-out glass sphere + a mirror)",
+                     "readme_glass1": "synthetic (README scene + server.go's commented-out glass sphere)",
+                     "readme_filter15": "synthetic (the README scene with a radius-1.5 box filter)",
                      }[cfg["scene"]],
             "config": {
                 "workload": cfg["text"].format(W=W, H=H, S=S, T=S * S - 1) + ", "
@@ -459,7 +534,7 @@ def main():
                 "parallelism": f"tiles mod {world}" + (" + RCCL film reduce" if world > 1 else "")
                                + (f"; ONE GPU rendering rank {shard_r}'s shard of {shard_n} (tiles t mod {shard_n} == "
                                   f"{shard_r})" if args.shard else ""),
-                "kernel": {1: "serial", 2: "wave", 3: "wavefront", 4: "wave_ci"}.get(kernel_kind, "?"),
+                "kernel": {1: "serial", 2: "wave", 3: "wavefront", 4: "wave_ci", 5: "wave_dl"}.get(kernel_kind, "?"),
             },
             "pipeline_ms": {"kernels": kern_ms, "chain": chain_ms, "paths": paths_ms, "merge": merge_ms},
             # nominal W*H*spp, and the reference's ray segments counted in-kernel
@@ -469,6 +544,7 @@ def main():
                      "shadow_per_frame": rays_s / len(stats) * (world if world > 1 else 1),
                      "per_s": (rays_c + rays_s) * (world if world > 1 else 1) / elapsed,
                      "unit": "rays/s", "note": "reference ray segments (rank 0's count x N for N > 1)"},
+            "build_id": BUILD_ID,
             "first_frame_ms": first_ms,
             "first_frame_chain_ms": first.chain_ms,
             "roofline": roof,
@@ -478,8 +554,10 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             cb = cpu_baseline(args, cfg["scene"], rd_kwargs, W, H, scene)
             cb["gpu_over_cpu"] = value / cb["value"]
-            if "whole_host" in cb:
-                cb["whole_host"]["gpu_over_cpu"] = value / cb["whole_host"]["value"]
+            if "per_gpu_share" in cb:
+                cb["per_gpu_share"]["gpu_over_cpu_extrapolated"] = value / cb["per_gpu_share"]["value_extrapolated"]
+            if "all_granted" in cb:
+                cb["all_granted"]["gpu_over_cpu"] = value / cb["all_granted"]["value"]
             out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)
     renderer.close()

@@ -1,4 +1,6 @@
 // k_chain.h — k_chain_ci, the continuous-issue offset chain (EXACT mode); instantiated in k_chain_*.hip
+// (Default template arguments live only in render_kernels.h, the declarations
+// the host code sees; the definitions here repeat none, so the unity build works.)
 #pragma once
 #pragma clang fp contract(off)
 
@@ -15,7 +17,7 @@ namespace pbrtk {
 // kDepth: traversal stack entries per lane. Trees of <= kLdsNodes (64) nodes
 // are staged in LDS and walk their leaves only (no stack); larger trees walk
 // with the reference's [64] stack (bvh.go:670).
-template <int kW, int kDepth = 0, bool kX = false>
+template <int kW, int kDepth, bool kX>
 __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT_CI_EU_WAVES, 8))) void k_chain_ci(
     DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
     int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr,

@@ -6,60 +6,85 @@
 namespace pbrtk {
 
 // One thread per tile-film pixel: the tile film of the serial replay.
+// One thread per tile-film pixel: the film pixel's sum in the reference's
+// order (its source pixels row-major, each pixel's samples in order,
+// film.go:211-248 / integrator.go:256-262). The lane whose film pixel is a
+// tile pixel also adds up that pixel's reference ray counts
+// (pbrt_gpu_stats.rays_*), so the counts need no pass of their own.
 __global__ __launch_bounds__(256) void k_film(const pbrt_film_desc* __restrict__ film_desc, RenderParams rp,
                                               WaveBufs wb, int64_t slot_base, int64_t nslots_batch,
-                                              double* __restrict__ films, const int* __restrict__ cancel_seen) {
+                                              double* __restrict__ films, const int* __restrict__ cancel_seen,
+                                              Counters* __restrict__ ctr) {
     // a cancelled render's samples are incomplete: its film is not valid (pbrt_gpu_cancel)
     if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(cancel_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
         return;
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t per = rp.slot_w * rp.slot_h;
-    if (gid >= nslots_batch * per) return;
-    const int64_t bslot = gid / per, fi = gid % per;
-    const int64_t slot = slot_base + bslot;
-    const pbrt_film_desc& film = *film_desc;
-    int64_t x0, y0, x1, y1, px0, py0, px1, py1;
-    tile_bounds(rp, tile_of_slot(rp, slot), x0, y0, x1, y1);
-    film_tile_bounds(film, x0, y0, x1, y1, px0, py0, px1, py1);
-    const int64_t tw = px1 - px0;
-    if (fi >= tw * (py1 - py0)) return;
-    const int64_t fx = px0 + fi % tw, fy = py0 + fi / tw;
-    const int n = rp.spp;
-    const int64_t npx = wb.tile_npx[bslot];
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-    // pixels whose footprint can reach (fx, fy): |p - f| < radius + 1, in row-major order
-    for (int64_t py = fy - 2; py <= fy + 2; py++) {
-        if (py < y0 || py >= y1) continue;
-        for (int64_t px = fx - 2; px <= fx + 2; px++) {
-            if (px < x0 || px >= x1) continue;
-            const int64_t pi = (py - y0) * (x1 - x0) + (px - x0);
-            if (pi >= npx) continue;
-            Footprint fp;
-            int64_t p0x, p0y, p1x, p1y;
-            footprint(film, (double)px + 0.0, (double)py + 0.0, px0, py0, px1, py1, fp, p0x, p0y, p1x, p1y);
-            const int64_t want = fi;
-            int f = -1;
-            for (int q = 0; q < fp.n; q++)
-                if (fp.off[q] == want) f = q;
-            if (f < 0) continue;
-            const double w = fp.w[f];
-            const int64_t rec = bslot * wb.ppt + pi;
-            const int nv = wb.prec[rec].nvalid;
-            const double* Lp = wb.L + rec * n * 3;
-            for (int k = 1; k < nv; k++) {
-                Spec Ls{Lp[k * 3 + 0], Lp[k * 3 + 1], Lp[k * 3 + 2]};
-                if (has_nans(Ls)) Ls = spec(0.1);   // integrator.go:256-262
-                if (0.0 > film.max_sample_luminance) Ls = smuls(Ls, film.max_sample_luminance / 0.0);
-                a0 += Ls.r * w;
-                a1 += Ls.g * w;
-                a2 += Ls.b * w;
+    unsigned long long cl = 0, sh = 0;
+    if (gid < nslots_batch * per) {
+        const int64_t bslot = gid / per, fi = gid % per;
+        const int64_t slot = slot_base + bslot;
+        const pbrt_film_desc& film = *film_desc;
+        int64_t x0, y0, x1, y1, px0, py0, px1, py1;
+        tile_bounds(rp, tile_of_slot(rp, slot), x0, y0, x1, y1);
+        film_tile_bounds(film, x0, y0, x1, y1, px0, py0, px1, py1);
+        const int64_t tw = px1 - px0;
+        if (fi < tw * (py1 - py0)) {
+            const int64_t fx = px0 + fi % tw, fy = py0 + fi / tw;
+            const int n = rp.spp;
+            const int64_t npx = wb.tile_npx[bslot];
+            double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+            // pixels whose footprint can reach (fx, fy): |p - f| < radius + 1, in row-major order
+            for (int64_t py = fy - 2; py <= fy + 2; py++) {
+                if (py < y0 || py >= y1) continue;
+                for (int64_t px = fx - 2; px <= fx + 2; px++) {
+                    if (px < x0 || px >= x1) continue;
+                    const int64_t pi = (py - y0) * (x1 - x0) + (px - x0);
+                    if (pi >= npx) continue;
+                    const int64_t rec = bslot * wb.ppt + pi;
+                    const int nv = wb.prec[rec].nvalid;
+                    if (px == fx && py == fy) {   // this lane counts the pixel's rays
+                        for (int k = 1; k < nv; k++) {
+                            const uint32_t v = wb.rays[sample_index(wb, rec, n, k)];
+                            cl += v & 0xFFFFu;
+                            sh += v >> 16;
+                        }
+                    }
+                    Footprint fp;
+                    int64_t p0x, p0y, p1x, p1y;
+                    footprint(film, (double)px + 0.0, (double)py + 0.0, px0, py0, px1, py1, fp, p0x, p0y, p1x, p1y);
+                    const int64_t want = fi;
+                    int f = -1;
+                    for (int q = 0; q < fp.n; q++)
+                        if (fp.off[q] == want) f = q;
+                    if (f < 0) continue;
+                    const double w = fp.w[f];
+                    const double* Lp = wb.L + sample_index(wb, rec, n, 0) * 3;
+                    const int64_t kst = wb.ppt * 3;   // one sample to the next, same pixel
+                    for (int k = 1; k < nv; k++) {
+                        Spec Ls{Lp[k * kst + 0], Lp[k * kst + 1], Lp[k * kst + 2]};
+                        if (has_nans(Ls)) Ls = spec(0.1);   // integrator.go:256-262
+                        if (0.0 > film.max_sample_luminance) Ls = smuls(Ls, film.max_sample_luminance / 0.0);
+                        a0 += Ls.r * w;
+                        a1 += Ls.g * w;
+                        a2 += Ls.b * w;
+                    }
+                }
             }
+            double* tf = films + slot * per * 3 + fi * 3;
+            tf[0] = a0;
+            tf[1] = a1;
+            tf[2] = a2;
         }
     }
-    double* tf = films + slot * per * 3 + fi * 3;
-    tf[0] = a0;
-    tf[1] = a1;
-    tf[2] = a2;
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+        cl += __shfl_down(cl, off);
+        sh += __shfl_down(sh, off);
+    }
+    if ((threadIdx.x & (kWave - 1)) == 0 && (cl | sh)) {
+        atomicAdd(&ctr->closest_rays, cl);
+        atomicAdd(&ctr->shadow_rays, sh);
+    }
 }
 
 // First panic of each tile slot in pixel order -> panics[slot].
@@ -78,35 +103,8 @@ __global__ void k_panic_reduce(WaveBufs wb, int64_t slot_base, int64_t nslots_ba
     }
 }
 
-// Bounce 1 of every pixel record of the batch: the camera ray through the
-// pixel corner (pFilm and pLens are (0,0) for every sample), its closest hit
-// and BSDF. The ray time is patched by the chain kernel once StartPixel gives it.
-// stats.rays_closest / rays_shadow of a batch: every valid sample's counts
-// (pixels with records, samples 1 .. nvalid-1), one atomic pair per wave
-__global__ __launch_bounds__(256) void k_ray_count(WaveBufs wb, int64_t nb, int n, Counters* __restrict__ ctr,
-                                                   const int* __restrict__ cancel_seen) {
-    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(cancel_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
-        return;   // a cancelled render reports no counts
-    unsigned long long cl = 0, sh = 0;
-    const int64_t total = nb * wb.ppt * n;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t rec = i / n, k = i - rec * n, bs = rec / wb.ppt, pi = rec % wb.ppt;
-        if (k < 1 || pi >= wb.tile_npx[bs] || k >= wb.prec[rec].nvalid) continue;
-        const uint32_t v = wb.rays[i];
-        cl += v & 0xFFFFu;
-        sh += v >> 16;
-    }
-    for (int off = kWave / 2; off > 0; off >>= 1) {
-        cl += __shfl_down(cl, off);
-        sh += __shfl_down(sh, off);
-    }
-    if ((threadIdx.x & (kWave - 1)) == 0) {
-        atomicAdd(&ctr->closest_rays, cl);
-        atomicAdd(&ctr->shadow_rays, sh);
-    }
-}
 
-template <bool kX = false>
+template <bool kX>
 __global__ __launch_bounds__(kWave) void k_wf_primary(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
                                                       int64_t nb) {
     __shared__ uint16_t stack_lds[64 * kStackStride];
@@ -229,7 +227,7 @@ __global__ __launch_bounds__(kWave) void k_dl_samples(DevScene sc, RenderParams 
         const int64_t bs = rec / wb.ppt, pi = rec % wb.ppt;
         if (pi >= wb.tile_npx[bs]) continue;
         const PixelRec& pr = wb.prec[rec];
-        double* o = wb.L + (rec * n + k) * 3;
+        double* o = wb.L + sample_index(wb, rec, n, k) * 3;
         Spec L = spec(0);
         int panic = pr.panic0;
         uint64_t shadow = 0;   // visibility rays traced (the camera ray's query is counted below)
@@ -270,7 +268,7 @@ __global__ __launch_bounds__(kWave) void k_dl_samples(DevScene sc, RenderParams 
         o[0] = L.r;
         o[1] = L.g;
         o[2] = L.b;
-        wb.rays[rec * n + k] = kRayClosest + (uint32_t)shadow * kRayShadow;
+        wb.rays[sample_index(wb, rec, n, k)] = kRayClosest + (uint32_t)shadow * kRayShadow;
         if (panic)
             atomicMin((unsigned long long*)&wb.memb[rec * n],
                       ((unsigned long long)k << 32) | (unsigned long long)((panic + 1) & 0xFF));
@@ -305,7 +303,7 @@ __global__ void k_dl_panics(RenderParams rp, WaveBufs wb, int64_t slot_base, int
     }
 }
 
-template <bool kX = false>
+template <bool kX>
 __global__ __launch_bounds__(kWave) void k_tile_cost(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
                                                      int64_t nb, float* __restrict__ feat,
                                                      uint64_t* __restrict__ keys) {

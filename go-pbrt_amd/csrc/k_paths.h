@@ -6,7 +6,7 @@
 
 namespace pbrtk {
 
-template <int P, bool kMB = false, bool kX = false>
+template <int P, bool kMB, bool kX>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kPathsWaves, 8))) void k_paths_ci(
     DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr,
     int s1d_lds) {
@@ -21,7 +21,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kPathsWav
 // (camera ray, first hit, BSDF), written to the PixelRec / s1d buffers the
 // EXACT pipeline fills with k_wf_primary + k_chain_ci. The same arithmetic as
 // the serial kernel's pixel prologue.
-template <bool kX = false>
+template <bool kX>
 __global__ __launch_bounds__(kWave) void k_mb_setup(DevScene sc, RenderParams rp, ChainLayout lay,
                                                     const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
                                                     int64_t nslots_batch) {

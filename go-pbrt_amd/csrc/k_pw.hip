@@ -5,7 +5,7 @@
 
 namespace pbrtk {
 
-template <bool kX = false>
+template <bool kX>
 __global__ __launch_bounds__(kWave) void k_pw_cache(DevScene sc, WaveBufs wb, int64_t rec0, int64_t nrec,
                                                     Spec* __restrict__ ldc, int* __restrict__ ldp) {
     __shared__ uint16_t stack_lds[64 * kStackStride];
@@ -26,7 +26,7 @@ __global__ __launch_bounds__(kWave) void k_pw_cache(DevScene sc, WaveBufs wb, in
     ldp[i] = pl | (traced ? kLdTraced : 0);
 }
 
-template <bool kMB, bool kX = false>
+template <bool kMB, bool kX>
 __global__ __launch_bounds__(kWave) void k_pw_start(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
                                                     int64_t rec0, int64_t nrec, const Spec* __restrict__ ldc,
                                                     const int* __restrict__ ldp, PwPath* __restrict__ paths,
@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256) void k_pw_scatter(const PwPath* __restrict__ p
     }
 }
 
-template <bool kX = false>
+template <bool kX>
 __global__ __launch_bounds__(kWave) void k_pw_shade(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
                                                     PwPath* __restrict__ paths, PwQueues qs, int sorted,
                                                     unsigned long long* __restrict__ pkey) {

@@ -1250,14 +1250,10 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                 }
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 2], c->stream));
                 hipLaunchKernelGGL(k_film, dim3((unsigned)((nb * per + 255) / 256)), dim3(256), 0, c->stream,
-                                   c->d_film, rp, c->wb, sb, nb, c->d_films, c->d_cancel_seen);
+                                   c->d_film, rp, c->wb, sb, nb, c->d_films, c->d_cancel_seen, c->d_ctr);
                 hipLaunchKernelGGL(k_panic_reduce, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, c->stream, c->wb,
                                    sb, nb, c->d_panics, c->d_ctr);
-                if (rp.spp > 1)
-                    hipLaunchKernelGGL(k_ray_count,
-                                       dim3((unsigned)std::min<int64_t>((nb * c->wb.ppt * rp.spp + 255) / 256,
-                                                                        (int64_t)c->n_simd * 16)),
-                                       dim3(256), 0, c->stream, c->wb, nb, rp.spp, c->d_ctr, c->d_cancel_seen);
+
             }
         } else {
             c->last_kernel = PBRT_KERNEL_SERIAL;
@@ -1704,6 +1700,11 @@ extern "C" int pbrt_gpu_step_cycles(uint64_t* out, int n, int reset) {
 #endif
     return 8;
 }
+
+#ifndef PBRT_BUILD_ID
+#define PBRT_BUILD_ID "unknown"
+#endif
+extern "C" const char* pbrt_gpu_build_id(void) { return PBRT_BUILD_ID; }
 
 extern "C" int pbrt_abi_sizes(size_t* out, int n) {
     const size_t s[] = {sizeof(pbrt_matrix4x4),   sizeof(pbrt_transform),    sizeof(pbrt_shape_desc),

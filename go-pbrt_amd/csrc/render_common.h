@@ -167,6 +167,14 @@ struct WaveBufs {
     int64_t ppt;        // pixel records per tile slot (tile_size^2)
     int64_t s1d_stride; // ndims * spp
 };
+// Per-sample outputs (wb.L, wb.rays) are sample-major within a tile slot:
+// [slot][k][pixel], so that k_film's lanes (consecutive film pixels) read
+// consecutive pixels of one sample -- coalesced -- while each lane still
+// walks its source pixels' samples in the reference's order.
+__device__ __forceinline__ int64_t sample_index(const WaveBufs& wb, int64_t rec, int n, int k) {
+    const int64_t bslot = rec / wb.ppt, pi = rec - bslot * wb.ppt;
+    return (bslot * n + k) * wb.ppt + pi;
+}
 struct ChainLayout {   // byte offsets into the chain / setup kernels' dynamic LDS block
     int s1d, other, sbuf, dbuf, vbuf, total;
     int ring;      // k_chain_ci: offset ring after the StartPixel staging (no sbuf / dbuf)
@@ -419,11 +427,11 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
                 k = 1 + (t - meta[j].cum);
                 const int64_t rec = rec0 + j;
                 if (!meta[j].hit) {   // no traced bounce: the sample's radiance is 0
-                    double* o = wb.L + (rec * n + k) * 3;
+                    double* o = wb.L + sample_index(wb, rec, n, k) * 3;
                     o[0] = 0.0;
                     o[1] = 0.0;
                     o[2] = 0.0;
-                    wb.rays[rec * n + k] = kRayClosest;   // the camera ray's (missed or maxDepth 1) query
+                    wb.rays[sample_index(wb, rec, n, k)] = kRayClosest;   // the camera ray's (missed or maxDepth 1) query
                 } else {
                     w = t;
                     c.rng.state = kMB ? mb_state(meta[j].tile, (uint64_t)(rec % wb.ppt), (uint64_t)k)
@@ -462,12 +470,12 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
                 done = path_step<2, kX>(sc, pcs[j], ss, c, ps, rp.max_depth, rp.rr_threshold, nullptr, pnc, bnc);
             if (done) {
                 const int64_t rec = rec0 + j;
-                double* o = wb.L + (rec * n + k) * 3;
+                double* o = wb.L + sample_index(wb, rec, n, k) * 3;
                 const Spec Lp = *ps.L;
                 o[0] = Lp.r;
                 o[1] = Lp.g;
                 o[2] = Lp.b;
-                wb.rays[rec * n + k] = *ps.rays;
+                wb.rays[sample_index(wb, rec, n, k)] = *ps.rays;
                 if (pnc)
                     atomicMin(&pkey[j], ((unsigned long long)k << 32) | ((unsigned long long)(bnc & 0xFFFFFF) << 8) |
                                             (unsigned long long)((pnc + 1) & 0xFF));
@@ -575,11 +583,11 @@ __device__ __forceinline__ uint32_t pw_add_by_key(uint32_t* ctr, int key) {
 }
 // a finished path: its radiance, and its panic into the pixel's key
 __device__ __forceinline__ void pw_finish(const WaveBufs& wb, int n, const PwPath& p, unsigned long long* pkey) {
-    double* o = wb.L + (p.rec * n + p.k) * 3;
+    double* o = wb.L + sample_index(wb, p.rec, n, p.k) * 3;
     o[0] = p.L.r;
     o[1] = p.L.g;
     o[2] = p.L.b;
-    wb.rays[p.rec * n + p.k] = p.rays;
+    wb.rays[sample_index(wb, p.rec, n, p.k)] = p.rays;
     if (p.pnc)
         atomicMin(&pkey[p.rec], ((unsigned long long)p.k << 32) | ((unsigned long long)(p.bnc & 0xFFFFFF) << 8) |
                                     (unsigned long long)((p.pnc + 1) & 0xFF));

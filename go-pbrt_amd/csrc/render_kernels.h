@@ -24,9 +24,8 @@ __global__ void k_pw_shadow(DevScene sc, RenderParams rp, WaveBufs wb, PwPath* _
 __global__ void k_pw_panics(RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t rec0, int64_t nrec, const unsigned long long* __restrict__ pkey, Counters* __restrict__ ctr);
 template <bool kX = false>
 __global__ void k_mb_setup(DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base, int64_t nslots_batch);
-__global__ void k_film(const pbrt_film_desc* __restrict__ film_desc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nslots_batch, double* __restrict__ films, const int* __restrict__ cancel_seen);
+__global__ void k_film(const pbrt_film_desc* __restrict__ film_desc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nslots_batch, double* __restrict__ films, const int* __restrict__ cancel_seen, Counters* __restrict__ ctr);
 __global__ void k_panic_reduce(WaveBufs wb, int64_t slot_base, int64_t nslots_batch, PanicRec* __restrict__ panics, Counters* __restrict__ ctr);
-__global__ void k_ray_count(WaveBufs wb, int64_t nb, int n, Counters* __restrict__ ctr, const int* __restrict__ cancel_seen);
 template <bool kX = false>
 __global__ void k_wf_primary(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nb);
 __global__ void k_dl_setup(DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base, int64_t nb);

@@ -42,6 +42,8 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise FileNotFoundError(f"{LIB_PATH} missing: run `make -C go-pbrt_amd` (or __graft_entry__.build())")
     L = C.CDLL(LIB_PATH)
+    L.pbrt_gpu_build_id.restype = C.c_char_p
+    L.pbrt_gpu_build_id.argtypes = []
     P, d, i64 = C.POINTER, C.c_double, C.c_int64
     T = P(abi.Transform)
     L.pbrt_gpu_create.argtypes = [P(abi.SceneDesc), P(abi.GpuOpts), P(C.c_void_p)]
@@ -128,6 +130,11 @@ def lib():
     L.pbrt_gpu_mesh_download.argtypes = [C.c_void_p, C.c_void_p, P(C.c_int32), P(C.c_float)]
     _lib = L
     return L
+
+
+def build_id():
+    """Content hash of the sources the loaded library was built from."""
+    return lib().pbrt_gpu_build_id().decode()
 
 
 def _d3(v):

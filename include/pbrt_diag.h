@@ -111,6 +111,11 @@ int pbrt_gpu_step_cycles(uint64_t* out, int n, int reset);
 /* sizeof() of every ABI struct, for binding checks (index order as in pbrt_gpu.h). */
 int pbrt_abi_sizes(size_t* out, int n);
 
+/* Content hash of the sources this library was built from (Makefile: the first
+ * 16 hex digits of sha256 over csrc/, the headers and the Makefile), so that
+ * profiles and bench lines can name the build they measured. */
+const char* pbrt_gpu_build_id(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -10,6 +10,7 @@
 #                         extra bench args after commas, e.g. bench=C,--steps,1
 #   benchfull=<cfg>       bench.py --config <cfg> with its CPU baseline and side mode
 #   profile=<cfg>         tools/profile_round.sh for that config
+#   phase=<diag|steptime> tools/phase_stats.py with lib/libpbrt_gpu_<build>.so (config B)
 #   smoke                 __graft_entry__.smoke()
 set -o pipefail
 TAG=$1
@@ -33,6 +34,9 @@ for step in "$@"; do
   profile=*)
     cfg=${step#profile=}
     bash tools/profile_round.sh ${TAG}/prof_$cfg --config $cfg || { echo "profile $cfg failed"; exit 1; } ;;
+  phase=*)   # phase=diag | phase=steptime: tools/phase_stats.py on that diagnostics build (config B)
+    lib=${step#phase=}
+    PBRT_GPU_LIB=go-pbrt_amd/lib/libpbrt_gpu_$lib.so timeout -k 10 300 python tools/phase_stats.py > $OUT/phase_$lib.txt 2>&1 || { echo "phase $lib failed"; tail -20 $OUT/phase_$lib.txt; exit 1; } ;;
   smoke)
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $OUT/smoke.log; exit 1; } ;;
   *) echo "unknown step $step"; exit 2 ;;

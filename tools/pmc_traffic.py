@@ -35,7 +35,13 @@ def per_kernel(path, counter):
 def main(d):
     fetch = per_kernel(os.path.join(d, "pmc_fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(d, "pmc_write", "write_counter_collection.csv"), "WRITE_SIZE")
-    res = {"source": d, "units": "bytes per launch (dispatch mean)",
+    build = None   # the library build the passes ran: profile_round.sh's bench.json of the same directory
+    try:
+        with open(os.path.join(d, "bench.json")) as f:
+            build = json.loads(f.read().strip().splitlines()[-1]).get("build_id")
+    except (OSError, ValueError, IndexError):
+        pass
+    res = {"source": d, "build_id": build, "units": "bytes per launch (dispatch mean)",
            "correction": "read = 2 x FETCH_SIZE KiB x 1024 (gfx950 half-count of 128-B requests); write = WRITE_SIZE KiB x 1024"}
     for k in sorted(set(fetch) | set(write)):
         if k.startswith("__amd") or "elementwise" in k:
