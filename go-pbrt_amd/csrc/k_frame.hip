@@ -126,11 +126,35 @@ __global__ __launch_bounds__(kWave) void k_wf_primary(DevScene sc, RenderParams 
     bx0.n = 0;
     Ray ray = camera_ray(*sc.camera, (double)px + 0.0, (double)py + 0.0, 0.0, V2{0.0, 0.0});
     // Path.Li traces bounce 1 only below maxDepth (path.go:66); DirectLighting always
-    if (rp.spp > 1 && (1 < rp.max_depth || rp.integrator == PBRT_INTEGRATOR_DIRECT_LIGHTING)) {
+    const bool dl = rp.integrator == PBRT_INTEGRATOR_DIRECT_LIGHTING;
+    if (rp.spp > 1 && (1 < rp.max_depth || dl)) {
         hit0 = bvh_traverse<false>(sc, ray, &si0, stack_lds + threadIdx.x, panic0) ? 1 : 0;
-        if (!panic0 && hit0 && (kX ? compute_bsdf_x(sc, si0, b0, bx0) : compute_bsdf(sc, si0, b0)) < 0) panic0 = -1;
+        // DirectLighting asks for one lobe per BxDF (directlighting.go:76)
+        if (!panic0 && hit0 && (kX ? compute_bsdf_x(sc, si0, b0, bx0, !dl) : compute_bsdf(sc, si0, b0)) < 0)
+            panic0 = -1;
+    }
+    // DirectLighting's recursion chain (dl_chain_draws): SpecularTransmit's
+    // direction reads no sample, so the levels it reaches are the pixel's
+    int levels = (hit0 && !panic0) ? 1 : 0;
+    if (kX && dl && levels) {
+        SI si = si0;
+        BSDF b = b0;
+        BSDFX x = bx0;
+        for (int depth = 0; depth + 1 < rp.max_depth && levels <= kDlMaxLevels; depth += 2) {
+            V3 wi;
+            double pdf;
+            const Spec f = spec_trans_sample(b, x, si.wo, V2{0.0, 0.0}, wi, pdf);
+            if (!(pdf > 0 && !is_black(f) && absdot(wi, si.sn) != 0.0)) break;
+            Ray r{offset_ray_origin(si.p, si.perr, si.n, wi), wi, kInf, si.time};   // local-frame wi (#7)
+            int pn = 0;
+            // a miss ends the chain; a panic ends the tile at that sample either way
+            if (!bvh_traverse<false>(sc, r, &si, stack_lds + threadIdx.x, pn) || pn) break;
+            if (compute_bsdf_x(sc, si, b, x, false) < 0) break;
+            levels++;
+        }
     }
     PixelRec& pr = wb.prec[rec];
+    pr.dl_levels = levels;
     pr.si = si0;
     pr.b = b0;
     if constexpr (kX) pr.x = bx0;
@@ -182,7 +206,7 @@ __global__ __launch_bounds__(kWave) void k_dl_setup(DevScene sc, RenderParams rp
             for (int idx = lane; idx < rp.ndims * n; idx += kWave) gs1d[idx] = s1d[idx];
         PixelRec& pr = wb.prec[rec];
         const int hit = pr.hit, panic0 = pr.panic0;
-        const uint64_t D = dl_draws(rp, hit, sc.n_lights);
+        const uint64_t D = dl_chain_draws(rp, hit ? pr.dl_levels : 0, sc.n_lights);
         uint64_t* mst = wb.memb + rec * n;
         for (int k = 1 + lane; k < n; k += kWave)
             mst[k] = mb ? mb_state((uint64_t)tile, (uint64_t)pi, (uint64_t)k) : pcg_advance(J, S1, inc, (uint64_t)(k - 1) * D);
@@ -208,6 +232,12 @@ __global__ __launch_bounds__(kWave) void k_dl_setup(DevScene sc, RenderParams rp
 // from the pixel's bounce-1 record, with the sample's own PCG32 state.
 // Radiance to wb.L; a panic lowers the pixel's key (sample << 32 | kind + 1)
 // in wb.memb[rec * spp + 0] (the first panic in sample order wins).
+// kX (Mirror / smooth Glass / OrenNayar scenes): DirectLighting.Li's whole
+// recursion per sample (directlighting.go:62-104, integrator.go:352-422), as the
+// serial kernel's direct_li folds it: SpecularReflect matches no lobe of these
+// materials, SpecularTransmit refracts through smooth glass (local-frame wi,
+// #7) into Li at depth + 2 (#23). A panic's bounce is that level's depth + 1.
+template <bool kX>
 __global__ __launch_bounds__(kWave) void k_dl_samples(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base,
                                                       int64_t nrec) {
     __shared__ uint16_t stack_lds[64 * kStackStride];
@@ -230,8 +260,90 @@ __global__ __launch_bounds__(kWave) void k_dl_samples(DevScene sc, RenderParams 
         double* o = wb.L + sample_index(wb, rec, n, k) * 3;
         Spec L = spec(0);
         int panic = pr.panic0;
+        int bounce = 1;
         uint64_t shadow = 0;   // visibility rays traced (the camera ray's query is counted below)
-        if (!panic && pr.hit) {
+        uint32_t closest = 1;
+        if (kX && !panic && pr.hit) {
+            Cursor c;
+            c.rng.state = wb.memb[rec * n + k];
+            c.rng.inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + bs));
+            c.draws = 0;
+            c.cur1d = c.cur2d = 0;
+            c.k = k;
+            c.kdep = 0;
+            const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, n, rp.ndims};
+            c_get2d(c, ss);   // camera: pFilm, pLens, time
+            c_get2d(c, ss);
+            c_get1d(c, ss);
+            Spec own[kDlMaxLevels], fk[kDlMaxLevels];
+            double wk[kDlMaxLevels];
+            int levels = 0;
+            SI si = pr.si;
+            BSDF b = pr.b;
+            BSDFX x = pr.x;
+            Ray ray;
+            uint16_t* stack = stack_lds + threadIdx.x;
+            for (int depth = 0;; depth += 2) {
+                L = spec(0);
+                bounce = depth + 1;
+                if (depth > 0) {   // the refracted ray of the level above (level 0: the pixel record)
+                    closest++;
+                    if (!bvh_traverse<false>(sc, ray, &si, stack, panic)) {
+                        for (int i = 0; i < sc.n_lights; i++) L = L + spec(0);
+                        break;
+                    }
+                    if (panic) break;
+                    if (compute_bsdf_x(sc, si, b, x, false) < 0) {
+                        panic = -1;
+                        break;
+                    }
+                }
+                L = L + spec(0);   // si.Le(si.Wo): no primitive carries an area light
+                const int nl = sc.n_lights;
+                if (nl > 0) {
+                    if (rp.dl_strategy == PBRT_DL_UNIFORM_SAMPLE_ALL) {   // integrator.go:23-46
+                        Spec acc = spec(0);
+                        for (int j = 0; j < nl && !panic; j++) {
+                            const V2 ul = c_get2d(c, ss);
+                            c_get2d(c, ss);
+                            acc = acc + estimate_direct_x(sc, stack, panic, si, b, x, j, ul, &shadow);
+                        }
+                        if (panic) break;
+                        L = L + acc;
+                    } else {   // UniformSampleOneLight with no distribution (integrator.go:48-77)
+                        const int ln = (int)gomath::to_int(gomath::min(c_get1d(c, ss) * (double)nl, (double)(nl - 1)));
+                        const V2 ul = c_get2d(c, ss);
+                        c_get2d(c, ss);
+                        const Spec s1 = estimate_direct_x(sc, stack, panic, si, b, x, ln, ul, &shadow);
+                        if (!panic && max_component(s1) > 10) panic = PBRT_PANIC_LD_GT_10;
+                        if (panic) break;
+                        L = L + s1;
+                    }
+                }
+                if (!(depth + 1 < rp.max_depth)) break;
+                c_get2d(c, ss);   // SpecularReflect (integrator.go:352-355): black
+                L = L + spec(0);
+                const V2 u = c_get2d(c, ss);   // SpecularTransmit (integrator.go:383-385)
+                V3 wi;
+                double pdf;
+                const Spec f = spec_trans_sample(b, x, si.wo, u, wi, pdf);
+                const double adn = absdot(wi, si.sn);
+                if (!(pdf > 0 && !is_black(f) && adn != 0.0) || levels == kDlMaxLevels) {
+                    L = L + spec(0);
+                    break;
+                }
+                own[levels] = L;
+                fk[levels] = f;
+                wk[levels] = adn / pdf;
+                levels++;
+                ray.o = offset_ray_origin(si.p, si.perr, si.n, wi);   // SpawnRay with the local-frame wi
+                ray.d = wi;
+                ray.tmax = kInf;
+                ray.time = si.time;
+            }
+            if (!panic)
+                for (int q = levels - 1; q >= 0; q--) L = own[q] + smuls(smul(fk[q], L), wk[q]);
+        } else if (!panic && pr.hit) {
             Cursor c;
             c.rng.state = wb.memb[rec * n + k];
             c.rng.inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + bs));
@@ -268,10 +380,11 @@ __global__ __launch_bounds__(kWave) void k_dl_samples(DevScene sc, RenderParams 
         o[0] = L.r;
         o[1] = L.g;
         o[2] = L.b;
-        wb.rays[sample_index(wb, rec, n, k)] = kRayClosest + (uint32_t)shadow * kRayShadow;
-        if (panic)
+        wb.rays[sample_index(wb, rec, n, k)] = closest * kRayClosest + (uint32_t)shadow * kRayShadow;
+        if (panic)   // key: sample << 32 | bounce << 8 | kind + 1 (the first panic in sample order wins)
             atomicMin((unsigned long long*)&wb.memb[rec * n],
-                      ((unsigned long long)k << 32) | (unsigned long long)((panic + 1) & 0xFF));
+                      ((unsigned long long)k << 32) | ((unsigned long long)(bounce & 0xFFFFFF) << 8) |
+                          (unsigned long long)((panic + 1) & 0xFF));
 
     }
 }
@@ -294,7 +407,7 @@ __global__ void k_dl_panics(RenderParams rp, WaveBufs wb, int64_t slot_base, int
     } else if (key != ~0ULL) {
         p.kind = (int)(key & 0xFF) - 1;
         p.sample = (int)(key >> 32);
-        p.bounce = 1;
+        p.bounce = (int)((key >> 8) & 0xFFFFFF);
     }
     wb.ppanic[rec] = p;
     if (!p.kind && rp.spp > 1) {
@@ -441,6 +554,8 @@ __global__ __launch_bounds__(kWave) void k_intersect(DevScene sc, int64_t n, con
     o[6] = si.n.x; o[7] = si.n.y; o[8] = si.n.z;
 }
 
+template __global__ void k_dl_samples<false>(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec);
+template __global__ void k_dl_samples<true>(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec);
 template __global__ void k_wf_primary<false>(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nb);
 template __global__ void k_wf_primary<true>(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nb);
 template __global__ void k_tile_cost<false>(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nb, float* __restrict__ feat, uint64_t* __restrict__ keys);

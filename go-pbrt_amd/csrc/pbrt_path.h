@@ -382,8 +382,11 @@ __device__ inline bool shape_hit(const pbrt_shape_desc& s, const Ray& r, double&
     return disk_hit(s, ray, t_hit, ph);
 }
 // the interaction at an accepted hit point ph; r in the shape's parent space
+// sphere_si / disk_si read only the object-space direction and the time, and
+// TransformRay's direction is TransformVector's (transform.go:279-300: the
+// origin push leaves it alone), so only the direction is transformed here.
 __device__ inline void shape_si(const pbrt_shape_desc& s, const Ray& r, V3 ph, SI& si) {
-    Ray ray = xf_ray(s.object_to_world.m_inv, r, nullptr, nullptr);   // the same o, d as in the hit test
+    const Ray ray{V3{0, 0, 0}, xf_vector(s.object_to_world.m_inv, r.d), r.tmax, r.time};
     if (s.type == PBRT_SHAPE_SPHERE) sphere_si(s, ray, ph, si);
     else disk_si(s, ray, ph, si);
 }
@@ -399,13 +402,29 @@ struct alignas(16) DevPrim {
     int32_t kind, material, prim_identity, fast;
 };
 
+#ifdef PBRT_XF_FAST
+// The shape test on the exact TransformRay with its errors (the cold path of
+// prim_hit_t). Out of line: inlined beside the value-only path it made every
+// traversal loop too large to stay in registers (k_chain_ci spilled 320 B/lane).
+__device__ __noinline__ bool prim_hit_exact(const DevScene& sc, int pi, const Ray& r, double& t_hit, V3& ph,
+                                            int& panic) {
+    const DevPrim& p = sc.fprims[pi];
+    Ray ray = r;
+    if (p.kind == PBRT_PRIM_TRANSFORMED) ray = xf_ray(p.prim_to_world.m_inv, r, nullptr, nullptr);
+    return shape_hit(p.shape, ray, t_hit, ph, panic);
+}
+#endif
+
 // Shape test without the SurfaceInteraction: the hit parameter and point.
-// The object-space ray comes from xf_fast where it applies (both transforms of
-// a TransformedPrimitive's shape); otherwise, and when the
-// sphere filter cannot decide, from the exact TransformRay with its errors.
+// Default: the exact TransformRay with its errors, then the shape's test (the
+// sphere's value-first filter, sphere_hit). Experiment builds (-DPBRT_XF_FAST)
+// take the object-space ray from xf_fast where it applies: exact,
+// but measured slower (the disk tests of rays leaving the floor fail its checks,
+// so most waves ran both paths).
 __device__ inline bool prim_hit_t(const DevScene& sc, int pi, const Ray& r, double& t_hit, V3& ph, int& panic) {
     const DevPrim& p = sc.fprims[pi];
     const bool xformed = p.kind == PBRT_PRIM_TRANSFORMED;
+#ifdef PBRT_XF_FAST   // experiment builds (-DPBRT_XF_FAST): measured slower, DESIGN.md 3.6
     {
         Ray ro = r;
         bool fast = !xformed || xf_fast(p.fast & 0xff, p.prim_to_world.m_inv, ro.o, ro.d);
@@ -419,9 +438,12 @@ __device__ inline bool prim_hit_t(const DevScene& sc, int pi, const Ray& r, doub
             if (fr > 0) return sphere_accept(p.shape, ro, rt, t_hit, ph);
         }
     }
+    return prim_hit_exact(sc, pi, r, t_hit, ph, panic);
+#else
     Ray ray = r;
     if (xformed) ray = xf_ray(p.prim_to_world.m_inv, r, nullptr, nullptr);
     return shape_hit(p.shape, ray, t_hit, ph, panic);
+#endif
 }
 
 // Mesh of global triangle index g (meshes are few: a linear scan)
@@ -475,8 +497,8 @@ __device__ inline void prim_si(const DevScene& sc, int pi, const Ray& r, V3 ph, 
     }
     const DevPrim& p = sc.fprims[pi];
     const bool xformed = p.kind == PBRT_PRIM_TRANSFORMED;
-    Ray ray = r;
-    if (xformed) ray = xf_ray(p.prim_to_world.m_inv, r, nullptr, nullptr);
+    Ray ray = r;   // shape_si reads the direction and the time only
+    if (xformed) ray.d = xf_vector(p.prim_to_world.m_inv, r.d);
     shape_si(p.shape, ray, ph, si);
     si.prim = pi;
     if (xformed && !p.prim_identity) transform_si_shared(si, p.prim_to_world.m, p.prim_to_world.m_inv);
@@ -1618,10 +1640,12 @@ __device__ inline Spec estimate_direct(const DevScene& sc, uint16_t* stack, int&
 // microfacet F and Pdf, and for an area light the BSDF-sampled half's
 // BSDF.SampleF panics (integrator.go:134-139 always runs it); every other BSDF
 // is the shared estimate_direct.
-__device__ inline Spec estimate_direct_x(const DevScene& sc, uint16_t* stack, int& panic, const SI& si, const BSDF& b,
-                                         const BSDFX& x, int li, V2 u_light, uint64_t* traced = nullptr) {
-    if (x.kind != BXDF_KIND_MICROFACET && x.kind != BXDF_KIND_OREN_NAYAR)
-        return estimate_direct(sc, stack, panic, si, b, li, u_light, traced);
+// The microfacet / OrenNayar half of estimate_direct_x, out of line: the
+// kernels that inline estimate_direct_x keep the common BSDFs' path small (an
+// out-of-line estimate_direct_x made every light sample of k_paths_ci<kX> a call).
+__device__ __forceinline__ Spec estimate_direct_rough(const DevScene& sc, uint16_t* stack, int& panic, const SI& si,
+                                                   const BSDF& b, const BSDFX& x, int li, V2 u_light,
+                                                   uint64_t* traced) {
     const pbrt_light_desc& L = sc.lights[li];
     const bool is_delta = L.type != PBRT_LIGHT_DIFFUSE_AREA;
     LightSample ls;
@@ -1650,6 +1674,13 @@ __device__ inline Spec estimate_direct_x(const DevScene& sc, uint16_t* stack, in
     }
     if (x.kind == BXDF_KIND_MICROFACET && !is_delta && x.n > 0 && w2l(b, si.wo).z != 0) panic = PBRT_PANIC_NIL_DEREF;
     return Ld;
+}
+__device__ __forceinline__ Spec estimate_direct_x(const DevScene& sc, uint16_t* stack, int& panic, const SI& si,
+                                                  const BSDF& b, const BSDFX& x, int li, V2 u_light,
+                                                  uint64_t* traced = nullptr) {
+    if (x.kind != BXDF_KIND_MICROFACET && x.kind != BXDF_KIND_OREN_NAYAR)
+        return estimate_direct(sc, stack, panic, si, b, li, u_light, traced);
+    return estimate_direct_rough(sc, stack, panic, si, b, x, li, u_light, traced);
 }
 
 // Sphere.PdfWi (sphere.go:350-363): the cone pdf from outside the sphere;

@@ -498,10 +498,13 @@ bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Rend
     // Mirror, smooth Glass and OrenNayar: Path renders run the kX instantiations
     // of the wave pipeline (trajectories and paths over BSDFX, with etaScale):
     // k_chain_ci for LDS-staged trees, then k_paths_ci (P = 4, 8) or the path
-    // wavefront (mesh scenes); DirectLighting's specular recursion, rough glass
-    // (whose every BSDF sample panics) and larger trees stay on the serial kernel
-    if (c->non_matte && (dl || c->rough_glass || c->host_scene.n_nodes > kLdsNodes ||
-                         (!paths_wf_enabled(c) && paths_ci_pixels(c, rp) > 0 && paths_ci_pixels(c, rp) < 4)))
+    // wavefront (mesh scenes); rough glass (whose every BSDF sample panics) and
+    // larger trees stay on the serial kernel
+    // DirectLighting over these materials runs k_dl_samples<kX> (the recursion per
+    // sample; maxDepth <= 64 as the serial kernel), rough glass stays serial
+    if (c->non_matte && (c->rough_glass || (dl && rd->max_depth > 64) ||
+                         (!dl && (c->host_scene.n_nodes > kLdsNodes ||
+                                  (!paths_wf_enabled(c) && paths_ci_pixels(c, rp) > 0 && paths_ci_pixels(c, rp) < 4)))))
         return false;
     if (dl) {   // k_dl_*: the camera ray must be per pixel (pFilm stratified; pLens stratified or unused)
         if (rd->n_dims < 1 || (rd->n_dims < 2 && c->host_scene.camera.lens_radius > 0)) return false;
@@ -1063,7 +1066,7 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 0], c->stream));
                 const int G = c->tiles_per_wave;
                 if (c->use_dl) {
-                    hipLaunchKernelGGL(k_wf_primary<false>, dim3((unsigned)((nb * c->wb.ppt + kWave - 1) / kWave)),
+                    hipLaunchKernelGGL(kx ? k_wf_primary<true> : k_wf_primary<false>, dim3((unsigned)((nb * c->wb.ppt + kWave - 1) / kWave)),
                                        dim3(kWave), 0, c->stream, with_slot(sc, 1), rp, c->wb, sb, nb);
                     unsigned lds = 0;
                     const ChainLayout lw = ci_layout(c->lay_ci, 1, 1, lds);
@@ -1205,7 +1208,7 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                 if (c->use_dl) {
                     const int64_t nrec = nb * c->wb.ppt;
                     if (rp.spp > 1)
-                        hipLaunchKernelGGL(k_dl_samples,
+                        hipLaunchKernelGGL(kx ? k_dl_samples<true> : k_dl_samples<false>,
                                            dim3((unsigned)std::min<int64_t>((nrec * (rp.spp - 1) + kWave - 1) / kWave,
                                                                             (int64_t)c->n_simd * 64)),
                                            dim3(kWave), 0, c->stream, with_slot(sc, 3), rp, c->wb, sb, nrec);

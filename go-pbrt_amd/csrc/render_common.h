@@ -154,7 +154,7 @@ struct PixelRec {
     int32_t hit;      // first hit exists and maxDepth > 1
     int32_t nvalid;   // samples 1 .. nvalid-1 have offsets (spp unless a panic cut the chain)
     int32_t panic0;   // the camera ray's traversal panics (kind), else 0
-    int32_t pad;
+    int32_t dl_levels;   // DirectLighting: levels of the pixel's hit chain (k_wf_primary; see dl_chain_draws)
 };
 struct WaveBufs {
     PixelRec* prec;     // [slot][ppt]
@@ -618,12 +618,17 @@ struct PwCache {
 // k_dl_setup replays the tile's pixels in order (StartPixel, then jump-ahead
 // over the pixel's samples); k_dl_samples runs every (pixel, sample) at once.
 //
-// Draws of one DirectLighting sample (pixel.go:60-80 counters): the camera's
-// Get2D pFilm, Get2D pLens, Get1D time (camera.go via integrator.go:240-255),
-// then on a hit UniformSampleAllLights' two Get2D per light (clones carry no
-// sample arrays, #23) or UniformSampleOneLight's Get1D + 2 Get2D, then the two
-// Get2D of SpecularReflect / SpecularTransmit when maxDepth > 1.
-__device__ __forceinline__ uint32_t dl_draws(const RenderParams& rp, int hit, int n_lights) {
+// PCG32 draws of one DirectLighting sample whose recursion chain hits `levels`
+// surfaces (directlighting.go:62-104 at depth 0, 2, 4, ...: the camera Get2D,
+// Get2D, Get1D; per hit level the light samples -- UniformSampleAllLights' two
+// Get2D per light (clones carry no sample arrays, #23) or UniformSampleOneLight's
+// Get1D + 2 Get2D -- then, while depth + 1 < maxDepth, the Get2D of
+// SpecularReflect and of SpecularTransmit (integrator.go:352-355, 383-385)),
+// stratified dims first (pixel.go:60-80 counters), then 1 / 2 draws each.
+// The chain is the same for every sample of a pixel: the camera ray is per
+// pixel (2D stratified values are (0,0), #3) and SpecularTransmission's
+// direction does not read its sample, so only the light samples differ.
+__device__ __forceinline__ uint32_t dl_chain_draws(const RenderParams& rp, int levels, int n_lights) {
     int c1 = 0, c2 = 0;
     uint32_t d = 0;
     auto g1 = [&]() { if (c1 < rp.ndims) c1++; else d += 1; };
@@ -631,7 +636,7 @@ __device__ __forceinline__ uint32_t dl_draws(const RenderParams& rp, int hit, in
     g2();
     g2();
     g1();
-    if (hit) {
+    for (int i = 0; i < levels; i++) {
         if (n_lights > 0) {
             if (rp.dl_strategy == PBRT_DL_UNIFORM_SAMPLE_ALL) {
                 for (int j = 0; j < n_lights; j++) {
@@ -644,14 +649,16 @@ __device__ __forceinline__ uint32_t dl_draws(const RenderParams& rp, int hit, in
                 g2();
             }
         }
-        if (1 < rp.max_depth) {
+        if (2 * i + 1 < rp.max_depth) {
             g2();
             g2();
         }
     }
     return d;
 }
-
+__device__ __forceinline__ uint32_t dl_draws(const RenderParams& rp, int hit, int n_lights) {
+    return dl_chain_draws(rp, hit ? 1 : 0, n_lights);
+}
 // Cold-frame schedule of k_chain_ci. Workgroups start in launch order, so a
 // heavy tile launched late stretches the frame; a context that has rendered
 // this configuration before orders its tiles by their measured chain times

@@ -29,6 +29,7 @@ __global__ void k_panic_reduce(WaveBufs wb, int64_t slot_base, int64_t nslots_ba
 template <bool kX = false>
 __global__ void k_wf_primary(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nb);
 __global__ void k_dl_setup(DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base, int64_t nb);
+template <bool kX = false>
 __global__ void k_dl_samples(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec);
 __global__ void k_dl_panics(RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr);
 template <bool kX = false>

@@ -88,7 +88,7 @@ def test_cancel_direct_lighting_wave():
     with G.Renderer(sc) as r:
         t8 = full_time(r, abi.render_desc(8, 8, **dl))
     side = 8
-    while side < 128 and t8 * (side / 8) ** 2 < 1.0:
+    while side < 32 and t8 * (side / 8) ** 2 < 1.0:   # the k_dl_* kernels stage <= 8192 stratified values
         side *= 2
     check_cancel_then_render(sc, abi.render_desc(side, side, **dl),
                              abi.render_desc(2, 2, tile_end=48, **dl), abi.PBRT_KERNEL_WAVE_DL,

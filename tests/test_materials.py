@@ -224,7 +224,31 @@ def test_device_materials_direct_lighting_vs_oracle(strategy):
     assert rc == 0
     with G.Renderer(sc) as r:
         film, st = r.render(rd)
+    assert st.kernel == abi.PBRT_KERNEL_WAVE_DL
     assert np.array_equal(bits(film), bits(of))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strategy", [abi.PBRT_DL_UNIFORM_SAMPLE_ALL, abi.PBRT_DL_UNIFORM_SAMPLE_ONE])
+def test_device_direct_lighting_glass_at_8x8_spp_and_tile_ranges(strategy):
+    """server.go:160's DirectLighting(UniformSampleAll, 10) through its glass
+    sphere (server.go:67-94) at Stratified(8,8) on a 160x96 film, on the
+    k_dl_* kernels: the whole film and a tile range bit-identical to the oracle,
+    with the reference ray counts."""
+    sc = readme_glass_scene(160, 96, mirror=False)
+    rd = abi.render_desc(8, 8, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING, dl_strategy=strategy, max_depth=10)
+    rc, of, ost = O.render(sc.desc, rd, threads=8)
+    assert rc == 0
+    with G.Renderer(sc) as r:
+        film, st = r.render(rd)
+        assert st.kernel == abi.PBRT_KERNEL_WAVE_DL and st.paths_traced == ost.paths
+        assert np.array_equal(bits(film), bits(of))
+        assert (st.rays_closest, st.rays_shadow) == (ost.closest_rays, ost.shadow_rays)
+        rd2 = abi.render_desc(8, 8, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING, dl_strategy=strategy,
+                              max_depth=10, tile_begin=7, tile_end=41, tile_stride=3)
+        f2, _ = r.render(rd2)
+    rc, of2, _ = O.render(sc.desc, rd2, threads=8)
+    assert rc == 0 and np.array_equal(bits(f2), bits(of2))
 
 
 @pytest.mark.gpu
@@ -308,7 +332,7 @@ def test_device_oren_nayar_vs_oracle(integrator, mode, sigma):
     assert rc == 0
     with G.Renderer(sc) as r:
         film, st = r.render(rd)
-    expect = path_kernel(4, mode) if integrator == abi.PBRT_INTEGRATOR_PATH else abi.PBRT_KERNEL_SERIAL
+    expect = path_kernel(4, mode) if integrator == abi.PBRT_INTEGRATOR_PATH else abi.PBRT_KERNEL_WAVE_DL
     assert st.kernel == expect
     assert np.array_equal(bits(film), bits(of))
 
@@ -358,12 +382,16 @@ def test_device_direct_lighting_through_glass_vs_oracle(strategy, mode, depth):
     sc = readme_glass_scene(mirror=True)
     rd = abi.render_desc(3, 3, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING, dl_strategy=strategy,
                          max_depth=depth, mode=mode)
-    rc, of, _ = O.render(sc.desc, rd, threads=8)
+    rc, of, ost = O.render(sc.desc, rd, threads=8)
     assert rc == 0
-    with G.Renderer(sc) as r:
-        film, st = r.render(rd)
-    assert st.kernel == abi.PBRT_KERNEL_SERIAL
-    assert np.array_equal(bits(film), bits(of))
+    # round 4: the recursion runs per sample on k_dl_samples<kX> (its chain of
+    # levels, hence the draw count, is the pixel's); the serial kernel too
+    for kernel, want in (("auto", abi.PBRT_KERNEL_WAVE_DL), ("serial", abi.PBRT_KERNEL_SERIAL)):
+        with G.Renderer(sc, kernel=kernel) as r:
+            film, st = r.render(rd)
+        assert st.kernel == want
+        assert np.array_equal(bits(film), bits(of)), kernel
+        assert (st.rays_closest, st.rays_shadow) == (ost.closest_rays, ost.shadow_rays), kernel
 
 
 @pytest.mark.gpu

@@ -11,6 +11,7 @@
 #   benchfull=<cfg>       bench.py --config <cfg> with its CPU baseline and side mode
 #   profile=<cfg>         tools/profile_round.sh for that config
 #   phase=<diag|steptime> tools/phase_stats.py with lib/libpbrt_gpu_<build>.so (config B)
+#   libbench=<v>,<cfg>    bench.py --config <cfg> --steps 2 with lib/libpbrt_gpu_<v>.so (experiment builds)
 #   smoke                 __graft_entry__.smoke()
 set -o pipefail
 TAG=$1
@@ -37,6 +38,9 @@ for step in "$@"; do
   phase=*)   # phase=diag | phase=steptime: tools/phase_stats.py on that diagnostics build (config B)
     lib=${step#phase=}
     PBRT_GPU_LIB=go-pbrt_amd/lib/libpbrt_gpu_$lib.so timeout -k 10 300 python tools/phase_stats.py > $OUT/phase_$lib.txt 2>&1 || { echo "phase $lib failed"; tail -20 $OUT/phase_$lib.txt; exit 1; } ;;
+  libbench=*)   # libbench=<variant>,<cfg>: bench.py --config <cfg> with lib/libpbrt_gpu_<variant>.so
+    spec=${step#libbench=}; v=${spec%%,*}; cfg=${spec#*,}
+    PBRT_GPU_LIB=go-pbrt_amd/lib/libpbrt_gpu_$v.so timeout -k 10 400 python bench.py --config $cfg --no-cpu-baseline --no-side-mode --steps 2 > $OUT/bench_${cfg}_$v.json 2> $OUT/bench_${cfg}_$v.err || { echo "bench $cfg $v failed"; tail -20 $OUT/bench_${cfg}_$v.err; exit 1; } ;;
   smoke)
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $OUT/smoke.log; exit 1; } ;;
   *) echo "unknown step $step"; exit 2 ;;
