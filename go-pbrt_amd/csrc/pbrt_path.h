@@ -402,7 +402,7 @@ struct alignas(16) DevPrim {
     int32_t kind, material, prim_identity, fast;
 };
 
-#ifdef PBRT_XF_FAST
+#if defined(PBRT_XF_FAST)
 // The shape test on the exact TransformRay with its errors (the cold path of
 // prim_hit_t). Out of line: inlined beside the value-only path it made every
 // traversal loop too large to stay in registers (k_chain_ci spilled 320 B/lane).
@@ -647,6 +647,12 @@ __device__ __forceinline__ int leaf_prims(const DevScene& sc, uint32_t first, ui
 // per lane, kStride apart), structured "while-while" for 64-lane waves: loop
 // A walks interior nodes until the lane reaches a leaf whose box it hits,
 // loop B tests that leaf's primitives.
+// Experiment builds may force the walk inline into its callers (-DPBRT_WALK_FORCE_INLINE).
+#ifdef PBRT_WALK_FORCE_INLINE
+#define PBRT_WALK_INLINE __forceinline__
+#else
+#define PBRT_WALK_INLINE inline
+#endif
 // kLB: leaf boxes tested per scan iteration (LDS-staged trees).
 template <bool kAny, int kStride = kStackStride, int kLB = 4>
 __device__ inline bool bvh_walk_analytic(const DevScene& sc, Ray& ray, uint16_t* stack, int& panic, int& best,
@@ -804,7 +810,7 @@ __device__ inline bool bvh_walk_analytic(const DevScene& sc, Ray& ray, uint16_t*
 // with a strictly smaller t, so an analytic primitive keeps a tie. A mesh hit
 // is reported as best = n_prims + its leaf slot.
 template <bool kAny, int kStride = kStackStride, int kLB = 4>
-__device__ inline bool bvh_walk(const DevScene& sc, Ray& ray, uint16_t* stack, int& panic, int& best, V3& best_ph) {
+__device__ PBRT_WALK_INLINE bool bvh_walk(const DevScene& sc, Ray& ray, uint16_t* stack, int& panic, int& best, V3& best_ph) {
     const bool hit = bvh_walk_analytic<kAny, kStride, kLB>(sc, ray, stack, panic, best, best_ph);
     if (sc.mesh.n_nodes == 0 || panic || (kAny && hit)) return hit;
     double tm = ray.tmax;

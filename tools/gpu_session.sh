@@ -35,9 +35,10 @@ for step in "$@"; do
   profile=*)
     cfg=${step#profile=}
     bash tools/profile_round.sh ${TAG}/prof_$cfg --config $cfg || { echo "profile $cfg failed"; exit 1; } ;;
-  phase=*)   # phase=diag | phase=steptime: tools/phase_stats.py on that diagnostics build (config B)
-    lib=${step#phase=}
-    PBRT_GPU_LIB=go-pbrt_amd/lib/libpbrt_gpu_$lib.so timeout -k 10 300 python tools/phase_stats.py > $OUT/phase_$lib.txt 2>&1 || { echo "phase $lib failed"; tail -20 $OUT/phase_$lib.txt; exit 1; } ;;
+  phase=*)   # phase=diag | phase=steptime[,scene]: tools/phase_stats.py on that diagnostics build
+    spec=${step#phase=}; lib=${spec%%,*}; scn=readme
+    [[ "$spec" == *,* ]] && scn=${spec#*,}
+    PBRT_GPU_LIB=go-pbrt_amd/lib/libpbrt_gpu_$lib.so timeout -k 10 300 python tools/phase_stats.py --scene $scn > $OUT/phase_${lib}_$scn.txt 2>&1 || { echo "phase $lib failed"; tail -20 $OUT/phase_${lib}_$scn.txt; exit 1; } ;;
   libbench=*)   # libbench=<variant>,<cfg>: bench.py --config <cfg> with lib/libpbrt_gpu_<variant>.so
     spec=${step#libbench=}; v=${spec%%,*}; cfg=${spec#*,}
     PBRT_GPU_LIB=go-pbrt_amd/lib/libpbrt_gpu_$v.so timeout -k 10 400 python bench.py --config $cfg --no-cpu-baseline --no-side-mode --steps 2 > $OUT/bench_${cfg}_$v.json 2> $OUT/bench_${cfg}_$v.err || { echo "bench $cfg $v failed"; tail -20 $OUT/bench_${cfg}_$v.err; exit 1; } ;;

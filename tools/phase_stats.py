@@ -20,12 +20,14 @@ ap.add_argument("--kernel", default="auto")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--occupancy", type=int, default=0)
 ap.add_argument("--tiles-per-wave", type=int, default=0)
+ap.add_argument("--scene", default="readme", choices=["readme", "readme_glass", "cornell"])
 a = ap.parse_args()
 
-scene = G.Scene.readme(a.width, a.height)
+scene = {"readme": G.Scene.readme, "readme_glass": G.Scene.readme_glass, "cornell": G.Scene.cornell}[a.scene](
+    a.width, a.height)
 names = ["paths", "camera_samples", "closest_rays", "shadow_rays", "any_panic", "windows",
-         "cyc_start_pixel", "cyc_bounce1", "cyc_trajectories", "cyc_chain_walk", "cyc_4",
-         "cyc_5", "cyc_6", "cyc_7"]
+         "cyc_start_pixel", "cyc_issue_first_scatter", "cyc_traversal", "cyc_hit_processing",
+         "cyc_barrier_walk", "cyc_5", "cyc_6", "cyc_7"]
 with G.Renderer(scene, kernel=a.kernel, occupancy=a.occupancy, lanes_per_wave=a.tiles_per_wave) as r:
     rd = abi.render_desc(a.spp, a.spp)
     for i in range(a.reps):
