@@ -18,7 +18,9 @@ namespace pbrtk {
 // are staged in LDS and walk their leaves only (no stack); larger trees walk
 // with the reference's [64] stack (bvh.go:670).
 template <int kW, int kDepth, bool kX>
-__global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT_CI_EU_WAVES, 8))) void k_chain_ci(
+// kDepth < 0 (kCiMeshOnly): scenes of triangle meshes only, no analytic walk
+// compiled in (189 VGPRs instead of 256), built for 3 waves per SIMD.
+__global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kDepth < 0 ? 3 : PBRT_CI_EU_WAVES, 8))) void k_chain_ci(
     DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
     int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr,
     const uint32_t* __restrict__ order, uint32_t* __restrict__ ticks, int cstride) {
@@ -262,12 +264,12 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(PBRT
         V3 ph{0, 0, 0};
         if (dense) bvh_walk_dense(sc, ray, tracing, panic, best, ph, dense_lds + (size_t)wv * kDenseScratch);
         if (tracing) {
-            if (!dense) bvh_walk<false, kT, PBRT_CHAIN_LB>(sc, ray, stack, panic, best, ph);
+            if (!dense) bvh_walk<false, kT, PBRT_CHAIN_LB, (kDepth < 0)>(sc, ray, stack, panic, best, ph);
 #else
         if (tracing) {
             int panic = 0, best;
             V3 ph;
-            bvh_walk<false, kT, PBRT_CHAIN_LB>(sc, ray, stack, panic, best, ph);
+            bvh_walk<false, kT, PBRT_CHAIN_LB, (kDepth < 0)>(sc, ray, stack, panic, best, ph);
 #endif
             mark(2);
             uint32_t d = kNoOff;

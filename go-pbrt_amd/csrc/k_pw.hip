@@ -95,6 +95,9 @@ __global__ __launch_bounds__(kWave) void k_pw_start(DevScene sc, RenderParams rp
 
 // in: trace queue `qin` (count cnt[cin]); out: hits (cnt[2], qs.q[2]) with
 // their material key counted in cnt[3 + key]
+// kMeshOnly: scenes of triangle meshes only (no analytic walk compiled in:
+// 88 instead of 184 VGPRs, 5 waves per SIMD instead of 2)
+template <bool kMeshOnly>
 __global__ __launch_bounds__(kWave) void k_pw_trace(DevScene sc, RenderParams rp, WaveBufs wb, PwPath* __restrict__ paths,
                                                     PwQueues qs, int cin, int n_keys,
                                                     unsigned long long* __restrict__ pkey) {
@@ -110,7 +113,7 @@ __global__ __launch_bounds__(kWave) void k_pw_trace(DevScene sc, RenderParams rp
         Ray ray = p.ray;
         int panic = 0, best;
         V3 ph{0, 0, 0};
-        const bool hit = bvh_walk<false>(sc, ray, stack_lds + threadIdx.x, panic, best, ph);
+        const bool hit = bvh_walk<false, kStackStride, 4, kMeshOnly>(sc, ray, stack_lds + threadIdx.x, panic, best, ph);
         if (!hit || panic) {   // path_step: a miss or a traversal panic ends the path
             if (panic) p.pnc = panic;
             pw_finish(wb, rp.spp, p, pkey);
@@ -248,6 +251,7 @@ __global__ __launch_bounds__(kWave) void k_pw_shade(DevScene sc, RenderParams rp
 }
 
 // in: the shaded paths (cnt[1], q[1]); out: the next trace queue (cnt[0], q[0])
+template <bool kMeshOnly>
 __global__ __launch_bounds__(kWave) void k_pw_shadow(DevScene sc, RenderParams rp, WaveBufs wb,
                                                      PwPath* __restrict__ paths, PwQueues qs,
                                                      unsigned long long* __restrict__ pkey) {
@@ -266,7 +270,7 @@ __global__ __launch_bounds__(kWave) void k_pw_shadow(DevScene sc, RenderParams r
                 int panic = 0;
                 Ray sr = p.sr;
                 p.rays += kRayShadow;
-                const bool occluded = bvh_traverse<true>(sc, sr, nullptr, stack_lds + threadIdx.x, panic);
+                const bool occluded = bvh_traverse<true, 4, kMeshOnly>(sc, sr, nullptr, stack_lds + threadIdx.x, panic);
                 if (panic) {
                     p.pnc = panic;
                     pw_finish(wb, rp.spp, p, pkey);
@@ -316,6 +320,10 @@ __global__ void k_pw_panics(RenderParams rp, WaveBufs wb, int64_t slot_base, int
     }
 }
 
+template __global__ void k_pw_trace<false>(DevScene sc, RenderParams rp, WaveBufs wb, PwPath* __restrict__ paths, PwQueues qs, int cin, int n_keys, unsigned long long* __restrict__ pkey);
+template __global__ void k_pw_trace<true>(DevScene sc, RenderParams rp, WaveBufs wb, PwPath* __restrict__ paths, PwQueues qs, int cin, int n_keys, unsigned long long* __restrict__ pkey);
+template __global__ void k_pw_shadow<false>(DevScene sc, RenderParams rp, WaveBufs wb, PwPath* __restrict__ paths, PwQueues qs, unsigned long long* __restrict__ pkey);
+template __global__ void k_pw_shadow<true>(DevScene sc, RenderParams rp, WaveBufs wb, PwPath* __restrict__ paths, PwQueues qs, unsigned long long* __restrict__ pkey);
 template __global__ void k_pw_cache<false>(DevScene sc, WaveBufs wb, int64_t rec0, int64_t nrec, Spec* __restrict__ ldc, int* __restrict__ ldp);
 template __global__ void k_pw_cache<true>(DevScene sc, WaveBufs wb, int64_t rec0, int64_t nrec, Spec* __restrict__ ldc, int* __restrict__ ldp);
 template __global__ void k_pw_start<false, false>(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t rec0, int64_t nrec, const Spec* __restrict__ ldc, const int* __restrict__ ldp, PwPath* __restrict__ paths, PwQueues qs, unsigned long long* __restrict__ pkey);

@@ -809,9 +809,14 @@ __device__ inline bool bvh_walk_analytic(const DevScene& sc, Ray& ray, uint16_t*
 // the triangle meshes (extension) with the TMax it left; a triangle wins only
 // with a strictly smaller t, so an analytic primitive keeps a tie. A mesh hit
 // is reported as best = n_prims + its leaf slot.
-template <bool kAny, int kStride = kStackStride, int kLB = 4>
+template <bool kAny, int kStride = kStackStride, int kLB = 4, bool kMeshOnly = false>
 __device__ PBRT_WALK_INLINE bool bvh_walk(const DevScene& sc, Ray& ray, uint16_t* stack, int& panic, int& best, V3& best_ph) {
-    const bool hit = bvh_walk_analytic<kAny, kStride, kLB>(sc, ray, stack, panic, best, best_ph);
+    // kMeshOnly: the scene has triangle meshes and no other primitive (host:
+    // n_prims == 0), so the analytic walk -- whose sphere / disk code sets the
+    // register peak of every traversal kernel -- is compiled out
+    bool hit = false;
+    if (kMeshOnly) best = -1;
+    else hit = bvh_walk_analytic<kAny, kStride, kLB>(sc, ray, stack, panic, best, best_ph);
     if (sc.mesh.n_nodes == 0 || panic || (kAny && hit)) return hit;
     double tm = ray.tmax;
     int32_t slot = -1, gid = -1;
@@ -822,11 +827,11 @@ __device__ PBRT_WALK_INLINE bool bvh_walk(const DevScene& sc, Ray& ray, uint16_t
     return true;
 }
 
-template <bool kAny, int kLB = 4>
+template <bool kAny, int kLB = 4, bool kMeshOnly = false>
 __device__ inline bool bvh_traverse(const DevScene& sc, Ray& ray, SI* si, uint16_t* stack, int& panic) {
     int best;
     V3 best_ph{0, 0, 0};
-    const bool hit = bvh_walk<kAny, kStackStride, kLB>(sc, ray, stack, panic, best, best_ph);
+    const bool hit = bvh_walk<kAny, kStackStride, kLB, kMeshOnly>(sc, ray, stack, panic, best, best_ph);
     STEP_T(StepTimer tt; tt.start();)
     if (!kAny && best >= 0) prim_si(sc, best, ray, best_ph, *si);
     STEP_T(if (!kAny) tt.mark(7);)

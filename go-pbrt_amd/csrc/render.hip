@@ -667,6 +667,12 @@ int paths_ci_pixels(const pbrt_gpu_ctx* c, const RenderParams& rp) {
 // profiles/r02/path_wavefront_ab.json). PBRT_PW_SORT=1 adds the material sort
 // between trace and shade: a loss on every scene measured (B 212 -> 245 ms: a
 // few matte materials leave no shading divergence to remove), so off by default.
+// Triangle meshes and no analytic primitive: the kMeshOnly kernels (k_chain_ci
+// kDepth < 0, k_pw_trace / k_pw_shadow<true>) compile the analytic walk out.
+bool mesh_only_scene(const pbrt_gpu_ctx* c) {
+    return c->host_scene.n_prims == 0 && c->mesh.n_nodes > 0 && !c->non_matte;
+}
+
 bool paths_wf_enabled(const pbrt_gpu_ctx* c) {
     if (c->knobs.paths_wf >= 0) return c->knobs.paths_wf == 1;
     return c->mesh.n_nodes > 0;
@@ -727,7 +733,7 @@ int paths_wavefront(pbrt_gpu_ctx* c, const DevScene& sc, int64_t sb, int64_t nb)
             hipLaunchKernelGGL(start, dim3((unsigned)((nr * per + kWave - 1) / kWave)), dim3(kWave), 0, c->stream,
                                sc, rp, c->wb, sb, r0, nr, ldc, ldp, paths, qs, pkey);
             for (int pass = 0; pass + 1 < rp.max_depth; pass++) {
-                hipLaunchKernelGGL(k_pw_trace, dim3(G), dim3(kWave), 0, c->stream, sc, rp, c->wb, paths, qs, 0,
+                hipLaunchKernelGGL(mesh_only_scene(c) ? k_pw_trace<true> : k_pw_trace<false>, dim3(G), dim3(kWave), 0, c->stream, sc, rp, c->wb, paths, qs, 0,
                                    n_keys, pkey);
                 if (sort && n_keys > 1) {
                     hipLaunchKernelGGL(k_pw_scan, dim3(1), dim3(1), 0, c->stream, qs, n_keys);
@@ -736,7 +742,7 @@ int paths_wavefront(pbrt_gpu_ctx* c, const DevScene& sc, int64_t sb, int64_t nb)
                 hipLaunchKernelGGL(kx ? k_pw_shade<true> : k_pw_shade<false>, dim3(G), dim3(kWave), 0, c->stream, sc,
                                    rp, c->wb, sb, paths, qs,
                                    sort && n_keys > 1 ? 1 : 0, pkey);
-                hipLaunchKernelGGL(k_pw_shadow, dim3(G), dim3(kWave), 0, c->stream, sc, rp, c->wb, paths, qs, pkey);
+                hipLaunchKernelGGL(mesh_only_scene(c) ? k_pw_shadow<true> : k_pw_shadow<false>, dim3(G), dim3(kWave), 0, c->stream, sc, rp, c->wb, paths, qs, pkey);
             }
         }
         hipLaunchKernelGGL(k_pw_panics, dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, c->stream, rp, c->wb, sb, r0,
@@ -1054,6 +1060,7 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                              : rp.mode == PBRT_MODE_THROUGHPUT ? PBRT_KERNEL_WAVE : PBRT_KERNEL_WAVE_CI;
             const bool lds_nodes = c->host_scene.n_nodes <= kLdsNodes;
             const bool kx = c->non_matte;   // Mirror / smooth Glass / OrenNayar: the kX instantiations
+            const bool mesh_only = mesh_only_scene(c);   // triangle meshes and nothing else: no analytic walk
             const int64_t per = rp.slot_w * rp.slot_h;
             c->n_batches = (int)((rp.n_slots + c->wave_batch - 1) / c->wave_batch);
             while ((int)c->bev.size() < 3 * c->n_batches) {
@@ -1145,6 +1152,7 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                             }
                             // kX: LDS-staged trees only, at most 4 waves per tile (wave_eligible, ci_waves)
                             auto kern = kx ? (w == 2 ? k_chain_ci<2, 0, true> : k_chain_ci<4, 0, true>)
+                                        : mesh_only ? (w == 2 ? k_chain_ci<2, -1> : w == 4 ? k_chain_ci<4, -1> : k_chain_ci<8, -1>)
                                            : (w == 2   ? (lds_nodes ? k_chain_ci<2> : k_chain_ci<2, 64>)
                                               : w == 4 ? (lds_nodes ? k_chain_ci<4> : k_chain_ci<4, 64>)
                                                        : (lds_nodes ? k_chain_ci<8> : k_chain_ci<8, 64>));
@@ -1156,7 +1164,8 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                             const int ring = kCiRingBytes / (int)sizeof(RingEnt) / Gc;
                             unsigned lds = 0;
                             const ChainLayout lw = ci_layout(c->lay_ci, 1, Gc, lds);
-                            auto kern1 = kx ? k_chain_ci<1, 0, true> : (lds_nodes ? k_chain_ci<1> : k_chain_ci<1, 64>);
+                            auto kern1 = kx ? k_chain_ci<1, 0, true>
+                                            : mesh_only ? k_chain_ci<1, -1> : (lds_nodes ? k_chain_ci<1> : k_chain_ci<1, 64>);
                             hipLaunchKernelGGL(kern1, dim3((unsigned)((n + Gc - 1) / Gc)), dim3(kWave),
                                                lds, st, with_slot(sc, 2), rp, lw, c->d_jump, c->wb, sb,
                                                nb, kWave / Gc, ring, c->d_ctr, Gc == 1 ? ord : nullptr,
@@ -1252,7 +1261,7 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                                        c->d_ctr, sl);
                 }
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 2], c->stream));
-                hipLaunchKernelGGL(k_film, dim3((unsigned)((nb * per + 255) / 256)), dim3(256), 0, c->stream,
+                hipLaunchKernelGGL(k_film, dim3((unsigned)nb), dim3(kFilmThreads), 0, c->stream,
                                    c->d_film, rp, c->wb, sb, nb, c->d_films, c->d_cancel_seen, c->d_ctr);
                 hipLaunchKernelGGL(k_panic_reduce, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, c->stream, c->wb,
                                    sb, nb, c->d_panics, c->d_ctr);

@@ -185,6 +185,7 @@ struct ChainLayout {   // byte offsets into the chain / setup kernels' dynamic L
 #define PBRT_CI_RING_KB 4
 #endif
 constexpr int kCiRingBytes = PBRT_CI_RING_KB * 1024;   // k_chain_ci offset ring (all lane groups of a wave)
+constexpr int kFilmThreads = 384;        // k_film workgroup: the 18 x 18 film of a 16-px tile in one pass
 constexpr int kCiMaxGroups = 4;          // k_chain_ci lane groups (tiles) per wave
 
 __device__ __forceinline__ double pcg_float_of(uint32_t v) {

@@ -15,11 +15,13 @@ template <bool kX = false>
 __global__ void k_pw_cache(DevScene sc, WaveBufs wb, int64_t rec0, int64_t nrec, Spec* __restrict__ ldc, int* __restrict__ ldp);
 template <bool kMB, bool kX = false>
 __global__ void k_pw_start(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t rec0, int64_t nrec, const Spec* __restrict__ ldc, const int* __restrict__ ldp, PwPath* __restrict__ paths, PwQueues qs, unsigned long long* __restrict__ pkey);
+template <bool kMeshOnly = false>
 __global__ void k_pw_trace(DevScene sc, RenderParams rp, WaveBufs wb, PwPath* __restrict__ paths, PwQueues qs, int cin, int n_keys, unsigned long long* __restrict__ pkey);
 __global__ void k_pw_scan(PwQueues qs, int n_keys);
 __global__ void k_pw_scatter(const PwPath* __restrict__ paths, PwQueues qs);
 template <bool kX = false>
 __global__ void k_pw_shade(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, PwPath* __restrict__ paths, PwQueues qs, int sorted, unsigned long long* __restrict__ pkey);
+template <bool kMeshOnly = false>
 __global__ void k_pw_shadow(DevScene sc, RenderParams rp, WaveBufs wb, PwPath* __restrict__ paths, PwQueues qs, unsigned long long* __restrict__ pkey);
 __global__ void k_pw_panics(RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t rec0, int64_t nrec, const unsigned long long* __restrict__ pkey, Counters* __restrict__ ctr);
 template <bool kX = false>

@@ -5,13 +5,15 @@
 #   tools/gpu_session.sh <tag> <step> [<step> ...]
 # steps:
 #   tests                 the whole GPU suite
-#   tests=<expr>          GPU tests selected with pytest -k <expr>
+#   tests=<expr>          GPU tests selected with pytest -k <expr> (commas read as spaces: a,or,b)
 #   bench=<cfg>[,args]    bench.py --config <cfg> (no CPU baseline, no side mode);
 #                         extra bench args after commas, e.g. bench=C,--steps,1
 #   benchfull=<cfg>       bench.py --config <cfg> with its CPU baseline and side mode
 #   profile=<cfg>         tools/profile_round.sh for that config
 #   phase=<diag|steptime> tools/phase_stats.py with lib/libpbrt_gpu_<build>.so (config B)
 #   libbench=<v>,<cfg>    bench.py --config <cfg> --steps 2 with lib/libpbrt_gpu_<v>.so (experiment builds)
+#   envbench=VAR=V[+VAR2=V2],<cfg>[,args]  bench.py --config <cfg> with those environment variables
+#   py=<script>[,args]    python tools/<script>.py <args> (output under <tag>/)
 #   smoke                 __graft_entry__.smoke()
 set -o pipefail
 TAG=$1
@@ -24,7 +26,7 @@ for step in "$@"; do
   tests)
     timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo "tests failed"; tail -30 $OUT/pytest.log; exit 1; } ;;
   tests=*)
-    timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -k "${step#tests=}" > $OUT/pytest_k.log 2>&1 || { echo "tests failed"; tail -30 $OUT/pytest_k.log; exit 1; } ;;
+    timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -k "$(echo "${step#tests=}" | tr ',' ' ')" > $OUT/pytest_k.log 2>&1 || { echo "tests failed"; tail -30 $OUT/pytest_k.log; exit 1; } ;;
   bench=*)
     spec=${step#bench=}; cfg=${spec%%,*}; extra=""
     [[ "$spec" == *,* ]] && extra=$(echo "${spec#*,}" | tr ',' ' ')
@@ -42,6 +44,15 @@ for step in "$@"; do
   libbench=*)   # libbench=<variant>,<cfg>: bench.py --config <cfg> with lib/libpbrt_gpu_<variant>.so
     spec=${step#libbench=}; v=${spec%%,*}; cfg=${spec#*,}
     PBRT_GPU_LIB=go-pbrt_amd/lib/libpbrt_gpu_$v.so timeout -k 10 400 python bench.py --config $cfg --no-cpu-baseline --no-side-mode --steps 2 > $OUT/bench_${cfg}_$v.json 2> $OUT/bench_${cfg}_$v.err || { echo "bench $cfg $v failed"; tail -20 $OUT/bench_${cfg}_$v.err; exit 1; } ;;
+  envbench=*)   # envbench=VAR=VALUE,<cfg>[,args]: bench.py --config <cfg> (no CPU baseline / side mode) with VAR=VALUE
+    spec=${step#envbench=}; kv=${spec%%,*}; rest=${spec#*,}; cfg=${rest%%,*}; extra=""
+    [[ "$rest" == *,* ]] && extra=$(echo "${rest#*,}" | tr ',' ' ')
+    env $(echo "$kv" | tr '+' ' ') timeout -k 10 500 python bench.py --config $cfg --no-cpu-baseline --no-side-mode $extra > $OUT/bench_${cfg}_${kv}.json 2> $OUT/bench_${cfg}_${kv}.err || { echo "bench $cfg $kv failed"; tail -20 $OUT/bench_${cfg}_${kv}.err; exit 1; } ;;
+  py=*)   # py=<tools script>[,args]: python tools/<script>.py args, output to <script>_<args>.txt
+    spec=${step#py=}; scr=${spec%%,*}; args=""
+    [[ "$spec" == *,* ]] && args=$(echo "${spec#*,}" | tr ',' ' ')
+    tagf=$(echo "$scr $args" | tr -c 'A-Za-z0-9=.\n-' '_')
+    timeout -k 10 400 python tools/$scr.py $args > $OUT/$tagf.txt 2>&1 || { echo "py $scr failed"; tail -20 $OUT/$tagf.txt; exit 1; } ;;
   smoke)
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $OUT/smoke.log; exit 1; } ;;
   *) echo "unknown step $step"; exit 2 ;;
