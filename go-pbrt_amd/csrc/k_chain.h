@@ -17,10 +17,18 @@ namespace pbrtk {
 // kDepth: traversal stack entries per lane. Trees of <= kLdsNodes (64) nodes
 // are staged in LDS and walk their leaves only (no stack); larger trees walk
 // with the reference's [64] stack (bvh.go:670).
+// The ring entry's D of a trajectory with cursor c (kX: flagged when it
+// recorded RR decisions; see kRrFlag)
+template <bool kX>
+__device__ __forceinline__ uint32_t ring_d(const Cursor& c, const SpecSampler& ss, uint32_t d) {
+    if (!kX || c.rri < 0 || d == kBadExactD || ss.rrb[c.rri].n == 0) return d;
+    return kRrFlag | (d == kBadSpecD ? kRrTailBad : d);
+}
+
 template <int kW, int kDepth, bool kX>
 // kDepth < 0 (kCiMeshOnly): scenes of triangle meshes only, no analytic walk
 // compiled in (189 VGPRs instead of 256), built for 3 waves per SIMD.
-__global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kDepth < 0 ? 3 : PBRT_CI_EU_WAVES, 8))) void k_chain_ci(
+__global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kDepth < 0 ? PBRT_CI_MESH_EU_WAVES : PBRT_CI_EU_WAVES, 8))) void k_chain_ci(
     DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
     int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr,
     const uint32_t* __restrict__ order, uint32_t* __restrict__ ticks, int cstride) {
@@ -109,6 +117,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kDep
     uint64_t st0 = 0;
     bool tracing = false;
     Cursor c;
+    c.rri = -1;
     c.rng.state = 0;
     c.rng.inc = inc;
     c.draws = 0;
@@ -192,7 +201,8 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kDep
         // ---- (2) idle lanes take the next offsets of their group
         const CiGroup sg = gs[g];
         const int64_t rec = bs * wb.ppt + sg.pi;
-        const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, n, ndims};
+        const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, n, ndims,
+                             kX && wb.rrb ? wb.rrb + bs * kCiMaxRing : nullptr};
         {
             const bool idle = sg.phase == 1 && off == kNoOff;
             const unsigned long long m = __ballot(idle) & gmask;
@@ -240,6 +250,10 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kDep
                 c.cur2d = 2;
                 c.k = exact ? sg.kh : -1;
                 c.kdep = 0;
+                if constexpr (kX) {   // speculative: RR decisions on stratified values are recorded
+                    c.rri = (!exact && ss.rrb) ? (int)(off & (R - 1u)) : -1;
+                    if (c.rri >= 0) ss.rrb[c.rri].n = 0;
+                }
                 beta = spec(1);
                 eta_scale = 1.0;
                 bounces = 1;
@@ -250,7 +264,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kDep
                 if (r != 0) {
                     RingEnt& e = ring[off & (R - 1u)];
                     e.st = st0;
-                    e.d = r == 1 ? c.draws : (c.k >= 0 ? kBadExactD : kBadSpecD);
+                    e.d = ring_d<kX>(c, ss, r == 1 ? c.draws : (c.k >= 0 ? kBadExactD : kBadSpecD));
                     e.tag = off;
                     off = kNoOff;
                 }
@@ -294,7 +308,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kDep
             if (d != kNoOff) {
                 RingEnt& e = ring[off & (R - 1u)];
                 e.st = st0;
-                e.d = d;
+                e.d = ring_d<kX>(c, ss, d);
                 e.tag = off;
                 off = kNoOff;
                 tracing = false;
@@ -314,7 +328,21 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kDep
             for (; s.phase == 1;) {
                 RingEnt& e = ring[s.head & (R - 1u)];
                 if (e.tag != s.head) break;
-                const uint32_t d = e.d;
+                uint32_t d = e.d;
+                if (kX && d < kBadExactD && (d & kRrFlag)) {
+                    // the trajectory survived RR decisions on stratified values of
+                    // the then unknown sample index: with k = kh the first one whose
+                    // value is below its q ends the path there
+                    const RrBranches& b = ss.rrb[s.head & (R - 1u)];
+                    d = (d & kRrTailBad) == kRrTailBad ? kBadSpecD : (d & kRrTailBad);
+                    for (uint32_t i = 0; i < b.n; i++) {
+                        const uint32_t cd = b.cd[i];
+                        if (ss.s1d[(int)(cd & 0xFFu) * n + s.kh] < b.q[i]) {
+                            d = cd >> 8;
+                            break;
+                        }
+                    }
+                }
                 if (d == kBadSpecD) {   // re-run the head with its sample index known
                     e.tag = kNoOff;
                     s.reissue = 1;

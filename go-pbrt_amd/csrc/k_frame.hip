@@ -266,6 +266,7 @@ __global__ __launch_bounds__(kWave) void k_dl_samples(DevScene sc, RenderParams 
         uint32_t closest = 1;
         if (kX && !panic && pr.hit) {
             Cursor c;
+            c.rri = -1;
             c.rng.state = wb.memb[rec * n + k];
             c.rng.inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + bs));
             c.draws = 0;
@@ -346,6 +347,7 @@ __global__ __launch_bounds__(kWave) void k_dl_samples(DevScene sc, RenderParams 
                 for (int q = levels - 1; q >= 0; q--) L = own[q] + smuls(smul(fk[q], L), wk[q]);
         } else if (!panic && pr.hit) {
             Cursor c;
+            c.rri = -1;
             c.rng.state = wb.memb[rec * n + k];
             c.rng.inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + bs));
             c.draws = 0;
@@ -441,6 +443,7 @@ __global__ __launch_bounds__(kWave) void k_tile_cost(DevScene sc, RenderParams r
         if (!pr.hit) continue;
         hits += (it % kProbes) == 0;
         Cursor c;
+        c.rri = -1;
         c.rng.state = mb_state((uint64_t)tile, (uint64_t)pi, 0x70726f6265ULL + (uint64_t)(it % kProbes));
         c.rng.inc = inc;
         c.draws = 0;

@@ -55,6 +55,7 @@ __global__ __launch_bounds__(kWave) void k_pw_start(DevScene sc, RenderParams rp
     }
     const uint64_t tile = (uint64_t)tile_of_slot(rp, slot_base + bs);
     Cursor c;
+    c.rri = -1;
     c.rng.state = kMB ? mb_state(tile, (uint64_t)pi, (uint64_t)k) : wb.memb[rec * n + k];
     c.rng.inc = pcg_inc_of(tile);
     c.draws = 0;
@@ -171,6 +172,7 @@ __global__ __launch_bounds__(kWave) void k_pw_shade(DevScene sc, RenderParams rp
         const V3 wo = p.ray.d;
         const int64_t bs = p.rec / wb.ppt;
         Cursor c;
+        c.rri = -1;
         c.rng.state = p.rng;
         c.rng.inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + bs));
         c.draws = 0;

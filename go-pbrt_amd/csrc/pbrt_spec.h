@@ -49,16 +49,31 @@ __device__ __forceinline__ uint32_t pcg_output(uint64_t old) {   // rng.go:36-42
 
 // Stratified sampler of one path (pixel.go:60-80) positioned at an RNG
 // offset; k < 0 while the sample index is still unknown (speculation).
+// Russian-roulette decisions of a speculative trajectory (k < 0) whose RR value
+// is a stratified 1D value, i.e. depends on the sample index the chain has not
+// reached yet (traj_scatter<kX>, k_chain_ci<kX>): the trajectory continues as
+// if the path survived and records each such decision -- the draws so far, the
+// dimension and the threshold q. At the chain head, with the sample index k
+// known, the draw count is the first recorded draws whose s1d[dim][k] < q
+// (the path ends there), else the trajectory's own.
+constexpr int kRrBranches = 3;
+struct RrBranches {
+    double q[kRrBranches];
+    uint32_t cd[kRrBranches];   // draws << 8 | dimension
+    uint32_t n;
+};
 struct SpecSampler {
     const double* s1d;   // ndims x spp shuffled 1D values of the pixel (LDS)
     int spp, ndims;
+    RrBranches* rrb;     // k_chain_ci<kX>: the group's RR decision records (by ring index), else null
 };
 struct Cursor {
     Pcg rng;
     uint32_t draws;
     int cur1d, cur2d;
     int k;
-    int kdep;   // a stratified value was needed while k < 0
+    int kdep;          // a stratified value was needed while k < 0
+    int rri;           // k < 0 in k_chain_ci<kX>: ss.rrb[rri] takes the RR decisions (else -1)
 };
 __device__ __forceinline__ double c_get1d(Cursor& c, const SpecSampler& s) {
     if (c.cur1d < s.ndims) {
@@ -335,10 +350,23 @@ __device__ inline int traj_scatter(const DevScene& sc, const SI& isect, const BS
     Spec rr = smuls(beta, kX ? eta_scale : 1.0);
     if (max_component(rr) < rr_threshold && bounces > 3) {
         double q = gomath::max(0.05, 1 - max_component(rr));
-        double u1 = c_get1d(c, ss);
-        if (c.kdep) return 2;
-        if (u1 < q) return 1;
-        beta = sdivs(beta, 1 - q);
+        if (kX && c.k < 0 && c.rri >= 0 && c.cur1d < ss.ndims) {
+            // the RR value is s1d[cur1d][k] for a sample index not known yet
+            // (specular bounces draw no light sample, so RR reaches the
+            // stratified dims): record the decision, continue as a survivor
+            RrBranches& rb = ss.rrb[c.rri];
+            if (rb.n == (uint32_t)kRrBranches || c.draws >= (1u << 24)) return 2;
+            rb.q[rb.n] = q;
+            rb.cd[rb.n] = (c.draws << 8) | (uint32_t)c.cur1d;
+            rb.n++;
+            c.cur1d++;
+            beta = sdivs(beta, 1 - q);
+        } else {
+            double u1 = c_get1d(c, ss);
+            if (c.kdep) return 2;
+            if (u1 < q) return 1;
+            beta = sdivs(beta, 1 - q);
+        }
     }
     bounces++;
     return bounces >= max_depth ? 1 : 0;

@@ -761,8 +761,11 @@ int wave_buffers(pbrt_gpu_ctx* c) {
     const RenderParams& rp = c->rp;
     const int64_t ppt = rp.tile_size * rp.tile_size, n = rp.spp, nd = rp.ndims > 0 ? rp.ndims : 1;
     auto al = [](int64_t b) { return (b + 255) & ~int64_t(255); };
+    // k_chain_ci<kX>'s RR decision records, one per ring entry (Path renders of non-Matte scenes)
+    const int64_t rrb_bytes = c->non_matte ? (int64_t)kCiMaxRing * (int64_t)sizeof(RrBranches) : 0;
     const int64_t per_tile = al(ppt * (int64_t)sizeof(PixelRec)) + al(ppt * nd * n * 8) + al(ppt * n * 8) +
-                             al(ppt * n * 24) + al(ppt * n * 4) + al(ppt * (int64_t)sizeof(PanicRec)) + al(4);
+                             al(ppt * n * 24) + al(ppt * n * 4) + al(ppt * (int64_t)sizeof(PanicRec)) + al(4) +
+                             al(rrb_bytes);
     double gb = 96.0;
     {
         size_t free_b = 0, total_b = 0;
@@ -795,6 +798,7 @@ int wave_buffers(pbrt_gpu_ctx* c) {
     wb.rays = (uint32_t*)take(ppt * n * 4);
     wb.ppanic = (PanicRec*)take(ppt * (int64_t)sizeof(PanicRec));
     wb.tile_npx = (int32_t*)take(4);
+    wb.rrb = rrb_bytes ? (RrBranches*)take(rrb_bytes) : nullptr;
     wb.ppt = ppt;
     wb.s1d_stride = nd * n;
     c->wave_batch = batch;

@@ -164,6 +164,8 @@ struct WaveBufs {
     uint32_t* rays;     // [slot][ppt][spp]      the sample's reference ray counts (kRayClosest / kRayShadow)
     PanicRec* ppanic;   // [slot][ppt]        first panic of the pixel in sample order
     int32_t* tile_npx;  // [slot]             pixels with records (a panic ends the tile)
+    RrBranches* rrb;    // [slot][kCiMaxRing] k_chain_ci<kX>: RR decisions of the speculative trajectory
+                        //                    at each ring entry (null for Matte-only scenes)
     int64_t ppt;        // pixel records per tile slot (tile_size^2)
     int64_t s1d_stride; // ndims * spp
 };
@@ -187,6 +189,11 @@ struct ChainLayout {   // byte offsets into the chain / setup kernels' dynamic L
 constexpr int kCiRingBytes = PBRT_CI_RING_KB * 1024;   // k_chain_ci offset ring (all lane groups of a wave)
 constexpr int kFilmThreads = 384;        // k_film workgroup: the 18 x 18 film of a 16-px tile in one pass
 constexpr int kCiMaxGroups = 4;          // k_chain_ci lane groups (tiles) per wave
+constexpr int kCiMaxRing = 4 * kCiRingBytes / 16;   // ring entries of a tile at the most waves of a kX tile (4)
+// k_chain_ci ring entry D with recorded RR decisions (RrBranches at the entry):
+// the low 30 bits are the survivor's D, or kRrTailBad when the survivor's own
+// trajectory could not resolve D (then it is kBadSpecD unless a decision ends it)
+constexpr uint32_t kRrFlag = 0x40000000u, kRrTailBad = 0x3FFFFFFFu;
 
 __device__ __forceinline__ double pcg_float_of(uint32_t v) {
     return gomath::min(gomath::kOneMinusEpsilon, (double)v * 2.3283064365386963e-10);
@@ -415,6 +422,7 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
     ps.aux = aux;
     ps.rays = rslot;
     Cursor c;
+    c.rri = -1;
     int pnc = 0, bnc = 1;
     for (;;) {
         const bool idle = w < 0;
@@ -694,6 +702,9 @@ constexpr double kCostPixel = 150.0;   // one StartPixel ~ this many trajectory 
 // the sample index) is re-run there with the sample index known; an exact
 // panic ends the tile at that sample. Bit-identical to the
 // serial replay: only the schedule changes.
+#ifndef PBRT_CI_MESH_EU_WAVES
+#define PBRT_CI_MESH_EU_WAVES 3   // k_chain_ci's mesh-only instantiations (kDepth < 0): waves/SIMD (build option)
+#endif
 #ifndef PBRT_CI_EU_WAVES
 #define PBRT_CI_EU_WAVES 2   // k_chain_ci waves/SIMD (build option)
 #endif

@@ -13,7 +13,7 @@
 #   phase=<diag|steptime> tools/phase_stats.py with lib/libpbrt_gpu_<build>.so (config B)
 #   libbench=<v>,<cfg>    bench.py --config <cfg> --steps 2 with lib/libpbrt_gpu_<v>.so (experiment builds)
 #   envbench=VAR=V[+VAR2=V2],<cfg>[,args]  bench.py --config <cfg> with those environment variables
-#   py=<script>[,args]    python tools/<script>.py <args> (output under <tag>/)
+#   py=<script>[~args]    python tools/<script>.py <args> ('~' between args; output under <tag>/)
 #   smoke                 __graft_entry__.smoke()
 set -o pipefail
 TAG=$1
@@ -48,9 +48,9 @@ for step in "$@"; do
     spec=${step#envbench=}; kv=${spec%%,*}; rest=${spec#*,}; cfg=${rest%%,*}; extra=""
     [[ "$rest" == *,* ]] && extra=$(echo "${rest#*,}" | tr ',' ' ')
     env $(echo "$kv" | tr '+' ' ') timeout -k 10 500 python bench.py --config $cfg --no-cpu-baseline --no-side-mode $extra > $OUT/bench_${cfg}_${kv}.json 2> $OUT/bench_${cfg}_${kv}.err || { echo "bench $cfg $kv failed"; tail -20 $OUT/bench_${cfg}_${kv}.err; exit 1; } ;;
-  py=*)   # py=<tools script>[,args]: python tools/<script>.py args, output to <script>_<args>.txt
-    spec=${step#py=}; scr=${spec%%,*}; args=""
-    [[ "$spec" == *,* ]] && args=$(echo "${spec#*,}" | tr ',' ' ')
+  py=*)   # py=<tools script>[~args]: python tools/<script>.py args ('~' separates; commas stay), output to <script>_<args>.txt
+    spec=${step#py=}; scr=${spec%%~*}; args=""
+    [[ "$spec" == *~* ]] && args=$(echo "${spec#*~}" | tr '~' ' ')
     tagf=$(echo "$scr $args" | tr -c 'A-Za-z0-9=.\n-' '_')
     timeout -k 10 400 python tools/$scr.py $args > $OUT/$tagf.txt 2>&1 || { echo "py $scr failed"; tail -20 $OUT/$tagf.txt; exit 1; } ;;
   smoke)

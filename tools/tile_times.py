@@ -21,21 +21,26 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="B", choices=["B", "G", "C"])
     ap.add_argument("--top", type=int, default=20)
+    ap.add_argument("--env", action="append", default=[], help="KEY=VALUE knob (read when the context is created)")
+    ap.add_argument("--frames", type=int, default=2, help="frames rendered; the last one is reported")
     a = ap.parse_args()
+    for kv in a.env:
+        k, v = kv.split("=", 1)
+        os.environ[k] = v
     import pbrtgpu as G
     W, H = 1920, 1080
     scene = {"B": G.Scene.readme, "G": G.Scene.readme_glass, "C": G.Scene.cornell}[a.config](W, H)
     spp, depth = (16, 8) if a.config == "C" else (8, 10)
     rd = G.render_desc(spp_x=spp, spp_y=spp, max_depth=depth)
     with G.Renderer(scene) as r:
-        r.render(rd)
-        _, st = r.render(rd)   # the measured order of the first frame
+        for _ in range(a.frames):   # from the second frame on: the measured order of the previous one
+            _, st = r.render(rd)
         ticks, heavy = r.tile_ticks()
     t = np.asarray(ticks, dtype=np.float64) / 1e5   # 100 MHz ticks -> ms
     ntx = (W + 15) // 16
     order = np.argsort(-t)[:a.top]
     print(json.dumps({
-        "config": a.config, "chain_ms": st.chain_ms, "tiles": int(t.size),
+        "config": a.config, "env": a.env, "chain_ms": st.chain_ms, "tiles": int(t.size), "heavy_slots": heavy,
         "tile_ms": {"mean": float(t.mean()), "p50": float(np.median(t)), "p99": float(np.percentile(t, 99)),
                     "max": float(t.max())},
         "sum_over_2048_slots_ms": float(t.sum() / 2048.0),
