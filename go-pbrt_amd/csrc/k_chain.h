@@ -114,7 +114,20 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kDep
     uint64_t last_host_poll = t_begin;   // when this workgroup last read the host flag
     // lane trajectory state
     uint32_t off = kNoOff;
-    uint64_t st0 = 0;
+    // kX: the trajectory's throughput, etaScale and start state live in LDS
+    // (the BSDFX bounce needs their registers; 0 B of scratch)
+    __shared__ Spec xs_beta[kX ? kT : 1];
+    __shared__ double xs_eta[kX ? kT : 1];
+    __shared__ uint64_t xs_st0[kX ? kT : 1];
+    uint64_t st0_r = 0;
+    Spec beta_r = spec(1);
+    double eta_r = 1.0;
+    uint64_t& st0 = [&]() -> uint64_t& { if constexpr (kX) return xs_st0[tid]; else return st0_r; }();
+    Spec& beta = [&]() -> Spec& { if constexpr (kX) return xs_beta[tid]; else return beta_r; }();
+    double& eta_scale = [&]() -> double& { if constexpr (kX) return xs_eta[tid]; else return eta_r; }();
+    st0 = 0;
+    beta = spec(1);
+    eta_scale = 1.0;
     bool tracing = false;
     Cursor c;
     c.rri = -1;
@@ -124,8 +137,6 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kDep
     c.cur1d = c.cur2d = 0;
     c.k = -1;
     c.kdep = 0;
-    Spec beta = spec(1);
-    double eta_scale = 1.0;
     int bounces = 1;
     Ray ray;
     ray.o = ray.d = V3{0, 0, 0};

@@ -14,6 +14,7 @@
 #   libbench=<v>,<cfg>    bench.py --config <cfg> --steps 2 with lib/libpbrt_gpu_<v>.so (experiment builds)
 #   envbench=VAR=V[+VAR2=V2],<cfg>[,args]  bench.py --config <cfg> with those environment variables
 #   py=<script>[~args]    python tools/<script>.py <args> ('~' between args; output under <tag>/)
+#   libpy=<v>,<script>[~args]  py= with lib/libpbrt_gpu_<v>.so (diag / experiment builds)
 #   smoke                 __graft_entry__.smoke()
 set -o pipefail
 TAG=$1
@@ -53,6 +54,11 @@ for step in "$@"; do
     [[ "$spec" == *~* ]] && args=$(echo "${spec#*~}" | tr '~' ' ')
     tagf=$(echo "$scr $args" | tr -c 'A-Za-z0-9=.\n-' '_')
     timeout -k 10 400 python tools/$scr.py $args > $OUT/$tagf.txt 2>&1 || { echo "py $scr failed"; tail -20 $OUT/$tagf.txt; exit 1; } ;;
+  libpy=*)   # libpy=<variant>,<script>[~args]: as py= with lib/libpbrt_gpu_<variant>.so
+    spec=${step#libpy=}; v=${spec%%,*}; spec=${spec#*,}; scr=${spec%%~*}; args=""
+    [[ "$spec" == *~* ]] && args=$(echo "${spec#*~}" | tr '~' ' ')
+    tagf=$(echo "$v $scr $args" | tr -c 'A-Za-z0-9=.\n-' '_')
+    PBRT_GPU_LIB=go-pbrt_amd/lib/libpbrt_gpu_$v.so timeout -k 10 400 python tools/$scr.py $args > $OUT/$tagf.txt 2>&1 || { echo "libpy $scr failed"; tail -20 $OUT/$tagf.txt; exit 1; } ;;
   smoke)
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $OUT/smoke.log; exit 1; } ;;
   *) echo "unknown step $step"; exit 2 ;;

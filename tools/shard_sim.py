@@ -23,7 +23,11 @@ def main():
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--rows", action="store_true", help="time each tile row alone instead (the row's slowest tile)")
+    ap.add_argument("--env", action="append", default=[], help="KEY=VALUE knob (read when the context is created)")
     a = ap.parse_args()
+    for kv in a.env:
+        k, v = kv.split("=", 1)
+        os.environ[k] = v
     import torch
     import pbrtgpu as G
     W, H = 1920, 1080
@@ -57,7 +61,7 @@ def main():
                 best = dt if best is None else min(best, dt)
             print(json.dumps({"n": n, "rank": rank, "wall_ms": best * 1e3, "kernel_ms": st.kernel_ms,
                               "chain_ms": st.chain_ms, "paths_ms": st.paths_ms, "paths": int(st.paths_traced),
-                              "kernel": int(st.kernel)}), flush=True)
+                              "kernel": int(st.kernel), "env": a.env}), flush=True)
 
 
 if __name__ == "__main__":
