@@ -116,15 +116,20 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kDep
     uint32_t off = kNoOff;
     // kX: the trajectory's throughput, etaScale and start state live in LDS
     // (the BSDFX bounce needs their registers; 0 B of scratch)
-    __shared__ Spec xs_beta[kX ? kT : 1];
-    __shared__ double xs_eta[kX ? kT : 1];
-    __shared__ uint64_t xs_st0[kX ? kT : 1];
+#ifdef PBRT_CI_LDS_STATE   // experiment: the Matte chain too
+    constexpr bool kLdsState = true;
+#else
+    constexpr bool kLdsState = kX;
+#endif
+    __shared__ Spec xs_beta[kLdsState ? kT : 1];
+    __shared__ double xs_eta[kLdsState ? kT : 1];
+    __shared__ uint64_t xs_st0[kLdsState ? kT : 1];
     uint64_t st0_r = 0;
     Spec beta_r = spec(1);
     double eta_r = 1.0;
-    uint64_t& st0 = [&]() -> uint64_t& { if constexpr (kX) return xs_st0[tid]; else return st0_r; }();
-    Spec& beta = [&]() -> Spec& { if constexpr (kX) return xs_beta[tid]; else return beta_r; }();
-    double& eta_scale = [&]() -> double& { if constexpr (kX) return xs_eta[tid]; else return eta_r; }();
+    uint64_t& st0 = [&]() -> uint64_t& { if constexpr (kLdsState) return xs_st0[tid]; else return st0_r; }();
+    Spec& beta = [&]() -> Spec& { if constexpr (kLdsState) return xs_beta[tid]; else return beta_r; }();
+    double& eta_scale = [&]() -> double& { if constexpr (kLdsState) return xs_eta[tid]; else return eta_r; }();
     st0 = 0;
     beta = spec(1);
     eta_scale = 1.0;

@@ -61,6 +61,7 @@ struct Knobs {
     double pw_gb = 24.0;       // PBRT_PW_GB
     double wave_buffer_gb = 0; // PBRT_WAVE_BUFFER_GB (0: min(96 GB, half the free HBM))
     bool ci_async = false;     // PBRT_CI_ASYNC=1: multi-wave Matte tiles on k_chain_async (asynchronous waves)
+    bool ci_heavy8 = false;    // PBRT_CI_HEAVY8=1: 4-wave shards run their heaviest tiles at 8 waves
     int ci_mc = 0;             // PBRT_CI_MC = 2, 4, 8: the heavy tiles on k_chain_mc with that many CUs each
     int ci_mc_waves = 8;       // PBRT_CI_MC_WAVES = 4, 8: waves per k_chain_mc workgroup
     int64_t ci_exclusive = 0;  // PBRT_CI_EXCLUSIVE = K: a shard's K heaviest tiles get a CU each (LDS pad)
@@ -85,6 +86,7 @@ struct Knobs {
         if (const char* e = getenv("PBRT_CI_SPLIT")) k.ci_split = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_DENSE")) k.ci_dense = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_ASYNC")) k.ci_async = atoi(e) != 0;
+        if (const char* e = getenv("PBRT_CI_HEAVY8")) k.ci_heavy8 = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_MC")) {
             const int v = atoi(e);
             if (v == 1 || v == 2 || v == 4 || v == 8) k.ci_mc = v;
@@ -1213,8 +1215,10 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                         heavy = std::min<int64_t>(ci_heavy_override(c), nb);
                     if (heavy >= nb) heavy = 0;   // nothing left for the light launch: one launch at kw
                     // 4-wave shards: the heaviest tiles at 8 waves, the rest at 4 beside them
-                    int64_t heavy8 = (learned && kw == 4 && !kx && G == 1 && heavy == 0 && excl == 0 &&
-                                      ci_split_enabled(c) && ci_heavy_override(c) < 0)
+                    // (PBRT_CI_HEAVY8=1; measured a loss on 1/8 shards of B: 127-128 vs 117-126 ms,
+                    // the 8-wave workgroups wait for whole CUs the 4-wave launch keeps refilling)
+                    int64_t heavy8 = (learned && c->knobs.ci_heavy8 && kw == 4 && !kx && G == 1 && heavy == 0 &&
+                                      excl == 0 && ci_split_enabled(c) && ci_heavy_override(c) < 0)
                                          ? std::min<int64_t>(c->heavy8_k, nb - 1) : 0;
                     c->last_heavy = heavy + heavy8;
                     if (ticks) {   // label every slot with the waves it actually runs at
@@ -1448,9 +1452,8 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
         while (k < (int64_t)t.size() && cost[c->h_slot_order[(size_t)k]] > thr) k++;
         c->heavy_k = std::min<int64_t>(k, c->n_simd / 4);   // at most a quarter of the wave slots
         if (ci_heavy_override(c) >= 0) c->heavy_k = ci_heavy_override(c);
-        // shards that fit the wave slots at 4 waves per tile (1/8 frame): the
-        // tiles within 0.8x of the heaviest get 8 waves (a CU each); the frame's
-        // chain is the heaviest tile's (tile 5389 of B: 118 -> 92 ms at 8 waves)
+        // PBRT_CI_HEAVY8: on shards that fit the wave slots at 4 waves per tile
+        // (1/8 frame), the tiles within 0.8x of the heaviest at 8 waves (a CU each)
         k = 0;
         const double top = t.empty() ? 0.0 : cost[c->h_slot_order[0]];
         while (k < (int64_t)t.size() && k < 16 && cost[c->h_slot_order[(size_t)k]] > 0.8 * top) k++;
