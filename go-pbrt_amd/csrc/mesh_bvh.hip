@@ -459,7 +459,8 @@ int mesh_bvh_build(const pbrt_scene_desc* s, hipStream_t st, MeshBuild& out, std
         MB_CHK(hipGetLastError());
         MB_CHK(hipMemcpyAsync(&n_out, sz, sizeof(int32_t), hipMemcpyDeviceToHost, st));   // root = node 0
         MB_CHK(hipStreamSynchronize(st));
-        MB_CHK(dmalloc(&out.nodes, (size_t)kMeshOrders * n_out));
+        MB_CHK(dmalloc(&out.nodes, (size_t)kMeshOrders * n_out + kMeshPad));
+        MB_CHK(hipMemsetAsync(out.nodes + (size_t)kMeshOrders * n_out, 0, sizeof(MeshNode) * kMeshPad, st));
         hipLaunchKernelGGL(k_flatten, dim3((unsigned)((2 * n - 1 + kB - 1) / kB)), dim3(kB), 0, st, n, cl, cr, par,
                            rfirst, box, tc, sz, n_out, out.nodes, depth);
         MB_CHK(hipEventRecord(e1, st));

@@ -40,8 +40,12 @@ struct alignas(16) MeshNode {
 };
 static_assert(sizeof(MeshNode) == 32, "MeshNode is two 16-byte loads");
 constexpr uint32_t kMeshInterior = 0xFFFFFFFFu;
-constexpr int kMeshLeafMax = 4;   // triangles per leaf (subtrees this small are collapsed)
+#ifndef PBRT_MESH_LEAF_MAX
+#define PBRT_MESH_LEAF_MAX 1   // build option (1..7); 1 measured best on D (chain 667 / 699 / 746 / 802 / 898 ms at 1 / 2 / 3 / 4 / 6)
+#endif
+constexpr int kMeshLeafMax = PBRT_MESH_LEAF_MAX;   // triangles per leaf (subtrees this small are collapsed)
 constexpr int kMeshOrders = 8;    // threaded orderings, one per ray-direction octant
+constexpr int kMeshPad = 2;       // nodes allocated past the last ordering (mesh_walk's look-ahead loads)
 
 struct DevMesh {
     const MeshNode* nodes;       // [kMeshOrders][n_nodes]
@@ -116,7 +120,12 @@ GO_HD bool tri_hit(const double* v, const Ray& r, double& t_out, double& b0o, do
 }
 
 // Ordering of the threaded node arrays for a ray: its direction octant
-GO_HD int mesh_ordering(V3 d) { return (d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0); }
+#ifndef PBRT_MESH_ORDER_MASK
+#define PBRT_MESH_ORDER_MASK 7   // experiment builds: octant bits that select an ordering (7: all three)
+#endif
+GO_HD int mesh_ordering(V3 d) {
+    return ((d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0)) & PBRT_MESH_ORDER_MASK;
+}
 
 #ifdef __HIPCC__
 __device__ __forceinline__ void load_tri(const float* __restrict__ tris, uint32_t slot, double v[9]) {
@@ -184,19 +193,47 @@ __device__ inline bool mesh_walk(const DevMesh& m, const Ray& ray, double& tmax,
 #else
 #define MESH_COUNT(x)
 #endif
+#ifdef PBRT_MESH_PREFETCH
+    // (experiment build, a loss on D: chain 897 vs 798 ms, paths 272 vs 229)
+    // node i in (a, b) and node i + 1 in (a2, b2): a hit interior node's first
+    // child is the next node of the threaded order, so the walk down a hit
+    // path moves to a node already loaded and fetches the one after it while
+    // testing this one (the arrays carry kMeshPad nodes past their end)
+    auto load_node = [&](uint32_t j, uint4& x, uint4& y) {
+        const uint4* q = reinterpret_cast<const uint4*>(N + j);
+        x = q[0];
+        y = q[1];
+    };
+    uint4 a, b, a2, b2;
+    load_node(0, a, b);
+    load_node(1, a2, b2);
+#endif
     while (i < n) {
         MESH_COUNT(c_nodes++;)
+#ifndef PBRT_MESH_PREFETCH
         const uint4* q = reinterpret_cast<const uint4*>(N + i);
         const uint4 a = q[0], b = q[1];
+#endif
         const float bmin[3] = {__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z)};
         const float bmax[3] = {__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z)};
         const uint32_t escape = a.w, leaf = b.w;
         if (!mesh_box_hit(bmin, bmax, ray, inv, zero_mask, tmax)) {
             i = escape;
+#ifdef PBRT_MESH_PREFETCH
+            if (i < n) {
+                load_node(i, a, b);
+                load_node(i + 1, a2, b2);
+            }
+#endif
             continue;
         }
         if (leaf == kMeshInterior) {
             i++;
+#ifdef PBRT_MESH_PREFETCH
+            a = a2;
+            b = b2;
+            load_node(i + 1, a2, b2);
+#endif
             continue;
         }
         const uint32_t first = leaf >> 3, cnt = leaf & 7u;
@@ -217,6 +254,12 @@ __device__ inline bool mesh_walk(const DevMesh& m, const Ray& ray, double& tmax,
             }
         }
         i = escape;
+#ifdef PBRT_MESH_PREFETCH
+        if (i < n) {
+            load_node(i, a, b);
+            load_node(i + 1, a2, b2);
+        }
+#endif
     }
     return found;
 }
