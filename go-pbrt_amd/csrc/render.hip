@@ -1346,7 +1346,7 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                                        c->d_ctr, sl);
                 }
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 2], c->stream));
-                hipLaunchKernelGGL(k_film, dim3((unsigned)nb), dim3(kFilmThreads), 0, c->stream,
+                hipLaunchKernelGGL(k_film, dim3((unsigned)((nb * per + kFilmThreads - 1) / kFilmThreads)), dim3(kFilmThreads), 0, c->stream,
                                    c->d_film, rp, c->wb, sb, nb, c->d_films, c->d_cancel_seen, c->d_ctr);
                 hipLaunchKernelGGL(k_panic_reduce, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, c->stream, c->wb,
                                    sb, nb, c->d_panics, c->d_ctr);

@@ -187,7 +187,7 @@ struct ChainLayout {   // byte offsets into the chain / setup kernels' dynamic L
 #define PBRT_CI_RING_KB 4
 #endif
 constexpr int kCiRingBytes = PBRT_CI_RING_KB * 1024;   // k_chain_ci offset ring (all lane groups of a wave)
-constexpr int kFilmThreads = 384;        // k_film workgroup: the 18 x 18 film of a 16-px tile in one pass
+constexpr int kFilmThreads = 256;        // k_film workgroup (one thread per tile-film pixel)
 constexpr int kCiMaxGroups = 4;          // k_chain_ci lane groups (tiles) per wave
 constexpr int kCiMaxRing = 4 * kCiRingBytes / 16;   // ring entries of a tile at the most waves of a kX tile (4)
 // k_chain_ci ring entry D with recorded RR decisions (RrBranches at the entry):
