@@ -459,3 +459,26 @@ def test_oracle_mesh_material_changes_the_image():
         assert rc == 0
     assert not np.array_equal(films["glass"], films["mirror"])
     assert not np.array_equal(films["glass"], films["oren"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ci_waves", ["1", "2", "4"])
+@pytest.mark.parametrize("nd,depth,rr", [(4, 10, 1.0), (6, 24, 1.0), (10, 32, 0.7), (3, 16, 1.0)])
+def test_device_glass_rr_on_stratified_dims_vs_oracle(monkeypatch, ci_waves, nd, depth, rr):
+    """Russian roulette after >= 3 glass bounces reads stratified 1D values (a
+    glass bounce samples no light): speculative trajectories record up to three
+    such decisions and the chain head resolves them with its sample index; a
+    fourth falls back to a re-run at the head. Deep paths through the glass
+    sphere and 3 to 10 sampled dims cover the recorded, exhausted and mixed
+    cases, at every ring size (waves per tile)."""
+    monkeypatch.setenv("PBRT_CI_WAVES", ci_waves)
+    sc = readme_glass_scene(64, 48)
+    rd = abi.render_desc(4, 4, n_dims=nd, max_depth=depth, rr_threshold=rr)
+    rc, of, ost = O.render(sc.desc, rd, threads=8)
+    assert rc == 0
+    with G.Renderer(sc) as r:
+        film, st = r.render(rd)
+        film2, _ = r.render(rd)   # the measured tile order
+    assert st.kernel == abi.PBRT_KERNEL_WAVE_CI and st.paths_traced == ost.paths
+    assert np.array_equal(bits(film), bits(of)) and np.array_equal(bits(film2), bits(of))
+    assert (st.rays_closest, st.rays_shadow) == (ost.closest_rays, ost.shadow_rays)

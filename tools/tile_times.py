@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--top", type=int, default=20)
     ap.add_argument("--env", action="append", default=[], help="KEY=VALUE knob (read when the context is created)")
     ap.add_argument("--frames", type=int, default=2, help="frames rendered; the last one is reported")
+    ap.add_argument("--dump", action="store_true", help="add every tile's ms (slot order) to the JSON line")
     a = ap.parse_args()
     for kv in a.env:
         k, v = kv.split("=", 1)
@@ -45,6 +46,7 @@ def main():
                     "max": float(t.max())},
         "sum_over_2048_slots_ms": float(t.sum() / 2048.0),
         "heaviest": [{"tile": int(i), "tx": int(i % ntx), "ty": int(i // ntx), "ms": float(t[i])} for i in order],
+        **({"all_ms": [round(float(x), 3) for x in t]} if a.dump else {}),
     }))
 
 
