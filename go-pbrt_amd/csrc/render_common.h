@@ -706,7 +706,10 @@ constexpr double kCostPixel = 150.0;   // one StartPixel ~ this many trajectory 
 #define PBRT_CI_MESH_EU_WAVES 3   // k_chain_ci's mesh-only instantiations (kDepth < 0): waves/SIMD (build option)
 #endif
 #ifndef PBRT_CI_EU_WAVES
-#define PBRT_CI_EU_WAVES 2   // k_chain_ci waves/SIMD (build option)
+#define PBRT_CI_EU_WAVES 3   // k_chain_ci waves/SIMD, Matte analytic scenes (build option)
+#endif
+#ifndef PBRT_CI_X_EU_WAVES
+#define PBRT_CI_X_EU_WAVES 2   // k_chain_ci waves/SIMD, Mirror / Glass / OrenNayar scenes (build option)
 #endif
 #ifndef PBRT_CHAIN_LB
 #define PBRT_CHAIN_LB 1   // leaf boxes per scan iteration in k_chain_ci's traversal (build option)
