@@ -25,12 +25,14 @@ __device__ __forceinline__ uint32_t ring_d(const Cursor& c, const SpecSampler& s
     return kRrFlag | (d == kBadSpecD ? kRrTailBad : d);
 }
 
-template <int kW, int kDepth, bool kX>
+template <int kW, int kDepth, bool kX, int kEu>
 // kDepth < 0 (kCiMeshOnly): scenes of triangle meshes only, no analytic walk
 // compiled in (149 VGPRs), built for 3 waves per SIMD; Matte analytic scenes
 // at PBRT_CI_EU_WAVES (3: 168 VGPRs, a few spills, faster than 2), kX at
-// PBRT_CI_X_EU_WAVES (2).
-__global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kDepth < 0 ? PBRT_CI_MESH_EU_WAVES : kX ? PBRT_CI_X_EU_WAVES : PBRT_CI_EU_WAVES, 8))) void k_chain_ci(
+// PBRT_CI_X_EU_WAVES (2). kEu > 0 sets the waves/SIMD the registers are
+// budgeted for (the host picks <1, *, false, 2> where the workgroup's LDS
+// allows fewer than 3 waves/SIMD anyway: then the 3-wave build only spills).
+__global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu > 0 ? kEu : kDepth < 0 ? PBRT_CI_MESH_EU_WAVES : kX ? PBRT_CI_X_EU_WAVES : PBRT_CI_EU_WAVES, 8))) void k_chain_ci(
     DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
     int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr,
     const uint32_t* __restrict__ order, uint32_t* __restrict__ ticks, int cstride) {

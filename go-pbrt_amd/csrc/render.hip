@@ -148,6 +148,7 @@ struct pbrt_gpu_ctx {
     int n_batches = 0;
     int n_simd = 1024;                 // SIMDs of the device (4 per CU)
     size_t lds_per_block = 65536;      // the device's LDS limit per workgroup (sharedMemPerBlock)
+    size_t lds_per_cu = 160 * 1024;    // LDS of a CU (maxSharedMemoryPerMultiProcessor)
     WaveBufs wb{};
     bool use_ci = false;   // the Path chain stage (k_chain_ci)
     bool use_dl = false;   // DirectLighting on k_dl_setup / k_dl_samples
@@ -624,6 +625,17 @@ int ci_waves(const pbrt_gpu_ctx* c, int64_t nb) {
 // 387 -> 305 ms and 524 -> 472 ms per rank). PBRT_CI_SPLIT=0 disables it;
 // PBRT_CI_HEAVY=K forces the heavy count (tests).
 bool ci_split_enabled(const pbrt_gpu_ctx* c) { return c->knobs.ci_split; }
+// Does a one-wave Matte k_chain_ci workgroup with `dyn_lds` bytes of dynamic
+// LDS leave room for 3 waves per SIMD (12 workgroups on a CU's LDS)?
+bool ci_eu3_fits(const pbrt_gpu_ctx* c, unsigned dyn_lds, bool lds_nodes) {
+    hipFuncAttributes fa;
+    const void* f = lds_nodes ? reinterpret_cast<const void*>(&k_chain_ci<1>)
+                              : reinterpret_cast<const void*>(&k_chain_ci<1, 64>);
+    size_t stat = 0;
+    if (hipFuncGetAttributes(&fa, f) == hipSuccess) stat = fa.sharedSizeBytes;
+    const size_t per_wg = stat + dyn_lds;
+    return per_wg > 0 && c->lds_per_cu / per_wg >= 12;
+}
 int64_t ci_heavy_override(const pbrt_gpu_ctx* c) { return c->knobs.ci_heavy; }
 // k_chain_ci candidate stride: 2 issues candidates at the chain head's parity
 // only (dropped when an odd draw count flips it), 1 at every offset (twice
@@ -958,6 +970,7 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
         if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0) {
             c->n_simd = 4 * prop.multiProcessorCount;
             c->lds_per_block = prop.sharedMemPerBlock;
+            if (prop.maxSharedMemoryPerMultiProcessor > 0) c->lds_per_cu = prop.maxSharedMemoryPerMultiProcessor;
         }
     }
     std::vector<uint32_t> order;
@@ -1188,8 +1201,15 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                             const int ring = kCiRingBytes / (int)sizeof(RingEnt) / Gc;
                             unsigned lds = 0;
                             const ChainLayout lw = ci_layout(c->lay_ci, 1, Gc, lds);
+                            // Matte analytic scenes: the 3-waves/SIMD build unless the
+                            // workgroup's LDS (large spp: StartPixel staging) caps the CU
+                            // below 3 waves/SIMD, where the 2-wave build (no spills) is faster
+                            // (config C: 6.53 vs 7.41 s)
+                            const bool eu2 = !kx && !mesh_only && !ci_eu3_fits(c, lds, lds_nodes);
                             auto kern1 = kx ? k_chain_ci<1, 0, true>
-                                            : mesh_only ? k_chain_ci<1, -1> : (lds_nodes ? k_chain_ci<1> : k_chain_ci<1, 64>);
+                                         : mesh_only ? k_chain_ci<1, -1>
+                                         : eu2 ? (lds_nodes ? k_chain_ci<1, 0, false, 2> : k_chain_ci<1, 64, false, 2>)
+                                               : (lds_nodes ? k_chain_ci<1> : k_chain_ci<1, 64>);
                             hipLaunchKernelGGL(kern1, dim3((unsigned)((n + Gc - 1) / Gc)), dim3(kWave),
                                                lds, st, with_slot(sc, 2), rp, lw, c->d_jump, c->wb, sb,
                                                nb, kWave / Gc, ring, c->d_ctr, Gc == 1 ? ord : nullptr,

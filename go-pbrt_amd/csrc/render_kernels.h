@@ -37,7 +37,7 @@ __global__ void k_dl_panics(RenderParams rp, WaveBufs wb, int64_t slot_base, int
 template <bool kX = false>
 __global__ void k_tile_cost(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nb, float* __restrict__ feat, uint64_t* __restrict__ keys);
 __global__ void k_order_of_keys(const uint64_t* __restrict__ keys, int64_t nb, uint32_t* __restrict__ order);
-template <int kW, int kDepth = 0, bool kX = false>
+template <int kW, int kDepth = 0, bool kX = false, int kEu = 0>
 __global__ void k_chain_ci(DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base, int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr, const uint32_t* __restrict__ order, uint32_t* __restrict__ ticks, int cstride);
 template <int kW, int kDepth = 0, bool kX = false>
 __global__ void k_chain_async(DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base, int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr, const uint32_t* __restrict__ order, uint32_t* __restrict__ ticks, int cstride);
