@@ -125,6 +125,7 @@ struct pbrt_gpu_ctx {
     MeshBuild mesh;                      // triangle meshes + their LBVH (extension)
     int64_t heavy_k = 0;                 // slots at the front of h_slot_order that get 4 waves
     int64_t heavy8_k = 0;                // 4-wave shards: slots at the front that get 8 waves
+    int ci_wps = 2;                      // waves/SIMD of the last one-wave k_chain_ci launch (3 or 2)
     int64_t last_heavy = 0;              // heavy slots of the last EXACT launch (0: no split)
     std::vector<uint32_t> h_last_ticks;  // per-slot chain ticks of the last EXACT frame
     std::vector<uint8_t> h_slot_kw;      // waves per tile each slot ran with in the last frame
@@ -1206,6 +1207,7 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                             // below 3 waves/SIMD, where the 2-wave build (no spills) is faster
                             // (config C: 6.53 vs 7.41 s)
                             const bool eu2 = !kx && !mesh_only && !ci_eu3_fits(c, lds, lds_nodes);
+                            c->ci_wps = (kx || eu2) ? 2 : 3;
                             auto kern1 = kx ? k_chain_ci<1, 0, true>
                                          : mesh_only ? k_chain_ci<1, -1>
                                          : eu2 ? (lds_nodes ? k_chain_ci<1, 0, false, 2> : k_chain_ci<1, 64, false, 2>)
@@ -1223,7 +1225,18 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                     // tile, the most efficient per lane)
                     // measured wins at 1/2 and 1/4 shards (nb > n_simd); a loss at 1/8
                     // (1020 tiles: 294 -> 307 ms), so smaller launches never split
-                    int64_t heavy = (learned && kw > 1 && G == 1 && nb > c->n_simd && ci_split_enabled(c))
+                    // one GPU (kw == 1): since the Matte chain runs 3 waves/SIMD the whole
+                    // frame's lane time is below its heaviest tile's chain, so the heaviest
+                    // tiles get 4 waves there too (config B: chain 328.5 -> 313.3 ms)
+                    // (measured a loss on the mesh chain, D 825 -> 920 ms, and on kX, G 509 -> 517 ms:
+                    // one GPU splits only the 3-wave Matte analytic chain)
+                    bool split1 = false;
+                    if (kw == 1 && G == 1 && !kx && !mesh_only) {
+                        unsigned lds1 = 0;
+                        (void)ci_layout(c->lay_ci, 1, 1, lds1);
+                        split1 = ci_eu3_fits(c, lds1, lds_nodes);
+                    }
+                    int64_t heavy = (learned && G == 1 && (kw > 1 ? nb > c->n_simd : split1) && ci_split_enabled(c))
                                         ? std::min<int64_t>(c->heavy_k, nb) : 0;
                     // PBRT_CI_EXCLUSIVE = K (experiment): the K heaviest tiles of a shard run first with
                     // a CU each; the rest at kw waves beside them on the second stream
@@ -1466,8 +1479,8 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
         std::stable_sort(c->h_slot_order.begin(), c->h_slot_order.end(),
                          [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
         // heavy: tiles whose 1-wave chain alone would take over 0.7x the
-        // frame's throughput bound (summed cost over 2 waves/SIMD)
-        const double thr = 0.7 * sum / (2.0 * (double)c->n_simd);
+        // frame's throughput bound (summed cost over the chain's waves/SIMD)
+        const double thr = 0.7 * sum / ((double)c->ci_wps * (double)c->n_simd);
         int64_t k = 0;
         while (k < (int64_t)t.size() && cost[c->h_slot_order[(size_t)k]] > thr) k++;
         c->heavy_k = std::min<int64_t>(k, c->n_simd / 4);   // at most a quarter of the wave slots
