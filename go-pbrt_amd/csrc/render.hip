@@ -508,6 +508,17 @@ const PcgJump& pcg_jump_table() {
 int paths_ci_pixels(const pbrt_gpu_ctx* c, const RenderParams& rp);
 bool paths_wf_enabled(const pbrt_gpu_ctx* c);
 // Can the wave-parallel kernels replay this render exactly? (conditions: pbrt_spec.h)
+#ifndef PBRT_SP_SERIAL_KB
+// above this many KB of raw StartPixel draws, StartPixel runs on one lane and
+// its buffers leave LDS (build option). 4: config C's 256-spp pixels (9.5 KB
+// of draws) then cost a k_chain_ci workgroup 11 KB of LDS instead of 27, 12
+// workgroups share a CU and the chain runs the 3-wave build: C 6.50 -> 5.14 s
+// (a pixel's serial StartPixel, ~20 us, is under 0.5% of a C tile's chain)
+#define PBRT_SP_SERIAL_KB 4
+#endif
+#ifndef PBRT_CI_STAGE_KB
+#define PBRT_CI_STAGE_KB 8   // k_chain_ci stages StartPixel's stratified values in LDS up to this (build option)
+#endif
 bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const RenderParams& rp, ChainLayout& L,
                    ChainLayout& Lci) {
     if (rd->flags & PBRT_FLAG_PANIC_FIDELITY) return false;   // the serial kernel traces the extra rays
@@ -556,16 +567,18 @@ bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Rend
     // k_chain_ci: the same staging without the window buffers, then the ring
     off = 0;
     // the pixel's stratified values are staged in LDS while the staging of one
-    // 1-wave tile (aliased with the ring) stays <= 20 KB (5+ workgroups per CU;
-    // config C's 256 spp needs 19.3 KB); above, StartPixel writes them straight
-    // to the pixel's global record (always with the serial StartPixel, large spp)
+    // 1-wave tile (aliased with the ring) stays <= PBRT_CI_STAGE_KB; above,
+    // StartPixel writes them straight to the pixel's global record (always with
+    // the serial StartPixel, large spp): the trajectories read them from there
+    // anyway, and a smaller workgroup lets more share a CU (config C at 8 KB:
+    // 6.50 -> 5.25 s)
     const int64_t al16 = 15;
     const int64_t lds_staging = ((nd * n * 8 + al16) & ~al16) + ((nd * n * 2 + al16) & ~al16) +
                                 (((rp.sp_serial ? 4 : (int64_t)rp.sp_draws * 4) + al16) & ~al16);
     if (rp.sp_serial) {
         Lci.s1d = -1;
         Lci.other = put(16);
-    } else if (lds_staging > 20 * 1024) {
+    } else if (lds_staging > PBRT_CI_STAGE_KB * 1024) {
         Lci.s1d = -1;
         Lci.other = put(nd * n * 2);
     } else {
@@ -895,7 +908,7 @@ int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
         const int64_t E = (int64_t)rp.ndims * (s1 + s2), V = E + 64 + E / 8;
         rp.sp_events = (int32_t)E;
         rp.sp_draws = (int32_t)V;
-        rp.sp_serial = V * 4 <= 16 * 1024 ? 0 : 1;
+        rp.sp_serial = V * 4 <= PBRT_SP_SERIAL_KB * 1024 ? 0 : 1;
     }
     c->use_spec = c->kernel_req != PBRT_KERNEL_SERIAL && wave_eligible(c, rd, rp, c->lay, c->lay_ci);
     if ((c->kernel_req == PBRT_KERNEL_WAVE || c->kernel_req == PBRT_KERNEL_WAVEFRONT ||
