@@ -233,11 +233,17 @@ def pmc_fields(pmc, name, ms, frame_ms):
     """`traffic` and the north_star's "HBM GB/s vs peak" from the PMC passes
     (profiles/pmc_*.json: rocprofv3 FETCH_SIZE / WRITE_SIZE runs of the same
     bench command, tools/pmc_traffic.py), named by the library build they
-    measured: `traffic_same_build` says whether that is the build running now."""
-    traffic = (pmc.get(name) or {}).get("hbm_bytes_per_launch")
-    frame_bytes = sum(v.get("hbm_bytes_per_launch", 0) for v in pmc.values() if isinstance(v, dict))
+    measured: `traffic_same_build` says whether that is the build running now.
+    `traffic` is the kernel family's stage bytes per steady-state frame: the
+    sum over its launches of one frame (the N=1 chain stage is two concurrent
+    k_chain_ci launches), against the stage time `ms`."""
+    stages = pmc.get("stages") or {}
+    traffic = (stages.get(name) or {}).get("hbm_bytes_per_frame")
+    frame_bytes = sum(v.get("hbm_bytes_per_frame", 0) for v in stages.values())
     pmc_build = pmc.get("build_id")
     return {"traffic": traffic,
+            "traffic_unit": "HBM bytes per frame of the stage (PMC FETCH_SIZE + WRITE_SIZE, gfx950-corrected)",
+            "traffic_instantiations": (stages.get(name) or {}).get("instantiations"),
             "traffic_source": pmc.get("source"), "traffic_build_id": pmc_build,
             "traffic_same_build": bool(pmc_build) and pmc_build == BUILD_ID,
             "hbm": {"kernel_gbs": traffic / (ms / 1e3) / 1e9 if traffic else None,
@@ -303,12 +309,16 @@ def make_scene(G, cfg, W, H):
     return G.Scene.heightfield(W, H, quads=cfg["quads"], seed=1)
 
 
-def mesh_roofline(cfg, W, H, S, mode, stats_ms, paths):
-    """HBM roofline of the mesh traversal: the kernel's algorithmic bytes
-    (nodes x 32 B + triangles x 36 B per path, counted by
-    tools/count_mesh_bytes.py into profiles/meshbytes_*.json) x the paths of
-    this frame, over the kernel's duration measured here with HIP events; the
-    dominant of k_chain_ci / k_paths_ci by time."""
+def mesh_roofline(cfg, W, H, S, mode, stats_ms, paths, rays_closest, rays_shadow):
+    """HBM roofline of the mesh traversal, priced on the REFERENCE's rays: the
+    frame's closest-hit queries beyond the camera ray (the chain's on-chain
+    trajectories and the path stage trace exactly these; the camera ray is
+    traced once per pixel by k_wf_primary) and its visibility rays, each at
+    the bytes one reference walk fetches (nodes x 32 B + triangles x 36 B,
+    the path stage's per-walk means, counted by tools/count_mesh_bytes.py into
+    profiles/meshbytes_*.json), over the dominant stage's time measured here
+    with HIP events. The chain's speculative off-chain walks are not
+    algorithmic work: they lower `frac`."""
     mb = load_json(os.path.join(REPO, "profiles", f"meshbytes_heightfield{cfg['quads']}_{W}x{H}_s{S}x{S}_{mode}.json"))
     if not mb:
         return None
@@ -316,17 +326,33 @@ def mesh_roofline(cfg, W, H, S, mode, stats_ms, paths):
     cand = [("k_chain_ci", stats_ms["chain"]), ("k_paths_ci", stats_ms["paths"])] if mode == "exact" else \
         [("k_paths_ci_mb", stats_ms["paths"])]
     name, ms = max(cand, key=lambda x: x[1])
-    k = mb["kernels"].get(name)
-    if not k or ms <= 0:
+    ref = mb["kernels"].get("k_paths_ci") or {}
+    if "closest" not in ref or ms <= 0:
         return None
-    frame_bytes = k["bytes_per_path"] * paths
-    achieved = frame_bytes / (ms / 1e3) / 1e9
-    pf = pmc_fields(pmc, name.replace("_mb", ""), ms, stats_ms["kernels"])
+    per_closest = ref["closest"]["nodes_per_walk"] * mb["bytes_per_node"] + \
+        ref["closest"]["triangles_per_walk"] * mb["bytes_per_triangle"]
+    anyw = ref.get("any") or {"nodes_per_walk": 0.0, "triangles_per_walk": 0.0}
+    per_any = anyw["nodes_per_walk"] * mb["bytes_per_node"] + anyw["triangles_per_walk"] * mb["bytes_per_triangle"]
+    traced_closest = max(rays_closest - paths, 0.0)   # the camera ray's query is per pixel on the device
+    if name == "k_chain_ci":   # the trajectories: closest-hit walks only
+        algo = traced_closest * per_closest
+    else:
+        algo = traced_closest * per_closest + rays_shadow * per_any
+    achieved = algo / (ms / 1e3) / 1e9
+    fam = {"k_chain_ci": "k_chain_ci", "k_paths_ci": "k_paths_ci", "k_paths_ci_mb": "k_paths_ci"}[name]
+    pf = pmc_fields(pmc, fam, ms, stats_ms["kernels"])
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, **pf, "kernel": name, "kernel_ms": ms,
-            "bytes_per_launch": frame_bytes, "bytes_per_path": k["bytes_per_path"],
-            "per_walk": {q: {"nodes": k[q]["nodes_per_walk"], "triangles": k[q]["triangles_per_walk"]}
-                         for q in ("closest", "any") if q in k},
+            "bytes_per_launch": algo,
+            "algorithmic": {"reference_closest_walks_beyond_camera": traced_closest,
+                            "reference_shadow_walks": rays_shadow,
+                            "bytes_per_closest_walk": per_closest, "bytes_per_shadow_walk": per_any,
+                            "source": f"profiles/meshbytes_heightfield{cfg['quads']}_{W}x{H}_s{S}x{S}_{mode}.json "
+                                      f"(k_paths_ci per-walk means)"},
+            "kernel_walks": {q: {"nodes": k[q]["nodes_per_walk"], "triangles": k[q]["triangles_per_walk"],
+                                 "walks": k[q]["walks"]}
+                             for kn, k in mb["kernels"].items() for q in ("closest", "any") if q in k
+                             and kn == name.replace("_mb", "")},
             "pipeline": {"kernels_ms": stats_ms["kernels"], "k_chain_ms": stats_ms["chain"],
                          "k_paths_ms": stats_ms["paths"]}}
 
@@ -502,7 +528,7 @@ def main():
             roof = None   # no algorithmic-FLOP count of these variants (profiles/flops_* are B, C, G)
         elif cfg["scene"] == "heightfield":
             roof = mesh_roofline(cfg, W, H, S, args.mode, {"chain": chain_ms, "paths": paths_ms, "kernels": kern_ms},
-                                 paths_local / len(stats))
+                                 paths_local / len(stats), rays_c / len(stats), rays_s / len(stats))
         else:
             roof = roofline(cfg["scene"], W, H, S, paths_local / len(stats), kernel_kind, kern_ms, chain_ms,
                             paths_ms, merge_ms, args.mode)

@@ -60,11 +60,6 @@ struct Knobs {
     bool pw_sort = false;      // PBRT_PW_SORT=1
     double pw_gb = 24.0;       // PBRT_PW_GB
     double wave_buffer_gb = 0; // PBRT_WAVE_BUFFER_GB (0: min(96 GB, half the free HBM))
-    bool ci_async = false;     // PBRT_CI_ASYNC=1: multi-wave Matte tiles on k_chain_async (asynchronous waves)
-    bool ci_heavy8 = false;    // PBRT_CI_HEAVY8=1: 4-wave shards run their heaviest tiles at 8 waves
-    int ci_mc = 0;             // PBRT_CI_MC = 2, 4, 8: the heavy tiles on k_chain_mc with that many CUs each
-    int ci_mc_waves = 8;       // PBRT_CI_MC_WAVES = 4, 8: waves per k_chain_mc workgroup
-    int64_t ci_exclusive = 0;  // PBRT_CI_EXCLUSIVE = K: a shard's K heaviest tiles get a CU each (LDS pad)
     bool ci_dense = false;     // PBRT_CI_DENSE=1 (builds with -DPBRT_CI_DENSE_WALK): k_chain_ci's closest hit by
                                // bvh_walk_dense (bit-exact; slower on B)
     int cull_group = 4;        // PBRT_CULL_GROUP: leaves per culling group
@@ -85,14 +80,6 @@ struct Knobs {
         if (const char* e = getenv("PBRT_CI_HEAVY")) k.ci_heavy = (int64_t)atoll(e);
         if (const char* e = getenv("PBRT_CI_SPLIT")) k.ci_split = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_DENSE")) k.ci_dense = atoi(e) != 0;
-        if (const char* e = getenv("PBRT_CI_ASYNC")) k.ci_async = atoi(e) != 0;
-        if (const char* e = getenv("PBRT_CI_HEAVY8")) k.ci_heavy8 = atoi(e) != 0;
-        if (const char* e = getenv("PBRT_CI_MC")) {
-            const int v = atoi(e);
-            if (v == 1 || v == 2 || v == 4 || v == 8) k.ci_mc = v;
-        }
-        if (const char* e = getenv("PBRT_CI_MC_WAVES")) k.ci_mc_waves = atoi(e) == 4 ? 4 : 8;
-        if (const char* e = getenv("PBRT_CI_EXCLUSIVE")) k.ci_exclusive = std::max<int64_t>(0, (int64_t)atoll(e));
         if (const char* e = getenv("PBRT_CI_ORDER")) k.ci_order = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_PROBE")) k.ci_probe = atoi(e) != 0;
         if (const char* e = getenv("PBRT_PATHS_S1D")) k.paths_s1d_lds = std::strcmp(e, "lds") == 0;
@@ -124,7 +111,6 @@ struct pbrt_gpu_ctx {
     hipEvent_t ev_split = nullptr, ev_join = nullptr;
     MeshBuild mesh;                      // triangle meshes + their LBVH (extension)
     int64_t heavy_k = 0;                 // slots at the front of h_slot_order that get 4 waves
-    int64_t heavy8_k = 0;                // 4-wave shards: slots at the front that get 8 waves
     int ci_wps = 2;                      // waves/SIMD of the last one-wave k_chain_ci launch (3 or 2)
     int64_t last_heavy = 0;              // heavy slots of the last EXACT launch (0: no split)
     std::vector<uint32_t> h_last_ticks;  // per-slot chain ticks of the last EXACT frame
@@ -185,9 +171,6 @@ struct pbrt_gpu_ctx {
     // EXACT frame (wall_clock64 ticks) and the slot order derived from it
     uint32_t* d_ticks = nullptr;
     uint32_t* d_slot_order = nullptr;
-    McTile* d_mc = nullptr;                 // k_chain_mc tile records and rings
-    unsigned long long* d_mc_rings = nullptr;
-    int64_t mc_cap = 0;
     int64_t ticks_cap = 0;
     std::vector<uint32_t> h_slot_order;
     // path wavefront (k_pw_*, PBRT_PATHS_WF=1): path records, queues, counters,
@@ -1184,25 +1167,13 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                         c->ticks_n = nb;
                     }
                     // one launch of n workgroups, workgroup b on slot ord[b] (identity if null)
-                    // excl: pad the dynamic LDS so that no other chain workgroup fits
-                    // beside one of these on a CU (a heavy tile's waves issue alone)
-                    auto launch_ci = [&](int w, int64_t n, const uint32_t* ord, hipStream_t st, bool excl = false) {
+                    auto launch_ci = [&](int w, int64_t n, const uint32_t* ord, hipStream_t st) {
                         if (w > 1) {   // one tile per workgroup of w waves; the ring grows with the lanes
                             const int ring = w * kCiRingBytes / (int)sizeof(RingEnt);
                             unsigned lds = 0;
                             const ChainLayout lw = ci_layout(c->lay_ci, w, 1, lds);
-                            if (excl) {
-                                // half the CU's LDS (160 KB on gfx950) plus a bit, within the per-workgroup limit
-                                const size_t want = 84 * 1024;
-                                if (c->lds_per_block >= want + 16 * 1024) lds = std::max<unsigned>(lds, (unsigned)want);
-                            }
                             // kX: LDS-staged trees only, at most 4 waves per tile (wave_eligible, ci_waves)
-                            auto kern = (!kx && c->knobs.ci_async)
-                                            ? (mesh_only ? (w == 2 ? k_chain_async<2, -1> : w == 4 ? k_chain_async<4, -1> : k_chain_async<8, -1>)
-                                               : w == 2 ? (lds_nodes ? k_chain_async<2> : k_chain_async<2, 64>)
-                                               : w == 4 ? (lds_nodes ? k_chain_async<4> : k_chain_async<4, 64>)
-                                                        : (lds_nodes ? k_chain_async<8> : k_chain_async<8, 64>))
-                                        : kx ? (w == 2 ? k_chain_ci<2, 0, true> : k_chain_ci<4, 0, true>)
+                            auto kern = kx ? (w == 2 ? k_chain_ci<2, 0, true> : k_chain_ci<4, 0, true>)
                                         : mesh_only ? (w == 2 ? k_chain_ci<2, -1> : w == 4 ? k_chain_ci<4, -1> : k_chain_ci<8, -1>)
                                            : (w == 2   ? (lds_nodes ? k_chain_ci<2> : k_chain_ci<2, 64>)
                                               : w == 4 ? (lds_nodes ? k_chain_ci<4> : k_chain_ci<4, 64>)
@@ -1251,89 +1222,15 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                     }
                     int64_t heavy = (learned && G == 1 && (kw > 1 ? nb > c->n_simd : split1) && ci_split_enabled(c))
                                         ? std::min<int64_t>(c->heavy_k, nb) : 0;
-                    // PBRT_CI_EXCLUSIVE = K (experiment): the K heaviest tiles of a shard run first with
-                    // a CU each; the rest at kw waves beside them on the second stream
-                    int64_t excl = (learned && kw > 1 && G == 1 && c->knobs.ci_exclusive > 0)
-                                       ? std::min<int64_t>({c->knobs.ci_exclusive, nb - 1, (int64_t)c->n_simd / 8})
-                                       : 0;
-                    if (excl > 0) heavy = 0;
                     if (ci_heavy_override(c) >= 0 && learned && G == 1)   // tests and experiments force the split
                         heavy = std::min<int64_t>(ci_heavy_override(c), nb);
                     if (heavy >= nb) heavy = 0;   // nothing left for the light launch: one launch at kw
-                    // 4-wave shards: the heaviest tiles at 8 waves, the rest at 4 beside them
-                    // (PBRT_CI_HEAVY8=1; measured a loss on 1/8 shards of B: 127-128 vs 117-126 ms,
-                    // the 8-wave workgroups wait for whole CUs the 4-wave launch keeps refilling)
-                    int64_t heavy8 = (learned && c->knobs.ci_heavy8 && kw == 4 && !kx && G == 1 && heavy == 0 &&
-                                      excl == 0 && ci_split_enabled(c) && ci_heavy_override(c) < 0)
-                                         ? std::min<int64_t>(c->heavy8_k, nb - 1) : 0;
-                    c->last_heavy = heavy + heavy8;
+                    c->last_heavy = heavy;
                     if (ticks) {   // label every slot with the waves it actually runs at
                         c->h_slot_kw.assign((size_t)nb, (uint8_t)(heavy > 0 ? 1 : kw));
                         for (int64_t i = 0; i < heavy; i++) c->h_slot_kw[c->h_slot_order[(size_t)i]] = (uint8_t)ci_heavy_waves(c);
-                        for (int64_t i = 0; i < heavy8; i++) c->h_slot_kw[c->h_slot_order[(size_t)i]] = (uint8_t)8;
                     }
-                    // PBRT_CI_MC = M (Matte): the heavy tiles run on k_chain_mc, M CUs each
-                    // (at most one workgroup per CU in that launch: all of a tile's
-                    // workgroups are resident together); the rest at kw waves beside them
-                    int64_t mc = 0;
-                    const int mcM = c->knobs.ci_mc;
-                    if (mcM > 0 && !kx && G == 1 && (learned || ci_heavy_override(c) >= 0)) {
-                        const int64_t cus = std::max<int64_t>(1, (int64_t)c->n_simd / 4);
-                        mc = ci_heavy_override(c) >= 0 ? ci_heavy_override(c) : (learned ? c->heavy_k : 0);
-                        mc = std::min<int64_t>({mc, nb, cus / mcM});
-                        if (!order && mc < nb) mc = 0;   // the light launch needs the order's tail
-                    }
-                    if (mc > 0) {
-                        excl = 0;
-                        heavy = 0;
-                        c->last_heavy = mc;
-                        if (ticks && learned)
-                            for (int64_t i = 0; i < mc; i++) c->h_slot_kw[c->h_slot_order[(size_t)i]] = (uint8_t)8;
-                    }
-                    if (mc > 0) {
-                        constexpr int kMcRing = 4096;
-                        if (c->mc_cap < mc) {
-                            if (c->d_mc) (void)hipFree(c->d_mc);
-                            if (c->d_mc_rings) (void)hipFree(c->d_mc_rings);
-                            c->d_mc = nullptr;
-                            c->d_mc_rings = nullptr;
-                            c->mc_cap = 0;
-                            HIPCHK(c, hipMalloc((void**)&c->d_mc, sizeof(McTile) * (size_t)mc));
-                            HIPCHK(c, hipMalloc((void**)&c->d_mc_rings, sizeof(unsigned long long) * kMcRing * (size_t)mc));
-                            c->mc_cap = mc;
-                        }
-                        HIPCHK(c, hipMemsetAsync(c->d_mc, 0, sizeof(McTile) * (size_t)mc, c->stream));
-                        const int w = c->knobs.ci_mc_waves;
-                        unsigned lds = 0;
-                        const ChainLayout lw = ci_layout(c->lay_ci, w, 1, lds);
-                        auto kern = mesh_only ? (w == 4 ? k_chain_mc<4, -1> : k_chain_mc<8, -1>)
-                                    : w == 4 ? (lds_nodes ? k_chain_mc<4> : k_chain_mc<4, 64>)
-                                             : (lds_nodes ? k_chain_mc<8> : k_chain_mc<8, 64>);
-                        HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
-                        hipLaunchKernelGGL(kern, dim3((unsigned)(mc * mcM)), dim3(kWave * w), lds, c->stream,
-                                           with_slot(sc, 2), rp, lw, c->d_jump, c->wb, sb, nb, c->d_mc, c->d_mc_rings,
-                                           kMcRing, mcM, order, ticks);
-                        if (mc < nb) {
-                            HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
-                            launch_ci(kw, nb - mc, order ? order + mc : nullptr, c->stream2);
-                            HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
-                            HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
-                        }
-                    } else if (heavy8 > 0) {
-                        HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
-                        launch_ci(8, heavy8, order, c->stream);
-                        HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
-                        launch_ci(kw, nb - heavy8, order + heavy8, c->stream2);
-                        HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
-                        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
-                    } else if (excl > 0) {
-                        HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
-                        launch_ci(kw, excl, order, c->stream, true);
-                        HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
-                        launch_ci(kw, nb - excl, order + excl, c->stream2);
-                        HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
-                        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
-                    } else if (heavy > 0) {
+                    if (heavy > 0) {
                         HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
                         launch_ci(ci_heavy_waves(c), heavy, order, c->stream);
                         HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
@@ -1498,12 +1395,6 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
         while (k < (int64_t)t.size() && cost[c->h_slot_order[(size_t)k]] > thr) k++;
         c->heavy_k = std::min<int64_t>(k, c->n_simd / 4);   // at most a quarter of the wave slots
         if (ci_heavy_override(c) >= 0) c->heavy_k = ci_heavy_override(c);
-        // PBRT_CI_HEAVY8: on shards that fit the wave slots at 4 waves per tile
-        // (1/8 frame), the tiles within 0.8x of the heaviest at 8 waves (a CU each)
-        k = 0;
-        const double top = t.empty() ? 0.0 : cost[c->h_slot_order[0]];
-        while (k < (int64_t)t.size() && k < 16 && cost[c->h_slot_order[(size_t)k]] > 0.8 * top) k++;
-        c->heavy8_k = k;
         c->order_key = c->ticks_key;
     }
     if (ctr.any_panic) {
@@ -1632,7 +1523,7 @@ void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
     void* bufs[] = {c->d_shapes, c->d_materials, c->d_prims, c->d_nodes, c->d_order, c->d_lights, c->d_camera, c->d_film,
                     c->d_dist,   c->d_films,     c->d_s1d,   c->d_panics, c->d_ctr,   c->d_out,    c->d_jump,
                     c->d_wave,   c->d_fprims, c->d_ticks, c->d_slot_order, c->d_groups,
-                    c->d_gmasks, c->d_cost,   c->d_cost_keys, c->d_pw, c->d_cancel_seen, c->d_mc, c->d_mc_rings};
+                    c->d_gmasks, c->d_cost,   c->d_cost_keys, c->d_pw, c->d_cancel_seen};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     mesh_bvh_free(c->mesh);

@@ -733,16 +733,5 @@ struct CiGroup {
     int reissue;    // the head must be re-run with its sample index known
     int pad;
 };
-// k_chain_mc: one tile's chain state shared by the workgroups (CUs) that run it
-// (global memory, agent-scope atomics; zeroed by the host before each launch)
-struct alignas(128) McTile {
-    uint64_t S;         // PCG32 state at the current pixel's offset 0
-    uint64_t st_head;   // PCG32 state at the head offset
-    int64_t pi, npx;    // current pixel, pixels of the tile
-    uint32_t head, nxt; // offset of sample kh; next offset to issue
-    int kh, phase, reissue;
-    uint32_t walk_lock;
-    uint32_t bar_count, bar_gen;   // the workgroups' meeting (mc_barrier)
-};
 
 }  // namespace pbrtk

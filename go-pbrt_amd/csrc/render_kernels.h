@@ -39,10 +39,6 @@ __global__ void k_tile_cost(DevScene sc, RenderParams rp, WaveBufs wb, int64_t s
 __global__ void k_order_of_keys(const uint64_t* __restrict__ keys, int64_t nb, uint32_t* __restrict__ order);
 template <int kW, int kDepth = 0, bool kX = false, int kEu = 0>
 __global__ void k_chain_ci(DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base, int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr, const uint32_t* __restrict__ order, uint32_t* __restrict__ ticks, int cstride);
-template <int kW, int kDepth = 0, bool kX = false>
-__global__ void k_chain_async(DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base, int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr, const uint32_t* __restrict__ order, uint32_t* __restrict__ ticks, int cstride);
-template <int kW, int kDepth = 0, bool kX = false>
-__global__ void k_chain_mc(DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base, int64_t nslots_batch, McTile* __restrict__ tiles, unsigned long long* __restrict__ rings, int ring_size, int M, const uint32_t* __restrict__ order, uint32_t* __restrict__ ticks);
 __global__ void k_merge_film(const pbrt_film_desc* __restrict__ film_desc, RenderParams rp, const double* __restrict__ films, double* __restrict__ out, const int* __restrict__ cancel_seen);
 __global__ void k_intersect(DevScene sc, int64_t n, const double* __restrict__ rays, double* __restrict__ out, int any_hit);
 

@@ -83,7 +83,7 @@ SF_HD int sphere_roots_filter(double ox, double oy, double oz, double dx, double
     const double qv = (bv < 0 ? bv - rd : bv + rd) * -0.5;
     const double aq = sf_abs(qv);
     const double Mq = 0.5 * (2.0 * ((sf_abs(dx * ox) + sf_abs(dy * oy)) + sf_abs(dz * oz)) + rd);
-    const double Rq = 32.0 * SF_EPS * Mq;
+    const double Rq = 36.0 * SF_EPS * Mq;   /* >= 2 x 17.5 eps */
     if (!(av >= S && aq >= S && aq > 2.0 * Rq)) return -1;
     const double Mc = ((ox * ox + oy * oy) + oz * oz) + radius * radius;
     const double r0v = qv / av, r1v = cv / qv;

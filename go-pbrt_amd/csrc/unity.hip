@@ -7,7 +7,6 @@
 #include "mesh_bvh.hip"
 #include "k_chain_1.hip"
 #include "k_chain_n.hip"
-#include "k_chain_a.hip"
 #include "k_chain_x.hip"
 #include "k_paths_m.hip"
 #include "k_paths_x.hip"

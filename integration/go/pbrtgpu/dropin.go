@@ -406,6 +406,11 @@ type cArena struct {
 	off  uintptr
 }
 
+// maxBatchRays bounds one device batch: its arrays fit the fixed-size-array
+// casts below ([1 << 28]float64) and its arena size, n*(14*8+4+1)+128 bytes,
+// fits a 32-bit int; IntersectBatch / IntersectPBatch split larger batches.
+const maxBatchRays = 1 << 24
+
 func newArena(bytes int) *cArena {
 	if bytes < 8 {
 		bytes = 8
@@ -453,6 +458,18 @@ func (b *BVH) IntersectBatch(rays []*pbrt.Ray, hits []Hit) error {
 	if len(hits) < n {
 		return fmt.Errorf("pbrtgpu: %d hits for %d rays", len(hits), n)
 	}
+	if n > maxBatchRays { // the arena's slices and its byte count stay in range
+		for i := 0; i < n; i += maxBatchRays {
+			j := i + maxBatchRays
+			if j > n {
+				j = n
+			}
+			if err := b.IntersectBatch(rays[i:j], hits[i:j]); err != nil {
+				return err
+			}
+		}
+		return nil
+	}
 	if n == 0 {
 		return nil
 	}
@@ -494,6 +511,18 @@ func (b *BVH) IntersectPBatch(rays []*pbrt.Ray, occluded []bool) error {
 	n := len(rays)
 	if len(occluded) < n {
 		return fmt.Errorf("pbrtgpu: %d results for %d rays", len(occluded), n)
+	}
+	if n > maxBatchRays {
+		for i := 0; i < n; i += maxBatchRays {
+			j := i + maxBatchRays
+			if j > n {
+				j = n
+			}
+			if err := b.IntersectPBatch(rays[i:j], occluded[i:j]); err != nil {
+				return err
+			}
+		}
+		return nil
 	}
 	if n == 0 {
 		return nil

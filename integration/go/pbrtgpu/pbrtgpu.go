@@ -227,6 +227,11 @@ func (r *Renderer) RenderFrame(ctx context.Context, rd *C.pbrt_render_desc, film
 	// The watcher is joined before RenderFrame returns: a cancel racing the end
 	// of the render must not reach pbrt_gpu_cancel after the caller's Close
 	// (pbrt_gpu_destroy frees the context the cancel locks).
+	// a context cancelled before the frame starts renders nothing (the
+	// reference's tile producer returns gtx.Err(), integrator.go:333-336)
+	if err := ctx.Err(); err != nil {
+		return err
+	}
 	done := make(chan struct{})
 	exited := make(chan struct{})
 	go func() {
@@ -243,11 +248,11 @@ func (r *Renderer) RenderFrame(ctx context.Context, rd *C.pbrt_render_desc, film
 	<-exited
 	switch rc {
 	case C.PBRT_OK:
-		// a cancel that landed before the render was in flight is not seen by
-		// the device; the frame completed, but the caller asked to stop
-		if err := ctx.Err(); err != nil {
-			return err
-		}
+		// the frame is complete: a cancel that reached the device while the
+		// render was in flight returns PBRT_E_CANCELLED instead, and one that
+		// came after the last kernel (or in the instant before the render was
+		// in flight) leaves a valid film, as the reference's g.Wait() returns
+		// nil once every tile was handed out (integrator.go:311-347)
 		return nil
 	case C.PBRT_E_CANCELLED:
 		if err := ctx.Err(); err != nil {

@@ -150,6 +150,7 @@ def test_config_D_full_size_properties_and_heaviest_tiles():
         info = r.mesh_info()
         film, st = r.render(rd)
         ticks, _ = r.tile_ticks()
+        film2, _ = r.render(rd)   # the steady-state frame: learned heaviest-first order
     assert info["tris"] == 999698
     print(f"config D LBVH: {info}")
     assert st.tiles_rendered == 8160 and st.paths_traced == W * H * 63
@@ -162,6 +163,10 @@ def test_config_D_full_size_properties_and_heaviest_tiles():
             g, _ = r.render(one)
         rc, o, _ = O.render(scene.desc, one, threads=1)
         assert rc == 0 and same_bits(g, o), t
+        # pixels only tile t's samples reach, in the cold and the second frame
+        x0, y0 = (t % 120) * 16, (t // 120) * 16
+        for f in (film, film2):
+            assert np.all(f[y0:y0 + 15, x0:x0 + 15] == o[y0:y0 + 15, x0:x0 + 15]), t
 
 
 @pytest.mark.slow

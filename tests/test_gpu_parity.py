@@ -440,55 +440,6 @@ def test_wave_ci_stride_1_keeps_bits(ci_waves, monkeypatch):
     check(G.Scene.cornell(48, 32), abi.render_desc(6, 6, max_depth=12, rr_threshold=0.5), kernel="wave_ci")
 
 
-@pytest.mark.parametrize("ci_waves", ["2", "4", "8"])
-def test_wave_ci_async_waves_keep_bits(ci_waves, monkeypatch):
-    """PBRT_CI_ASYNC=1: multi-wave tiles on k_chain_async, whose waves step
-    on their own (LDS atomics for the issue counter, the ring and the walk lock)
-    and meet only at a new pixel; only the schedule changes."""
-    monkeypatch.setenv("PBRT_CI_ASYNC", "1")
-    monkeypatch.setenv("PBRT_CI_WAVES", ci_waves)
-    check(G.Scene.readme(112, 80), abi.render_desc(8, 8), kernel="wave_ci")
-    check(G.Scene.readme(48, 40), abi.render_desc(4, 4, jitter=True), kernel="wave_ci")
-    check(G.Scene.cornell(48, 32), abi.render_desc(6, 6, max_depth=12, rr_threshold=0.5), kernel="wave_ci")
-    check(G.Scene.readme(64, 48), abi.render_desc(3, 5, tile_begin=1, tile_stride=3), kernel="wave_ci")
-    scene = panic_scene()
-    rd = abi.render_desc(2, 2)
-    rc, _, ost = O.render(scene.desc, rd, threads=1)
-    assert rc == abi.PBRT_E_REF_PANIC
-    with G.Renderer(scene, kernel="wave_ci") as r:
-        with pytest.raises(G.PbrtError) as ei:
-            r.render(rd)
-    st = ei.value.stats
-    assert ei.value.code == abi.PBRT_E_REF_PANIC
-    assert (st.panic_kind, st.panic_tile, st.panic_pixel_x, st.panic_pixel_y, st.panic_sample, st.panic_bounce) == (
-        ost.panic_kind, ost.panic_tile, ost.panic_px, ost.panic_py, ost.panic_sample, ost.panic_bounce)
-
-
-@pytest.mark.parametrize("mc", ["1", "2", "4"])
-@pytest.mark.parametrize("mc_waves", ["4", "8"])
-def test_wave_ci_multi_cu_tiles_keep_bits(mc, mc_waves, monkeypatch):
-    """PBRT_CI_MC=M: the heaviest tiles' chains run on k_chain_mc, M workgroups
-    (CUs) per tile sharing the chain through global atomics and meeting at each
-    pixel; the other tiles run beside them. Only the schedule changes."""
-    monkeypatch.setenv("PBRT_CI_MC", mc)
-    monkeypatch.setenv("PBRT_CI_MC_WAVES", mc_waves)
-    monkeypatch.setenv("PBRT_CI_WAVES", "4")
-    monkeypatch.setenv("PBRT_CI_HEAVY", "5")
-    scene = G.Scene.readme(112, 80)
-    rds = [abi.render_desc(8, 8), abi.render_desc(4, 4, tile_begin=1, tile_stride=2),
-           abi.render_desc(6, 6, max_depth=12, rr_threshold=0.5), abi.render_desc(3, 3, tile_begin=7, tile_end=8)]
-    with G.Renderer(scene, kernel="wave_ci") as r:
-        for rd in rds:
-            ofilm, _ = oracle_render(scene, rd)
-            for frame in range(2):
-                film, st = r.render(rd)
-                assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
-                assert same_bits(film, ofilm), (rd.sampler_x, frame)
-                ticks, heavy = r.tile_ticks()
-                assert len(ticks) == st.tiles_rendered and ticks.min() > 0
-    check(G.Scene.cornell(48, 32), abi.render_desc(6, 6, max_depth=12, rr_threshold=0.5), kernel="wave_ci")
-
-
 @pytest.mark.parametrize("ci_waves", ["1", "2", "4", "8"])
 def test_wave_ci_waves_per_tile_larger_frames(ci_waves, monkeypatch):
     monkeypatch.setenv("PBRT_CI_WAVES", ci_waves)

@@ -5,7 +5,7 @@ mesh walks count the nodes they fetch (32 B each) and the triangles they test
 bench.py --config D for the HBM roofline (achieved = these bytes / the
 kernel's measured time).
 
-    PBRT_GPU_LIB=go-pbrt_amd/lib/libpbrt_gpu_meshcount.so \\
+    PBRT_GPU_LIB=go-pbrt_amd/lib/exp/libpbrt_gpu_meshcount.so \\
         python tools/count_mesh_bytes.py [--quads 707 --width 1920 --height 1080 --spp 8]
 """
 import argparse
@@ -16,7 +16,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "go-pbrt_amd"))
-os.environ.setdefault("PBRT_GPU_LIB", os.path.join(REPO, "go-pbrt_amd", "lib", "libpbrt_gpu_meshcount.so"))
+os.environ.setdefault("PBRT_GPU_LIB", os.path.join(REPO, "go-pbrt_amd", "lib", "exp", "libpbrt_gpu_meshcount.so"))
 
 SLOTS = {1: "k_wf_primary", 2: "k_chain_ci", 3: "k_paths_ci", 4: "k_mb_setup", 5: "k_paths_ci_mb",
          6: "k_render_exact", 7: "k_intersect"}

@@ -10,11 +10,11 @@
 #                         extra bench args after commas, e.g. bench=C,--steps,1
 #   benchfull=<cfg>       bench.py --config <cfg> with its CPU baseline and side mode
 #   profile=<cfg>         tools/profile_round.sh for that config
-#   phase=<diag|steptime> tools/phase_stats.py with lib/libpbrt_gpu_<build>.so (config B)
-#   libbench=<v>,<cfg>    bench.py --config <cfg> --steps 2 with lib/libpbrt_gpu_<v>.so (experiment builds)
+#   phase=<diag|steptime> tools/phase_stats.py with lib/exp/libpbrt_gpu_<build>.so (config B)
+#   libbench=<v>,<cfg>    bench.py --config <cfg> --steps 2 with lib/exp/libpbrt_gpu_<v>.so (experiment builds)
 #   envbench=VAR=V[+VAR2=V2],<cfg>[,args]  bench.py --config <cfg> with those environment variables
 #   py=<script>[~args]    python tools/<script>.py <args> ('~' between args; output under <tag>/)
-#   libpy=<v>,<script>[~args]  py= with lib/libpbrt_gpu_<v>.so (diag / experiment builds)
+#   libpy=<v>,<script>[~args]  py= with lib/exp/libpbrt_gpu_<v>.so (diag / experiment builds)
 #   smoke                 __graft_entry__.smoke()
 set -o pipefail
 TAG=$1
@@ -41,10 +41,10 @@ for step in "$@"; do
   phase=*)   # phase=diag | phase=steptime[,scene]: tools/phase_stats.py on that diagnostics build
     spec=${step#phase=}; lib=${spec%%,*}; scn=readme
     [[ "$spec" == *,* ]] && scn=${spec#*,}
-    PBRT_GPU_LIB=go-pbrt_amd/lib/libpbrt_gpu_$lib.so timeout -k 10 300 python tools/phase_stats.py --scene $scn > $OUT/phase_${lib}_$scn.txt 2>&1 || { echo "phase $lib failed"; tail -20 $OUT/phase_${lib}_$scn.txt; exit 1; } ;;
-  libbench=*)   # libbench=<variant>,<cfg>: bench.py --config <cfg> with lib/libpbrt_gpu_<variant>.so
+    PBRT_GPU_LIB=go-pbrt_amd/lib/exp/libpbrt_gpu_$lib.so timeout -k 10 300 python tools/phase_stats.py --scene $scn > $OUT/phase_${lib}_$scn.txt 2>&1 || { echo "phase $lib failed"; tail -20 $OUT/phase_${lib}_$scn.txt; exit 1; } ;;
+  libbench=*)   # libbench=<variant>,<cfg>: bench.py --config <cfg> with lib/exp/libpbrt_gpu_<variant>.so
     spec=${step#libbench=}; v=${spec%%,*}; cfg=${spec#*,}
-    PBRT_GPU_LIB=go-pbrt_amd/lib/libpbrt_gpu_$v.so timeout -k 10 400 python bench.py --config $cfg --no-cpu-baseline --no-side-mode --steps 2 > $OUT/bench_${cfg}_$v.json 2> $OUT/bench_${cfg}_$v.err || { echo "bench $cfg $v failed"; tail -20 $OUT/bench_${cfg}_$v.err; exit 1; } ;;
+    PBRT_GPU_LIB=go-pbrt_amd/lib/exp/libpbrt_gpu_$v.so timeout -k 10 400 python bench.py --config $cfg --no-cpu-baseline --no-side-mode --steps 2 > $OUT/bench_${cfg}_$v.json 2> $OUT/bench_${cfg}_$v.err || { echo "bench $cfg $v failed"; tail -20 $OUT/bench_${cfg}_$v.err; exit 1; } ;;
   envbench=*)   # envbench=VAR=VALUE,<cfg>[,args]: bench.py --config <cfg> (no CPU baseline / side mode) with VAR=VALUE
     spec=${step#envbench=}; kv=${spec%%,*}; rest=${spec#*,}; cfg=${rest%%,*}; extra=""
     [[ "$rest" == *,* ]] && extra=$(echo "${rest#*,}" | tr ',' ' ')
@@ -54,11 +54,11 @@ for step in "$@"; do
     [[ "$spec" == *~* ]] && args=$(echo "${spec#*~}" | tr '~' ' ')
     tagf=$(echo "$scr $args" | tr -c 'A-Za-z0-9=.\n-' '_')
     timeout -k 10 400 python tools/$scr.py $args > $OUT/$tagf.txt 2>&1 || { echo "py $scr failed"; tail -20 $OUT/$tagf.txt; exit 1; } ;;
-  libpy=*)   # libpy=<variant>,<script>[~args]: as py= with lib/libpbrt_gpu_<variant>.so
+  libpy=*)   # libpy=<variant>,<script>[~args]: as py= with lib/exp/libpbrt_gpu_<variant>.so
     spec=${step#libpy=}; v=${spec%%,*}; spec=${spec#*,}; scr=${spec%%~*}; args=""
     [[ "$spec" == *~* ]] && args=$(echo "${spec#*~}" | tr '~' ' ')
     tagf=$(echo "$v $scr $args" | tr -c 'A-Za-z0-9=.\n-' '_')
-    PBRT_GPU_LIB=go-pbrt_amd/lib/libpbrt_gpu_$v.so timeout -k 10 400 python tools/$scr.py $args > $OUT/$tagf.txt 2>&1 || { echo "libpy $scr failed"; tail -20 $OUT/$tagf.txt; exit 1; } ;;
+    PBRT_GPU_LIB=go-pbrt_amd/lib/exp/libpbrt_gpu_$v.so timeout -k 10 400 python tools/$scr.py $args > $OUT/$tagf.txt 2>&1 || { echo "libpy $scr failed"; tail -20 $OUT/$tagf.txt; exit 1; } ;;
   smoke)
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $OUT/smoke.log; exit 1; } ;;
   *) echo "unknown step $step"; exit 2 ;;

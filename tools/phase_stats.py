@@ -50,7 +50,8 @@ with G.Renderer(scene, kernel=a.kernel, occupancy=a.occupancy, lanes_per_wave=a.
         if tot_s:
             labels = ["loop top", "closest hit + SI", "BSDF setup", "light sampling", "BSDF sample+spawn+RR"]
             print("  step regions: " + ", ".join(f"{l} {v / tot_s * 100:.1f}%" for l, v in zip(labels, sc_[:5])))
-            tt = sum(sc_[5:8]) or 1
+        tt = sum(sc_[5:8])
+        if tt:   # the steptime build records the traversal regions on their own
             print("  closest-hit traversal: node walk %.1f%%, leaf tests %.1f%%, interaction %.1f%%" % tuple(
                 v / tt * 100 for v in sc_[5:8]))
         for k in names[6:13]:
