@@ -5,84 +5,146 @@
 
 namespace pbrtk {
 
-// One thread per tile-film pixel: the tile film of the serial replay, the
-// film pixel's sum in the reference's order (its source pixels row-major, each
-// pixel's samples in order, film.go:211-248 / integrator.go:256-262). The lane
-// whose film pixel is a tile pixel also adds up that pixel's reference ray
-// counts (pbrt_gpu_stats.rays_*), so the counts need no pass of their own.
-// (One workgroup per tile, to keep a source pixel's four readers on one CU,
-// measured slower: 5.3 vs 3.6 ms on config B.)
+// One workgroup per tile slot: the tile film of the serial replay
+// (FilmTile.AddSample, film.go:211-248; integrator.go:256-262). Each film
+// pixel's value is the sum, in the reference's order, of its source pixels
+// (row-major) and of each source's samples (in order): one sequential chain
+// per film pixel and channel, which no reassociation may shorten.
+//
+// The tile's source pixels stream through LDS in row-major runs of S pixels
+// (S x (spp - 1) samples of L, S = the run that fits kFilmStageBytes: a whole
+// 16-px row at 64 spp, one pixel at 1024 spp), each run read from HBM once,
+// with contiguous loads (pixel-major L). A film pixel's thread adds the run's
+// sources whose footprint holds it, in order; since every film pixel sees its
+// sources in the global row-major order, every chain keeps the reference's
+// order for any filter radius (< tile size; footprints of up to
+// (2 floor(r + 0.5))^2 film pixels, the reference's BoxFilter of radius 1.5
+// included). The footprint test and weight are film.go's own arithmetic
+// (render_common.h footprint()). The running sums live in LDS, one per film
+// pixel and channel. The workgroup also adds up its pixels' reference ray
+// counts (pbrt_gpu_stats.rays_*).
+__device__ __forceinline__ bool film_weight(const pbrt_film_desc& f, int64_t sx, int64_t sy, int64_t fx, int64_t fy,
+                                            double& w) {
+    // film.go:216-246 with pFilm = the source pixel's corner (2D stratified values are (0,0), #3);
+    // the tile-film clip [px0, px1) holds for every film pixel of the slot
+    const double dx = (double)sx + 0.0 - 0.5, dy = (double)sy + 0.0 - 0.5;
+    const double p0x = gomath::ceil(dx - f.filter_radius_x), p0y = gomath::ceil(dy - f.filter_radius_y);
+    const double p1x = gomath::floor(dx + f.filter_radius_x) + 1, p1y = gomath::floor(dy + f.filter_radius_y) + 1;
+    if (!((double)fx >= p0x && (double)fx < p1x && (double)fy >= p0y && (double)fy < p1y)) return false;
+    const double ifx = 1.0 / f.filter_radius_x, ify = 1.0 / f.filter_radius_y;
+    const int iy = (int)gomath::to_int(gomath::min(gomath::floor(gomath::abs(((double)fy - dy) * ify * 16.0)), 16.0 - 1));
+    const int ix = (int)gomath::to_int(gomath::min(gomath::floor(gomath::abs(((double)fx - dx) * ifx * 16.0)), 16.0 - 1));
+    w = 1.0 * f.filter_table[iy * 16 + ix];
+    return true;
+}
+
 __global__ __launch_bounds__(kFilmThreads) void k_film(const pbrt_film_desc* __restrict__ film_desc, RenderParams rp,
                                                        WaveBufs wb, int64_t slot_base, int64_t nslots_batch,
                                                        double* __restrict__ films, const int* __restrict__ cancel_seen,
                                                        Counters* __restrict__ ctr) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    __shared__ int nvs[kFilmThreads];   // nvalid of the run's pixels (0: no record)
     // a cancelled render's samples are incomplete: its film is not valid (pbrt_gpu_cancel)
     if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(cancel_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
         return;
-    const int64_t per = rp.slot_w * rp.slot_h;
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t bslot = blockIdx.x;
+    if (bslot >= nslots_batch) return;
+    const int tid = threadIdx.x;
+    const pbrt_film_desc& film = *film_desc;
+    const int64_t slot = slot_base + bslot;
+    int64_t x0, y0, x1, y1, px0, py0, px1, py1;
+    tile_bounds(rp, tile_of_slot(rp, slot), x0, y0, x1, y1);
+    film_tile_bounds(film, x0, y0, x1, y1, px0, py0, px1, py1);
+    const int tw = (int)(px1 - px0), nfp = (int)(tw * (py1 - py0));
+    const int sw = (int)(x1 - x0);
+    const int n = rp.spp, m = n - 1;   // traced samples 1 .. n-1
+    const int npx = wb.tile_npx[bslot];
+    const int S = film_run_pixels(rp);
+    // a source pixel reaches film pixels within (int)r + 2 of it (footprint: |f - s| < r + 1.5)
+    const int rx = (int)film.filter_radius_x + 2, ry = (int)film.filter_radius_y + 2;
+    // LDS: running sums [nfp][3], then the staged run [S][m][3]
+    double* acc = (double*)lds;
+    double* stg = acc + ((nfp * 3 + 1) & ~1);
+    for (int i = tid; i < nfp * 3; i += kFilmThreads) acc[i] = 0.0;
+    const int64_t rec0 = bslot * wb.ppt;
     unsigned long long cl = 0, sh = 0;
-    if (gid < nslots_batch * per) {
-        const int64_t bslot = gid / per, fi = gid % per;
-        const int64_t slot = slot_base + bslot;
-        const pbrt_film_desc& film = *film_desc;
-        int64_t x0, y0, x1, y1, px0, py0, px1, py1;
-        tile_bounds(rp, tile_of_slot(rp, slot), x0, y0, x1, y1);
-        film_tile_bounds(film, x0, y0, x1, y1, px0, py0, px1, py1);
-        const int64_t tw = px1 - px0;
-        if (fi < tw * (py1 - py0)) {
+    for (int s0 = 0; s0 < npx && m > 0; s0 += S) {
+        const int ns = min(S, npx - s0);
+        __syncthreads();   // the previous run is consumed
+        if (tid < ns) nvs[tid] = wb.prec[rec0 + s0 + tid].nvalid;
+        __syncthreads();
+        // stage the run's samples 1 .. nvalid-1: one contiguous stretch of L but
+        // for each pixel's sample 0 (pixel-major); the ray counts on the way
+        const double* Lrun = wb.L + (rec0 + s0) * (int64_t)n * 3;
+        for (int i = tid; i < ns * m * 3; i += kFilmThreads) {
+            const int s = i / (m * 3), j = i - s * (m * 3);
+            if (j / 3 < nvs[s] - 1) stg[i] = Lrun[(int64_t)s * n * 3 + 3 + j];
+        }
+        for (int i = tid; i < ns * m; i += kFilmThreads) {
+            const int s = i / m, k = i - s * m;
+            if (k < nvs[s] - 1) {
+                const uint32_t v = wb.rays[(rec0 + s0 + s) * n + 1 + k];
+                cl += v & 0xFFFFu;
+                sh += v >> 16;
+            }
+        }
+        __syncthreads();
+        // NaN guard and luminance clamp per sample (integrator.go:256-262)
+        for (int i = tid; i < ns * m; i += kFilmThreads) {
+            const int s = i / m, k = i - s * m;
+            if (k >= nvs[s] - 1) continue;
+            double* d = stg + (int64_t)i * 3;
+            Spec Ls{d[0], d[1], d[2]};
+            const bool nan = has_nans(Ls);
+            if (nan) Ls = spec(0.1);
+            if (0.0 > film.max_sample_luminance) Ls = smuls(Ls, film.max_sample_luminance / 0.0);
+            if (nan || 0.0 > film.max_sample_luminance) {
+                d[0] = Ls.r;
+                d[1] = Ls.g;
+                d[2] = Ls.b;
+            }
+        }
+        __syncthreads();
+        // every film pixel adds the run's sources that reach it, in order
+        for (int fi = tid; fi < nfp; fi += kFilmThreads) {
             const int64_t fx = px0 + fi % tw, fy = py0 + fi / tw;
-            const int n = rp.spp;
-            const int64_t npx = wb.tile_npx[bslot];
-            double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-            // pixels whose footprint can reach (fx, fy): |p - f| < radius + 1, in row-major order
-            for (int64_t py = fy - 2; py <= fy + 2; py++) {
-                if (py < y0 || py >= y1) continue;
-                for (int64_t px = fx - 2; px <= fx + 2; px++) {
-                    if (px < x0 || px >= x1) continue;
-                    const int64_t pi = (py - y0) * (x1 - x0) + (px - x0);
-                    if (pi >= npx) continue;
-                    const int64_t rec = bslot * wb.ppt + pi;
-                    const int nv = wb.prec[rec].nvalid;
-                    if (px == fx && py == fy) {   // this lane counts the pixel's rays
-                        for (int k = 1; k < nv; k++) {
-                            const uint32_t v = wb.rays[sample_index(wb, rec, n, k)];
-                            cl += v & 0xFFFFu;
-                            sh += v >> 16;
-                        }
-                    }
-                    Footprint fp;
-                    int64_t p0x, p0y, p1x, p1y;
-                    footprint(film, (double)px + 0.0, (double)py + 0.0, px0, py0, px1, py1, fp, p0x, p0y, p1x, p1y);
-                    const int64_t want = fi;
-                    int f = -1;
-                    for (int q = 0; q < fp.n; q++)
-                        if (fp.off[q] == want) f = q;
-                    if (f < 0) continue;
-                    const double w = fp.w[f];
-                    const double* Lp = wb.L + sample_index(wb, rec, n, 0) * 3;
-                    const int64_t kst = wb.ppt * 3;   // one sample to the next, same pixel
-                    for (int k = 1; k < nv; k++) {
-                        Spec Ls{Lp[k * kst + 0], Lp[k * kst + 1], Lp[k * kst + 2]};
-                        if (has_nans(Ls)) Ls = spec(0.1);   // integrator.go:256-262
-                        if (0.0 > film.max_sample_luminance) Ls = smuls(Ls, film.max_sample_luminance / 0.0);
-                        a0 += Ls.r * w;
-                        a1 += Ls.g * w;
-                        a2 += Ls.b * w;
-                    }
+            double a0 = 0, a1 = 0, a2 = 0;
+            bool any = false;
+            for (int s = 0; s < ns; s++) {
+                const int pi = s0 + s;
+                const int64_t sx = x0 + pi % sw, sy = y0 + pi / sw;
+                if (sx - fx > rx || fx - sx > rx || sy - fy > ry || fy - sy > ry) continue;
+                double w;
+                if (!film_weight(film, sx, sy, fx, fy, w)) continue;
+                if (!any) {
+                    a0 = acc[fi * 3 + 0];
+                    a1 = acc[fi * 3 + 1];
+                    a2 = acc[fi * 3 + 2];
+                    any = true;
+                }
+                const int nk = nvs[s] - 1;
+                const double* d = stg + (int64_t)s * m * 3;
+                for (int k = 0; k < nk; k++) {
+                    a0 += d[k * 3 + 0] * w;
+                    a1 += d[k * 3 + 1] * w;
+                    a2 += d[k * 3 + 2] * w;
                 }
             }
-            double* tf = films + slot * per * 3 + fi * 3;
-            tf[0] = a0;
-            tf[1] = a1;
-            tf[2] = a2;
+            if (any) {
+                acc[fi * 3 + 0] = a0;
+                acc[fi * 3 + 1] = a1;
+                acc[fi * 3 + 2] = a2;
+            }
         }
     }
+    __syncthreads();
+    double* tf = films + slot * rp.slot_w * rp.slot_h * 3;
+    for (int i = tid; i < nfp * 3; i += kFilmThreads) tf[i] = acc[i];
     for (int off = kWave / 2; off > 0; off >>= 1) {
         cl += __shfl_down(cl, off);
         sh += __shfl_down(sh, off);
     }
-    if ((threadIdx.x & (kWave - 1)) == 0 && (cl | sh)) {
+    if ((tid & (kWave - 1)) == 0 && (cl | sh)) {
         atomicAdd(&ctr->closest_rays, cl);
         atomicAdd(&ctr->shadow_rays, sh);
     }
@@ -447,8 +509,7 @@ __global__ __launch_bounds__(kWave) void k_tile_cost(DevScene sc, RenderParams r
         c.rng.state = mb_state((uint64_t)tile, (uint64_t)pi, 0x70726f6265ULL + (uint64_t)(it % kProbes));
         c.rng.inc = inc;
         c.draws = 0;
-        c.cur1d = 1;
-        c.cur2d = 2;
+        c_camera(c, rp.ndims);
         c.k = -1;
         c.kdep = 0;
         Spec beta = spec(1);

@@ -31,8 +31,12 @@ __global__ __launch_bounds__(kWave) void k_pw_start(DevScene sc, RenderParams rp
                                                     int64_t rec0, int64_t nrec, const Spec* __restrict__ ldc,
                                                     const int* __restrict__ ldp, PwPath* __restrict__ paths,
                                                     PwQueues qs, unsigned long long* __restrict__ pkey) {
+    // bounce 1's shadow ray is traced here when its light sample is not the
+    // pixel's cached one (n_dims < 3, path_step): trees beyond LDS need the stack
+    __shared__ uint16_t stack_lds[64 * kStackStride];
     const int n = rp.spp;
     if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;
+    stage_nodes(sc);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (n < 2 || i >= nrec * (n - 1)) return;
     const int64_t r = i / (n - 1);
@@ -59,8 +63,7 @@ __global__ __launch_bounds__(kWave) void k_pw_start(DevScene sc, RenderParams rp
     c.rng.state = kMB ? mb_state(tile, (uint64_t)pi, (uint64_t)k) : wb.memb[rec * n + k];
     c.rng.inc = pcg_inc_of(tile);
     c.draws = 0;
-    c.cur1d = 1;   // camera: Get2D pFilm, Get2D pLens, Get1D time (stratified)
-    c.cur2d = 2;
+    c_camera(c, rp.ndims);   // camera: Get2D pFilm, Get2D pLens, Get1D time
     c.k = k;
     c.kdep = 0;
     PathState s;
@@ -73,7 +76,7 @@ __global__ __launch_bounds__(kWave) void k_pw_start(DevScene sc, RenderParams rp
     const PwCache pc{pr.si, pr.b, pr.x, pr.wo, ldc + r * sc.n_lights, ldp + r * sc.n_lights};
     const SpecSampler ss{wb.s1d + rec * wb.s1d_stride, n, rp.ndims};
     int pnc = 0, bnc = 1;
-    bool done = path_step<1, kX>(sc, pc, ss, c, s, rp.max_depth, rp.rr_threshold, nullptr, pnc, bnc);
+    bool done = path_step<1, kX>(sc, pc, ss, c, s, rp.max_depth, rp.rr_threshold, stack_lds + threadIdx.x, pnc, bnc);
     p.L = s.L;
     p.beta = s.beta;
     p.eta = s.eta_scale;

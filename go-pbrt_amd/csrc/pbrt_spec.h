@@ -107,6 +107,40 @@ __device__ __forceinline__ V2 c_get2d(Cursor& c, const SpecSampler& s) {
     return V2{x, y};
 }
 
+// a 2D value whose only effect is on radiance, or none at all: consume it
+__device__ __forceinline__ void c_skip2d(Cursor& c, int ndims) {
+    if (c.cur2d < ndims) {
+        c.cur2d++;
+        return;
+    }
+    c.draws += 2;
+    pcg_next(c.rng);
+    pcg_next(c.rng);
+}
+// A sample's CameraSample (sampler.go:75-80 GetCameraSample: pFilm = pixel +
+// Get2D, pLens = Get2D, time = Get1D), from a fresh cursor: stratified while
+// the dimension is below n_dims (pixel.go:60-80), PCG32 draws beyond. The wave
+// pipeline runs only where the camera ray is the pixel's own (pFilm
+// stratified: n_dims >= 1; pLens stratified or a pinhole), so only the draws
+// count here: n_dims = 1 draws pLens (2), n_dims >= 2 draws nothing.
+__device__ __forceinline__ void c_camera(Cursor& c, int ndims) {
+    c.cur1d = c.cur2d = 0;
+    c_skip2d(c, ndims);   // pFilm
+    c_skip2d(c, ndims);   // pLens
+    if (c.cur1d < ndims) {   // time
+        c.cur1d++;
+    } else {
+        c.draws++;
+        pcg_next(c.rng);
+    }
+}
+
+// PCG32 draws of a CameraSample (c_camera): 2 for pFilm and for pLens, 1 for
+// time, each beyond the sampled dims
+__host__ __device__ __forceinline__ uint32_t camera_draws(int ndims) {
+    return (ndims < 1 ? 2u : 0u) + (ndims < 2 ? 2u : 0u) + (ndims < 1 ? 1u : 0u);
+}
+
 constexpr int kMaxCachedLights = 16;
 // a cached bounce-1 light estimate traced its visibility ray (ray counters;
 // or-ed into the estimate's panic word, whose low 16 bits are the panic kind)
@@ -234,9 +268,13 @@ __device__ __forceinline__ bool path_step(const DevScene& sc, const Cache& pc, c
             } else {
                 ln = (int)gomath::to_int(gomath::min(c_get1d(c, ss) * (double)nl, (double)(nl - 1)));
             }
+            // bounce 1's light sample is the pixel's cached estimate where uLight is
+            // the stratified (0,0) (n_dims >= 3); with fewer sampled dims it is a
+            // PCG32 draw per sample, estimated here like any later bounce's
+            const bool ul_strat = c.cur2d < ss.ndims;
             V2 ul = c_get2d(c, ss);
             c_get2d(c, ss);
-            if (first) {
+            if (first && ul_strat) {
                 const Spec ld = pc.ld[ln];
                 const int lp = pc.ld_panic[ln];
                 if (lp & kLdTraced) add_rays(s, kRayShadow);

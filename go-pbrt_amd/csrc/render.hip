@@ -65,6 +65,7 @@ struct Knobs {
     int cull_group = 4;        // PBRT_CULL_GROUP: leaves per culling group
     int cull_min = 2;          // PBRT_CULL_MIN
     bool cull_groups = true;   // PBRT_CULL_GROUPS=0
+    bool ci_succ = true;       // PBRT_CI_SUCC=0: no successor speculation in multi-wave k_chain_ci tiles
     static Knobs from_env() {
         Knobs k;
         auto ival = [](const char* n, int& out) { if (const char* e = getenv(n)) out = atoi(e); };
@@ -79,6 +80,7 @@ struct Knobs {
         if (const char* e = getenv("PBRT_CI_HEAVY_WAVES")) k.ci_heavy_waves = atoi(e) == 8 ? 8 : 4;
         if (const char* e = getenv("PBRT_CI_HEAVY")) k.ci_heavy = (int64_t)atoll(e);
         if (const char* e = getenv("PBRT_CI_SPLIT")) k.ci_split = atoi(e) != 0;
+        if (const char* e = getenv("PBRT_CI_SUCC")) k.ci_succ = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_DENSE")) k.ci_dense = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_ORDER")) k.ci_order = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_PROBE")) k.ci_probe = atoi(e) != 0;
@@ -519,8 +521,12 @@ bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Rend
         return false;
     if (dl) {   // k_dl_*: the camera ray must be per pixel (pFilm stratified; pLens stratified or unused)
         if (rd->n_dims < 1 || (rd->n_dims < 2 && c->host_scene.camera.lens_radius > 0)) return false;
-    } else if (rd->integrator != PBRT_INTEGRATOR_PATH || rd->n_dims < 3 || rd->max_depth > 2048) {
+    } else if (rd->integrator != PBRT_INTEGRATOR_PATH || rd->max_depth > 2048) {
         return false;   // D < 2^32
+    } else if (rd->n_dims < 2 && !(rd->n_dims == 1 && c->host_scene.camera.lens_radius == 0)) {
+        // the camera ray must be the pixel's (k_wf_primary): pFilm stratified
+        // (n_dims >= 1), and pLens stratified (n_dims >= 2) or unused (a pinhole)
+        return false;
     }
     const int nl = c->host_scene.n_lights;
     if (!dl && nl > kMaxCachedLights) return false;
@@ -530,8 +536,9 @@ bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Rend
         for (int i = 0; i < d.count; i++)
             if (!(d.func[i] > 0)) return false;   // a zero-pdf light changes the draw count
     }
-    const pbrt_film_desc& f = c->host_scene.film;
-    if (!(f.filter_radius_x < 1.5 && f.filter_radius_y < 1.5)) return false;   // <= 2x2 pixel footprint
+    // k_film stages the tile film's running sums and a run of source pixels in LDS
+    // (any filter radius below the tile size: footprints beyond 2x2 included)
+    if ((size_t)film_lds_bytes(rp) > c->lds_per_block) return false;
     const int64_t n = rp.spp, nd = rp.ndims;
     if (n > 4096 || nd * n > 8192) return false;
     int64_t off = 0;
@@ -540,6 +547,7 @@ bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Rend
         off += (bytes + 15) & ~int64_t(15);
         return (int)o;
     };
+    L.succ = Lci.succ = 0;
     L.s1d = put(nd * n * 8);
     L.other = put(nd * n * 2);
     L.sbuf = put(kWave * 8);
@@ -580,9 +588,17 @@ bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Rend
 // tile per workgroup (G == 1) the StartPixel staging aliases the offset ring:
 // a group starts a pixel only after its chain has dropped every candidate,
 // so the two are never live together (config C, 256 spp: 19 KB of staging).
-ChainLayout ci_layout(const ChainLayout& base, int w, int G, unsigned& lds_bytes) {
+// succ: successor speculation (k_chain_ci, multi-wave tiles): two rings after
+// the staging (a successor's StartPixel runs while the current pixel's ring is
+// live) and two ChainCache records.
+ChainLayout ci_layout(const ChainLayout& base, int w, int G, unsigned& lds_bytes, bool succ = false) {
     ChainLayout l = base;
-    if (G == 1) {
+    l.succ = 0;
+    if (succ && G == 1) {
+        l.ring = (base.staging + 15) & ~15;
+        lds_bytes = (unsigned)(l.ring + 2 * w * kCiRingBytes);
+        l.succ = 1;
+    } else if (G == 1) {
         l.ring = 0;
         lds_bytes = (unsigned)std::max(base.staging, w * kCiRingBytes);
     } else {
@@ -590,7 +606,7 @@ ChainLayout ci_layout(const ChainLayout& base, int w, int G, unsigned& lds_bytes
     }
     // then one ChainCache per lane group (only the groups in use: G, not kCiMaxGroups)
     l.pcs = (int)((lds_bytes + 15u) & ~15u);
-    lds_bytes = (unsigned)l.pcs + (unsigned)(G * sizeof(ChainCache));
+    lds_bytes = (unsigned)l.pcs + (unsigned)((l.succ ? 2 : G) * sizeof(ChainCache));
     l.total = (int)lds_bytes;
     return l;
 }
@@ -1090,7 +1106,6 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
             const bool lds_nodes = c->host_scene.n_nodes <= kLdsNodes;
             const bool kx = c->non_matte;   // Mirror / smooth Glass / OrenNayar: the kX instantiations
             const bool mesh_only = mesh_only_scene(c);   // triangle meshes and nothing else: no analytic walk
-            const int64_t per = rp.slot_w * rp.slot_h;
             c->n_batches = (int)((rp.n_slots + c->wave_batch - 1) / c->wave_batch);
             while ((int)c->bev.size() < 3 * c->n_batches) {
                 hipEvent_t e;
@@ -1171,7 +1186,12 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                         if (w > 1) {   // one tile per workgroup of w waves; the ring grows with the lanes
                             const int ring = w * kCiRingBytes / (int)sizeof(RingEnt);
                             unsigned lds = 0;
-                            const ChainLayout lw = ci_layout(c->lay_ci, w, 1, lds);
+                            // successor speculation: 2- and 4-wave Matte tiles of LDS-staged or
+                            // stack-walked analytic trees, candidate stride 1
+                            const bool succ = c->knobs.ci_succ && !kx && !mesh_only && (w == 2 || w == 4) &&
+                                              ci_stride(c, w) == 1;
+                            ChainLayout lw = ci_layout(c->lay_ci, w, 1, lds, succ);
+                            if (lds > c->lds_per_block) lw = ci_layout(c->lay_ci, w, 1, lds, false);
                             // kX: LDS-staged trees only, at most 4 waves per tile (wave_eligible, ci_waves)
                             auto kern = kx ? (w == 2 ? k_chain_ci<2, 0, true> : k_chain_ci<4, 0, true>)
                                         : mesh_only ? (w == 2 ? k_chain_ci<2, -1> : w == 4 ? k_chain_ci<4, -1> : k_chain_ci<8, -1>)
@@ -1289,7 +1309,7 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                                        c->d_ctr, sl);
                 }
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 2], c->stream));
-                hipLaunchKernelGGL(k_film, dim3((unsigned)((nb * per + kFilmThreads - 1) / kFilmThreads)), dim3(kFilmThreads), 0, c->stream,
+                hipLaunchKernelGGL(k_film, dim3((unsigned)nb), dim3(kFilmThreads), (unsigned)film_lds_bytes(rp), c->stream,
                                    c->d_film, rp, c->wb, sb, nb, c->d_films, c->d_cancel_seen, c->d_ctr);
                 hipLaunchKernelGGL(k_panic_reduce, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, c->stream, c->wb,
                                    sb, nb, c->d_panics, c->d_ctr);

@@ -169,25 +169,42 @@ struct WaveBufs {
     int64_t ppt;        // pixel records per tile slot (tile_size^2)
     int64_t s1d_stride; // ndims * spp
 };
-// Per-sample outputs (wb.L, wb.rays) are sample-major within a tile slot:
-// [slot][k][pixel], so that k_film's lanes (consecutive film pixels) read
-// consecutive pixels of one sample -- coalesced -- while each lane still
-// walks its source pixels' samples in the reference's order.
+// Per-sample outputs (wb.L, wb.rays) are pixel-major: [slot][pixel][k]. A
+// pixel's samples are one contiguous run (63 x 24 B of L at 64 spp), so the
+// path stage's lanes, which hold samples of the same few pixels, write into a
+// few KB that the L2 fills whole before write-back, and k_film stages a run of
+// source pixels into LDS with contiguous loads.
 __device__ __forceinline__ int64_t sample_index(const WaveBufs& wb, int64_t rec, int n, int k) {
-    const int64_t bslot = rec / wb.ppt, pi = rec - bslot * wb.ppt;
-    return (bslot * n + k) * wb.ppt + pi;
+    (void)wb;
+    return rec * n + k;
+}
+constexpr int kFilmThreads = 256;           // k_film workgroup (one per tile slot)
+constexpr int kFilmStageBytes = 24 * 1024;  // k_film: LDS staging of a run of source pixels' L
+// k_film: source pixels per staged run (a row of a 16-px tile at 64 spp, one
+// pixel at 1024), and its dynamic LDS: running sums [slot_w x slot_h][3],
+// then the run [S][spp - 1][3]
+__host__ __device__ inline int film_run_pixels(const RenderParams& rp) {
+    const int64_t m = rp.spp - 1, npx = rp.tile_size * rp.tile_size;
+    int64_t S = m > 0 ? kFilmStageBytes / (m * 24) : 1;
+    if (S > npx) S = npx;
+    if (S > kFilmThreads) S = kFilmThreads;
+    return S < 1 ? 1 : (int)S;
+}
+__host__ __device__ inline int film_lds_bytes(const RenderParams& rp) {
+    const int64_t nfp = rp.slot_w * rp.slot_h, m = rp.spp - 1;
+    return (int)(((nfp * 3 + 1) & ~int64_t(1)) * 8 + (int64_t)film_run_pixels(rp) * (m > 0 ? m : 1) * 24);
 }
 struct ChainLayout {   // byte offsets into the chain / setup kernels' dynamic LDS block
     int s1d, other, sbuf, dbuf, vbuf, total;
     int ring;      // k_chain_ci: offset ring after the StartPixel staging (no sbuf / dbuf)
     int staging;   // k_chain_ci: bytes of the StartPixel staging (s1d, other, vbuf)
     int pcs;       // k_chain_ci: the lane groups' bounce-1 ChainCache records (ci_layout)
+    int succ;      // k_chain_ci: successor speculation (two rings, two ChainCaches, no aliasing)
 };
 #ifndef PBRT_CI_RING_KB
 #define PBRT_CI_RING_KB 4
 #endif
 constexpr int kCiRingBytes = PBRT_CI_RING_KB * 1024;   // k_chain_ci offset ring (all lane groups of a wave)
-constexpr int kFilmThreads = 256;        // k_film workgroup (one thread per tile-film pixel)
 constexpr int kCiMaxGroups = 4;          // k_chain_ci lane groups (tiles) per wave
 constexpr int kCiMaxRing = 4 * kCiRingBytes / 16;   // ring entries of a tile at the most waves of a kX tile (4)
 // k_chain_ci ring entry D with recorded RR decisions (RrBranches at the entry):
@@ -447,8 +464,7 @@ __device__ __forceinline__ void paths_group(const DevScene& sc, const RenderPara
                                       : wb.memb[rec * n + k];
                     c.rng.inc = meta[j].inc;
                     c.draws = 0;
-                    c.cur1d = 1;   // camera: Get2D pFilm, Get2D pLens, Get1D time (stratified)
-                    c.cur2d = 2;
+                    c_camera(c, ndims);   // camera: Get2D pFilm, Get2D pLens, Get1D time
                     c.k = k;
                     c.kdep = 0;
                     *ps.L = spec(0);
@@ -733,5 +749,17 @@ struct CiGroup {
     int reissue;    // the head must be re-run with its sample index known
     int pad;
 };
+// k_chain_ci successor speculation (multi-wave tiles): the next pixel's chain
+// started from a guessed end bE of the current one, on the other ring
+struct CiSucc {
+    uint64_t bS;       // the successor's PCG32 state at its offset 0
+    uint32_t bE;       // the guessed end offset of the current pixel (relative to S)
+    uint32_t bnxt;     // the successor's next offset to issue
+    uint32_t gen[2];   // generation of each ring: a lane's trajectory is live while its ring's matches
+    int cur;           // ring (and ChainCache) of the current pixel: 0 / 1
+    int bstate;        // 0 none, 1 its StartPixel is due, 2 running
+};
+constexpr uint32_t kInflight = 0x80000000u;   // RingEnt tag of an offset still traced (d: its draws so far)
+constexpr int kSuccGuesses = 2;   // unresolved chain entries a successor guess may assume
 
 }  // namespace pbrtk

@@ -73,11 +73,11 @@ def test_cancel_throughput_mode_paths():
 
 
 def test_cancel_serial_kernel():
-    """Stratified with n_dims = 2 (< 3: the bounce-1 light sample is not per
-    pixel) renders on the serial kernel (one lane per tile), whose pixels poll
+    """Stratified with n_dims = 0 (pFilm from the RNG: the camera ray is per
+    sample) renders on the serial kernel (one lane per tile), whose pixels poll
     the flag by wall clock."""
     sc = G.Scene.readme(1920, 1080)
-    check_cancel_then_render(sc, abi.render_desc(8, 8, n_dims=2), abi.render_desc(2, 2, n_dims=2, tile_end=32),
+    check_cancel_then_render(sc, abi.render_desc(8, 8, n_dims=0), abi.render_desc(2, 2, n_dims=0, tile_end=32),
                              abi.PBRT_KERNEL_SERIAL, delay=0.3)
 
 

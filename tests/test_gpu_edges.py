@@ -129,13 +129,13 @@ def test_disk_inner_radius_and_phi_max(integ):
     assert of.max() > 0
 
 
-@pytest.mark.parametrize("n_dims", [4, 0])
+@pytest.mark.parametrize("n_dims", [4, 2, 1, 0])
 def test_thin_lens_camera(n_dims):
     """lensRadius > 0: with stratified dims pLens = (0, 0) maps to a fixed lens
-    point (ConcentricSampleDisk(0, 0) = -(cos, sin)(pi/4)); with n_dims 0 every
-    sample draws its own lens point from the RNG (serial kernel only)."""
+    point (ConcentricSampleDisk(0, 0) = -(cos, sin)(pi/4)); with n_dims 0 or 1
+    every sample draws its own lens point from the RNG (serial kernel only)."""
     sc = edge_scene(lens=0.4, focal=12.0)
-    auto = PATH_AUTO if n_dims >= 3 else abi.PBRT_KERNEL_SERIAL
+    auto = PATH_AUTO if n_dims >= 2 else abi.PBRT_KERNEL_SERIAL
     of = check(sc, abi.render_desc(3, 3, n_dims=n_dims, **PATH_RD), auto)
     pin = edge_scene()
     _, pf, _ = O.render(pin.desc, abi.render_desc(3, 3, n_dims=n_dims, **PATH_RD), threads=8)
@@ -165,16 +165,15 @@ def test_crop_and_screen_window(crop, screen):
         assert of.shape == (H, W, 3)
 
 
-@pytest.mark.parametrize("radius", [0.5, 1.5, 2.0])
+@pytest.mark.parametrize("radius", [0.5, 1.3, 1.5, 2.0, 2.7])
 def test_filter_radius(radius):
-    """BoxFilter radius r: a sample at the pixel corner covers ceil-ed footprints
-    of 1 (r 0.5), 9 (1.5) or 16 (2) pixels; the tile films' aprons grow with r.
-    The wave kernels handle footprints of at most 2x2 pixels (r < 1.5)."""
+    """BoxFilter radius r: a sample at the pixel corner covers a footprint of
+    2x2 (r < 1.5), 4x4 (1.5 <= r < 2.5) or 6x6 film pixels; the tile films'
+    aprons grow with r. k_film runs every radius below the tile size."""
     sc = edge_scene(filter_radius=radius)
-    auto_p = PATH_AUTO if radius < 1.5 else abi.PBRT_KERNEL_SERIAL
-    auto_d = DL_AUTO if radius < 1.5 else abi.PBRT_KERNEL_SERIAL
-    check(sc, abi.render_desc(2, 2, **PATH_RD), auto_p)
-    check(sc, abi.render_desc(2, 2, **DL_RD), auto_d)
+    check(sc, abi.render_desc(2, 2, **PATH_RD), PATH_AUTO)
+    check(sc, abi.render_desc(2, 2, **DL_RD), DL_AUTO)
+    check(sc, abi.render_desc(3, 2, n_dims=2, **PATH_RD), PATH_AUTO)
 
 
 def test_two_sided_area_light():

@@ -46,7 +46,9 @@ def gpu_render(scene, rd, lanes_per_wave=0, kernel="auto"):
 
 
 def wave_eligible(rd):
-    return (rd.integrator == abi.PBRT_INTEGRATOR_PATH and rd.n_dims >= 3
+    """Path renders whose camera ray is the pixel's (pFilm stratified: n_dims
+    >= 1; the scenes here are pinholes, so pLens may be a draw)."""
+    return (rd.integrator == abi.PBRT_INTEGRATOR_PATH and rd.n_dims >= 1
             and rd.light_strategy == abi.PBRT_LIGHT_STRATEGY_UNIFORM)
 
 
@@ -368,6 +370,8 @@ WAVE_VARIANTS = [
     dict(spp_x=4, spp_y=4, max_depth=3),
     dict(spp_x=4, spp_y=4, max_depth=12, rr_threshold=0.0),
     dict(spp_x=4, spp_y=4, max_depth=2),
+    dict(spp_x=8, spp_y=8, n_dims=2),            # bounce-1 light sample from the RNG (per sample)
+    dict(spp_x=6, spp_y=5, n_dims=1, jitter=True),   # pLens from the RNG too (a pinhole: same ray)
 ]
 
 
@@ -547,7 +551,7 @@ def test_wave_ci_panic_is_reported_like_the_oracle(ci_waves, monkeypatch):
 def test_wave_kernel_rejects_ineligible_render():
     with G.Renderer(G.Scene.readme(16, 16), kernel="wave") as r:
         with pytest.raises(G.PbrtError) as ei:
-            r.render(abi.render_desc(2, 2, n_dims=2))
+            r.render(abi.render_desc(2, 2, n_dims=0))
     assert ei.value.code == abi.PBRT_E_UNSUPPORTED
 
 
@@ -689,7 +693,7 @@ def test_throughput_mode_bitexact_vs_oracle(case, kernel):
     check(scene, abi.render_desc(**kw, mode=MB), kernel=kernel)
 
 
-@pytest.mark.parametrize("kw", [dict(n_dims=1), dict(integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING, n_dims=0),
+@pytest.mark.parametrize("kw", [dict(n_dims=0), dict(integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING, n_dims=0),
                                 dict(light_strategy=abi.PBRT_LIGHT_STRATEGY_POWER)])
 def test_throughput_mode_serial_fallback(kw):
     """Renders the wave path cannot take run Mode B on the serial kernel."""

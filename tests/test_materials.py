@@ -25,10 +25,10 @@ Quirks restated (and therefore tested here):
   own quirks (D's alphaX*alphaY, MicrofacetTransmission.F's inverted hemisphere
   test, its unset TransportMode) are restated.
 
-Path renders of these scenes (smooth glass, mirror, OrenNayar; n_dims >= 3)
+Path renders of these scenes (smooth glass, mirror, OrenNayar; n_dims >= 1)
 run on the wave pipeline's kX instantiations (k_wf_primary / k_chain_ci /
 k_paths_ci / k_mb_setup over BSDFX, with Path.Li's etaScale); everything else
-(n_dims < 3, DirectLighting's specular recursion, rough glass) on the serial
+(n_dims 0, DirectLighting's specular recursion, rough glass) on the serial
 kernel. Both are checked bit for bit against the oracle.
 
 No reference test covers these materials and there is no Go toolchain here:
@@ -158,8 +158,9 @@ def test_material_desc_layout():
 
 # ------------------------------------------------------------------ GPU tests
 def path_kernel(nd, mode):
-    """The kernel a Path render of a Mirror/Glass/OrenNayar scene runs on."""
-    if nd < 3:
+    """The kernel a Path render of a Mirror/Glass/OrenNayar scene runs on (a
+    pinhole camera: n_dims >= 1 keeps the camera ray the pixel's)."""
+    if nd < 1:
         return abi.PBRT_KERNEL_SERIAL
     return abi.PBRT_KERNEL_WAVE_CI if mode == abi.PBRT_MODE_EXACT else abi.PBRT_KERNEL_WAVE
 
