@@ -25,9 +25,6 @@ __device__ __forceinline__ uint32_t ring_d(const Cursor& c, const SpecSampler& s
     return kRrFlag | (d == kBadSpecD ? kRrTailBad : d);
 }
 
-#ifndef PBRT_CI_SUCC
-#define PBRT_CI_SUCC 0   // build option: successor speculation in 2- and 4-wave Matte tiles
-#endif
 template <int kW, int kDepth, bool kX, int kEu>
 // kDepth < 0 (kCiMeshOnly): scenes of triangle meshes only, no analytic walk
 // compiled in (149 VGPRs), built for 3 waves per SIMD; Matte analytic scenes
@@ -50,7 +47,6 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
     __shared__ __attribute__((aligned(16))) unsigned char dense_lds[kDepth > 0 ? 16 : kW * kDenseScratch];
 #endif
     __shared__ CiGroup gs[kCiMaxGroups];
-    __shared__ CiSucc gsx;   // successor speculation state (one group per workgroup)
     __shared__ uint64_t sh_state;
     __shared__ int wcnt[kW];
 #ifdef PBRT_CI_DIAG
@@ -70,17 +66,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
     double* s1d = lay.s1d >= 0 ? (double*)(lds + lay.s1d) : nullptr;
     uint16_t* other = (uint16_t*)(lds + lay.other);
     uint32_t* vbuf = (uint32_t*)(lds + lay.vbuf);
-    // successor speculation (multi-wave Matte tiles, candidate stride 1; host: lay.succ):
-    // when the current pixel's chain is blocked only on trajectories still in flight,
-    // the leader guesses the pixel's end E from their draws so far, and the next
-    // pixel's StartPixel and trajectories start from E on the second ring. If the
-    // chain ends at E, the successor becomes the current pixel with its work done;
-    // otherwise it is dropped. Only the schedule changes, never a result.
-    constexpr bool kSuccCap = PBRT_CI_SUCC && (kW == 2 || kW == 4) && !kX && kDepth >= 0;
-    const bool succ = kSuccCap && lay.succ && cs == 1u;
-    RingEnt* const ring0 = (RingEnt*)(lds + lay.ring);
-    auto ringp = [&](int r) -> RingEnt* { return ring0 + (size_t)(kSuccCap ? r : g) * R; };
-    RingEnt* const ring = ringp(0);
+    RingEnt* ring = (RingEnt*)(lds + lay.ring) + (size_t)g * R;
     ChainCache* pcs = (ChainCache*)(lds + lay.pcs);
     uint16_t* stack = stack_lds + tid;
     const int n = rp.spp, ndims = rp.ndims;
@@ -111,13 +97,6 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
         s.kh = 1;
         s.head = s.nxt = 0;
         s.reissue = 0;
-        if (tid == 0) {
-            gsx.cur = 0;
-            gsx.bstate = 0;
-            gsx.bE = gsx.bnxt = 0;
-            gsx.bS = 0;
-            gsx.gen[0] = gsx.gen[1] = 0;
-        }
         if (b < nslots_batch) {
             int64_t x0, y0, x1, y1;
             tile_bounds(rp, tile_of_slot(rp, slot_base + b), x0, y0, x1, y1);
@@ -139,9 +118,6 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
     uint64_t last_host_poll = t_begin;   // when this workgroup last read the host flag
     // lane trajectory state
     uint32_t off = kNoOff;
-    // successor speculation: the lane's trajectory's ring (bit 0) and that ring's
-    // generation when it was issued (gen << 1): live while gen[ring] still matches
-    uint32_t ltag = 0;
     // kX: the trajectory's throughput, etaScale and start state live in LDS
     // (the BSDFX bounce needs their registers; 0 B of scratch)
 #ifdef PBRT_CI_LDS_STATE   // experiment: the Matte chain too
@@ -149,24 +125,14 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
 #else
     constexpr bool kLdsState = kX;
 #endif
-#ifdef PBRT_CI_LDS_BETA   // build option: the Matte chain's throughput in LDS (1.5 KB per wave)
-    constexpr bool kLdsBeta = kLdsState || kDepth >= 0;
-#else
-    constexpr bool kLdsBeta = kLdsState;
-#endif
-#ifdef PBRT_CI_ST0_RING   // build option: the Matte chain's start state in its ring entry from issue on
-    constexpr bool kSt0Ring = !kLdsState;
-#else
-    constexpr bool kSt0Ring = false;
-#endif
-    __shared__ Spec xs_beta[kLdsBeta ? kT : 1];
+    __shared__ Spec xs_beta[kLdsState ? kT : 1];
     __shared__ double xs_eta[kLdsState ? kT : 1];
     __shared__ uint64_t xs_st0[kLdsState ? kT : 1];
     uint64_t st0_r = 0;
     Spec beta_r = spec(1);
     double eta_r = 1.0;
     uint64_t& st0 = [&]() -> uint64_t& { if constexpr (kLdsState) return xs_st0[tid]; else return st0_r; }();
-    Spec& beta = [&]() -> Spec& { if constexpr (kLdsBeta) return xs_beta[tid]; else return beta_r; }();
+    Spec& beta = [&]() -> Spec& { if constexpr (kLdsState) return xs_beta[tid]; else return beta_r; }();
     double& eta_scale = [&]() -> double& { if constexpr (kLdsState) return xs_eta[tid]; else return eta_r; }();
     st0 = 0;
     beta = spec(1);
@@ -207,7 +173,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
                 // clear: with one tile per workgroup the StartPixel staging aliases the ring)
                 const double time_u = sp[1 < n ? 1 : 0];
                 __syncthreads();
-                RingEnt* rq = kSuccCap ? ringp(gsx.cur) : ring0 + (size_t)q * R;
+                RingEnt* rq = (RingEnt*)(lds + lay.ring) + (size_t)q * R;
                 for (uint32_t i = (uint32_t)tid; i < R; i += kT) rq[i].tag = kNoOff;
                 // bounce 1 (camera ray, first hit, BSDF) was computed for every
                 // pixel record by k_wf_primary; only the ray time needs StartPixel
@@ -223,14 +189,12 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
                 if (tid == 0 && gs[q].phase == 0) {
                     if (hit0)   // the camera ray's time (Get1D after pFilm, pLens) of the pixel's first traced sample
                         pr.si.time = camera_ray(cam, (double)px, (double)py, time_u, V2{0.0, 0.0}).time;
-                    ChainCache& pq = pcs[kSuccCap ? gsx.cur : q];
-                    pq.si = pr.si;
-                    pq.b = pr.b;
-                    if constexpr (kX) pq.x = pr.x;
-                    pq.wo = pr.wo;
-                    pq.hit = hit0;
+                    pcs[q].si = pr.si;
+                    pcs[q].b = pr.b;
+                    if constexpr (kX) pcs[q].x = pr.x;
+                    pcs[q].wo = pr.wo;
+                    pcs[q].hit = hit0;
                     CiGroup& s = gs[q];
-                    if constexpr (kSuccCap) gsx.gen[gsx.cur]++;   // the previous pixel's trajectories of this ring are stale
                     s.S = S1;
                     s.head = s.nxt = 0;
                     s.kh = 1;
@@ -249,38 +213,6 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
                 }
                 __syncthreads();
             }
-        }
-        if (succ && gsx.bstate == 1) {   // the successor's StartPixel (every thread; the first wave works)
-            const CiGroup s0 = gs[0];
-            const CiSucc xs = gsx;
-            const int64_t pb = s0.pi + 1, recb = bs * wb.ppt + pb;
-            int64_t x0, y0, x1, y1;
-            tile_bounds(rp, tile_of_slot(rp, slot_base + bs), x0, y0, x1, y1);
-            const int64_t px = x0 + pb % (x1 - x0), py = y0 + pb / (x1 - x0);
-            double* gs1d = wb.s1d + recb * wb.s1d_stride;
-            double* sp = s1d ? s1d : gs1d;
-            const uint64_t S1 = start_pixel_wave(rp, J, pcg_advance(J, s0.S, inc, (uint64_t)xs.bE), inc, sp, other, vbuf,
-                                                 &sh_state);
-            if (s1d)
-                for (int idx = tid; idx < ndims * n; idx += kT) gs1d[idx] = s1d[idx];
-            const double time_u = sp[1 < n ? 1 : 0];
-            const int rb = xs.cur ^ 1;
-            RingEnt* rq = ringp(rb);
-            for (uint32_t i = (uint32_t)tid; i < R; i += kT) rq[i].tag = kNoOff;
-            if (tid == 0) {
-                PixelRec& pr = wb.prec[recb];
-                pr.si.time = camera_ray(cam, (double)px, (double)py, time_u, V2{0.0, 0.0}).time;
-                ChainCache& pq = pcs[rb];
-                pq.si = pr.si;
-                pq.b = pr.b;
-                pq.wo = pr.wo;
-                pq.hit = pr.hit;
-                gsx.gen[rb]++;
-                gsx.bS = S1;
-                gsx.bnxt = 0;
-                gsx.bstate = 2;
-            }
-            __syncthreads();
         }
         mark(0);
         bool any_chain = false;
@@ -312,52 +244,29 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
             }
             const int re = (sg.reissue && nidle > 0) ? 1 : 0;
             const uint32_t nx0 = sg.nxt;
-            // offsets < head + R keep the ring collision-free; with a successor
-            // running, the current pixel's offsets past its guessed end wait (they
-            // are needed only if the guess is wrong, and then the head issues them)
-            CiSucc sx{};
-            if (succ) sx = gsx;
-            const bool brun = succ && sx.bstate == 2;
-            const uint32_t lim = brun ? min(sg.head + R, max(sx.bE, sg.head + 1u)) : sg.head + R;
-            const int avail = nx0 < lim ? (int)((lim - nx0 + cs - 1) / cs) : 0;
+            // offsets < head + R keep the ring collision-free
+            const int avail = nx0 < sg.head + R ? (int)((sg.head + R - nx0 + cs - 1) / cs) : 0;
             const int nspec = min(nidle - re, avail);
-            // then the successor's offsets (its head is 0 until it becomes current)
-            const int bavail = brun && sx.bnxt < R ? (int)(R - sx.bnxt) : 0;
-            const int nbspec = brun ? min(nidle - re - max(nspec, 0), bavail) : 0;
             uint32_t o = kNoOff;
-            bool exact = false, ob = false;
+            bool exact = false;
             if (idle) {
                 if (re && rank == 0) {
                     o = sg.head;
                     exact = true;
                 } else {
                     rank -= re;
-                    if (rank < nspec) {
-                        o = nx0 + cs * (uint32_t)rank;
-                    } else if (rank - max(nspec, 0) < nbspec) {
-                        o = sx.bnxt + (uint32_t)(rank - max(nspec, 0));
-                        ob = true;
-                    }
+                    if (rank < nspec) o = nx0 + cs * (uint32_t)rank;
                 }
             }
             if (gl == 0 && sg.phase == 1) {
                 gs[g].nxt = nx0 + cs * (uint32_t)max(nspec, 0);
-                if (nbspec > 0) gsx.bnxt = sx.bnxt + (uint32_t)nbspec;
-                CI_DIAG(ph[5] += (unsigned long long)(max(nspec, 0) + max(nbspec, 0) + re);)   // candidate trajectories issued
+                CI_DIAG(ph[5] += (unsigned long long)(max(nspec, 0) + re);)   // candidate trajectories issued
                 if (re) gs[g].reissue = 0;
             }
             if (o != kNoOff) {
                 off = o;
-                if constexpr (kSuccCap) {
-                    const int lr = ob ? (sx.cur ^ 1) : sx.cur;
-                    ltag = (sx.gen[lr] << 1) | (uint32_t)lr;
-                }
-                const uint64_t s0 = pcg_advance(J, ob ? sx.bS : sg.S, inc, (uint64_t)o);
-                // kSt0Ring: the entry of offset o is not read before its tag says o
-                // (the walk matches tags; a slot's older offset o - R is behind the head)
-                if constexpr (kSt0Ring) ring[o & (R - 1u)].st = s0;
-                else st0 = s0;
-                c.rng.state = s0;
+                st0 = pcg_advance(J, sg.S, inc, (uint64_t)o);
+                c.rng.state = st0;
                 c.draws = 0;
                 c_camera(c, ndims);   // camera: Get2D pFilm, Get2D pLens, Get1D time
                 c.k = exact ? sg.kh : -1;
@@ -369,18 +278,13 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
                 beta = spec(1);
                 eta_scale = 1.0;
                 bounces = 1;
-                const ChainCache& pc = pcs[kSuccCap ? (int)(ltag & 1u) : g];
+                const ChainCache& pc = pcs[g];
                 const int r = traj_scatter<kX>(sc, pc.si, pc.b, pc.x, pc.wo, c, ss, beta, eta_scale, bounces, ray,
                                                rp.max_depth, rp.rr_threshold);
                 tracing = r == 0;
-                if (succ && tracing) {   // in flight: its draws so far, for the leader's successor guess
-                    RingEnt& e = ringp((int)(ltag & 1u))[off & (R - 1u)];
-                    e.d = c.draws;
-                    e.tag = off | kInflight;
-                }
                 if (r != 0) {
-                    RingEnt& e = (kSuccCap ? ringp((int)(ltag & 1u)) : ring)[off & (R - 1u)];
-                    if constexpr (!kSt0Ring) e.st = st0;
+                    RingEnt& e = ring[off & (R - 1u)];
+                    e.st = st0;
                     e.d = ring_d<kX>(c, ss, r == 1 ? c.draws : (c.k >= 0 ? kBadExactD : kBadSpecD));
                     e.tag = off;
                     off = kNoOff;
@@ -422,16 +326,13 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
                     else if (r == 2) d = c.k >= 0 ? kBadExactD : kBadSpecD;
                 }
             }
-            RingEnt& e = (kSuccCap ? ringp((int)(ltag & 1u)) : ring)[off & (R - 1u)];
             if (d != kNoOff) {
-                if constexpr (!kSt0Ring) e.st = st0;
+                RingEnt& e = ring[off & (R - 1u)];
+                e.st = st0;
                 e.d = ring_d<kX>(c, ss, d);
                 e.tag = off;
                 off = kNoOff;
                 tracing = false;
-            } else if (succ) {   // still in flight: its draws so far
-                e.d = c.draws;
-                e.tag = off | kInflight;
             }
         }
         mark(3);
@@ -445,9 +346,8 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
                 if (host) last_host_poll = now;
                 if (cancel_requested(sc, host)) s.phase = 2;
             }
-            int64_t wrec = rec;   // the current pixel's record (changes when a successor takes over)
             for (; s.phase == 1;) {
-                RingEnt& e = (kSuccCap ? ringp(gsx.cur) : ring)[s.head & (R - 1u)];
+                RingEnt& e = ring[s.head & (R - 1u)];
                 if (e.tag != s.head) break;
                 uint32_t d = e.d;
                 if (kX && d < kBadExactD && (d & kRrFlag)) {
@@ -469,9 +369,9 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
                     s.reissue = 1;
                     break;
                 }
-                wb.memb[wrec * n + s.kh] = e.st;
+                wb.memb[rec * n + s.kh] = e.st;
                 if (d == kBadExactD) {   // the exact head's trajectory panics: the tile ends at this sample
-                    wb.prec[wrec].nvalid = s.kh + 1;
+                    wb.prec[rec].nvalid = s.kh + 1;
                     s.phase = 2;
                     break;
                 }
@@ -479,63 +379,10 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
                 s.kh++;
                 s.head += d;
                 if (s.kh >= n) {   // every sample of the pixel has its offset; the next StartPixel starts here
-                    if (succ && gsx.bstate == 2 && gsx.bE == s.head) {
-                        // the guess was right: the successor is the current pixel, its
-                        // StartPixel done and its ring holding what its lanes resolved
-                        CiSucc& x = gsx;
-                        x.gen[x.cur]++;   // the finished pixel's trajectories are stale
-                        x.cur ^= 1;
-                        s.S = x.bS;
-                        s.pi++;
-                        s.head = 0;
-                        s.nxt = x.bnxt;
-                        s.kh = 1;
-                        s.reissue = 0;
-                        x.bstate = 0;
-                        wb.tile_npx[bs] = (int32_t)(s.pi + 1);
-                        wrec = bs * wb.ppt + s.pi;
-                        continue;
-                    }
-                    if (succ && gsx.bstate != 0) {   // a wrong guess: the successor is dropped
-                        gsx.gen[gsx.cur ^ 1]++;
-                        gsx.bstate = 0;
-                    }
                     s.S = pcg_advance(J, s.S, inc, (uint64_t)s.head);
                     s.pi++;
                     s.phase = s.pi < s.npx ? 0 : 2;
                     break;
-                }
-            }
-            if (succ && s.phase == 1 && gsx.bstate == 0 && s.pi + 1 < s.npx) {
-                // guess the pixel's end: walk on through resolved entries, taking an
-                // entry still in flight to end at its next traversal (a miss: D = its
-                // draws so far), at most kSuccGuesses times
-                const PixelRec& nr = wb.prec[bs * wb.ppt + s.pi + 1];
-                if (nr.hit && !nr.panic0) {
-                    const RingEnt* rc = ringp(gsx.cur);
-                    uint32_t h = s.head;
-                    int k = s.kh, guesses = 0;
-                    bool ok = true;
-                    while (k < n) {
-                        const RingEnt& e = rc[h & (R - 1u)];
-                        uint32_t d;
-                        if (e.tag == h) {
-                            d = e.d;
-                            if (d >= kBadExactD) { ok = false; break; }
-                        } else if (e.tag == (h | kInflight) && guesses < kSuccGuesses) {
-                            d = e.d;
-                            guesses++;
-                        } else {
-                            ok = false;
-                            break;
-                        }
-                        h += d;
-                        k++;
-                    }
-                    if (ok && guesses > 0) {
-                        gsx.bE = h;
-                        gsx.bstate = 1;
-                    }
                 }
             }
             if (s.nxt < s.head || (cs == 2u && ((s.nxt ^ s.head) & 1u))) s.nxt = s.head;
@@ -545,14 +392,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
         // ---- (5) drop candidates the chain has left behind
         if (off != kNoOff) {
             const CiGroup s2 = gs[g];
-            bool drop;
-            if (succ) {   // a ring's generation changes when its pixel does
-                const int lr = (int)(ltag & 1u);
-                drop = s2.phase != 1 || ((gsx.gen[lr] << 1) | (uint32_t)lr) != ltag || (lr == gsx.cur && off < s2.head);
-            } else {
-                drop = s2.phase != 1 || off < s2.head || (cs == 2u && ((off ^ s2.head) & 1u)) || s2.pi != sg.pi;
-            }
-            if (drop) {
+            if (s2.phase != 1 || off < s2.head || (cs == 2u && ((off ^ s2.head) & 1u)) || s2.pi != sg.pi) {
                 off = kNoOff;
                 tracing = false;
             }

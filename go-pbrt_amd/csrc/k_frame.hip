@@ -23,20 +23,21 @@ namespace pbrtk {
 // (render_common.h footprint()). The running sums live in LDS, one per film
 // pixel and channel. The workgroup also adds up its pixels' reference ray
 // counts (pbrt_gpu_stats.rays_*).
-__device__ __forceinline__ bool film_weight(const pbrt_film_desc& f, int64_t sx, int64_t sy, int64_t fx, int64_t fy,
-                                            double& w) {
+__device__ __forceinline__ bool film_weight(const pbrt_film_desc& f, double ifx, double ify, int64_t sx, int64_t sy,
+                                            int64_t fx, int64_t fy, double& w) {
     // film.go:216-246 with pFilm = the source pixel's corner (2D stratified values are (0,0), #3);
     // the tile-film clip [px0, px1) holds for every film pixel of the slot
     const double dx = (double)sx + 0.0 - 0.5, dy = (double)sy + 0.0 - 0.5;
     const double p0x = gomath::ceil(dx - f.filter_radius_x), p0y = gomath::ceil(dy - f.filter_radius_y);
     const double p1x = gomath::floor(dx + f.filter_radius_x) + 1, p1y = gomath::floor(dy + f.filter_radius_y) + 1;
     if (!((double)fx >= p0x && (double)fx < p1x && (double)fy >= p0y && (double)fy < p1y)) return false;
-    const double ifx = 1.0 / f.filter_radius_x, ify = 1.0 / f.filter_radius_y;
     const int iy = (int)gomath::to_int(gomath::min(gomath::floor(gomath::abs(((double)fy - dy) * ify * 16.0)), 16.0 - 1));
     const int ix = (int)gomath::to_int(gomath::min(gomath::floor(gomath::abs(((double)fx - dx) * ifx * 16.0)), 16.0 - 1));
     w = 1.0 * f.filter_table[iy * 16 + ix];
     return true;
 }
+
+constexpr int kFilmLoads = 12;   // k_film staging: loads in flight per thread
 
 __global__ __launch_bounds__(kFilmThreads) void k_film(const pbrt_film_desc* __restrict__ film_desc, RenderParams rp,
                                                        WaveBufs wb, int64_t slot_base, int64_t nslots_batch,
@@ -61,7 +62,11 @@ __global__ __launch_bounds__(kFilmThreads) void k_film(const pbrt_film_desc* __r
     const int npx = wb.tile_npx[bslot];
     const int S = film_run_pixels(rp);
     // a source pixel reaches film pixels within (int)r + 2 of it (footprint: |f - s| < r + 1.5)
-    const int rx = (int)film.filter_radius_x + 2, ry = (int)film.filter_radius_y + 2;
+    const double ifx = 1.0 / film.filter_radius_x, ify = 1.0 / film.filter_radius_y;   // film.go:231-232
+    // a source pixel's footprint relative to it, [fa, fb) x [ga, gb) (film.go:216-219 with
+    // pFilm = the pixel corner); the work items cover it widened by one, the exact test is film_weight
+    const int fa = (int)gomath::ceil(-0.5 - film.filter_radius_x), fb = (int)gomath::floor(film.filter_radius_x - 0.5) + 1;
+    const int ga = (int)gomath::ceil(-0.5 - film.filter_radius_y), gb = (int)gomath::floor(film.filter_radius_y - 0.5) + 1;
     // LDS: running sums [nfp][3], then the staged run [S][m][3]
     double* acc = (double*)lds;
     double* stg = acc + ((nfp * 3 + 1) & ~1);
@@ -74,18 +79,37 @@ __global__ __launch_bounds__(kFilmThreads) void k_film(const pbrt_film_desc* __r
         if (tid < ns) nvs[tid] = wb.prec[rec0 + s0 + tid].nvalid;
         __syncthreads();
         // stage the run's samples 1 .. nvalid-1: one contiguous stretch of L but
-        // for each pixel's sample 0 (pixel-major); the ray counts on the way
+        // for each pixel's sample 0 (pixel-major); the ray counts on the way.
+        // kFilmLoads loads per thread are in flight at once (a whole 16-px row
+        // at 64 spp in one round): the HBM latency is paid once per run
         const double* Lrun = wb.L + (rec0 + s0) * (int64_t)n * 3;
-        for (int i = tid; i < ns * m * 3; i += kFilmThreads) {
-            const int s = i / (m * 3), j = i - s * (m * 3);
-            if (j / 3 < nvs[s] - 1) stg[i] = Lrun[(int64_t)s * n * 3 + 3 + j];
+        const int tot = ns * m * 3;
+        for (int i0 = tid; i0 < tot; i0 += kFilmThreads * kFilmLoads) {
+            double v[kFilmLoads];
+#pragma unroll
+            for (int u = 0; u < kFilmLoads; u++) {
+                const int i = i0 + u * kFilmThreads;
+                v[u] = 0.0;
+                if (i < tot) {
+                    const int s = i / (m * 3), j = i - s * (m * 3);
+                    if (j / 3 < nvs[s] - 1) v[u] = Lrun[(int64_t)s * n * 3 + 3 + j];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kFilmLoads; u++)
+                if (i0 + u * kFilmThreads < tot) stg[i0 + u * kFilmThreads] = v[u];
         }
-        for (int i = tid; i < ns * m; i += kFilmThreads) {
-            const int s = i / m, k = i - s * m;
-            if (k < nvs[s] - 1) {
-                const uint32_t v = wb.rays[(rec0 + s0 + s) * n + 1 + k];
-                cl += v & 0xFFFFu;
-                sh += v >> 16;
+        for (int i0 = tid; i0 < ns * m; i0 += kFilmThreads * 4) {
+            uint32_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = i0 + u * kFilmThreads, s = i / m, k = i - s * m;
+                v[u] = (i < ns * m && k < nvs[s] - 1) ? wb.rays[(rec0 + s0 + s) * n + 1 + k] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                cl += v[u] & 0xFFFFu;
+                sh += v[u] >> 16;
             }
         }
         __syncthreads();
@@ -105,36 +129,54 @@ __global__ __launch_bounds__(kFilmThreads) void k_film(const pbrt_film_desc* __r
             }
         }
         __syncthreads();
-        // every film pixel adds the run's sources that reach it, in order
-        for (int fi = tid; fi < nfp; fi += kFilmThreads) {
-            const int64_t fx = px0 + fi % tw, fy = py0 + fi / tw;
-            double a0 = 0, a1 = 0, a2 = 0;
+        // the film pixels the run can reach (a source pixel's footprint spans
+        // [sx + fa, sx + fb), widened by one), one work item per (film pixel,
+        // channel): each adds the run's sources that reach it, in order -- the
+        // sources in the window its footprint allows, row-major, each checked
+        // with film.go's own test (film_weight)
+        const int sy0 = s0 / sw, sy1 = (s0 + ns - 1) / sw;   // the run's source rows (tile-relative)
+        const int sxa = s0 - sy0 * sw, sxb = s0 + ns - 1 - sy1 * sw;   // first row from sxa, last row to sxb
+        const int sxl = sy0 == sy1 ? sxa : 0, sxh = sy0 == sy1 ? sxb : sw - 1;
+        const int fxl = max((int)x0 + sxl + fa - 1, (int)px0) - (int)px0;
+        const int fxh = min((int)x0 + sxh + fb, (int)px1 - 1) - (int)px0;
+        const int fyl = max((int)y0 + sy0 + ga - 1, (int)py0) - (int)py0;
+        const int fyh = min((int)y0 + sy1 + gb, (int)py1 - 1) - (int)py0;
+        const int nfx = fxh - fxl + 1, nit = nfx > 0 && fyh >= fyl ? nfx * (fyh - fyl + 1) * 3 : 0;
+        for (int it = tid; it < nit; it += kFilmThreads) {
+            const int f = it / 3, ch = it - f * 3;
+            const int fr = f / nfx, fcol = fxl + (f - fr * nfx), frow = fyl + fr;
+            const int fi = frow * tw + fcol;
+            const int64_t fx = px0 + fcol, fy = py0 + frow;
+            // candidate sources (tile-relative): rows (fy - gb, fy - ga], columns (fx - fb, fx - fa], widened by one
+            const int ry0 = max(sy0, (int)(fy - y0) - gb), ry1 = min(sy1, (int)(fy - y0) - ga + 1);
+            const int cx0 = (int)(fx - x0) - fb, cx1 = (int)(fx - x0) - fa + 1;
+            double a = 0;
             bool any = false;
-            for (int s = 0; s < ns; s++) {
-                const int pi = s0 + s;
-                const int64_t sx = x0 + pi % sw, sy = y0 + pi / sw;
-                if (sx - fx > rx || fx - sx > rx || sy - fy > ry || fy - sy > ry) continue;
-                double w;
-                if (!film_weight(film, sx, sy, fx, fy, w)) continue;
-                if (!any) {
-                    a0 = acc[fi * 3 + 0];
-                    a1 = acc[fi * 3 + 1];
-                    a2 = acc[fi * 3 + 2];
-                    any = true;
-                }
-                const int nk = nvs[s] - 1;
-                const double* d = stg + (int64_t)s * m * 3;
-                for (int k = 0; k < nk; k++) {
-                    a0 += d[k * 3 + 0] * w;
-                    a1 += d[k * 3 + 1] * w;
-                    a2 += d[k * 3 + 2] * w;
+            for (int sy = ry0; sy <= ry1; sy++) {
+                const int lo = max(cx0, sy == sy0 ? sxa : 0), hi = min(cx1, sy == sy1 ? sxb : sw - 1);
+                for (int sx = lo; sx <= hi; sx++) {
+                    double w;
+                    if (!film_weight(film, ifx, ify, x0 + sx, y0 + sy, fx, fy, w)) continue;
+                    const int s = sy * sw + sx - s0;
+                    if (!any) {
+                        a = acc[fi * 3 + ch];
+                        any = true;
+                    }
+                    // the chain of adds is sequential; the LDS loads run 8 samples ahead
+                    const int nk = nvs[s] - 1;
+                    const double* d = stg + (int64_t)s * m * 3 + ch;
+                    int k = 0;
+                    for (; k + 8 <= nk; k += 8) {
+                        double v[8];
+#pragma unroll
+                        for (int u = 0; u < 8; u++) v[u] = d[(k + u) * 3];
+#pragma unroll
+                        for (int u = 0; u < 8; u++) a += v[u] * w;
+                    }
+                    for (; k < nk; k++) a += d[k * 3] * w;
                 }
             }
-            if (any) {
-                acc[fi * 3 + 0] = a0;
-                acc[fi * 3 + 1] = a1;
-                acc[fi * 3 + 2] = a2;
-            }
+            if (any) acc[fi * 3 + ch] = a;
         }
     }
     __syncthreads();

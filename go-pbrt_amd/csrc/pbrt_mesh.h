@@ -161,6 +161,19 @@ __device__ __forceinline__ bool mesh_box_hit(const float* bmin, const float* bma
     return t0 <= t1 && t0 <= tmax;
 }
 
+// Leaf tests batched across the wave (build option PBRT_MESH_BATCH, default on).
+// With one-triangle leaves about one node visit in 17 is a leaf, so in a
+// 64-lane wave nearly every step of a per-lane walk has some lane at a leaf,
+// and the wave pays a triangle test (~5x a box test) on almost every step. A
+// lane that reaches a leaf here waits with it while the others walk on; the
+// wave tests its pending triangles together once half of its live lanes hold
+// one, or no lane can walk further. A waiting lane makes no box test (none sees
+// an older TMax than in the per-lane walk), and the closest hit is the smallest
+// (t, index) whatever the order of the tests: the results are the same.
+#ifndef PBRT_MESH_BATCH
+#define PBRT_MESH_BATCH 1
+#endif
+
 // Closest (kAny = false) or any (kAny) triangle of the scene's meshes.
 // Closest: a hit must have t < tmax, or t == tmax and a smaller global index
 // than best_gid (-1: nothing of the meshes yet, TMax exclusive). On return
@@ -207,6 +220,60 @@ __device__ inline bool mesh_walk(const DevMesh& m, const Ray& ray, double& tmax,
     uint4 a, b, a2, b2;
     load_node(0, a, b);
     load_node(1, a2, b2);
+#endif
+#if PBRT_MESH_BATCH && !defined(PBRT_MESH_PREFETCH)
+    uint32_t pend = 0;   // a leaf word waiting for the wave's triangle batch (0: none)
+    for (;;) {
+        // nodes: until half the live lanes wait with a leaf, or none walks on
+        for (;;) {
+            const bool walking = i < n && pend == 0;
+            const unsigned long long mw = __ballot(walking);
+            if (mw == 0) break;
+            const unsigned long long mp = __ballot(pend != 0), ml = mw | mp;
+            if (2 * __popcll(mp) >= __popcll(ml)) break;
+            if (walking) {
+                MESH_COUNT(c_nodes++;)
+                const uint4* q = reinterpret_cast<const uint4*>(N + i);
+                const uint4 a = q[0], b = q[1];
+                const float bmin[3] = {__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z)};
+                const float bmax[3] = {__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z)};
+                if (!mesh_box_hit(bmin, bmax, ray, inv, zero_mask, tmax)) {
+                    i = a.w;   // escape
+                } else if (b.w == kMeshInterior) {
+                    i++;
+                } else {
+                    pend = b.w;
+                    i = a.w;
+                }
+            }
+        }
+        if (!__any(pend != 0)) break;
+        if (pend != 0) {   // the batch: every waiting lane tests its leaf
+            const uint32_t first = pend >> 3, cnt = pend & 7u;
+            pend = 0;
+            for (uint32_t k = 0; k < cnt; k++) {
+                double v[9], t, b0, b1, b2;
+                load_tri(m.tris, first + k, v);
+                MESH_COUNT(c_tris++;)
+                if (!tri_hit(v, ray, t, b0, b1, b2)) continue;
+                if (kAny) {
+                    if (t < tmax) {
+                        found = true;
+                        i = n;   // answered
+                        break;
+                    }
+                    continue;
+                }
+                if (t < tmax || (t == tmax && m.gid[first + k] < best_gid)) {
+                    tmax = t;
+                    best_slot = (int32_t)(first + k);
+                    best_gid = m.gid[first + k];
+                    found = true;
+                }
+            }
+        }
+    }
+    return found;
 #endif
     while (i < n) {
         MESH_COUNT(c_nodes++;)

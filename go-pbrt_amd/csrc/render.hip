@@ -65,7 +65,6 @@ struct Knobs {
     int cull_group = 4;        // PBRT_CULL_GROUP: leaves per culling group
     int cull_min = 2;          // PBRT_CULL_MIN
     bool cull_groups = true;   // PBRT_CULL_GROUPS=0
-    bool ci_succ = true;       // PBRT_CI_SUCC=0: no successor speculation in multi-wave k_chain_ci tiles
     static Knobs from_env() {
         Knobs k;
         auto ival = [](const char* n, int& out) { if (const char* e = getenv(n)) out = atoi(e); };
@@ -80,7 +79,6 @@ struct Knobs {
         if (const char* e = getenv("PBRT_CI_HEAVY_WAVES")) k.ci_heavy_waves = atoi(e) == 8 ? 8 : 4;
         if (const char* e = getenv("PBRT_CI_HEAVY")) k.ci_heavy = (int64_t)atoll(e);
         if (const char* e = getenv("PBRT_CI_SPLIT")) k.ci_split = atoi(e) != 0;
-        if (const char* e = getenv("PBRT_CI_SUCC")) k.ci_succ = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_DENSE")) k.ci_dense = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_ORDER")) k.ci_order = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_PROBE")) k.ci_probe = atoi(e) != 0;
@@ -547,7 +545,6 @@ bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Rend
         off += (bytes + 15) & ~int64_t(15);
         return (int)o;
     };
-    L.succ = Lci.succ = 0;
     L.s1d = put(nd * n * 8);
     L.other = put(nd * n * 2);
     L.sbuf = put(kWave * 8);
@@ -588,17 +585,9 @@ bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Rend
 // tile per workgroup (G == 1) the StartPixel staging aliases the offset ring:
 // a group starts a pixel only after its chain has dropped every candidate,
 // so the two are never live together (config C, 256 spp: 19 KB of staging).
-// succ: successor speculation (k_chain_ci, multi-wave tiles): two rings after
-// the staging (a successor's StartPixel runs while the current pixel's ring is
-// live) and two ChainCache records.
-ChainLayout ci_layout(const ChainLayout& base, int w, int G, unsigned& lds_bytes, bool succ = false) {
+ChainLayout ci_layout(const ChainLayout& base, int w, int G, unsigned& lds_bytes) {
     ChainLayout l = base;
-    l.succ = 0;
-    if (succ && G == 1) {
-        l.ring = (base.staging + 15) & ~15;
-        lds_bytes = (unsigned)(l.ring + 2 * w * kCiRingBytes);
-        l.succ = 1;
-    } else if (G == 1) {
+    if (G == 1) {
         l.ring = 0;
         lds_bytes = (unsigned)std::max(base.staging, w * kCiRingBytes);
     } else {
@@ -606,7 +595,7 @@ ChainLayout ci_layout(const ChainLayout& base, int w, int G, unsigned& lds_bytes
     }
     // then one ChainCache per lane group (only the groups in use: G, not kCiMaxGroups)
     l.pcs = (int)((lds_bytes + 15u) & ~15u);
-    lds_bytes = (unsigned)l.pcs + (unsigned)((l.succ ? 2 : G) * sizeof(ChainCache));
+    lds_bytes = (unsigned)l.pcs + (unsigned)(G * sizeof(ChainCache));
     l.total = (int)lds_bytes;
     return l;
 }
@@ -1186,12 +1175,7 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                         if (w > 1) {   // one tile per workgroup of w waves; the ring grows with the lanes
                             const int ring = w * kCiRingBytes / (int)sizeof(RingEnt);
                             unsigned lds = 0;
-                            // successor speculation: 2- and 4-wave Matte tiles of LDS-staged or
-                            // stack-walked analytic trees, candidate stride 1
-                            const bool succ = c->knobs.ci_succ && !kx && !mesh_only && (w == 2 || w == 4) &&
-                                              ci_stride(c, w) == 1;
-                            ChainLayout lw = ci_layout(c->lay_ci, w, 1, lds, succ);
-                            if (lds > c->lds_per_block) lw = ci_layout(c->lay_ci, w, 1, lds, false);
+                            const ChainLayout lw = ci_layout(c->lay_ci, w, 1, lds);
                             // kX: LDS-staged trees only, at most 4 waves per tile (wave_eligible, ci_waves)
                             auto kern = kx ? (w == 2 ? k_chain_ci<2, 0, true> : k_chain_ci<4, 0, true>)
                                         : mesh_only ? (w == 2 ? k_chain_ci<2, -1> : w == 4 ? k_chain_ci<4, -1> : k_chain_ci<8, -1>)

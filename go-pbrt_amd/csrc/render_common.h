@@ -199,7 +199,6 @@ struct ChainLayout {   // byte offsets into the chain / setup kernels' dynamic L
     int ring;      // k_chain_ci: offset ring after the StartPixel staging (no sbuf / dbuf)
     int staging;   // k_chain_ci: bytes of the StartPixel staging (s1d, other, vbuf)
     int pcs;       // k_chain_ci: the lane groups' bounce-1 ChainCache records (ci_layout)
-    int succ;      // k_chain_ci: successor speculation (two rings, two ChainCaches, no aliasing)
 };
 #ifndef PBRT_CI_RING_KB
 #define PBRT_CI_RING_KB 4
@@ -749,17 +748,5 @@ struct CiGroup {
     int reissue;    // the head must be re-run with its sample index known
     int pad;
 };
-// k_chain_ci successor speculation (multi-wave tiles): the next pixel's chain
-// started from a guessed end bE of the current one, on the other ring
-struct CiSucc {
-    uint64_t bS;       // the successor's PCG32 state at its offset 0
-    uint32_t bE;       // the guessed end offset of the current pixel (relative to S)
-    uint32_t bnxt;     // the successor's next offset to issue
-    uint32_t gen[2];   // generation of each ring: a lane's trajectory is live while its ring's matches
-    int cur;           // ring (and ChainCache) of the current pixel: 0 / 1
-    int bstate;        // 0 none, 1 its StartPixel is due, 2 running
-};
-constexpr uint32_t kInflight = 0x80000000u;   // RingEnt tag of an offset still traced (d: its draws so far)
-constexpr int kSuccGuesses = 2;   // unresolved chain entries a successor guess may assume
 
 }  // namespace pbrtk

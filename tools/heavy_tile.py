@@ -60,6 +60,8 @@ def main():
                     tot = float(sum(ph))
                     rec["steps"] = vals[5]
                     rec["phase_share"] = {k: round(v / tot, 4) for k, v in zip(PHASES, ph)}
+                    if len(vals) >= 14:   # candidates issued; successor promotions / discards (PBRT_CI_SUCC)
+                        rec["issued"], rec["succ_promoted"], rec["succ_dropped"] = vals[11], vals[12], vals[13]
                 print(json.dumps(rec), flush=True)
 
 
