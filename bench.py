@@ -339,11 +339,16 @@ def mesh_roofline(cfg, W, H, S, mode, stats_ms, paths, rays_closest, rays_shadow
     else:
         algo = traced_closest * per_closest + rays_shadow * per_any
     achieved = algo / (ms / 1e3) / 1e9
+    # the same pricing with every reference closest-hit query, the per-sample camera
+    # ray included (the reference traces it per sample; the device once per pixel)
+    algo_cam = (rays_closest * per_closest if name == "k_chain_ci"
+                else rays_closest * per_closest + rays_shadow * per_any)
     fam = {"k_chain_ci": "k_chain_ci", "k_paths_ci": "k_paths_ci", "k_paths_ci_mb": "k_paths_ci"}[name]
     pf = pmc_fields(pmc, fam, ms, stats_ms["kernels"])
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, **pf, "kernel": name, "kernel_ms": ms,
             "bytes_per_launch": algo,
+            "frac_incl_camera_rays": algo_cam / (ms / 1e3) / 1e9 / HBM_PEAK_GBS,
             "algorithmic": {"reference_closest_walks_beyond_camera": traced_closest,
                             "reference_shadow_walks": rays_shadow,
                             "bytes_per_closest_walk": per_closest, "bytes_per_shadow_walk": per_any,

@@ -215,7 +215,8 @@ __device__ __forceinline__ int32_t ld_coherent(const int32_t* p) {
 // triangles -> one node). The second child to finish climbs to the parent.
 __global__ __launch_bounds__(kB) void k_up(const float* __restrict__ tris_s, int n, const int32_t* __restrict__ cl,
                                            const int32_t* __restrict__ cr, const int32_t* __restrict__ parent,
-                                           float* box, int32_t* tc, int32_t* sz, uint32_t* __restrict__ flag) {
+                                           float* box, int32_t* tc, int32_t* sz, int32_t* ht,
+                                           uint32_t* __restrict__ flag) {
     const int k = blockIdx.x * kB + threadIdx.x;
     if (k >= n) return;
     const int id = n - 1 + k;
@@ -228,6 +229,7 @@ __global__ __launch_bounds__(kB) void k_up(const float* __restrict__ tris_s, int
     }
     tc[id] = 1;
     sz[id] = 1;
+    ht[id] = 0;
     int p = parent[id];
     while (p >= 0) {
         __threadfence();
@@ -242,6 +244,7 @@ __global__ __launch_bounds__(kB) void k_up(const float* __restrict__ tris_s, int
         const int t = ld_coherent(&tc[l]) + ld_coherent(&tc[r]);
         tc[p] = t;
         sz[p] = t <= kMeshLeafMax ? 1 : 1 + ld_coherent(&sz[l]) + ld_coherent(&sz[r]);
+        ht[p] = 1 + max(ld_coherent(&ht[l]), ld_coherent(&ht[r]));
         p = parent[p];
     }
 }
@@ -306,6 +309,92 @@ __global__ __launch_bounds__(kB) void k_flatten(int n, const int32_t* __restrict
         nd.escape = pos[o] + (uint32_t)sz[v];
         out[(size_t)o * n_out + pos[o]] = nd;
     }
+}
+
+// Wide layout (PBRT_MESH_WIDE): one level of the 4-ary tree per launch. Node
+// i (binary node bin_of[i]) takes its binary children and opens the highest
+// child subtree until it holds four slots, so that every slot is at least two
+// binary levels below the node: with the Karras tree's <= 64 levels of inner
+// nodes the wide tree has <= 32 levels (kMeshWideLevels). The slots are stored
+// in ascending centre order along the axis of their centres' largest spread;
+// the level's inner slots get consecutive indices after the level (atomic
+// counter), so the tree is laid out level by level, siblings together.
+__global__ __launch_bounds__(kB) void k_collapse(int n, const int32_t* __restrict__ cl, const int32_t* __restrict__ cr,
+                                                 const float* __restrict__ box, const int32_t* __restrict__ tc,
+                                                 const int32_t* __restrict__ ht, int32_t* __restrict__ bin_of,
+                                                 uint32_t* __restrict__ par4, uint32_t lvl_begin, uint32_t lvl_end,
+                                                 uint32_t* __restrict__ counter, MeshNode4* __restrict__ out) {
+    const uint32_t i = lvl_begin + blockIdx.x * kB + threadIdx.x;
+    if (i >= lvl_end) return;
+    const int v = bin_of[i];
+    int s[4] = {v, -1, -1, -1}, ns = 1;
+    if (v < n - 1) {
+        s[0] = cl[v];
+        s[1] = cr[v];
+        ns = 2;
+    }
+    while (ns < 4) {
+        int best = -1;
+        for (int j = 0; j < ns; j++) {
+            if (s[j] >= n - 1) continue;   // a triangle
+            if (best < 0 || ht[s[j]] > ht[s[best]] || (ht[s[j]] == ht[s[best]] && tc[s[j]] > tc[s[best]])) best = j;
+        }
+        if (best < 0) break;
+        const int w = s[best];
+        s[best] = cl[w];
+        s[ns++] = cr[w];
+    }
+    float c[4][3];
+    for (int j = 0; j < ns; j++)
+        for (int a = 0; a < 3; a++) c[j][a] = box[(size_t)s[j] * 6 + a] + box[(size_t)s[j] * 6 + 3 + a];
+    int axis = 0;
+    float spread = -1;
+    for (int a = 0; a < 3; a++) {
+        float mn = c[0][a], mx = c[0][a];
+        for (int j = 1; j < ns; j++) {
+            mn = fminf(mn, c[j][a]);
+            mx = fmaxf(mx, c[j][a]);
+        }
+        if (mx - mn > spread) {
+            spread = mx - mn;
+            axis = a;
+        }
+    }
+    for (int j = 1; j < ns; j++)   // insertion sort by centre along the axis
+        for (int k = j; k > 0 && c[k][axis] < c[k - 1][axis]; k--) {
+            const int t = s[k];
+            s[k] = s[k - 1];
+            s[k - 1] = t;
+            for (int a = 0; a < 3; a++) {
+                const float f = c[k][a];
+                c[k][a] = c[k - 1][a];
+                c[k - 1][a] = f;
+            }
+        }
+    int nin = 0;
+    for (int j = 0; j < ns; j++) nin += s[j] < n - 1;
+    uint32_t next = nin ? atomicAdd(counter, (uint32_t)nin) : 0u;
+    MeshNode4 nd;
+    for (int j = 0; j < 4; j++) {
+        for (int a = 0; a < 3; a++) {
+            nd.lo[a][j] = j < ns ? box[(size_t)s[j] * 6 + a] : 0.0f;
+            nd.hi[a][j] = j < ns ? box[(size_t)s[j] * 6 + 3 + a] : 0.0f;
+        }
+        if (j >= ns) {
+            nd.child[j] = kMeshEmpty;
+        } else if (s[j] >= n - 1) {
+            nd.child[j] = kMeshTri | (uint32_t)(s[j] - (n - 1));
+        } else {
+            bin_of[next] = s[j];
+            par4[next] = i;
+            nd.child[j] = next++;
+        }
+    }
+    nd.parent = par4[i];
+    nd.axis = (uint32_t)axis;
+    nd.count = (uint32_t)ns;
+    nd.pad = 0;
+    out[i] = nd;
 }
 
 template <class T>
@@ -386,8 +475,8 @@ int mesh_bvh_build(const pbrt_scene_desc* s, hipStream_t st, MeshBuild& out, std
     {
         float *tris = nullptr, *cen = nullptr, *box = nullptr;
         int32_t *gid = nullptr, *cl = nullptr, *cr = nullptr, *par = nullptr, *rfirst = nullptr, *tc = nullptr,
-                *sz = nullptr;
-        uint32_t *bounds = nullptr, *flag = nullptr;
+                *sz = nullptr, *ht = nullptr, *bin_of = nullptr;
+        uint32_t *bounds = nullptr, *flag = nullptr, *par4 = nullptr, *counter = nullptr;
         uint64_t* keys = nullptr;
         int* depth = nullptr;
         hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -403,7 +492,8 @@ int mesh_bvh_build(const pbrt_scene_desc* s, hipStream_t st, MeshBuild& out, std
                     if (*e) (void)hipEventDestroy(*e);
             }
         } temps{{(void**)&tris, (void**)&gid, (void**)&cen, (void**)&bounds, (void**)&keys, (void**)&cl, (void**)&cr,
-                 (void**)&par, (void**)&rfirst, (void**)&box, (void**)&tc, (void**)&sz, (void**)&flag, (void**)&depth},
+                 (void**)&par, (void**)&rfirst, (void**)&box, (void**)&tc, (void**)&sz, (void**)&flag, (void**)&depth,
+                 (void**)&ht, (void**)&bin_of, (void**)&par4, (void**)&counter},
                 {&e0, &e1}};
         int npad = 2048;
         while (npad < n) npad <<= 1;
@@ -434,6 +524,7 @@ int mesh_bvh_build(const pbrt_scene_desc* s, hipStream_t st, MeshBuild& out, std
         MB_CHK(dmalloc(&box, (size_t)(2 * n) * 6));
         MB_CHK(dmalloc(&tc, (size_t)2 * n));
         MB_CHK(dmalloc(&sz, (size_t)2 * n));
+        MB_CHK(dmalloc(&ht, (size_t)2 * n));
         MB_CHK(dmalloc(&flag, (size_t)n));
         MB_CHK(dmalloc(&depth, 1));
         MB_CHK(hipMemcpyAsync(tris, V.data(), sizeof(float) * V.size(), hipMemcpyHostToDevice, st));
@@ -455,17 +546,52 @@ int mesh_bvh_build(const pbrt_scene_desc* s, hipStream_t st, MeshBuild& out, std
         if (n > 1)
             hipLaunchKernelGGL(k_karras, dim3((unsigned)((n - 1 + kB - 1) / kB)), dim3(kB), 0, st, keys, n, cl, cr,
                                par, rfirst);
-        hipLaunchKernelGGL(k_up, dim3(gb), dim3(kB), 0, st, out.tris, n, cl, cr, par, box, tc, sz, flag);
+        hipLaunchKernelGGL(k_up, dim3(gb), dim3(kB), 0, st, out.tris, n, cl, cr, par, box, tc, sz, ht, flag);
         MB_CHK(hipGetLastError());
+#if PBRT_MESH_WIDE
+        {
+            const uint32_t cap = (uint32_t)std::max(n - 1, 1);   // one wide node per kept inner binary node
+            const uint32_t one = 1, none = kMeshEmpty;
+            MB_CHK(dmalloc(&bin_of, (size_t)cap));
+            MB_CHK(dmalloc(&par4, (size_t)cap));
+            MB_CHK(dmalloc(&counter, 1));
+            MB_CHK(dmalloc(reinterpret_cast<MeshNode4**>(&out.nodes), (size_t)cap));
+            MB_CHK(hipMemsetAsync(bin_of, 0, sizeof(int32_t), st));   // the root: binary node 0
+            MB_CHK(hipMemcpyAsync(par4, &none, sizeof(uint32_t), hipMemcpyHostToDevice, st));
+            MB_CHK(hipMemcpyAsync(counter, &one, sizeof(uint32_t), hipMemcpyHostToDevice, st));
+            uint32_t b = 0, e = 1;
+            int levels = 0;
+            while (b < e) {
+                if (++levels > kMeshWideLevels) {
+                    err = "mesh BVH: wide tree deeper than 32 levels";
+                    mesh_bvh_free(out);
+                    return PBRT_E_UNSUPPORTED;
+                }
+                hipLaunchKernelGGL(k_collapse, dim3((e - b + kB - 1) / kB), dim3(kB), 0, st, n, cl, cr, box, tc, ht,
+                                   bin_of, par4, b, e, counter, reinterpret_cast<MeshNode4*>(out.nodes));
+                MB_CHK(hipGetLastError());
+                uint32_t next = 0;
+                MB_CHK(hipMemcpyAsync(&next, counter, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+                MB_CHK(hipStreamSynchronize(st));
+                b = e;
+                e = next;
+            }
+            n_out = (int)e;
+            out.depth = levels;
+        }
+#else
         MB_CHK(hipMemcpyAsync(&n_out, sz, sizeof(int32_t), hipMemcpyDeviceToHost, st));   // root = node 0
         MB_CHK(hipStreamSynchronize(st));
         MB_CHK(dmalloc(&out.nodes, (size_t)kMeshOrders * n_out + kMeshPad));
         MB_CHK(hipMemsetAsync(out.nodes + (size_t)kMeshOrders * n_out, 0, sizeof(MeshNode) * kMeshPad, st));
         hipLaunchKernelGGL(k_flatten, dim3((unsigned)((2 * n - 1 + kB - 1) / kB)), dim3(kB), 0, st, n, cl, cr, par,
                            rfirst, box, tc, sz, n_out, out.nodes, depth);
+#endif
         MB_CHK(hipEventRecord(e1, st));
         MB_CHK(hipGetLastError());
+#if !PBRT_MESH_WIDE
         MB_CHK(hipMemcpyAsync(&out.depth, depth, sizeof(int), hipMemcpyDeviceToHost, st));
+#endif
         MB_CHK(hipStreamSynchronize(st));
         {
             float ms = 0;

@@ -28,6 +28,8 @@
 #pragma once
 #pragma clang fp contract(off)
 
+#include <cstring>
+
 #include "pbrt_core.h"
 
 namespace pbrt {
@@ -47,8 +49,46 @@ constexpr int kMeshLeafMax = PBRT_MESH_LEAF_MAX;   // triangles per leaf (subtre
 constexpr int kMeshOrders = 8;    // threaded orderings, one per ray-direction octant
 constexpr int kMeshPad = 2;       // nodes allocated past the last ordering (mesh_walk's look-ahead loads)
 
+// Wide layout (build option PBRT_MESH_WIDE, default off: measured slower): a 4-ary tree
+// collapsed from the same LBVH, one array for every ray. A node holds its up
+// to four children's boxes (structure of arrays, so a visit is eight 16-byte
+// loads and four independent slab tests), their child words, its parent and
+// the axis along which the children are stored in ascending centre order.
+// A ray visits the hit children front to back along that axis (ascending for
+// a non-negative direction component) and keeps, per level, a 4-bit mask of
+// the hit children still to visit (the trail: 32 levels in two 64-bit words);
+// going back up reads the parent's last 32 bytes (child words, parent, axis).
+// Triangles are child slots (one per slot: every triangle box is tested before
+// its triangle). The builder guarantees <= kMeshWideLevels levels.
+// Config D (float32 box tests, batched triangle tests): frame 1139 ms (chain
+// 876) against the binary threaded walk's 723 ms (chain 547). A wide visit
+// moves 128 B and tests four boxes; the binary walk's next node is mostly the
+// next 32 bytes of the line it already holds (depth-first threading), and its
+// 84 steps per closest walk cost less than the wide walk's ~25 visits + ~18
+// steps back up (profiles/r05/mesh_wide/).
+#ifndef PBRT_MESH_WIDE
+#define PBRT_MESH_WIDE 0
+#endif
+struct alignas(16) MeshNode4 {
+    float lo[3][4];        // [axis][child slot]
+    float hi[3][4];
+    uint32_t child[4];     // node index, kMeshTri | triangle slot, or kMeshEmpty
+    uint32_t parent;       // kMeshEmpty at the root
+    uint32_t axis;         // children stored in ascending centre order along it
+    uint32_t count;        // children (slots count..3 are empty)
+    uint32_t pad;
+};
+static_assert(sizeof(MeshNode4) == 128, "MeshNode4 is eight 16-byte loads");
+constexpr uint32_t kMeshTri = 0x80000000u;
+constexpr uint32_t kMeshEmpty = 0xFFFFFFFFu;
+constexpr int kMeshWideLevels = 32;
+// bytes of a scene's node array(s) of n_nodes nodes
+constexpr size_t mesh_node_bytes(int n_nodes) {
+    return PBRT_MESH_WIDE ? (size_t)n_nodes * sizeof(MeshNode4) : (size_t)n_nodes * kMeshOrders * sizeof(MeshNode);
+}
+
 struct DevMesh {
-    const MeshNode* nodes;       // [kMeshOrders][n_nodes]
+    const MeshNode* nodes;       // [kMeshOrders][n_nodes] (wide: MeshNode4 [n_nodes])
     const float* tris;           // [n_tris][9]
     const int32_t* gid;          // [n_tris]
     const int32_t* mesh_first;   // [n_meshes + 1] first global index of each mesh
@@ -127,18 +167,10 @@ GO_HD int mesh_ordering(V3 d) {
     return ((d.x < 0 ? 1 : 0) | (d.y < 0 ? 2 : 0) | (d.z < 0 ? 4 : 0)) & PBRT_MESH_ORDER_MASK;
 }
 
-#ifdef __HIPCC__
-__device__ __forceinline__ void load_tri(const float* __restrict__ tris, uint32_t slot, double v[9]) {
-    const float* q = tris + (size_t)slot * 9;
-#pragma unroll
-    for (int k = 0; k < 9; k++) v[k] = (double)q[k];
-}
-
 // Slab test of a float32 box (rounded out), inclusive of tmax so a triangle at
 // exactly the current TMax with a smaller index is never culled. An axis with
 // d == 0 (inverse +-Inf) constrains only through the origin's position.
-__device__ __forceinline__ bool mesh_box_hit(const float* bmin, const float* bmax, const Ray& r, V3 inv,
-                                             int zero_mask, double tmax) {
+GO_HD bool mesh_box_hit(const float* bmin, const float* bmax, const Ray& r, V3 inv, int zero_mask, double tmax) {
     const double robust = 1 + 2 * tri_gamma(3);
     double t0 = 0, t1 = kInf;
     const double o[3] = {r.o.x, r.o.y, r.o.z}, iv[3] = {inv.x, inv.y, inv.z};
@@ -161,6 +193,89 @@ __device__ __forceinline__ bool mesh_box_hit(const float* bmin, const float* bma
     return t0 <= t1 && t0 <= tmax;
 }
 
+// Box tests in float32 (build option PBRT_MESH_F32, default on): an interval
+// that contains the float64 test's [n, f * robust] above, so the float32 test
+// culls no box the float64 test keeps (and the closest hit, the smallest (t,
+// index) over the triangles whose boxes pass, is unchanged). Per slab, with
+// o32 = fl32(o) and iv32 = fl32(iv), the float32 n32 = fl32(fl32(l - o32) iv32)
+// differs from the float64 n64 = fl64(fl64(l - o) iv) by at most
+// 3.01 * 2^-24 |n32| + 1.0001 * 2^-24 |o iv| (three float32 roundings, the
+// origin's rounding, two float64 roundings); the test widens each bound by
+// m = 2^-20 (|x| + |o32 iv32|) + 1e-35 (16x that, plus the rounding of the
+// widening itself and of underflow), and compares with fl32 of TMax rounded
+// up. A zero direction component keeps the origin-only test: rounding to
+// nearest keeps o32 inside [l, h] whenever o is (l and h are float32).
+// Rays with a nonzero |d_i| outside [1e-30, 1e30] take the float64 test.
+#ifndef PBRT_MESH_F32
+#define PBRT_MESH_F32 1
+#endif
+struct MeshRay32 {
+    float o[3], iv[3], m0[3];   // fl32(o), fl32(1/d), 2^-20 |o32 iv32| + 1e-35
+    float tmax_hi;              // fl32(TMax) rounded up
+    int zero_mask;
+    bool ok;                    // the float32 test applies
+};
+GO_HD float mesh_f32_up(double t) {
+    const float f = (float)t;
+    if (!((double)f < t)) return f;
+    if (f == 0) return 0x1p-149f;   // the smallest positive float
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    u = f > 0 ? u + 1 : u - 1;   // the next float up
+    float g;
+    std::memcpy(&g, &u, 4);
+    return g;
+}
+GO_HD MeshRay32 mesh_ray32(const Ray& r, int zero_mask, double tmax) {
+    MeshRay32 q;
+    const double o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
+    q.ok = true;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const double ad = d[a] < 0 ? -d[a] : d[a];
+        q.ok = q.ok && (ad == 0 || (ad >= 1e-30 && ad <= 1e30));
+        q.o[a] = (float)o[a];
+        q.iv[a] = (float)(1 / d[a]);
+        const float oi = q.o[a] * q.iv[a];
+        q.m0[a] = (zero_mask >> a) & 1 ? 0.0f : 0x1p-20f * (oi < 0 ? -oi : oi) + 1e-35f;
+    }
+    q.tmax_hi = mesh_f32_up(tmax);
+    q.zero_mask = zero_mask;
+    return q;
+}
+GO_HD bool mesh_box32_hit(const float* bmin, const float* bmax, const MeshRay32& q) {
+    float t0 = 0, t1 = __builtin_inff();
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const float x = (bmin[a] - q.o[a]) * q.iv[a], y = (bmax[a] - q.o[a]) * q.iv[a];
+        float n = x < y ? x : y, f = x < y ? y : x;
+        n = n - (0x1p-20f * (n < 0 ? -n : n) + q.m0[a]);
+        f = f + (0x1p-20f * (f < 0 ? -f : f) + q.m0[a]);
+        const bool in = bmin[a] <= q.o[a] && q.o[a] <= bmax[a];
+        const bool zero = (q.zero_mask >> a) & 1;
+        n = zero ? (in ? -__builtin_inff() : __builtin_inff()) : n;
+        f = zero ? (in ? __builtin_inff() : -__builtin_inff()) : f;
+        t0 = n > t0 ? n : t0;
+        t1 = f < t1 ? f : t1;
+    }
+    return t0 <= t1 && t0 <= q.tmax_hi;
+}
+// the box test a walk runs: float32 where it applies, else float64
+GO_HD bool mesh_box_test(const float* bmin, const float* bmax, const Ray& r, V3 inv, int zero_mask, double tmax,
+                         const MeshRay32& q) {
+#if PBRT_MESH_F32
+    if (q.ok) return mesh_box32_hit(bmin, bmax, q);
+#endif
+    return mesh_box_hit(bmin, bmax, r, inv, zero_mask, tmax);
+}
+
+#ifdef __HIPCC__
+__device__ __forceinline__ void load_tri(const float* __restrict__ tris, uint32_t slot, double v[9]) {
+    const float* q = tris + (size_t)slot * 9;
+#pragma unroll
+    for (int k = 0; k < 9; k++) v[k] = (double)q[k];
+}
+
 // Leaf tests batched across the wave (build option PBRT_MESH_BATCH, default on).
 // With one-triangle leaves about one node visit in 17 is a leaf, so in a
 // 64-lane wave nearly every step of a per-lane walk has some lane at a leaf,
@@ -173,12 +288,292 @@ __device__ __forceinline__ bool mesh_box_hit(const float* bmin, const float* bma
 #ifndef PBRT_MESH_BATCH
 #define PBRT_MESH_BATCH 1
 #endif
+#ifndef PBRT_MESH_BATCH_Q8
+#define PBRT_MESH_BATCH_Q8 2   // the batch runs once Q8/8 of the live lanes wait with a leaf (build option; D chain 567 / 612 / 771 / 1201 ms at Q8 = 2 / 4 / 6 / 8)
+#endif
+static_assert(PBRT_MESH_BATCH_Q8 >= 1, "a batch needs a waiting lane");
 
 // Closest (kAny = false) or any (kAny) triangle of the scene's meshes.
 // Closest: a hit must have t < tmax, or t == tmax and a smaller global index
 // than best_gid (-1: nothing of the meshes yet, TMax exclusive). On return
 // tmax, best_slot and best_gid describe the winner; returns whether any
 // triangle won. Any: returns true on the first triangle with t < tmax.
+#if PBRT_MESH_WIDE
+__device__ __forceinline__ uint32_t u4_at(const uint4& v, int k) {
+    return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
+}
+
+// Slab test of child slot k of a wide node (the binary test's arithmetic);
+// nf: the node as 32 floats (lo[a][k] at 4a + k, hi[a][k] at 12 + 4a + k).
+__device__ __forceinline__ bool mesh_box4_hit(const float* __restrict__ nf, uint32_t k, const double* o,
+                                              const double* iv, int zero_mask, double tmax) {
+    const double robust = 1 + 2 * tri_gamma(3);
+    double t0 = 0, t1 = kInf;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const double l = (double)nf[4 * a + k], h = (double)nf[12 + 4 * a + k];
+        double n, f;
+        if (zero_mask & (1 << a)) {
+            const bool in = l <= o[a] && o[a] <= h;
+            n = in ? -kInf : kInf;
+            f = in ? kInf : -kInf;
+        } else {
+            const double x = (l - o[a]) * iv[a], y = (h - o[a]) * iv[a];
+            n = x < y ? x : y;
+            f = (x < y ? y : x) * robust;
+        }
+        t0 = n > t0 ? n : t0;
+        t1 = f < t1 ? f : t1;
+    }
+    return t0 <= t1 && t0 <= tmax;
+}
+
+// A whole wide-node visit: the node's eight 16-byte loads issued together, the
+// four slab tests without branches (the same arithmetic as mesh_box4_hit; a
+// zero direction component's axis selects the origin-only test), the hit
+// slots (below `count`) and which of them are triangles.
+__device__ __forceinline__ void mesh_visit4(const MeshNode4* __restrict__ node, const double* o, const double* iv,
+                                            int zero_mask, double tmax, const MeshRay32& r32, uint4& ch, uint4& meta,
+                                            uint32_t& hit, uint32_t& tri) {
+    const uint4* q = reinterpret_cast<const uint4*>(node);
+    const uint4 L[3] = {q[0], q[1], q[2]}, H[3] = {q[3], q[4], q[5]};
+    ch = q[6];
+    meta = q[7];
+    const double robust = 1 + 2 * tri_gamma(3);
+    hit = 0;
+#if PBRT_MESH_F32
+    if (r32.ok) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const float bmin[3] = {__uint_as_float(u4_at(L[0], k)), __uint_as_float(u4_at(L[1], k)),
+                                   __uint_as_float(u4_at(L[2], k))};
+            const float bmax[3] = {__uint_as_float(u4_at(H[0], k)), __uint_as_float(u4_at(H[1], k)),
+                                   __uint_as_float(u4_at(H[2], k))};
+            hit |= mesh_box32_hit(bmin, bmax, r32) ? 1u << k : 0u;
+        }
+    } else
+#endif
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        double t0 = 0, t1 = kInf;
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            const double l = (double)__uint_as_float(u4_at(L[a], k)), h = (double)__uint_as_float(u4_at(H[a], k));
+            const double x = (l - o[a]) * iv[a], y = (h - o[a]) * iv[a];
+            double n = x < y ? x : y, f = (x < y ? y : x) * robust;
+            const bool in = l <= o[a] && o[a] <= h;
+            const bool zero = (zero_mask >> a) & 1;
+            n = zero ? (in ? -kInf : kInf) : n;
+            f = zero ? (in ? kInf : -kInf) : f;
+            t0 = n > t0 ? n : t0;
+            t1 = f < t1 ? f : t1;
+        }
+        hit |= (t0 <= t1 && t0 <= tmax) ? 1u << k : 0u;
+    }
+    hit &= (1u << meta.z) - 1u;
+    tri = hit & (((ch.x >> 31) << 0) | ((ch.y >> 31) << 1) | ((ch.z >> 31) << 2) | ((ch.w >> 31) << 3));
+}
+
+// kLean: one child's box at a time (the copy that kernels over analytic
+// scenes carry for mixed scenes, where the four boxes' registers would raise
+// the kernel's peak); else the four boxes' loads are issued together.
+template <bool kAny, bool kLean = false>
+__device__ inline bool mesh_walk(const DevMesh& m, const Ray& ray, double& tmax, int32_t& best_slot,
+                                 int32_t& best_gid) {
+    if (m.n_nodes == 0) return false;
+    const MeshNode4* __restrict__ N = reinterpret_cast<const MeshNode4*>(m.nodes);
+    const double o[3] = {ray.o.x, ray.o.y, ray.o.z};
+    const double iv[3] = {1 / ray.d.x, 1 / ray.d.y, 1 / ray.d.z};
+    const int zero_mask = (ray.d.x == 0 ? 1 : 0) | (ray.d.y == 0 ? 2 : 0) | (ray.d.z == 0 ? 4 : 0);
+    const int neg = (ray.d.x < 0 ? 1 : 0) | (ray.d.y < 0 ? 2 : 0) | (ray.d.z < 0 ? 4 : 0);
+    bool found = false;
+    uint32_t cur = 0, par = kMeshEmpty;
+    uint64_t tr0 = 0, tr1 = 0;   // the trail: 4-bit masks, the deepest level in tr0's low bits
+    int depth = 0;
+    MeshRay32 q32 = mesh_ray32(ray, zero_mask, tmax);
+#ifdef PBRT_MESH_COUNT
+    unsigned long long c_nodes = 0, c_tris = 0;   // c_nodes in 32-byte blocks
+    struct Flush {
+        int slot;
+        unsigned long long &nn, &tt;
+        __device__ ~Flush() {
+            if (slot > 0 && slot < kMeshCountSlots) {
+                atomicAdd(&g_mesh_count[slot][kAny ? 1 : 0][0], 1ull);
+                atomicAdd(&g_mesh_count[slot][kAny ? 1 : 0][1], nn);
+                atomicAdd(&g_mesh_count[slot][kAny ? 1 : 0][2], tt);
+            }
+        }
+    } flush{m.count_slot, c_nodes, c_tris};
+#define MESH_COUNT(x) x
+#else
+#define MESH_COUNT(x)
+#endif
+#if PBRT_MESH_BATCH
+    if constexpr (!kLean) {
+        // Triangle tests batched across the wave, as in the binary walk: a lane
+        // whose visit hits triangle slots waits with them (pnode, ptri) and the
+        // node's hit inner children (pin); the wave tests the waiting lanes'
+        // triangles together once Q8/8 of its live lanes wait or no lane can
+        // move. A move is one node visit or one level back up.
+        bool up = false, done = false;
+        uint32_t pnode = 0, ptri = 0, pin = 0;
+        auto go_down = [&](uint32_t axis, const uint4& ch, uint32_t inner) {
+            if (!inner) {
+                up = true;
+                return;
+            }
+            const int s = ((neg >> axis) & 1) ? 31 - __clz(inner) : __ffs(inner) - 1;
+            tr1 = (tr1 << 4) | (tr0 >> 60);
+            tr0 = (tr0 << 4) | (inner & ~(1u << s));
+            depth++;
+            cur = u4_at(ch, s);
+        };
+        for (;;) {
+            for (;;) {
+                const bool moving = !done && ptri == 0;
+                const unsigned long long mw = __ballot(moving);
+                if (mw == 0) break;
+                const unsigned long long mp = __ballot(ptri != 0), ml = mw | mp;
+                if (8 * __popcll(mp) >= PBRT_MESH_BATCH_Q8 * __popcll(ml)) break;
+                if (!moving) continue;
+                if (up) {
+                    if (depth == 0) {
+                        done = true;
+                        continue;
+                    }
+                    const uint32_t rest = (uint32_t)tr0 & 15u;
+                    const uint4* pq = reinterpret_cast<const uint4*>(N + par);
+                    const uint4 pch = pq[6], pmeta = pq[7];
+                    MESH_COUNT(c_nodes += 1;)
+                    if (rest) {
+                        const int s = ((neg >> pmeta.y) & 1) ? 31 - __clz(rest) : __ffs(rest) - 1;
+                        tr0 &= ~(uint64_t)(1u << s);
+                        cur = u4_at(pch, s);
+                        up = false;
+                    } else {
+                        tr0 = (tr0 >> 4) | (tr1 << 60);
+                        tr1 >>= 4;
+                        depth--;
+                        par = pmeta.x;
+                    }
+                    continue;
+                }
+                uint4 ch, meta;
+                uint32_t hit, tri;
+                mesh_visit4(N + cur, o, iv, zero_mask, tmax, q32, ch, meta, hit, tri);
+                MESH_COUNT(c_nodes += 4;)
+                par = meta.x;
+                if (tri) {
+                    pnode = cur;
+                    ptri = tri;
+                    pin = hit & ~tri;
+                } else {
+                    go_down(meta.y, ch, hit);
+                }
+            }
+            if (!__any(ptri != 0)) break;
+            if (ptri != 0) {   // the batch
+                const uint4* q = reinterpret_cast<const uint4*>(N + pnode);
+                const uint4 ch = q[6], meta = q[7];
+                for (uint32_t h = ptri; h; h &= h - 1) {
+                    const uint32_t slot = u4_at(ch, __ffs(h) - 1) & ~kMeshTri;
+                    double v[9], t, b0, b1, b2;
+                    load_tri(m.tris, slot, v);
+                    MESH_COUNT(c_tris++;)
+                    if (!tri_hit(v, ray, t, b0, b1, b2)) continue;
+                    if (kAny) {
+                        if (t < tmax) {
+                            found = true;
+                            done = true;
+                            break;
+                        }
+                        continue;
+                    }
+                    if (t < tmax || (t == tmax && m.gid[slot] < best_gid)) {
+                        tmax = t;
+                        q32.tmax_hi = mesh_f32_up(t);
+                        best_slot = (int32_t)slot;
+                        best_gid = m.gid[slot];
+                        found = true;
+                    }
+                }
+                ptri = 0;
+                if (!done) go_down(meta.y, ch, pin);
+            }
+        }
+        return found;
+    }
+#endif
+    for (;;) {
+        // visit node cur: test its children's boxes, its triangles, then go
+        // down to the nearest hit child node
+        const float* __restrict__ nf = reinterpret_cast<const float*>(N + cur);
+        const uint32_t* __restrict__ nu = reinterpret_cast<const uint32_t*>(N + cur);
+        MESH_COUNT(c_nodes += 4;)
+        par = nu[28];
+        const uint32_t axis = nu[29], nch = nu[30];
+        uint32_t hit = 0;
+        if constexpr (kLean) {
+#pragma unroll 1
+            for (uint32_t k = 0; k < nch; k++)
+                if (mesh_box4_hit(nf, k, o, iv, zero_mask, tmax)) hit |= 1u << k;
+        } else {
+            uint4 ch, meta;
+            uint32_t tri;
+            mesh_visit4(N + cur, o, iv, zero_mask, tmax, q32, ch, meta, hit, tri);
+        }
+        uint32_t inner = 0;
+        for (uint32_t h = hit; h; h &= h - 1) {
+            const uint32_t k = (uint32_t)__ffs(h) - 1, c = nu[24 + k];
+            if (!(c & kMeshTri)) {
+                inner |= 1u << k;
+                continue;
+            }
+            const uint32_t slot = c & ~kMeshTri;
+            double v[9], t, b0, b1, b2;
+            load_tri(m.tris, slot, v);
+            MESH_COUNT(c_tris++;)
+            if (!tri_hit(v, ray, t, b0, b1, b2)) continue;
+            if (kAny) {
+                if (t < tmax) return true;
+                continue;
+            }
+            if (t < tmax || (t == tmax && m.gid[slot] < best_gid)) {
+                tmax = t;
+                q32.tmax_hi = mesh_f32_up(t);
+                best_slot = (int32_t)slot;
+                best_gid = m.gid[slot];
+                found = true;
+            }
+        }
+        if (inner) {
+            const int s = ((neg >> axis) & 1) ? 31 - __clz(inner) : __ffs(inner) - 1;
+            tr1 = (tr1 << 4) | (tr0 >> 60);
+            tr0 = (tr0 << 4) | (inner & ~(1u << s));
+            depth++;
+            cur = nu[24 + s];
+            continue;
+        }
+        // back up: the deepest level with a hit child left
+        for (;;) {
+            if (depth == 0) return found;
+            const uint32_t rest = (uint32_t)tr0 & 15u;
+            const uint32_t* __restrict__ pu = reinterpret_cast<const uint32_t*>(N + par);
+            MESH_COUNT(c_nodes += 1;)
+            if (rest) {
+                const int s = ((neg >> pu[29]) & 1) ? 31 - __clz(rest) : __ffs(rest) - 1;
+                tr0 &= ~(uint64_t)(1u << s);
+                cur = pu[24 + s];
+                break;
+            }
+            tr0 = (tr0 >> 4) | (tr1 << 60);
+            tr1 >>= 4;
+            depth--;
+            par = pu[28];
+        }
+    }
+}
+#else
 template <bool kAny>
 __device__ inline bool mesh_walk(const DevMesh& m, const Ray& ray, double& tmax, int32_t& best_slot,
                                  int32_t& best_gid) {
@@ -189,6 +584,7 @@ __device__ inline bool mesh_walk(const DevMesh& m, const Ray& ray, double& tmax,
     const uint32_t n = (uint32_t)m.n_nodes;
     bool found = false;
     uint32_t i = 0;
+    MeshRay32 q32 = mesh_ray32(ray, zero_mask, tmax);
 #ifdef PBRT_MESH_COUNT
     unsigned long long c_nodes = 0, c_tris = 0;
     struct Flush {
@@ -230,14 +626,14 @@ __device__ inline bool mesh_walk(const DevMesh& m, const Ray& ray, double& tmax,
             const unsigned long long mw = __ballot(walking);
             if (mw == 0) break;
             const unsigned long long mp = __ballot(pend != 0), ml = mw | mp;
-            if (2 * __popcll(mp) >= __popcll(ml)) break;
+            if (8 * __popcll(mp) >= PBRT_MESH_BATCH_Q8 * __popcll(ml)) break;
             if (walking) {
                 MESH_COUNT(c_nodes++;)
                 const uint4* q = reinterpret_cast<const uint4*>(N + i);
                 const uint4 a = q[0], b = q[1];
                 const float bmin[3] = {__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z)};
                 const float bmax[3] = {__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z)};
-                if (!mesh_box_hit(bmin, bmax, ray, inv, zero_mask, tmax)) {
+                if (!mesh_box_test(bmin, bmax, ray, inv, zero_mask, tmax, q32)) {
                     i = a.w;   // escape
                 } else if (b.w == kMeshInterior) {
                     i++;
@@ -266,6 +662,7 @@ __device__ inline bool mesh_walk(const DevMesh& m, const Ray& ray, double& tmax,
                 }
                 if (t < tmax || (t == tmax && m.gid[first + k] < best_gid)) {
                     tmax = t;
+                    q32.tmax_hi = mesh_f32_up(t);
                     best_slot = (int32_t)(first + k);
                     best_gid = m.gid[first + k];
                     found = true;
@@ -284,7 +681,7 @@ __device__ inline bool mesh_walk(const DevMesh& m, const Ray& ray, double& tmax,
         const float bmin[3] = {__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z)};
         const float bmax[3] = {__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z)};
         const uint32_t escape = a.w, leaf = b.w;
-        if (!mesh_box_hit(bmin, bmax, ray, inv, zero_mask, tmax)) {
+        if (!mesh_box_test(bmin, bmax, ray, inv, zero_mask, tmax, q32)) {
             i = escape;
 #ifdef PBRT_MESH_PREFETCH
             if (i < n) {
@@ -315,6 +712,7 @@ __device__ inline bool mesh_walk(const DevMesh& m, const Ray& ray, double& tmax,
             }
             if (t < tmax || (t == tmax && m.gid[first + k] < best_gid)) {
                 tmax = t;
+                q32.tmax_hi = mesh_f32_up(t);
                 best_slot = (int32_t)(first + k);
                 best_gid = m.gid[first + k];
                 found = true;
@@ -330,7 +728,19 @@ __device__ inline bool mesh_walk(const DevMesh& m, const Ray& ray, double& tmax,
     }
     return found;
 }
+#endif   // PBRT_MESH_WIDE
 #undef MESH_COUNT
+
+// the walk as kernels over scenes with analytic primitives carry it
+template <bool kAny>
+__device__ __forceinline__ bool mesh_walk_mixed(const DevMesh& m, const Ray& ray, double& tmax, int32_t& best_slot,
+                                                int32_t& best_gid) {
+#if PBRT_MESH_WIDE
+    return mesh_walk<kAny, true>(m, ray, tmax, best_slot, best_gid);
+#else
+    return mesh_walk<kAny>(m, ray, tmax, best_slot, best_gid);
+#endif
+}
 #endif
 
 }  // namespace pbrt

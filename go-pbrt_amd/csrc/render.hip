@@ -1672,7 +1672,7 @@ extern "C" int pbrt_gpu_counters(pbrt_gpu_ctx* c, uint64_t* out, int n) {
 extern "C" int pbrt_gpu_mesh_info(pbrt_gpu_ctx* c, double* out, int n) {
     if (!c || !out) return -PBRT_E_INVALID;
     const double v[] = {(double)c->mesh.n_tris, (double)c->mesh.n_nodes, (double)c->mesh.depth, c->mesh.build_ms,
-                        (double)c->mesh.n_meshes};
+                        (double)c->mesh.n_meshes, (double)PBRT_MESH_WIDE};
     const int m = (int)(sizeof(v) / sizeof(v[0]));
     for (int i = 0; i < n && i < m; i++) out[i] = v[i];
     return m;
@@ -1696,8 +1696,8 @@ extern "C" int pbrt_gpu_mesh_counters(uint64_t* out, int n, int reset) {
 extern "C" int pbrt_gpu_mesh_download(pbrt_gpu_ctx* c, void* nodes, int32_t* gid, float* tris) {
     if (!c) return PBRT_E_INVALID;
     if (hipSetDevice(c->device) != hipSuccess) return PBRT_E_HIP;
-    const size_t nn = (size_t)c->mesh.n_nodes * kMeshOrders, nt = (size_t)c->mesh.n_tris;
-    if (nodes && nn && hipMemcpy(nodes, c->mesh.nodes, nn * sizeof(MeshNode), hipMemcpyDeviceToHost) != hipSuccess)
+    const size_t nn = mesh_node_bytes(c->mesh.n_nodes), nt = (size_t)c->mesh.n_tris;
+    if (nodes && nn && hipMemcpy(nodes, c->mesh.nodes, nn, hipMemcpyDeviceToHost) != hipSuccess)
         return PBRT_E_HIP;
     if (gid && nt && hipMemcpy(gid, c->mesh.gid, nt * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
         return PBRT_E_HIP;

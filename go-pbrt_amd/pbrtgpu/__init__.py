@@ -405,25 +405,32 @@ class Renderer:
         return lib().pbrt_gpu_stream(self.h)
 
     def mesh_info(self):
-        """{tris, nodes, depth, build_ms, meshes} of the context's device LBVH."""
+        """{tris, nodes, depth, build_ms, meshes, wide} of the context's device LBVH
+        (wide: the 4-ary layout, MeshNode4; else eight threaded binary orderings)."""
         out = (C.c_double * 8)()
         lib().pbrt_gpu_mesh_info(self.h, out, 8)
         return {"tris": int(out[0]), "nodes": int(out[1]), "depth": int(out[2]), "build_ms": out[3],
-                "meshes": int(out[4])}
+                "meshes": int(out[4]), "wide": bool(out[5])}
 
     def mesh_download(self):
-        """(nodes [8, n] structured array, gid [tris], tris [tris, 9]) of the device LBVH."""
+        """(nodes, gid [tris], tris [tris, 9]) of the device LBVH; nodes is a [n]
+        MeshNode4 structured array for the wide layout, else [8, n] MeshNode."""
         info = self.mesh_info()
-        dt = np.dtype([("bmin", np.float32, 3), ("escape", np.uint32), ("bmax", np.float32, 3),
-                       ("leaf", np.uint32)])
-        nodes = np.zeros(8 * info["nodes"], dtype=dt)
+        if info["wide"]:
+            dt = np.dtype([("lo", np.float32, (3, 4)), ("hi", np.float32, (3, 4)), ("child", np.uint32, 4),
+                           ("parent", np.uint32), ("axis", np.uint32), ("count", np.uint32), ("pad", np.uint32)])
+            nodes = np.zeros(info["nodes"], dtype=dt)
+        else:
+            dt = np.dtype([("bmin", np.float32, 3), ("escape", np.uint32), ("bmax", np.float32, 3),
+                           ("leaf", np.uint32)])
+            nodes = np.zeros(8 * info["nodes"], dtype=dt)
         gid = np.zeros(info["tris"], dtype=np.int32)
         tris = np.zeros((info["tris"], 9), dtype=np.float32)
         rc = lib().pbrt_gpu_mesh_download(self.h, nodes.ctypes.data_as(C.c_void_p),
                                           gid.ctypes.data_as(C.POINTER(C.c_int32)),
                                           tris.ctypes.data_as(C.POINTER(C.c_float)))
         self._check(rc)
-        return nodes.reshape(8, info["nodes"]), gid, tris
+        return (nodes if info["wide"] else nodes.reshape(8, info["nodes"])), gid, tris
 
     def tile_ticks(self):
         """(per-slot chain ticks of the last EXACT frame at 100 MHz, heavy slots of its split)."""

@@ -34,6 +34,49 @@ def mesh_tris(scene):
     return p[idx].reshape(-1, 9)
 
 
+def check_wide_tree(nodes, tris, nt, info):
+    """The 4-ary layout (pbrt_mesh.h MeshNode4): one tree; every node but the
+    root is the child of exactly one node and names it as parent; slots
+    0..count-1 hold a node or a triangle, the rest are empty; child boxes
+    contain their subtree's boxes and triangles; the slots are in ascending
+    centre order along the node's axis; every triangle is one slot; the depth
+    is the builder's level count and at most 32."""
+    EMPTY, TRI = 0xFFFFFFFF, 0x80000000
+    n = len(nodes)
+    assert n >= 1 and nodes[0]["parent"] == EMPTY
+    seen = np.zeros(n, dtype=np.int32)
+    covered = np.zeros(nt, dtype=np.int32)
+    levels = 0
+    stack = [(0, 1, None)]
+    while stack:
+        i, lev, box = stack.pop()
+        seen[i] += 1
+        levels = max(levels, lev)
+        nd = nodes[i]
+        cnt, ax = int(nd["count"]), int(nd["axis"])
+        assert 1 <= cnt <= 4 and ax < 3
+        lo, hi = nd["lo"], nd["hi"]   # [3][4]
+        if box is not None:
+            assert (lo[:, :cnt] >= box[0][:, None]).all() and (hi[:, :cnt] <= box[1][:, None]).all()
+        cen = lo[ax, :cnt] + hi[ax, :cnt]
+        assert (np.diff(cen) >= 0).all()
+        for k in range(4):
+            c = int(nd["child"][k])
+            if k >= cnt:
+                assert c == EMPTY
+                continue
+            if c & TRI:
+                s = c & ~TRI
+                covered[s] += 1
+                t = tris[s].reshape(3, 3)
+                assert (t >= lo[:, k]).all() and (t <= hi[:, k]).all()
+            else:
+                assert 0 < c < n and nodes[c]["parent"] == i
+                stack.append((c, lev + 1, (lo[:, k], hi[:, k])))
+    assert (seen == 1).all() and (covered == 1).all()
+    assert levels == info["depth"] <= 32
+
+
 @pytest.mark.parametrize("quads", [1, 2, 3, 16, 100])
 def test_lbvh_structure(quads):
     """Every ordering is a depth-first threading of one binary tree: leaves
@@ -50,6 +93,9 @@ def test_lbvh_structure(quads):
     assert sorted(gid.tolist()) == list(range(nt))
     assert np.array_equal(tris, tris_in[gid])
     n = info["nodes"]
+    if info["wide"]:
+        check_wide_tree(nodes, tris, nt, info)
+        return
     assert nodes.shape == (8, n) and n >= 1
     recs = None
     for o in range(8):

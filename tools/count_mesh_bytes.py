@@ -1,7 +1,8 @@
 """Algorithmic HBM bytes of the mesh traversal (configs D/E), per kernel: one
 frame rendered with the counting build (make -C go-pbrt_amd meshcount), whose
-mesh walks count the nodes they fetch (32 B each) and the triangles they test
-(36 B each). Needs a GPU. The result is committed under profiles/ and read by
+mesh walks count the node bytes they fetch in 32-byte blocks (a binary node is
+one block; a wide node visit reads four, going back up through a wide parent
+one) and the triangles they test (36 B each). Needs a GPU. The result is committed under profiles/ and read by
 bench.py --config D for the HBM roofline (achieved = these bytes / the
 kernel's measured time).
 
@@ -49,8 +50,10 @@ def main():
     out = {"scene": f"heightfield quads={a.quads} seed=1", "triangles": info["tris"], "nodes": info["nodes"],
            "depth": info["depth"], "width": a.width, "height": a.height, "sampler": f"Stratified({a.spp},{a.spp})",
            "mode": a.mode, "paths": int(st.paths_traced), "tiles": a.shard or "all", "bytes_per_node": 32, "bytes_per_triangle": 36,
-           "definition": "per launch: nodes fetched x 32 B + triangles tested x 36 B over every mesh walk "
-                         "of the kernel (libpbrt_gpu_meshcount.so counters)", "kernels": {}}
+           "layout": "wide (MeshNode4, 128 B)" if info.get("wide") else "binary (8 threaded orderings, 32 B)",
+           "definition": "per launch: node blocks fetched x 32 B + triangles tested x 36 B over every mesh "
+                         "walk of the kernel (libpbrt_gpu_meshcount.so counters; 'nodes' counts 32-byte "
+                         "blocks: a wide node visit is 4, a wide parent read 1)", "kernels": {}}
     for slot, name in SLOTS.items():
         k = {}
         for q, qn in ((0, "closest"), (1, "any")):
