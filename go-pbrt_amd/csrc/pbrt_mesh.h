@@ -289,7 +289,7 @@ __device__ __forceinline__ void load_tri(const float* __restrict__ tris, uint32_
 #define PBRT_MESH_BATCH 1
 #endif
 #ifndef PBRT_MESH_BATCH_Q8
-#define PBRT_MESH_BATCH_Q8 2   // the batch runs once Q8/8 of the live lanes wait with a leaf (build option; D chain 567 / 612 / 771 / 1201 ms at Q8 = 2 / 4 / 6 / 8)
+#define PBRT_MESH_BATCH_Q8 2   // the batch runs once Q8/8 of the live lanes wait with a leaf (build option; D chain with float64 boxes 567 / 612 / 771 / 1201 ms at Q8 = 2 / 4 / 6 / 8, with float32 boxes 564 / 547 / 555 ms at Q8 = 1 / 2 / 3)
 #endif
 static_assert(PBRT_MESH_BATCH_Q8 >= 1, "a batch needs a waiting lane");
 
