@@ -21,7 +21,7 @@ namespace pbrtk {
 // recorded RR decisions; see kRrFlag)
 template <bool kX>
 __device__ __forceinline__ uint32_t ring_d(const Cursor& c, const SpecSampler& ss, uint32_t d) {
-    if (!kX || c.rri < 0 || d == kBadExactD || ss.rrb[c.rri].n == 0) return d;
+    if (!kX || c.rri < 0 || d == kBadExactD || c.rrn == 0) return d;
     return kRrFlag | (d == kBadSpecD ? kRrTailBad : d);
 }
 
@@ -152,6 +152,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
     bool tracing = false;
     Cursor c;
     c.rri = -1;
+    c.rrn = 0;
     c.rng.state = 0;
     c.rng.inc = inc;
     c.draws = 0;
@@ -291,7 +292,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
                 c.kdep = 0;
                 if constexpr (kX) {   // speculative: RR decisions on stratified values are recorded
                     c.rri = (!exact && ss.rrb) ? (int)(off & (R - 1u)) : -1;
-                    if (c.rri >= 0) ss.rrb[c.rri].n = 0;
+                    c.rrn = 0;
                 }
                 beta = spec(1);
                 eta_scale = 1.0;

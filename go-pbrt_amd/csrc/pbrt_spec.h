@@ -74,6 +74,8 @@ struct Cursor {
     int k;
     int kdep;          // a stratified value was needed while k < 0
     int rri;           // k < 0 in k_chain_ci<kX>: ss.rrb[rri] takes the RR decisions (else -1)
+    int rrn;           // decisions recorded in ss.rrb[rri] (its `n` is written with each record,
+                       // so an issue writes nothing to the record)
 };
 __device__ __forceinline__ double c_get1d(Cursor& c, const SpecSampler& s) {
     if (c.cur1d < s.ndims) {
@@ -393,10 +395,10 @@ __device__ inline int traj_scatter(const DevScene& sc, const SI& isect, const BS
             // (specular bounces draw no light sample, so RR reaches the
             // stratified dims): record the decision, continue as a survivor
             RrBranches& rb = ss.rrb[c.rri];
-            if (rb.n == (uint32_t)kRrBranches || c.draws >= (1u << 24)) return 2;
-            rb.q[rb.n] = q;
-            rb.cd[rb.n] = (c.draws << 8) | (uint32_t)c.cur1d;
-            rb.n++;
+            if (c.rrn == kRrBranches || c.draws >= (1u << 24)) return 2;
+            rb.q[c.rrn] = q;
+            rb.cd[c.rrn] = (c.draws << 8) | (uint32_t)c.cur1d;
+            rb.n = (uint32_t)++c.rrn;
             c.cur1d++;
             beta = sdivs(beta, 1 - q);
         } else {
