@@ -429,7 +429,14 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
 #endif
 #undef CI_DIAG
     if (tid == 0) {
-        if (ticks && G == 1 && bs < nslots_batch) ticks[bs] = (uint32_t)min(wall_clock64() - t_begin, (uint64_t)0xFFFFFFFFu);
+        if (ticks && G == 1 && bs < nslots_batch) {
+            const uint64_t t_end = wall_clock64();
+            ticks[bs] = (uint32_t)min(t_end - t_begin, (uint64_t)0xFFFFFFFFu);
+#ifdef PBRT_CI_DIAG   // start and end clocks (low 32 bits) for the occupancy timeline
+            ticks[nslots_batch + bs] = (uint32_t)t_begin;
+            ticks[2 * nslots_batch + bs] = (uint32_t)t_end;
+#endif
+        }
     }
 }
 

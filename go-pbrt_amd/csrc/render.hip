@@ -44,6 +44,14 @@ using namespace pbrtk;
 
 
 // =============================================================== C ABI
+// per-slot chain clocks of the last EXACT frame: durations (the schedule's
+// input), and in diagnostics builds start and end clocks (pbrt_gpu_tile_clocks)
+#ifdef PBRT_CI_DIAG
+constexpr int kTickPlanes = 3;   // durations, start clocks, end clocks
+#else
+constexpr int kTickPlanes = 1;
+#endif
+
 // Experiment knobs (environment), read ONCE when a context is created
 // (pbrt_gpu_create), never per launch; defaults are the measured best.
 struct Knobs {
@@ -169,7 +177,8 @@ struct pbrt_gpu_ctx {
     Counters* d_ctr = nullptr;
     // k_chain_ci heaviest-first schedule: per-slot chain time of the last
     // EXACT frame (wall_clock64 ticks) and the slot order derived from it
-    uint32_t* d_ticks = nullptr;
+    uint32_t* d_ticks = nullptr;         // [kTickPlanes][slots]
+    std::vector<uint32_t> h_tick_clocks; // diagnostics builds: [start | end] clocks of the last frame
     uint32_t* d_slot_order = nullptr;
     int64_t ticks_cap = 0;
     std::vector<uint32_t> h_slot_order;
@@ -1128,7 +1137,7 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                             if (c->d_slot_order) (void)hipFree(c->d_slot_order);
                             c->d_ticks = c->d_slot_order = nullptr;
                             c->ticks_cap = 0;
-                            HIPCHK(c, hipMalloc((void**)&c->d_ticks, sizeof(uint32_t) * (size_t)nb));
+                            HIPCHK(c, hipMalloc((void**)&c->d_ticks, sizeof(uint32_t) * (size_t)nb * kTickPlanes));
                             HIPCHK(c, hipMalloc((void**)&c->d_slot_order, sizeof(uint32_t) * (size_t)nb));
                             c->ticks_cap = nb;
                         }
@@ -1380,6 +1389,11 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
         std::vector<uint32_t> t((size_t)c->ticks_n);
         HIPCHK(c, hipMemcpy(t.data(), c->d_ticks, sizeof(uint32_t) * t.size(), hipMemcpyDeviceToHost));
         c->h_last_ticks = t;   // pbrt_gpu_tile_ticks
+        if (kTickPlanes > 1) {   // diagnostics builds: start and end clocks (pbrt_gpu_tile_clocks)
+            c->h_tick_clocks.resize(2 * t.size());
+            HIPCHK(c, hipMemcpy(c->h_tick_clocks.data(), c->d_ticks + t.size(), sizeof(uint32_t) * 2 * t.size(),
+                                hipMemcpyDeviceToHost));
+        }
         // cost at 1 wave per tile: 2 and 4 waves measured 1.3x / 1.8x faster per tile
         std::vector<double> cost(t.size());
         double sum = 0;
@@ -1704,6 +1718,16 @@ extern "C" int pbrt_gpu_mesh_download(pbrt_gpu_ctx* c, void* nodes, int32_t* gid
     if (tris && nt && hipMemcpy(tris, c->mesh.tris, nt * 9 * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
         return PBRT_E_HIP;
     return PBRT_OK;
+}
+
+extern "C" int64_t pbrt_gpu_tile_clocks(pbrt_gpu_ctx* c, uint32_t* start, uint32_t* end, int64_t n) {
+    if (!c) return -PBRT_E_INVALID;
+    const int64_t m = (int64_t)c->h_tick_clocks.size() / 2;
+    for (int64_t i = 0; i < m && i < n; i++) {
+        if (start) start[i] = c->h_tick_clocks[(size_t)i];
+        if (end) end[i] = c->h_tick_clocks[(size_t)(m + i)];
+    }
+    return m;
 }
 
 extern "C" int64_t pbrt_gpu_tile_ticks(pbrt_gpu_ctx* c, uint32_t* out, int64_t n, int64_t* heavy) {

@@ -82,6 +82,13 @@ int pbrt_gpu_counters(struct pbrt_gpu_ctx* ctx, uint64_t* out, int n);
  * the last launch that ran at 4 waves in the heavy/light split (0: no split). */
 int64_t pbrt_gpu_tile_ticks(struct pbrt_gpu_ctx* ctx, uint32_t* out, int64_t n, int64_t* heavy);
 
+/* Diagnostics builds (make diag): the start and end wall_clock64 values (low 32
+ * bits, 100 MHz) of each slot's chain in the last EXACT frame, for the
+ * occupancy timeline of the launch (tools/tile_timeline.py). Copies min(n,
+ * slots) values into each non-null array and returns the slot count (0 in
+ * other builds). */
+int64_t pbrt_gpu_tile_clocks(struct pbrt_gpu_ctx* ctx, uint32_t* start, uint32_t* end, int64_t n);
+
 /* Cold-frame schedule estimate of the last EXACT frame, if that frame ran
  * render.hip's k_tile_cost probe (a fresh context or a new configuration):
  * per slot {chain work (lane-bounces), hit pixels, pixels, cost}. Copies
