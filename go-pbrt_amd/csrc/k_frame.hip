@@ -587,6 +587,14 @@ __global__ __launch_bounds__(kWave) void k_tile_cost(DevScene sc, RenderParams r
     }
 }
 
+// One lane that waits `ticks` of the 100 MHz wall clock (PBRT_PATHS_OVERLAP:
+// holds a stream's next launch back until the launches queued before it on
+// other streams have been dispatched).
+__global__ void k_delay(uint32_t ticks) {
+    const uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
 __global__ void k_order_of_keys(const uint64_t* __restrict__ keys, int64_t nb, uint32_t* __restrict__ order) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < nb) order[i] = (uint32_t)keys[i];

@@ -9,11 +9,17 @@ namespace pbrtk {
 template <int P, bool kMB, bool kX>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kPathsWaves, 8))) void k_paths_ci(
     DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr,
-    int s1d_lds) {
+    int s1d_lds, const uint32_t* __restrict__ order) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];   // paths_group_lds<P>
     if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;   // one wave per workgroup
     stage_nodes(sc);
-    paths_group<P, kMB, kX>(sc, rp, wb, slot_base, (int64_t)blockIdx.x * P, nrec, ctr, lds, s1d_lds);
+    int64_t rec0 = (int64_t)blockIdx.x * P, rec_end = nrec;
+    if (order) {   // the launch covers the slots order[0 .. nrec / ppt) (P divides ppt)
+        const int64_t slot = (int64_t)order[rec0 / wb.ppt];
+        rec0 = slot * wb.ppt + rec0 % wb.ppt;
+        rec_end = (slot + 1) * wb.ppt;
+    }
+    paths_group<P, kMB, kX>(sc, rp, wb, slot_base, rec0, rec_end, ctr, lds, s1d_lds);
 }
 
 // THROUGHPUT mode setup for k_paths_ci<P, true>, one wave per pixel record:

@@ -6,10 +6,10 @@
 
 namespace pbrtk {
 
-template __global__ void k_paths_ci<4, false, true>(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr, int s1d_lds);
-template __global__ void k_paths_ci<8, false, true>(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr, int s1d_lds);
-template __global__ void k_paths_ci<4, true, true>(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr, int s1d_lds);
-template __global__ void k_paths_ci<8, true, true>(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr, int s1d_lds);
+template __global__ void k_paths_ci<4, false, true>(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr, int s1d_lds, const uint32_t* __restrict__ order);
+template __global__ void k_paths_ci<8, false, true>(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr, int s1d_lds, const uint32_t* __restrict__ order);
+template __global__ void k_paths_ci<4, true, true>(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr, int s1d_lds, const uint32_t* __restrict__ order);
+template __global__ void k_paths_ci<8, true, true>(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nrec, Counters* __restrict__ ctr, int s1d_lds, const uint32_t* __restrict__ order);
 template __global__ void k_mb_setup<true>(DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base, int64_t nslots_batch);
 
 }  // namespace pbrtk

@@ -62,6 +62,10 @@ struct Knobs {
     bool ci_split = true;      // PBRT_CI_SPLIT=0
     bool ci_order = true;      // PBRT_CI_ORDER=0
     bool ci_probe = true;      // PBRT_CI_PROBE=0
+    int paths_overlap = 200;   // PBRT_PATHS_OVERLAP=T: one GPU's split frame runs the path stage of the heavy
+                               // tiles and of the light launch's first round beside the chain's tail; the
+                               // rest of the light launch waits T us on a high-priority stream (0: off;
+                               // config B 400 -> 381-389 ms at 100-200 us, a loss at 50)
     bool paths_s1d_lds = false;// PBRT_PATHS_S1D=lds
     int paths_ci = -1;         // PBRT_PATHS_CI = 0, 2, 4, 8 (-1: auto)
     int paths_wf = -1;         // PBRT_PATHS_WF = 0 / 1 (-1: mesh scenes)
@@ -90,6 +94,7 @@ struct Knobs {
         if (const char* e = getenv("PBRT_CI_DENSE")) k.ci_dense = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_ORDER")) k.ci_order = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_PROBE")) k.ci_probe = atoi(e) != 0;
+        if (const char* e = getenv("PBRT_PATHS_OVERLAP")) k.paths_overlap = std::max(0, atoi(e));
         if (const char* e = getenv("PBRT_PATHS_S1D")) k.paths_s1d_lds = std::strcmp(e, "lds") == 0;
         if (const char* e = getenv("PBRT_PATHS_CI")) {
             const int v = atoi(e);
@@ -117,6 +122,12 @@ struct pbrt_gpu_ctx {
     // the main stream, the rest on stream2, concurrently
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_split = nullptr, ev_join = nullptr;
+    // PBRT_PATHS_OVERLAP: a high-priority stream for the light launch's later rounds,
+    // and the events of the overlapped path stage
+    hipStream_t stream3 = nullptr;
+    hipEvent_t ev_heavy = nullptr, ev_l2 = nullptr, ev_p1 = nullptr;
+    int64_t ov_done = 0;                 // slots (front of ov_order) whose paths ran beside the chain
+    const uint32_t* ov_order = nullptr;
     MeshBuild mesh;                      // triangle meshes + their LBVH (extension)
     int64_t heavy_k = 0;                 // slots at the front of h_slot_order that get 4 waves
     int ci_wps = 2;                      // waves/SIMD of the last one-wave k_chain_ci launch (3 or 2)
@@ -1015,6 +1026,7 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
         pbrt_gpu_destroy(c);
         return PBRT_E_HIP;
     }
+
     if (hipHostMalloc((void**)&c->h_cancel, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void**)&c->d_cancel, c->h_cancel, 0) != hipSuccess) {
         pbrt_gpu_destroy(c);
@@ -1114,6 +1126,22 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                 const int64_t nb = std::min<int64_t>(c->wave_batch, rp.n_slots - sb);
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 0], c->stream));
                 const int G = c->tiles_per_wave;
+                // EXACT k_paths_ci over n slots (ord: the slots' order, else slots 0 .. n - 1)
+                const bool paths_ci_exact = !c->use_dl && rp.mode != PBRT_MODE_THROUGHPUT &&
+                                            !(paths_wf_enabled(c) || paths_ci_pixels(c, rp) == 0);
+                auto launch_paths = [&](const uint32_t* ord, int64_t n, hipStream_t st) {
+                    const int pp = paths_ci_pixels(c, rp);
+                    const int per = rp.ndims * rp.spp;
+                    auto kern = kx ? (pp == 8 ? k_paths_ci<8, false, true> : k_paths_ci<4, false, true>)
+                                   : (pp == 8 ? k_paths_ci<8> : pp == 2 ? k_paths_ci<2> : k_paths_ci<4>);
+                    const int sl = paths_ci_s1d_lds(c, rp, pp) ? 1 : 0;
+                    const int lds = pp == 8 ? paths_group_lds<8>(sl * per) : pp == 2 ? paths_group_lds<2>(sl * per)
+                                                                                     : paths_group_lds<4>(sl * per);
+                    hipLaunchKernelGGL(kern, dim3((unsigned)((n * c->wb.ppt + pp - 1) / pp)), dim3(kWave),
+                                       (unsigned)lds, st, with_slot(sc, 3), rp, c->wb, sb, n * c->wb.ppt,
+                                       c->d_ctr, sl, ord);
+                };
+                c->ov_done = 0;
                 if (c->use_dl) {
                     hipLaunchKernelGGL(kx ? k_wf_primary<true> : k_wf_primary<false>, dim3((unsigned)((nb * c->wb.ppt + kWave - 1) / kWave)),
                                        dim3(kWave), 0, c->stream, with_slot(sc, 1), rp, c->wb, sb, nb);
@@ -1243,7 +1271,45 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                         c->h_slot_kw.assign((size_t)nb, (uint8_t)(heavy > 0 ? 1 : kw));
                         for (int64_t i = 0; i < heavy; i++) c->h_slot_kw[c->h_slot_order[(size_t)i]] = (uint8_t)ci_heavy_waves(c);
                     }
-                    if (heavy > 0) {
+                    // PBRT_PATHS_OVERLAP (one GPU, a learned split): the light launch's first
+                    // round (the tiles that start at once) is a launch of its own; the rest
+                    // goes to a high-priority stream behind a short wait, so that it is queued
+                    // after the first round has been dispatched and wins every slot that
+                    // frees while it has workgroups left. Once the first round and the
+                    // heavy tiles are done, their path stage (normal priority) takes the slots
+                    // the chain no longer needs; the rest of the path stage follows the chains.
+                    const int64_t round1 = std::min<int64_t>(nb - heavy, (int64_t)c->n_simd * c->ci_wps -
+                                                                             heavy * ci_heavy_waves(c));
+                    bool overlap = heavy > 0 && kw == 1 && c->knobs.paths_overlap > 0 && paths_ci_exact &&
+                                   learned && round1 > 0 && round1 < nb - heavy;
+                    if (overlap && !c->stream3) {   // created on first use (one-GPU frames only)
+                        int least = 0, greatest = 0;
+                        HIPCHK(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
+                        HIPCHK(c, hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, greatest));
+                        HIPCHK(c, hipEventCreateWithFlags(&c->ev_heavy, hipEventDisableTiming));
+                        HIPCHK(c, hipEventCreateWithFlags(&c->ev_l2, hipEventDisableTiming));
+                        HIPCHK(c, hipEventCreateWithFlags(&c->ev_p1, hipEventDisableTiming));
+                    }
+                    if (overlap) {
+                        HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
+                        launch_ci(ci_heavy_waves(c), heavy, order, c->stream);
+                        HIPCHK(c, hipEventRecord(c->ev_heavy, c->stream));
+                        HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
+                        HIPCHK(c, hipStreamWaitEvent(c->stream3, c->ev_split, 0));
+                        launch_ci(1, round1, order + heavy, c->stream2);
+                        hipLaunchKernelGGL(k_delay, dim3(1), dim3(1), 0, c->stream3,
+                                           (uint32_t)c->knobs.paths_overlap * 100u);   // 100 MHz ticks
+                        launch_ci(1, nb - heavy - round1, order + heavy + round1, c->stream3);
+                        HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
+                        HIPCHK(c, hipEventRecord(c->ev_l2, c->stream3));
+                        HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_heavy, 0));
+                        launch_paths(order, heavy + round1, c->stream2);
+                        HIPCHK(c, hipEventRecord(c->ev_p1, c->stream2));
+                        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+                        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_l2, 0));
+                        c->ov_done = heavy + round1;
+                        c->ov_order = order;
+                    } else if (heavy > 0) {
                         HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
                         launch_ci(ci_heavy_waves(c), heavy, order, c->stream);
                         HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
@@ -1287,19 +1353,13 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                                                                                      : paths_group_lds<4>(sl * per);
                     hipLaunchKernelGGL(kern, dim3((unsigned)((nb * c->wb.ppt + pp - 1) / pp)), dim3(kWave),
                                        (unsigned)lds, c->stream, with_slot(sc, 5), rp, c->wb, sb, nb * c->wb.ppt,
-                                       c->d_ctr, sl);
+                                       c->d_ctr, sl, nullptr);
                 }
-                else {
-                    const int pp = paths_ci_pixels(c, rp);
-                    const int per = rp.ndims * rp.spp;
-                    auto kern = kx ? (pp == 8 ? k_paths_ci<8, false, true> : k_paths_ci<4, false, true>)
-                                   : (pp == 8 ? k_paths_ci<8> : pp == 2 ? k_paths_ci<2> : k_paths_ci<4>);
-                    const int sl = paths_ci_s1d_lds(c, rp, pp) ? 1 : 0;
-                    const int lds = pp == 8 ? paths_group_lds<8>(sl * per) : pp == 2 ? paths_group_lds<2>(sl * per)
-                                                                                     : paths_group_lds<4>(sl * per);
-                    hipLaunchKernelGGL(kern, dim3((unsigned)((nb * c->wb.ppt + pp - 1) / pp)), dim3(kWave),
-                                       (unsigned)lds, c->stream, with_slot(sc, 3), rp, c->wb, sb, nb * c->wb.ppt,
-                                       c->d_ctr, sl);
+                else if (c->ov_done > 0) {   // the rest of an overlapped path stage
+                    launch_paths(c->ov_order + c->ov_done, nb - c->ov_done, c->stream);
+                    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_p1, 0));
+                } else {
+                    launch_paths(nullptr, nb, c->stream);
                 }
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 2], c->stream));
                 hipLaunchKernelGGL(k_film, dim3((unsigned)nb), dim3(kFilmThreads), (unsigned)film_lds_bytes(rp), c->stream,
@@ -1551,6 +1611,12 @@ void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
     if (c->ev2) (void)hipEventDestroy(c->ev2);
     if (c->ev_split) (void)hipEventDestroy(c->ev_split);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    for (hipEvent_t e : {c->ev_heavy, c->ev_l2, c->ev_p1})
+        if (e) (void)hipEventDestroy(e);
+    if (c->stream3) {
+        (void)hipStreamSynchronize(c->stream3);
+        (void)hipStreamDestroy(c->stream3);
+    }
     if (c->stream2) {
         (void)hipStreamSynchronize(c->stream2);
         (void)hipStreamDestroy(c->stream2);

@@ -40,12 +40,34 @@ def tile_parity(film, ofilm, tile=16):
     return rms, ok / n
 
 
+def test_config_B_split_without_paths_overlap_vs_oracle(monkeypatch):
+    """PBRT_PATHS_OVERLAP=0: the heavy/light split with one light launch and
+    the whole path stage after the chains (the default overlaps the path stage
+    of the heavy tiles and the light launch's first round with the rest of the
+    chain, test_config_B_whole_frame_vs_oracle). Every frame is the oracle's,
+    bit for bit."""
+    monkeypatch.setenv("PBRT_PATHS_OVERLAP", "0")
+    scene = G.Scene.readme(1920, 1080)
+    rd = abi.render_desc(8, 8)
+    rc, ofilm, ost = O.render(scene.desc, rd, threads=THREADS)
+    assert rc == 0
+    with G.Renderer(scene) as r:
+        for frame in range(3):
+            film, st = r.render(rd)
+            _, heavy = r.tile_ticks()
+            assert (heavy > 0) == (frame > 0), (frame, heavy)
+            assert st.paths_traced == ost.paths
+            assert np.array_equal(bits(film), bits(ofilm)), frame
+
+
 def test_config_B_whole_frame_vs_oracle():
     """The cold frame of a fresh context (probe order) and the steady-state
     frames the bench times: from the second frame on, the learned LPT order and
     the one-GPU heavy/light split (the heaviest tiles at 4 waves on one stream
-    beside the rest at 1 wave on a second stream, render.hip launch_ci). Every
-    frame is the oracle's, bit for bit."""
+    beside the rest at 1 wave, render.hip launch_ci), with the path stage of the
+    heavy tiles and the light launch's first round overlapping the rest of the
+    chain (PBRT_PATHS_OVERLAP, default on). Every frame is the oracle's, bit
+    for bit."""
     scene = G.Scene.readme(1920, 1080)
     rd = abi.render_desc(8, 8)
     rc, ofilm, ost = O.render(scene.desc, rd, threads=THREADS)
