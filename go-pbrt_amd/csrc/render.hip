@@ -1271,7 +1271,8 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                         c->h_slot_kw.assign((size_t)nb, (uint8_t)(heavy > 0 ? 1 : kw));
                         for (int64_t i = 0; i < heavy; i++) c->h_slot_kw[c->h_slot_order[(size_t)i]] = (uint8_t)ci_heavy_waves(c);
                     }
-                    // PBRT_PATHS_OVERLAP (one GPU, a learned split): the light launch's first
+                    // PBRT_PATHS_OVERLAP (a learned split whose light tiles exceed one round:
+                    // one GPU, and 1/2 shards; 1/2 shard of B 240.7 -> 217.7 ms): the light launch's first
                     // round (the tiles that start at once) is a launch of its own; the rest
                     // goes to a high-priority stream behind a short wait, so that it is queued
                     // after the first round has been dispatched and wins every slot that
@@ -1280,7 +1281,7 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                     // the chain no longer needs; the rest of the path stage follows the chains.
                     const int64_t round1 = std::min<int64_t>(nb - heavy, (int64_t)c->n_simd * c->ci_wps -
                                                                              heavy * ci_heavy_waves(c));
-                    bool overlap = heavy > 0 && kw == 1 && c->knobs.paths_overlap > 0 && paths_ci_exact &&
+                    bool overlap = heavy > 0 && c->knobs.paths_overlap > 0 && paths_ci_exact &&
                                    learned && round1 > 0 && round1 < nb - heavy;
                     if (overlap && !c->stream3) {   // created on first use (one-GPU frames only)
                         int least = 0, greatest = 0;
