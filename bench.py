@@ -64,6 +64,8 @@ def parse():
                     help="mode of the headline line (exact = the reference's per-tile RNG, bit-exact)")
     ap.add_argument("--no-side-mode", action="store_true",
                     help="skip the extra frames in the other mode (reported under side_mode)")
+    ap.add_argument("--no-rpc", action="store_true",
+                    help="skip the per-request leg (rpc: fresh scene + context + frame + film download + RGBA8)")
     return ap.parse_args()
 
 
@@ -404,6 +406,43 @@ class GpuBackend:
         return self.torch.tensor(vals, dtype=self.torch.float64, device=self.dev)
 
 
+def rpc_leg(G, cfg, W, H, rd, local, args, steady_ms):
+    """What the reference's caller pays per request: internal/render/server.go:29-164
+    builds the scene, the integrator and (through the cgo shim) a renderer for
+    every RPC, renders one frame and writes the image. Timed here end to end on
+    the host clock: scene construction (host BVH build), pbrt_gpu_create, one
+    frame through pbrt_gpu_render (which includes the device-to-host film copy)
+    and pbrt_film_to_rgba8 (Film.WriteImage's pixel conversion). Two requests:
+    `cold` with the process-wide schedule cache emptied (the first request a
+    process serves: the cold-frame probe schedules it) and `cached` (a later
+    request: it starts from the schedule the bench's own context measured)."""
+    out = {}
+    for label in ("cached", "cold"):
+        if label == "cold":
+            G.schedule_cache_clear()
+        t0 = time.perf_counter()
+        scene = make_scene(G, cfg, W, H)
+        t1 = time.perf_counter()
+        r = G.Renderer(scene, device=local, kernel=args.kernel, lanes_per_wave=args.tiles_per_wave,
+                       occupancy=args.occupancy)
+        t2 = time.perf_counter()
+        film, st = r.render(rd)
+        t3 = time.perf_counter()
+        G.film_to_rgba8(film)
+        t4 = time.perf_counter()
+        src = r.schedule_source()
+        r.close()
+        out[label] = {"rpc_ms": (t4 - t0) * 1e3, "scene_ms": (t1 - t0) * 1e3, "create_ms": (t2 - t1) * 1e3,
+                      "render_ms": (t3 - t2) * 1e3, "frame_kernels_ms": st.kernel_ms, "chain_ms": st.chain_ms,
+                      "rgba8_ms": (t4 - t3) * 1e3, "schedule": src}
+    out["rpc_ms"] = out["cached"]["rpc_ms"]
+    out["cached_frame_over_steady"] = out["cached"]["render_ms"] / steady_ms if steady_ms else None
+    out["note"] = ("per request of internal/render/server.go: scene + pbrt_gpu_create + pbrt_gpu_render (frame + "
+                   "D2H film copy) + pbrt_film_to_rgba8, host wall clock; `cached`: a fresh context that starts "
+                   "from the process-wide schedule cache; `cold`: the cache emptied (the probe schedules it)")
+    return out
+
+
 def make_step(renderer, backend, film, rd, world):
     """One frame: the rank's shard into its full-size film, then (N > 1) one
     SUM reduce of the films onto rank 0 -- the additive MergeFilmTile."""
@@ -527,6 +566,10 @@ def main():
                 "note": "THROUGHPUT = one PCG32 stream per (pixel, sample): same arithmetic, statistically "
                         "(not bitwise) the reference image; EXACT is the headline"}
 
+    rpc = None
+    if world == 1 and not args.no_rpc:
+        rpc = rpc_leg(G, cfg, W, H, rd_of(args.mode), local, args, elapsed / args.steps * 1e3)
+
     if rank == 0:
         value = paths_total / elapsed / 1e6
         if cfg.get("integrator") or "n_dims" in cfg or cfg["scene"] == "readme_filter15":
@@ -545,6 +588,9 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
+            "timed_region": "render_async_into a device-resident film + synchronize per frame (inputs resident "
+                            "in HBM); the 50 MB device-to-host film copy of pbrt_gpu_render is excluded here and "
+                            "included in rpc.*.render_ms",
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -582,6 +628,8 @@ def main():
         }
         if side:
             out["side_mode"] = side
+        if rpc:
+            out["rpc"] = rpc
         if not args.no_cpu_baseline and world == 1:
             cb = cpu_baseline(args, cfg["scene"], rd_kwargs, W, H, scene)
             cb["gpu_over_cpu"] = value / cb["value"]

@@ -25,19 +25,25 @@ __device__ __forceinline__ uint32_t ring_d(const Cursor& c, const SpecSampler& s
     return kRrFlag | (d == kBadSpecD ? kRrTailBad : d);
 }
 
-template <int kW, int kDepth, bool kX, int kEu>
+template <int kW, int kDepth, bool kX, int kEu, bool kSpWin>
 // kDepth < 0 (kCiMeshOnly): scenes of triangle meshes only, no analytic walk
 // compiled in (149 VGPRs), built for 3 waves per SIMD; Matte analytic scenes
 // at PBRT_CI_EU_WAVES (3: 168 VGPRs, a few spills, faster than 2), kX at
 // PBRT_CI_X_EU_WAVES (2). kEu > 0 sets the waves/SIMD the registers are
 // budgeted for (the host picks <1, *, false, 2> where the workgroup's LDS
 // allows fewer than 3 waves/SIMD anyway: then the 3-wave build only spills).
+// kSpWin: the windowed wave StartPixel compiled in (rp.sp_window renders: large
+// spp without jitter, config C).
 __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu > 0 ? kEu : kDepth < 0 ? PBRT_CI_MESH_EU_WAVES : kX ? PBRT_CI_X_EU_WAVES : PBRT_CI_EU_WAVES, 8))) void k_chain_ci(
     DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base,
     int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr,
-    const uint32_t* __restrict__ order, uint32_t* __restrict__ ticks, int cstride) {
+    const uint32_t* __restrict__ order, uint32_t* __restrict__ ticks, int cstride, uint32_t* __restrict__ prog) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const uint64_t t_begin = wall_clock64();
+    // the frame's chain progress record (completion-driven path stage, render.hip;
+    // null elsewhere): [0] workgroups started, [1] completions, [2 + i] the slot of
+    // the i-th completion
+    if (prog && threadIdx.x == 0) __hip_atomic_fetch_add(&prog[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t cs = cstride == 1 ? 1u : 2u;   // candidate offsets head + cs * j
     constexpr int kT = kWave * kW;   // threads per workgroup (stack stride)
     // kDepth 0: an LDS-staged tree, walked without a stack (no stack array)
@@ -179,7 +185,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
                 const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
                 double* gs1d = wb.s1d + rec * wb.s1d_stride;
                 double* sp = s1d ? s1d : gs1d;
-                const uint64_t S1 = start_pixel_wave(rp, J, gs[q].S, incq, sp, other, vbuf, &sh_state);
+                const uint64_t S1 = start_pixel_wave<kSpWin>(rp, J, gs[q].S, incq, sp, other, vbuf, &sh_state);
                 if (s1d)
                     for (int idx = tid; idx < ndims * n; idx += kT) gs1d[idx] = s1d[idx];
                 // the first traced sample's camera time value (read before the ring
@@ -395,6 +401,9 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
                     break;
                 }
                 CI_DIAG(atomicAdd(&dh[min(d / 2u, 63u)], 1u);)
+                // the tail cap's bound (dmax per sample): an on-chain D above it would
+                // only slow the chain, never change a result; counted so tests can pin it
+                CI_DIAG(if (d > dmax) ph[6]++;)
                 s.kh++;
                 s.head += d;
                 if (s.kh >= n) {   // every sample of the pixel has its offset; the next StartPixel starts here
@@ -428,7 +437,15 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
     }
 #endif
 #undef CI_DIAG
+    if (prog) {   // every thread's writes of this tile (records, sample states) reach L2 first
+        __threadfence();
+        __syncthreads();
+    }
     if (tid == 0) {
+        if (prog && G == 1 && bs < nslots_batch) {   // publish the tile for the path stage
+            const uint32_t pos = __hip_atomic_fetch_add(&prog[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&prog[2 + pos], (uint32_t)bs, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
         if (ticks && G == 1 && bs < nslots_batch) {
             const uint64_t t_end = wall_clock64();
             ticks[bs] = (uint32_t)min(t_end - t_begin, (uint64_t)0xFFFFFFFFu);

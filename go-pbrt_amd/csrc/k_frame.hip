@@ -587,12 +587,53 @@ __global__ __launch_bounds__(kWave) void k_tile_cost(DevScene sc, RenderParams r
     }
 }
 
-// One lane that waits `ticks` of the 100 MHz wall clock (PBRT_PATHS_OVERLAP:
-// holds a stream's next launch back until the launches queued before it on
-// other streams have been dispatched).
-__global__ void k_delay(uint32_t ticks) {
-    const uint64_t t0 = wall_clock64();
-    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+// One wave that holds its stream's next launch back until the chain stage's
+// progress record (k_chain_ci's `prog`) allows it (the completion-driven path
+// stage, render.hip):
+//   b == e: until at least `b` chain workgroups have started (every one of them
+//           has been dispatched);
+//   b <  e: until the completion list's entries [b, e) are all written (those
+//           tiles' chains have ended and their records are visible).
+// Progress-driven, not timed: the chains waited for are queued before the gate
+// and always run to their end (a cancelled chain ends early, but ends). Only a
+// bug could stall the record; 60 s without progress ends the wait and flags the
+// frame (Counters.gate_stall), and the path launches skip unwritten entries.
+__global__ __launch_bounds__(kWave) void k_gate(const uint32_t* __restrict__ prog, uint32_t b, uint32_t e,
+                                                Counters* __restrict__ ctr) {
+    const int lane = threadIdx.x;
+    uint32_t cur = b == e ? 0u : b;   // b < e: entries before cur are known written
+    uint32_t seen = 0xFFFFFFFFu;
+    uint64_t t_prog = wall_clock64();
+    for (;;) {
+        uint32_t v;
+        if (b == e) {
+            v = __hip_atomic_load(&prog[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if (v >= b) return;
+        } else {
+            for (;;) {   // advance over written entries, 64 at a time
+                const uint32_t i = cur + (uint32_t)lane;
+                const bool ok = i >= e || __hip_atomic_load(&prog[2 + i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) !=
+                                              kNoSlot;
+                const unsigned long long bad = __ballot(!ok);
+                if (bad) {
+                    cur += (uint32_t)__builtin_ctzll(bad);
+                    break;
+                }
+                cur += kWave;
+                if (cur >= e) return;
+            }
+            v = cur;
+        }
+        const uint64_t now = wall_clock64();
+        if (v != seen) {
+            seen = v;
+            t_prog = now;
+        } else if (now - t_prog > 6000000000ull) {   // 60 s at 100 MHz without progress
+            if (lane == 0) atomicExch(&ctr->gate_stall, 1);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(32);
+    }
 }
 
 __global__ void k_order_of_keys(const uint64_t* __restrict__ keys, int64_t nb, uint32_t* __restrict__ order) {

@@ -14,9 +14,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(kPathsWav
     if (cancel_requested(sc, (blockIdx.x & 63) == 0)) return;   // one wave per workgroup
     stage_nodes(sc);
     int64_t rec0 = (int64_t)blockIdx.x * P, rec_end = nrec;
-    if (order) {   // the launch covers the slots order[0 .. nrec / ppt) (P divides ppt)
-        const int64_t slot = (int64_t)order[rec0 / wb.ppt];
-        rec0 = slot * wb.ppt + rec0 % wb.ppt;
+    if (order) {   // the launch covers the slots order[0 .. nrec / ppt), ceil(ppt / P) workgroups per slot
+        const int64_t gps = (wb.ppt + P - 1) / P;
+        const uint32_t o = order[blockIdx.x / gps];
+        if (o == kNoSlot) return;   // an unwritten completion entry (only after a k_gate stall)
+        const int64_t slot = (int64_t)o;
+        rec0 = slot * wb.ppt + (int64_t)(blockIdx.x % gps) * P;
         rec_end = (slot + 1) * wb.ppt;
     }
     paths_group<P, kMB, kX>(sc, rp, wb, slot_base, rec0, rec_end, ctr, lds, s1d_lds);

@@ -32,9 +32,11 @@
 #include <string>
 #include <functional>
 #include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/pbrt_gpu.h"
+#include "../../include/pbrt_diag.h"
 #include "../../include/pbrt_scene.h"
 #include "mesh_bvh.h"
 #include "render_kernels.h"
@@ -58,14 +60,17 @@ struct Knobs {
     int ci_waves = 0;          // PBRT_CI_WAVES = 1, 2, 4, 8 (0: by tile count)
     int ci_stride = 0;         // PBRT_CI_STRIDE = 1, 2 (0: 2 at one wave per tile, else 1)
     int ci_heavy_waves = 4;    // PBRT_CI_HEAVY_WAVES = 4, 8
+    int ci_eu = 0;             // PBRT_CI_EU = 2 / 3: the one-wave Matte chain's build (waves/SIMD its registers
+                               // are budgeted for); 0: by the workgroup's LDS (ci_eu3_fits)
     int64_t ci_heavy = -1;     // PBRT_CI_HEAVY = K forces the heavy tile count (tests)
     bool ci_split = true;      // PBRT_CI_SPLIT=0
     bool ci_order = true;      // PBRT_CI_ORDER=0
     bool ci_probe = true;      // PBRT_CI_PROBE=0
-    int paths_overlap = 200;   // PBRT_PATHS_OVERLAP=T: one GPU's split frame runs the path stage of the heavy
-                               // tiles and of the light launch's first round beside the chain's tail; the
-                               // rest of the light launch waits T us on a high-priority stream (0: off;
-                               // config B 400 -> 381-389 ms at 100-200 us, a loss at 50)
+    bool ci_order_cache = true;// PBRT_CI_ORDER_CACHE=0
+    bool sp_window = true;     // PBRT_SP_WINDOW=0: the lane-0 StartPixel replay instead of the windowed one
+    int paths_overlap = 5;     // PBRT_PATHS_OVERLAP=K: a split frame's path stage runs in K chunks of the
+                               // tiles in their chains' completion order, each released when its tiles'
+                               // chains have ended (render_enqueue; 0: off, the path stage after the chains)
     bool paths_s1d_lds = false;// PBRT_PATHS_S1D=lds
     int paths_ci = -1;         // PBRT_PATHS_CI = 0, 2, 4, 8 (-1: auto)
     int paths_wf = -1;         // PBRT_PATHS_WF = 0 / 1 (-1: mesh scenes)
@@ -89,12 +94,15 @@ struct Knobs {
             if (v == 1 || v == 2) k.ci_stride = v;
         }
         if (const char* e = getenv("PBRT_CI_HEAVY_WAVES")) k.ci_heavy_waves = atoi(e) == 8 ? 8 : 4;
+        if (const char* e = getenv("PBRT_CI_EU")) k.ci_eu = (atoi(e) == 2 || atoi(e) == 3) ? atoi(e) : 0;
         if (const char* e = getenv("PBRT_CI_HEAVY")) k.ci_heavy = (int64_t)atoll(e);
         if (const char* e = getenv("PBRT_CI_SPLIT")) k.ci_split = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_DENSE")) k.ci_dense = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_ORDER")) k.ci_order = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_PROBE")) k.ci_probe = atoi(e) != 0;
-        if (const char* e = getenv("PBRT_PATHS_OVERLAP")) k.paths_overlap = std::max(0, atoi(e));
+        if (const char* e = getenv("PBRT_CI_ORDER_CACHE")) k.ci_order_cache = atoi(e) != 0;
+        if (const char* e = getenv("PBRT_SP_WINDOW")) k.sp_window = atoi(e) != 0;
+        if (const char* e = getenv("PBRT_PATHS_OVERLAP")) k.paths_overlap = std::min(std::max(0, atoi(e)), 16);
         if (const char* e = getenv("PBRT_PATHS_S1D")) k.paths_s1d_lds = std::strcmp(e, "lds") == 0;
         if (const char* e = getenv("PBRT_PATHS_CI")) {
             const int v = atoi(e);
@@ -122,12 +130,14 @@ struct pbrt_gpu_ctx {
     // the main stream, the rest on stream2, concurrently
     hipStream_t stream2 = nullptr;
     hipEvent_t ev_split = nullptr, ev_join = nullptr;
-    // PBRT_PATHS_OVERLAP: a high-priority stream for the light launch's later rounds,
-    // and the events of the overlapped path stage
+    // PBRT_PATHS_OVERLAP: a high-priority stream for the light chain launch, the
+    // events of the completion-driven path stage, and k_chain_ci's progress record
+    // ([0] workgroups started, [1] completions, [2 ..] completion list)
     hipStream_t stream3 = nullptr;
-    hipEvent_t ev_heavy = nullptr, ev_l2 = nullptr, ev_p1 = nullptr;
-    int64_t ov_done = 0;                 // slots (front of ov_order) whose paths ran beside the chain
-    const uint32_t* ov_order = nullptr;
+    hipEvent_t ev_l2 = nullptr, ev_p1 = nullptr;
+    int64_t ov_done = 0;                 // slots whose path stage was launched beside the chains
+    uint32_t* d_prog = nullptr;
+    int64_t prog_cap = 0;
     MeshBuild mesh;                      // triangle meshes + their LBVH (extension)
     int64_t heavy_k = 0;                 // slots at the front of h_slot_order that get 4 waves
     int ci_wps = 2;                      // waves/SIMD of the last one-wave k_chain_ci launch (3 or 2)
@@ -203,6 +213,8 @@ struct pbrt_gpu_ctx {
     int64_t cost_cap = 0, cost_n = 0;
     bool probed = false;               // the last EXACT frame ran the cost probe
     uint64_t order_key = 0, ticks_key = 0;
+    uint64_t scene_hash = 0;           // content hash of the scene (process-wide schedule cache)
+    int sched_src = 0;                 // schedule of the last EXACT frame: PBRT_SCHED_* (pbrt_diag.h)
     int64_t ticks_n = 0;
     bool ticks_pending = false;
     double* d_out = nullptr;
@@ -225,6 +237,71 @@ struct pbrt_gpu_ctx {
 };
 
 namespace {
+
+// Process-wide schedule cache. internal/render/server.go:29-164 builds a fresh
+// scene, integrator and renderer for every request, so each request's context
+// would otherwise start from the cold-frame probe. A context that measured a
+// frame stores its heaviest-first slot order here, keyed by the scene's content
+// hash and the frame's schedule key; a fresh context on the same scene and
+// configuration starts from it. Only the schedule changes, never a result, so a
+// hash collision could only cost speed.
+struct SchedEntry {
+    std::vector<uint32_t> order;   // slot order, heaviest first
+    int64_t heavy_k = 0;           // slots at its front that run at 4 waves
+};
+std::mutex g_sched_mu;
+std::unordered_map<uint64_t, SchedEntry> g_sched;
+constexpr size_t kSchedCacheMax = 64;   // configurations kept (a full frame's order is 32 KB)
+
+uint64_t fnv_bytes(uint64_t h, const void* p, size_t n) {
+    const unsigned char* b = (const unsigned char*)p;
+    for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
+    return h;
+}
+// Content hash of a scene descriptor: every analytic record, the camera and
+// film, and per mesh its sizes plus up to 4096 evenly spread vertices and
+// triangles (a mesh of 10M triangles is not hashed whole on every create).
+uint64_t scene_content_hash(const pbrt_scene_desc* s) {
+    uint64_t h = 1469598103934665603ull;
+    const int32_t counts[] = {s->n_shapes, s->n_materials, s->n_prims, s->n_nodes, s->n_lights, s->n_meshes};
+    h = fnv_bytes(h, counts, sizeof(counts));
+    if (s->n_shapes > 0) h = fnv_bytes(h, s->shapes, sizeof(pbrt_shape_desc) * (size_t)s->n_shapes);
+    if (s->n_materials > 0) h = fnv_bytes(h, s->materials, sizeof(pbrt_material_desc) * (size_t)s->n_materials);
+    if (s->n_prims > 0) h = fnv_bytes(h, s->prims, sizeof(pbrt_primitive_desc) * (size_t)s->n_prims);
+    if (s->n_nodes > 0) h = fnv_bytes(h, s->nodes, sizeof(pbrt_bvh_node) * (size_t)s->n_nodes);
+    if (s->n_lights > 0) h = fnv_bytes(h, s->lights, sizeof(pbrt_light_desc) * (size_t)s->n_lights);
+    h = fnv_bytes(h, &s->camera, sizeof(s->camera));
+    h = fnv_bytes(h, &s->film, sizeof(s->film));
+    for (int m = 0; m < s->n_meshes && s->meshes; m++) {
+        const pbrt_mesh_desc& md = s->meshes[m];
+        const int32_t mc[] = {md.n_vertices, md.n_triangles, md.material, md.reverse_orientation};
+        h = fnv_bytes(h, mc, sizeof(mc));
+        const int64_t nv = md.n_vertices, nt = md.n_triangles;
+        for (int64_t i = 0, st = std::max<int64_t>(1, nv / 4096); md.p && i < nv; i += st)
+            h = fnv_bytes(h, md.p + 3 * i, 3 * sizeof(float));
+        for (int64_t i = 0, st = std::max<int64_t>(1, nt / 4096); md.indices && i < nt; i += st)
+            h = fnv_bytes(h, md.indices + 3 * i, 3 * sizeof(int32_t));
+    }
+    return h;
+}
+uint64_t sched_cache_key(const pbrt_gpu_ctx* c, uint64_t skey) {
+    uint64_t h = fnv_bytes(c->scene_hash, &skey, sizeof(skey));
+    return fnv_bytes(h, &c->n_simd, sizeof(c->n_simd));   // the device's size shapes the split
+}
+bool sched_cache_get(const pbrt_gpu_ctx* c, uint64_t skey, int64_t nb, SchedEntry& out) {
+    std::lock_guard<std::mutex> lk(g_sched_mu);
+    auto it = g_sched.find(sched_cache_key(c, skey));
+    if (it == g_sched.end() || (int64_t)it->second.order.size() != nb) return false;
+    out = it->second;
+    return true;
+}
+void sched_cache_put(const pbrt_gpu_ctx* c, uint64_t skey, const std::vector<uint32_t>& order, int64_t heavy_k) {
+    std::lock_guard<std::mutex> lk(g_sched_mu);
+    if (g_sched.size() >= kSchedCacheMax && !g_sched.count(sched_cache_key(c, skey))) g_sched.clear();
+    SchedEntry& e = g_sched[sched_cache_key(c, skey)];
+    e.order = order;
+    e.heavy_k = heavy_k;
+}
 
 int set_err(pbrt_gpu_ctx* c, int code, const std::string& m) {
     if (c) c->err = m;
@@ -519,6 +596,9 @@ bool paths_wf_enabled(const pbrt_gpu_ctx* c);
 // (a pixel's serial StartPixel, ~20 us, is under 0.5% of a C tile's chain)
 #define PBRT_SP_SERIAL_KB 4
 #endif
+#ifndef PBRT_SP_WINDOW_KB
+#define PBRT_SP_WINDOW_KB 6   // LDS for the windowed StartPixel's picks, permutations and draw ring (build option)
+#endif
 #ifndef PBRT_CI_STAGE_KB
 #define PBRT_CI_STAGE_KB 8   // k_chain_ci stages StartPixel's stratified values in LDS up to this (build option)
 #endif
@@ -556,7 +636,8 @@ bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Rend
     }
     // k_film stages the tile film's running sums and a run of source pixels in LDS
     // (any filter radius below the tile size: footprints beyond 2x2 included)
-    if ((size_t)film_lds_bytes(rp) > c->lds_per_block) return false;
+    // (+ its static per-run nvalid array, k_frame.hip)
+    if ((size_t)film_lds_bytes(rp) + kFilmThreads * sizeof(int) > c->lds_per_block) return false;
     const int64_t n = rp.spp, nd = rp.ndims;
     if (n > 4096 || nd * n > 8192) return false;
     int64_t off = 0;
@@ -569,7 +650,7 @@ bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Rend
     L.other = put(nd * n * 2);
     L.sbuf = put(kWave * 8);
     L.dbuf = put(kWave * 4);
-    L.vbuf = put(rp.sp_serial ? 4 : (int64_t)rp.sp_draws * 4);
+    L.vbuf = put(sp_vbuf_bytes(rp));
     L.total = (int)off;
     L.ring = 0;
     // k_chain_ci: the same staging without the window buffers, then the ring
@@ -582,8 +663,11 @@ bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Rend
     // 6.50 -> 5.25 s)
     const int64_t al16 = 15;
     const int64_t lds_staging = ((nd * n * 8 + al16) & ~al16) + ((nd * n * 2 + al16) & ~al16) +
-                                (((rp.sp_serial ? 4 : (int64_t)rp.sp_draws * 4) + al16) & ~al16);
-    if (rp.sp_serial) {
+                                ((sp_vbuf_bytes(rp) + al16) & ~al16);
+    if (rp.sp_window) {   // the windowed StartPixel: picks in LDS, values straight to the global record
+        Lci.s1d = -1;
+        Lci.other = put(nd * n * 2);
+    } else if (rp.sp_serial) {
         Lci.s1d = -1;
         Lci.other = put(16);
     } else if (lds_staging > PBRT_CI_STAGE_KB * 1024) {
@@ -594,7 +678,7 @@ bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Rend
         Lci.other = put(nd * n * 2);
     }
     Lci.sbuf = Lci.dbuf = 0;
-    Lci.vbuf = put(rp.sp_serial ? 4 : (int64_t)rp.sp_draws * 4);
+    Lci.vbuf = put(sp_vbuf_bytes(rp));
     Lci.staging = (int)off;
     Lci.ring = put(kCiRingBytes);
     Lci.total = (int)off;
@@ -669,6 +753,8 @@ int ci_stride(const pbrt_gpu_ctx* c, int w) {
 // PBRT_CI_HEAVY_WAVES = 4 (default) or 8: waves per heavy tile of the split
 int ci_heavy_waves(const pbrt_gpu_ctx* c) { return c->non_matte ? 4 : c->knobs.ci_heavy_waves; }
 bool ci_order_enabled(const pbrt_gpu_ctx* c) { return c->knobs.ci_order; }
+// PBRT_CI_ORDER_CACHE=0: no process-wide schedule cache (each context learns its own)
+bool ci_order_cache(const pbrt_gpu_ctx* c) { return c->knobs.ci_order_cache; }
 // PBRT_CI_PROBE=0: a fresh context's first frame runs in launch order (no k_tile_cost)
 bool ci_probe_enabled(const pbrt_gpu_ctx* c) { return c->knobs.ci_probe; }
 uint64_t schedule_key(const RenderParams& rp, int kw) {
@@ -917,6 +1003,14 @@ int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
         rp.sp_events = (int32_t)E;
         rp.sp_draws = (int32_t)V;
         rp.sp_serial = V * 4 <= PBRT_SP_SERIAL_KB * 1024 ? 0 : 1;
+        // the windowed wave StartPixel where the serial one would run, without
+        // jitter (values are functions of their index), while its picks and
+        // permutations fit PBRT_SP_WINDOW_KB of LDS (config C; E's 1024 spp stay serial)
+        // (k_chain_ci instantiates it for Matte scenes of LDS-staged trees, the
+        // analytic walk: the host runs those kernels below)
+        rp.sp_window = c->knobs.sp_window && rp.sp_serial && !rp.jitter && !c->non_matte && c->host_scene.n_nodes <= kLdsNodes &&
+                       c->mesh.n_nodes == 0 &&
+                       (int64_t)rp.ndims * n * 4 + kSpRing * 4 <= PBRT_SP_WINDOW_KB * 1024 ? 1 : 0;
     }
     c->use_spec = c->kernel_req != PBRT_KERNEL_SERIAL && wave_eligible(c, rd, rp, c->lay, c->lay_ci);
     if ((c->kernel_req == PBRT_KERNEL_WAVE || c->kernel_req == PBRT_KERNEL_WAVEFRONT ||
@@ -1001,6 +1095,7 @@ int pbrt_gpu_create(const pbrt_scene_desc* scene, const pbrt_gpu_opts* opts, pbr
         return PBRT_E_INVALID;
     }
     c->host_scene = *scene;
+    c->scene_hash = scene_content_hash(scene);
     c->non_matte = false;
     for (int i = 0; i < scene->n_materials; i++)   // Mirror, Glass or OrenNayar (Matte with sigma != 0)
         c->non_matte |= scene->materials[i].type != PBRT_MAT_MATTE ||
@@ -1104,6 +1199,7 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
     double* out = film_device ? film_device : c->d_out;
     c->film_target = out;
     c->last_heavy = 0;
+    c->sched_src = PBRT_SCHED_LAUNCH_ORDER;
     HIPCHK(c, hipMemsetAsync(c->d_ctr, 0, sizeof(Counters), c->stream));
     HIPCHK(c, hipMemsetAsync(c->d_cancel_seen, 0, sizeof(int), c->stream));
     if (rp.n_slots > 0) HIPCHK(c, hipMemsetAsync(c->d_panics, 0, sizeof(PanicRec) * (size_t)rp.n_slots, c->stream));
@@ -1137,7 +1233,9 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                     const int sl = paths_ci_s1d_lds(c, rp, pp) ? 1 : 0;
                     const int lds = pp == 8 ? paths_group_lds<8>(sl * per) : pp == 2 ? paths_group_lds<2>(sl * per)
                                                                                      : paths_group_lds<4>(sl * per);
-                    hipLaunchKernelGGL(kern, dim3((unsigned)((n * c->wb.ppt + pp - 1) / pp)), dim3(kWave),
+                    // ordered: whole slots, ceil(ppt / pp) workgroups each (pp need not divide ppt)
+                    const int64_t groups = ord ? n * ((c->wb.ppt + pp - 1) / pp) : (n * c->wb.ppt + pp - 1) / pp;
+                    hipLaunchKernelGGL(kern, dim3((unsigned)groups), dim3(kWave),
                                        (unsigned)lds, st, with_slot(sc, 3), rp, c->wb, sb, n * c->wb.ppt,
                                        c->d_ctr, sl, ord);
                 };
@@ -1170,7 +1268,18 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                             c->ticks_cap = nb;
                         }
                         const uint64_t key = schedule_key(rp, kw);
+                        c->sched_src = PBRT_SCHED_LAUNCH_ORDER;
+                        if (!(c->order_key == key && (int64_t)c->h_slot_order.size() == nb) && ci_order_cache(c)) {
+                            SchedEntry e;   // a fresh context: another context's measured order for this scene
+                            if (sched_cache_get(c, key, nb, e)) {
+                                c->h_slot_order = std::move(e.order);
+                                c->heavy_k = e.heavy_k;
+                                c->order_key = key;
+                                c->sched_src = PBRT_SCHED_CACHED;
+                            }
+                        }
                         if (c->order_key == key && (int64_t)c->h_slot_order.size() == nb) {
+                            if (c->sched_src != PBRT_SCHED_CACHED) c->sched_src = PBRT_SCHED_LEARNED;
                             HIPCHK(c, hipMemcpyAsync(c->d_slot_order, c->h_slot_order.data(), sizeof(uint32_t) * (size_t)nb,
                                                      hipMemcpyHostToDevice, c->stream));
                             order = c->d_slot_order;
@@ -1200,6 +1309,7 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                                                c->stream, c->d_cost_keys, nb, c->d_slot_order);
                             order = c->d_slot_order;
                             c->probed = true;
+                            c->sched_src = PBRT_SCHED_PROBE;
                             c->cost_n = nb;
                         }
                         ticks = c->d_ticks;
@@ -1208,7 +1318,7 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                         c->ticks_n = nb;
                     }
                     // one launch of n workgroups, workgroup b on slot ord[b] (identity if null)
-                    auto launch_ci = [&](int w, int64_t n, const uint32_t* ord, hipStream_t st) {
+                    auto launch_ci = [&](int w, int64_t n, const uint32_t* ord, hipStream_t st, uint32_t* prog) {
                         if (w > 1) {   // one tile per workgroup of w waves; the ring grows with the lanes
                             const int ring = w * kCiRingBytes / (int)sizeof(RingEnt);
                             unsigned lds = 0;
@@ -1216,12 +1326,15 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                             // kX: LDS-staged trees only, at most 4 waves per tile (wave_eligible, ci_waves)
                             auto kern = kx ? (w == 2 ? k_chain_ci<2, 0, true> : k_chain_ci<4, 0, true>)
                                         : mesh_only ? (w == 2 ? k_chain_ci<2, -1> : w == 4 ? k_chain_ci<4, -1> : k_chain_ci<8, -1>)
+                                        : rp.sp_window ? (w == 2 ? k_chain_ci<2, 0, false, 0, true>
+                                                          : w == 4 ? k_chain_ci<4, 0, false, 0, true>
+                                                                   : k_chain_ci<8, 0, false, 0, true>)
                                            : (w == 2   ? (lds_nodes ? k_chain_ci<2> : k_chain_ci<2, 64>)
                                               : w == 4 ? (lds_nodes ? k_chain_ci<4> : k_chain_ci<4, 64>)
                                                        : (lds_nodes ? k_chain_ci<8> : k_chain_ci<8, 64>));
                             hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3(kWave * w), lds, st, with_slot(sc, 2), rp, lw,
                                                c->d_jump, c->wb, sb, nb, kWave * w, ring, c->d_ctr, ord, ticks,
-                                               ci_stride(c, w));
+                                               ci_stride(c, w), prog);
                         } else {
                             const int Gc = std::min(G, kCiMaxGroups);
                             const int ring = kCiRingBytes / (int)sizeof(RingEnt) / Gc;
@@ -1231,16 +1344,18 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                             // workgroup's LDS (large spp: StartPixel staging) caps the CU
                             // below 3 waves/SIMD, where the 2-wave build (no spills) is faster
                             // (config C: 6.53 vs 7.41 s)
-                            const bool eu2 = !kx && !mesh_only && !ci_eu3_fits(c, lds, lds_nodes);
+                            const bool eu2 = !kx && !mesh_only &&
+                                             (c->knobs.ci_eu == 2 || (c->knobs.ci_eu != 3 && !ci_eu3_fits(c, lds, lds_nodes)));
                             c->ci_wps = (kx || eu2) ? 2 : 3;
                             auto kern1 = kx ? k_chain_ci<1, 0, true>
                                          : mesh_only ? k_chain_ci<1, -1>
+                                         : rp.sp_window ? (eu2 ? k_chain_ci<1, 0, false, 2, true> : k_chain_ci<1, 0, false, 0, true>)
                                          : eu2 ? (lds_nodes ? k_chain_ci<1, 0, false, 2> : k_chain_ci<1, 64, false, 2>)
                                                : (lds_nodes ? k_chain_ci<1> : k_chain_ci<1, 64>);
                             hipLaunchKernelGGL(kern1, dim3((unsigned)((n + Gc - 1) / Gc)), dim3(kWave),
                                                lds, st, with_slot(sc, 2), rp, lw, c->d_jump, c->wb, sb,
                                                nb, kWave / Gc, ring, c->d_ctr, Gc == 1 ? ord : nullptr,
-                                               Gc == 1 ? ticks : nullptr, ci_stride(c, 1));
+                                               Gc == 1 ? ticks : nullptr, ci_stride(c, 1), prog);
                         }
                     };
                     // the heaviest tiles of the last frame get 4 waves each; they are
@@ -1271,54 +1386,65 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                         c->h_slot_kw.assign((size_t)nb, (uint8_t)(heavy > 0 ? 1 : kw));
                         for (int64_t i = 0; i < heavy; i++) c->h_slot_kw[c->h_slot_order[(size_t)i]] = (uint8_t)ci_heavy_waves(c);
                     }
-                    // PBRT_PATHS_OVERLAP (a learned split whose light tiles exceed one round:
-                    // one GPU, and 1/2 shards; 1/2 shard of B 240.7 -> 217.7 ms): the light launch's first
-                    // round (the tiles that start at once) is a launch of its own; the rest
-                    // goes to a high-priority stream behind a short wait, so that it is queued
-                    // after the first round has been dispatched and wins every slot that
-                    // frees while it has workgroups left. Once the first round and the
-                    // heavy tiles are done, their path stage (normal priority) takes the slots
-                    // the chain no longer needs; the rest of the path stage follows the chains.
-                    const int64_t round1 = std::min<int64_t>(nb - heavy, (int64_t)c->n_simd * c->ci_wps -
-                                                                             heavy * ci_heavy_waves(c));
-                    bool overlap = heavy > 0 && c->knobs.paths_overlap > 0 && paths_ci_exact &&
-                                   learned && round1 > 0 && round1 < nb - heavy;
-                    if (overlap && !c->stream3) {   // created on first use (one-GPU frames only)
+                    // PBRT_PATHS_OVERLAP (a learned split, G == 1): the completion-driven path stage.
+                    //  - the heavy launch on the main stream (normal priority);
+                    //  - the light launch on stream3 (high priority: it wins every slot that frees
+                    //    while it has workgroups left), behind a k_gate that opens once every heavy
+                    //    workgroup has started, so it never delays a heavy tile's start;
+                    //  - the path stage on stream2 (normal priority): chunks of the tiles in their
+                    //    chains' completion order (k_chain_ci's completion list), each behind a k_gate
+                    //    that opens when its tiles' chains have ended. The chunks halve (1/2, 1/4, ...
+                    //    of the tiles; the last 1/2^(K-1)), so most path work is queued while the
+                    //    chains run and takes the slots they free once no chain workgroup waits.
+                    // Progress-driven, not timed (it replaces round 5's timed wait); only the
+                    // schedule changes, never a result.
+                    const bool overlap = heavy > 0 && c->knobs.paths_overlap > 0 && paths_ci_exact && learned;
+                    if (overlap && !c->stream3) {   // created on first use
                         int least = 0, greatest = 0;
                         HIPCHK(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
                         HIPCHK(c, hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, greatest));
-                        HIPCHK(c, hipEventCreateWithFlags(&c->ev_heavy, hipEventDisableTiming));
                         HIPCHK(c, hipEventCreateWithFlags(&c->ev_l2, hipEventDisableTiming));
                         HIPCHK(c, hipEventCreateWithFlags(&c->ev_p1, hipEventDisableTiming));
                     }
+                    if (overlap && c->prog_cap < nb + 2) {
+                        if (c->d_prog) (void)hipFree(c->d_prog);
+                        c->d_prog = nullptr;
+                        c->prog_cap = 0;
+                        HIPCHK(c, hipMalloc((void**)&c->d_prog, sizeof(uint32_t) * (size_t)(nb + 2)));
+                        c->prog_cap = nb + 2;
+                    }
                     if (overlap) {
+                        HIPCHK(c, hipMemsetAsync(c->d_prog, 0, 2 * sizeof(uint32_t), c->stream));
+                        HIPCHK(c, hipMemsetAsync(c->d_prog + 2, 0xFF, sizeof(uint32_t) * (size_t)nb, c->stream));
                         HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
-                        launch_ci(ci_heavy_waves(c), heavy, order, c->stream);
-                        HIPCHK(c, hipEventRecord(c->ev_heavy, c->stream));
-                        HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
+                        launch_ci(ci_heavy_waves(c), heavy, order, c->stream, c->d_prog);
+                        HIPCHK(c, hipGetLastError());   // the gates below wait for these workgroups
                         HIPCHK(c, hipStreamWaitEvent(c->stream3, c->ev_split, 0));
-                        launch_ci(1, round1, order + heavy, c->stream2);
-                        hipLaunchKernelGGL(k_delay, dim3(1), dim3(1), 0, c->stream3,
-                                           (uint32_t)c->knobs.paths_overlap * 100u);   // 100 MHz ticks
-                        launch_ci(1, nb - heavy - round1, order + heavy + round1, c->stream3);
-                        HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
+                        hipLaunchKernelGGL(k_gate, dim3(1), dim3(kWave), 0, c->stream3, c->d_prog, (uint32_t)heavy,
+                                           (uint32_t)heavy, c->d_ctr);
+                        launch_ci(1, nb - heavy, order + heavy, c->stream3, c->d_prog);
+                        HIPCHK(c, hipGetLastError());
                         HIPCHK(c, hipEventRecord(c->ev_l2, c->stream3));
-                        HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_heavy, 0));
-                        launch_paths(order, heavy + round1, c->stream2);
+                        HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
+                        for (int64_t s0 = 0, j = 0; s0 < nb; j++) {
+                            const int64_t e0 = j + 1 >= c->knobs.paths_overlap ? nb : s0 + std::max<int64_t>(1, (nb - s0) / 2);
+                            hipLaunchKernelGGL(k_gate, dim3(1), dim3(kWave), 0, c->stream2, c->d_prog, (uint32_t)s0,
+                                               (uint32_t)e0, c->d_ctr);
+                            launch_paths(c->d_prog + 2 + s0, e0 - s0, c->stream2);
+                            s0 = e0;
+                        }
                         HIPCHK(c, hipEventRecord(c->ev_p1, c->stream2));
-                        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
                         HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_l2, 0));
-                        c->ov_done = heavy + round1;
-                        c->ov_order = order;
+                        c->ov_done = nb;
                     } else if (heavy > 0) {
                         HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
-                        launch_ci(ci_heavy_waves(c), heavy, order, c->stream);
+                        launch_ci(ci_heavy_waves(c), heavy, order, c->stream, nullptr);
                         HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
-                        launch_ci(1, nb - heavy, order + heavy, c->stream2);
+                        launch_ci(1, nb - heavy, order + heavy, c->stream2, nullptr);
                         HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
                         HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
                     } else {
-                        launch_ci(kw, nb, order, c->stream);
+                        launch_ci(kw, nb, order, c->stream, nullptr);
                     }
                 }
                 HIPCHK(c, hipEventRecord(c->bev[3 * bi + 1], c->stream));
@@ -1356,8 +1482,7 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                                        (unsigned)lds, c->stream, with_slot(sc, 5), rp, c->wb, sb, nb * c->wb.ppt,
                                        c->d_ctr, sl, nullptr);
                 }
-                else if (c->ov_done > 0) {   // the rest of an overlapped path stage
-                    launch_paths(c->ov_order + c->ov_done, nb - c->ov_done, c->stream);
+                else if (c->ov_done > 0) {   // the completion-driven path stage (stream2) ends the chain stage
                     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_p1, 0));
                 } else {
                     launch_paths(nullptr, nb, c->stream);
@@ -1475,7 +1600,9 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
         c->heavy_k = std::min<int64_t>(k, c->n_simd / 4);   // at most a quarter of the wave slots
         if (ci_heavy_override(c) >= 0) c->heavy_k = ci_heavy_override(c);
         c->order_key = c->ticks_key;
+        if (ci_order_cache(c)) sched_cache_put(c, c->ticks_key, c->h_slot_order, c->heavy_k);
     }
+    if (ctr.gate_stall) rc = set_err(c, PBRT_E_HIP, "k_gate: the chain progress record stalled (60 s)");
     if (ctr.any_panic) {
         std::vector<PanicRec> pr((size_t)c->rp.n_slots);
         HIPCHK(c, hipMemcpy(pr.data(), c->d_panics, sizeof(PanicRec) * pr.size(), hipMemcpyDeviceToHost));
@@ -1598,11 +1725,12 @@ const char* pbrt_gpu_last_error(const pbrt_gpu_ctx* c) { return c ? c->err.c_str
 void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (hipStream_t st : {c->stream, c->stream2, c->stream3})
+        if (st) (void)hipStreamSynchronize(st);
     void* bufs[] = {c->d_shapes, c->d_materials, c->d_prims, c->d_nodes, c->d_order, c->d_lights, c->d_camera, c->d_film,
                     c->d_dist,   c->d_films,     c->d_s1d,   c->d_panics, c->d_ctr,   c->d_out,    c->d_jump,
                     c->d_wave,   c->d_fprims, c->d_ticks, c->d_slot_order, c->d_groups,
-                    c->d_gmasks, c->d_cost,   c->d_cost_keys, c->d_pw, c->d_cancel_seen};
+                    c->d_gmasks, c->d_cost,   c->d_cost_keys, c->d_pw, c->d_cancel_seen, c->d_prog};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     mesh_bvh_free(c->mesh);
@@ -1612,7 +1740,7 @@ void pbrt_gpu_destroy(pbrt_gpu_ctx* c) {
     if (c->ev2) (void)hipEventDestroy(c->ev2);
     if (c->ev_split) (void)hipEventDestroy(c->ev_split);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
-    for (hipEvent_t e : {c->ev_heavy, c->ev_l2, c->ev_p1})
+    for (hipEvent_t e : {c->ev_l2, c->ev_p1})
         if (e) (void)hipEventDestroy(e);
     if (c->stream3) {
         (void)hipStreamSynchronize(c->stream3);
@@ -1641,7 +1769,6 @@ int pbrt_film_to_rgba8(const double* film, int64_t w, int64_t h, uint8_t* rgba) 
 }  // extern "C"
 
 // ============================================================ diagnostics
-#include "../../include/pbrt_diag.h"
 
 namespace {
 __global__ void k_probe(int op, const double* __restrict__ in, int64_t n, int in_stride, double* __restrict__ out,
@@ -1803,6 +1930,16 @@ extern "C" int64_t pbrt_gpu_tile_ticks(pbrt_gpu_ctx* c, uint32_t* out, int64_t n
     const int64_t m = (int64_t)c->h_last_ticks.size();
     for (int64_t i = 0; out && i < n && i < m; i++) out[i] = c->h_last_ticks[(size_t)i];
     return m;
+}
+
+extern "C" void pbrt_gpu_schedule_cache_clear(void) {
+    std::lock_guard<std::mutex> lk(g_sched_mu);
+    g_sched.clear();
+}
+
+extern "C" int pbrt_gpu_schedule_source(pbrt_gpu_ctx* c) {
+    if (!c) return -PBRT_E_INVALID;
+    return c->sched_src;
 }
 
 extern "C" int64_t pbrt_gpu_tile_costs(pbrt_gpu_ctx* c, float* out, int64_t n) {

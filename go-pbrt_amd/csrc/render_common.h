@@ -34,6 +34,8 @@ struct RenderParams {
     int32_t flags;   // pbrt_render_desc.flags
     int32_t sp_events, sp_draws, sp_serial;   // wave kernel StartPixel: events, raw draws buffered
     int32_t mode;                             // PBRT_MODE_EXACT / _THROUGHPUT
+    int32_t sp_window;                        // sp_serial without jitter: the windowed wave StartPixel
+    int32_t pad0;
 };
 
 struct PanicRec {
@@ -47,7 +49,7 @@ struct PanicRec {
 struct Counters {
     unsigned long long paths, camera_samples, closest_rays, shadow_rays;
     int32_t any_panic;
-    int32_t pad;
+    int32_t gate_stall;   // a k_gate wait ended without the progress it waited for (never in a correct run)
     // wave kernel diagnostics (pbrt_gpu_counters): speculation windows, and
     // lane-0 clock64 cycles in StartPixel / bounce 1 / chain / full paths / film add
     unsigned long long windows, phase[8];
@@ -224,6 +226,18 @@ __device__ __forceinline__ uint64_t pcg_inc_of(uint64_t seed) { return (seed << 
 // the work. The shuffled 1D values are left in s1d (LDS); returns the PCG32
 // state after the pixel's draws.
 __shared__ int g_sp_overflow;
+constexpr int kSpRing = 256;   // windowed StartPixel: raw draws in flight (a power of two)
+// Bytes of the StartPixel draw area (ChainLayout.vbuf): every raw draw (the wave
+// StartPixel), or for the windowed one its uint16 permutations then the draw
+// ring, or nothing (the serial StartPixel)
+__host__ __device__ inline int64_t sp_vbuf_bytes(const RenderParams& rp) {
+    if (rp.sp_window) return (((int64_t)rp.ndims * rp.spp * 2 + 15) & ~int64_t(15)) + kSpRing * 4;
+    return rp.sp_serial ? 4 : (int64_t)rp.sp_draws * 4;
+}
+// kWin: the windowed version is compiled in (k_chain_ci instantiates it only
+// where the host runs it: its code in the chain kernel raised the spills of the
+// chain's main loop, config B 314 -> 340 ms)
+template <bool kWin = true>
 __device__ uint64_t start_pixel_wave(const RenderParams& rp, const PcgJump& J, uint64_t S, uint64_t inc, double* s1d,
                                      uint16_t* other, uint32_t* vbuf, uint64_t* sh_state) {
     const int lane = threadIdx.x;
@@ -240,7 +254,87 @@ __device__ uint64_t start_pixel_wave(const RenderParams& rp, const PcgJump& J, u
     // jump-ahead, then resolve R chunk by chunk: one ballot per
     // rejection shifts every later event by one draw.
     bool serial_sp = rp.sp_serial != 0;
-    if (!serial_sp) {
+    if (kWin && serial_sp && rp.sp_window && !(rp.flags & PBRT_FLAG_SERIAL_START_PIXEL)) {
+        // Windowed wave StartPixel (large spp without jitter, where a buffer of
+        // every raw draw would not fit LDS: config C's 256 spp). The same events
+        // and rejection resolution as above, but the raw draws pass through a
+        // ring of kSpRing entries, filled 64 at a time by jump-ahead as the
+        // events advance. The 1D picks land in `other`; the Fisher-Yates swaps
+        // (stratified.go:40-47, sampling.go:127-145) run on uint16 indices in
+        // LDS (perm), and the values, min((i + 0.5) / n, OneMinusEpsilon) of
+        // the index i a slot ends with (no jitter: a value is a function of its
+        // index), are written once, coalesced, to s1d (the pixel's global
+        // record). Replaces the lane-0 replay, whose swaps were dependent
+        // global-memory round trips (18% of config C's chain cycles).
+        uint16_t* perm = (uint16_t*)vbuf;
+        uint32_t* ring = (uint32_t*)((unsigned char*)vbuf + (((size_t)ndims * n * 2 + 15) & ~(size_t)15));
+        const int E = rp.sp_events;   // ndims * n 1D picks, then ndims * n 2D picks
+        bool overflow = false;
+        int R = 0;
+        if (w0) {
+            uint64_t st = pcg_advance(J, S, inc, (uint64_t)lane);
+            int filled = 0;   // draws [0, filled) have been written to the ring
+            auto fill64 = [&]() {
+                ring[(filled + lane) & (kSpRing - 1)] = pcg_output(st);
+                st = J.a[6] * st + inc * J.b[6];   // +64 draws
+                filled += kWave;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+            };
+            for (int cb = 0; cb < E; cb += kWave) {
+                while (filled < cb + R + 2 * kWave) fill64();   // the window covers the chunk and 64 rejections
+                const int e = cb + lane;
+                int kind = 0, slt = 0, i = 0;   // 2: 1D pick, 3: 2D pick
+                if (e < E) {
+                    if (e < ndims * n) { kind = 2; i = e % n; slt = e; }
+                    else { kind = 3; i = (e - ndims * n) % n; }
+                }
+                const uint32_t b = (uint32_t)(n - i);
+                const uint32_t thr = kind >= 2 ? (~b + 1u) % b : 0u;
+                int local = 0;
+                for (;;) {
+                    const int t = e + R + local;
+                    if (__any(kind != 0 && t >= filled)) {   // many rejections in one chunk
+                        if (filled + kWave - (cb + R) > kSpRing) { overflow = true; break; }
+                        fill64();
+                        continue;
+                    }
+                    const bool bad = kind != 0 && ring[t & (kSpRing - 1)] < thr;
+                    const unsigned long long m = __ballot(bad);
+                    if (m == 0) break;
+                    const int first = __ffsll((long long)m) - 1;
+                    if (lane >= first) local++;
+                }
+                if (overflow) break;
+                if (kind == 2) other[slt] = (uint16_t)(i + (int)(ring[(e + R + local) & (kSpRing - 1)] % b));
+                R = __builtin_amdgcn_readfirstlane(R + __shfl(local, kWave - 1));   // wave-uniform
+            }
+            if (lane == 0) g_sp_overflow = overflow;
+        }
+        __syncthreads();
+        if (!g_sp_overflow) {
+            const int nt = (int)blockDim.x, tid = (int)threadIdx.x;
+            for (int idx = tid; idx < ndims * n; idx += nt) perm[idx] = (uint16_t)(idx % n);
+            __syncthreads();
+            if (tid < ndims) {
+                uint16_t* pm = perm + tid * n;
+                const uint16_t* oth = other + tid * n;
+                for (int k = 0; k < n; k++) {
+                    const int o = oth[k];
+                    const uint16_t a = pm[k];
+                    pm[k] = pm[o];
+                    pm[o] = a;
+                }
+            }
+            __syncthreads();
+            for (int idx = tid; idx < ndims * n; idx += nt)
+                s1d[idx] = gomath::min(((double)perm[idx] + 0.5) * inv_n, gomath::kOneMinusEpsilon);
+            if (tid == 0) *sh_state = pcg_advance(J, S, inc, (uint64_t)(E + R));
+            __syncthreads();
+            return *sh_state;
+        }
+        // (a window overflow, never seen: the lane-0 replay below)
+    } else if (!serial_sp) {
         const int E = rp.sp_events, V = rp.sp_draws;
         if (w0) {
             uint64_t st = pcg_advance(J, S, inc, (uint64_t)lane);
@@ -730,6 +824,7 @@ constexpr double kCostPixel = 150.0;   // one StartPixel ~ this many trajectory 
 #define PBRT_CHAIN_LB 1   // leaf boxes per scan iteration in k_chain_ci's traversal (build option)
 #endif
 constexpr uint32_t kNoOff = 0xFFFFFFFFu;
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;   // an unwritten entry of k_chain_ci's completion list
 constexpr uint32_t kBadSpecD = 0xFFFFFFFEu;   // speculative lane could not resolve D
 constexpr uint32_t kBadExactD = 0xFFFFFFFDu;  // the exact head's trajectory panics
 struct RingEnt {

@@ -37,9 +37,9 @@ __global__ void k_dl_panics(RenderParams rp, WaveBufs wb, int64_t slot_base, int
 template <bool kX = false>
 __global__ void k_tile_cost(DevScene sc, RenderParams rp, WaveBufs wb, int64_t slot_base, int64_t nb, float* __restrict__ feat, uint64_t* __restrict__ keys);
 __global__ void k_order_of_keys(const uint64_t* __restrict__ keys, int64_t nb, uint32_t* __restrict__ order);
-__global__ void k_delay(uint32_t ticks);
-template <int kW, int kDepth = 0, bool kX = false, int kEu = 0>
-__global__ void k_chain_ci(DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base, int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr, const uint32_t* __restrict__ order, uint32_t* __restrict__ ticks, int cstride);
+__global__ void k_gate(const uint32_t* __restrict__ prog, uint32_t b, uint32_t e, Counters* __restrict__ ctr);
+template <int kW, int kDepth = 0, bool kX = false, int kEu = 0, bool kSpWin = false>
+__global__ void k_chain_ci(DevScene sc, RenderParams rp, ChainLayout lay, const PcgJump* __restrict__ jump, WaveBufs wb, int64_t slot_base, int64_t nslots_batch, int lanes_per_tile, int ring_size, Counters* __restrict__ ctr, const uint32_t* __restrict__ order, uint32_t* __restrict__ ticks, int cstride, uint32_t* __restrict__ prog);
 __global__ void k_merge_film(const pbrt_film_desc* __restrict__ film_desc, RenderParams rp, const double* __restrict__ films, double* __restrict__ out, const int* __restrict__ cancel_seen);
 __global__ void k_intersect(DevScene sc, int64_t n, const double* __restrict__ rays, double* __restrict__ out, int any_hit);
 

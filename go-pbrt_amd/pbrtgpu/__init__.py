@@ -70,6 +70,9 @@ def lib():
     L.pbrt_gpu_tile_costs.argtypes = [C.c_void_p, P(C.c_float), i64]
     L.pbrt_gpu_tile_costs.restype = i64
     L.pbrt_gpu_counters.argtypes = [C.c_void_p, P(C.c_uint64), C.c_int]
+    L.pbrt_gpu_schedule_source.argtypes = [C.c_void_p]
+    L.pbrt_gpu_schedule_cache_clear.argtypes = []
+    L.pbrt_gpu_schedule_cache_clear.restype = None
     for name in ("pbrt_translate", "pbrt_scale"):
         getattr(L, name).argtypes = [d, d, d, T]
         getattr(L, name).restype = None
@@ -452,6 +455,14 @@ class Renderer:
                 self._check(-rc)
         return out
 
+    SCHEDULE_SOURCES = {0: "launch order", 1: "probe", 2: "learned", 3: "cached"}
+
+    def schedule_source(self):
+        """Where the last EXACT frame's tile schedule came from: 'launch order', 'probe'
+        (cold-frame estimate), 'learned' (this context's previous frame) or 'cached'
+        (the process-wide cache: another context's frame of the same scene and configuration)."""
+        return self.SCHEDULE_SOURCES[lib().pbrt_gpu_schedule_source(self.h)]
+
     def counters(self):
         """pbrt_gpu_counters of the last render (include/pbrt_diag.h order)."""
         out = np.zeros(128, dtype=np.uint64)
@@ -497,6 +508,11 @@ class Renderer:
 
     def __del__(self):
         self.close()
+
+
+def schedule_cache_clear():
+    """Empty the process-wide schedule cache (pbrt_gpu_schedule_cache_clear)."""
+    lib().pbrt_gpu_schedule_cache_clear()
 
 
 def film_to_rgba8(film):

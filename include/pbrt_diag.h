@@ -89,6 +89,18 @@ int64_t pbrt_gpu_tile_ticks(struct pbrt_gpu_ctx* ctx, uint32_t* out, int64_t n, 
  * other builds). */
 int64_t pbrt_gpu_tile_clocks(struct pbrt_gpu_ctx* ctx, uint32_t* start, uint32_t* end, int64_t n);
 
+/* Where the last EXACT continuous-issue frame's tile schedule came from:
+ * PBRT_SCHED_LAUNCH_ORDER (none: identity order), PBRT_SCHED_PROBE (the
+ * cold-frame k_tile_cost estimate), PBRT_SCHED_LEARNED (this context's
+ * previous frame), PBRT_SCHED_CACHED (the process-wide cache: another context's
+ * measured frame of the same scene content and configuration). */
+enum { PBRT_SCHED_LAUNCH_ORDER = 0, PBRT_SCHED_PROBE = 1, PBRT_SCHED_LEARNED = 2, PBRT_SCHED_CACHED = 3 };
+int pbrt_gpu_schedule_source(struct pbrt_gpu_ctx* ctx);
+/* Empties the process-wide schedule cache (the next fresh context of any scene
+ * starts from the probe again). PBRT_CI_ORDER_CACHE=0 disables the cache for
+ * contexts created while it is set. */
+void pbrt_gpu_schedule_cache_clear(void);
+
 /* Cold-frame schedule estimate of the last EXACT frame, if that frame ran
  * render.hip's k_tile_cost probe (a fresh context or a new configuration):
  * per slot {chain work (lane-bounces), hit pixels, pixels, cost}. Copies

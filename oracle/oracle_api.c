@@ -104,6 +104,12 @@ void oracle_pcg_floats(uint64_t seed, int n, double* out) {
 void* oracle_scene_new(void) { return calloc(1, sizeof(orc_scene)); }
 void* oracle_scene_readme(int64_t w, int64_t h) { return orc_scene_readme(w, h); }
 void* oracle_scene_cornell(int64_t w, int64_t h) { return orc_scene_cornell(w, h); }
+void* oracle_scene_heightfield(int64_t w, int64_t h, int quads, uint64_t seed) {
+    return orc_scene_heightfield(w, h, quads, seed);
+}
+void* oracle_scene_readme_glass(int64_t w, int64_t h, int special, int mirror) {
+    return orc_scene_readme_glass(w, h, special, mirror);
+}
 int oracle_scene_add_shape(void* s, const pbrt_shape_desc* d) { return orc_add_shape((orc_scene*)s, *d); }
 int oracle_scene_add_material(void* s, const pbrt_material_desc* d) { return orc_add_material((orc_scene*)s, *d); }
 int oracle_scene_add_primitive(void* s, const pbrt_primitive_desc* d) {

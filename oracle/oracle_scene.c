@@ -453,47 +453,19 @@ static pbrt_material_desc matte_const(double r, double g, double b) {
     return m;
 }
 
-/* internal/render/server.go:29-164 */
-orc_scene* orc_scene_readme(int64_t w, int64_t h) {
-    orc_scene* sc = (orc_scene*)calloc(1, sizeof(orc_scene));
-    int n = 8;
-    for (int k = 1; k < n; k++) {
-        for (int i = 0; i < 3; i++) {
-            double x = 0, y = 0, z = 0, cr = 0, cg = 0, cb = 0;
-            if (i == 0) { x = (double)k / (double)n * 100; cr = 1; }
-            if (i == 1) { y = (double)k / (double)n * 100; cg = 1; }
-            if (i == 2) { z = (double)k / (double)n * 100; cb = 1; }
-            double radius = 2.0;
-            y = go_max(y, radius / 2);
-            pbrt_transform o2w = orc_translate(0, 0, 0);
-            int s = orc_add_shape(sc, orc_sphere(o2w, 1, radius, -radius, radius, 360.0));
-            int m = orc_add_material(sc, matte_const(cr, cg, cb));
-            pbrt_primitive_desc p;
-            memset(&p, 0, sizeof(p));
-            p.kind = PBRT_PRIM_TRANSFORMED; p.shape = s; p.material = m;
-            p.prim_to_world = orc_translate(x, y, z);
-            sc->prims_in[sc->n_prims_in++] = p;
-        }
-    }
+/* server.go:94-104: the floor's Checkerboard2D (1, 0.18), planar mapping vs (.2, 0, 0), vt (0, 0, .2) */
+static pbrt_material_desc readme_checker(void) {
     pbrt_material_desc chk;
     memset(&chk, 0, sizeof(chk));
     chk.kd_type = PBRT_TEX_CHECKERBOARD2D;
     chk.vs[0] = .2; chk.vt[2] = .2; chk.ds = 0; chk.dt = 0;
     chk.tex1[0] = chk.tex1[1] = chk.tex1[2] = 1.0;
     chk.tex2[0] = chk.tex2[1] = chk.tex2[2] = 0.18;
-    int mchk = orc_add_material(sc, chk);
-    pbrt_transform t0 = orc_translate(0, 0, 0);
-    pbrt_transform rx = orc_rotate(0, 90);
-    pbrt_transform dx1 = orc_xf_mul(&t0, &rx);
-    int d1 = orc_add_shape(sc, orc_disk(dx1, 0.01, 10000, 0, 360));
-    int d2 = orc_add_shape(sc, orc_disk(orc_translate(-50, 0, -50), 0.01, 10000, 0, 360));
-    pbrt_primitive_desc p;
-    memset(&p, 0, sizeof(p));
-    p.kind = PBRT_PRIM_GEOMETRIC; p.shape = d1; p.material = mchk;
-    sc->prims_in[sc->n_prims_in++] = p;
-    p.shape = d2;
-    sc->prims_in[sc->n_prims_in++] = p;
+    return chk;
+}
 
+/* server.go:106-159: the four lights, the film and the camera */
+static void readme_lights_camera(orc_scene* sc, int64_t w, int64_t h) {
     /* lights, server.go:106-130 */
     pbrt_light_desc l;
     memset(&l, 0, sizeof(l));
@@ -534,7 +506,178 @@ orc_scene* orc_scene_readme(int64_t w, int64_t h) {
     cam = orc_xf_mul(&cam, &ry);
     cam = orc_xf_mul(&cam, &rxx);
     set_film_camera(sc, w, h, cam, 100, 0, 20);
+}
+
+/* internal/render/server.go:29-164, up to (not including) the BVH build */
+static orc_scene* readme_unbuilt(int64_t w, int64_t h) {
+    orc_scene* sc = (orc_scene*)calloc(1, sizeof(orc_scene));
+    int n = 8;
+    for (int k = 1; k < n; k++) {
+        for (int i = 0; i < 3; i++) {
+            double x = 0, y = 0, z = 0, cr = 0, cg = 0, cb = 0;
+            if (i == 0) { x = (double)k / (double)n * 100; cr = 1; }
+            if (i == 1) { y = (double)k / (double)n * 100; cg = 1; }
+            if (i == 2) { z = (double)k / (double)n * 100; cb = 1; }
+            double radius = 2.0;
+            y = go_max(y, radius / 2);
+            pbrt_transform o2w = orc_translate(0, 0, 0);
+            int s = orc_add_shape(sc, orc_sphere(o2w, 1, radius, -radius, radius, 360.0));
+            int m = orc_add_material(sc, matte_const(cr, cg, cb));
+            pbrt_primitive_desc p;
+            memset(&p, 0, sizeof(p));
+            p.kind = PBRT_PRIM_TRANSFORMED; p.shape = s; p.material = m;
+            p.prim_to_world = orc_translate(x, y, z);
+            sc->prims_in[sc->n_prims_in++] = p;
+        }
+    }
+    int mchk = orc_add_material(sc, readme_checker());
+    pbrt_transform t0 = orc_translate(0, 0, 0);
+    pbrt_transform rx = orc_rotate(0, 90);
+    pbrt_transform dx1 = orc_xf_mul(&t0, &rx);
+    int d1 = orc_add_shape(sc, orc_disk(dx1, 0.01, 10000, 0, 360));
+    int d2 = orc_add_shape(sc, orc_disk(orc_translate(-50, 0, -50), 0.01, 10000, 0, 360));
+    pbrt_primitive_desc p;
+    memset(&p, 0, sizeof(p));
+    p.kind = PBRT_PRIM_GEOMETRIC; p.shape = d1; p.material = mchk;
+    sc->prims_in[sc->n_prims_in++] = p;
+    p.shape = d2;
+    sc->prims_in[sc->n_prims_in++] = p;
+
+    readme_lights_camera(sc, w, h);
+    return sc;
+}
+
+orc_scene* orc_scene_readme(int64_t w, int64_t h) {
+    orc_scene* sc = readme_unbuilt(w, h);
+    orc_scene_finalize(sc, 2);   /* server.go:162: NewBVH(primitives, 2, ...) */
+    return sc;
+}
+
+/* The README scene plus internal/render/server.go:67-91's commented-out sphere:
+ * radius 5 at (50, 2.5, 50) under a Translate, material NewGlass with Kr = Kt
+ * = 0.5, index 1.5 and no roughness (glass.go:15-26); special = 0 makes it a
+ * black Matte instead. mirror = 1 adds a NewMirror (Kr 0.9, mirror.go:9-14)
+ * sphere of radius 5 at (35, 5, 45). The primitives follow the README's in
+ * construction order (glass, then mirror), then the BVH is built with 2
+ * primitives per node as server.go:162 does. Restated here from that
+ * description, independently of the product's scene builder, so a
+ * construction error on either side shows up as a parity failure. */
+orc_scene* orc_scene_readme_glass(int64_t w, int64_t h, int special, int mirror) {
+    orc_scene* sc = readme_unbuilt(w, h);
+    pbrt_material_desc g;
+    memset(&g, 0, sizeof(g));
+    if (special) {
+        g.type = PBRT_MAT_GLASS;
+        for (int i = 0; i < 3; i++) { g.kr[i] = 0.5; g.kt[i] = 0.5; }
+        g.u_roughness = 0.0;
+        g.v_roughness = 0.0;
+        g.eta = 1.5;
+    } else {
+        g = matte_const(0.0, 0.0, 0.0);
+    }
+    double pos[2][3] = {{50, 2.5, 50}, {35, 5.0, 45}};
+    for (int k = 0; k < (mirror ? 2 : 1); k++) {
+        pbrt_material_desc m;
+        if (k == 0) {
+            m = g;
+        } else {
+            memset(&m, 0, sizeof(m));
+            m.type = PBRT_MAT_MIRROR;
+            m.kr[0] = m.kr[1] = m.kr[2] = 0.9;
+        }
+        int mi = orc_add_material(sc, m);
+        int s = orc_add_shape(sc, orc_sphere(orc_translate(0, 0, 0), 0, 5.0, -5.0, 5.0, 360.0));
+        pbrt_primitive_desc p;
+        memset(&p, 0, sizeof(p));
+        p.kind = PBRT_PRIM_TRANSFORMED; p.shape = s; p.material = mi;
+        p.prim_to_world = orc_translate(pos[k][0], pos[k][1], pos[k][2]);
+        sc->prims_in[sc->n_prims_in++] = p;
+    }
     orc_scene_finalize(sc, 2);
+    return sc;
+}
+
+/* Extension (BASELINE configs D/E; no reference arithmetic, parity unpinned
+ * against Go): the procedural height field of DESIGN.md §1, restated here
+ * from its description so the oracle's side of the mesh fixtures does not
+ * come from the product's builder. quads x quads cells over [-100, 200]^2
+ * (x, z), two triangles per cell, counter-clockwise from +y; vertex height
+ * y = 2 Sin(.3x) Cos(.2z) + 3 noise(x, z) in float64 (Go's Sin / Cos), stored
+ * as float32; noise = value noise on the lattice (x, z) / 10: lattice values
+ * in [-1, 1) from a splitmix64 finalizer of seed * phi ^ i * c1 ^ j * c2,
+ * blended with smoothstep weights. The README's checker material, lights,
+ * film and camera; no analytic primitive. The world bound is the union of the
+ * triangles' vertices (the aggregate holds the mesh). */
+static double hf_lattice(uint64_t seed, int64_t i, int64_t j) {
+    uint64_t z = (seed * 0x9e3779b97f4a7c15ULL) ^ ((uint64_t)i * 0xbf58476d1ce4e5b9ULL) ^
+                 ((uint64_t)j * 0x94d049bb133111ebULL);
+    z += 0x9e3779b97f4a7c15ULL;   /* splitmix64 */
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    z ^= z >> 31;
+    return (double)(z >> 11) / 9007199254740992.0 * 2.0 - 1.0;
+}
+static double hf_height(uint64_t seed, double x, double z) {
+    double gx = x / 10.0, gz = z / 10.0, fx = floor(gx), fz = floor(gz);
+    int64_t i = (int64_t)fx, j = (int64_t)fz;
+    double tx = gx - fx, tz = gz - fz;
+    double sx = tx * tx * (3.0 - 2.0 * tx), sz = tz * tz * (3.0 - 2.0 * tz);
+    double v00 = hf_lattice(seed, i, j), v10 = hf_lattice(seed, i + 1, j);
+    double v01 = hf_lattice(seed, i, j + 1), v11 = hf_lattice(seed, i + 1, j + 1);
+    double near = v00 + (v10 - v00) * sx, far = v01 + (v11 - v01) * sx;
+    double noise = near + (far - near) * sz;
+    return 2.0 * go_sin(0.3 * x) * go_cos(0.2 * z) + 3.0 * noise;
+}
+orc_scene* orc_scene_heightfield(int64_t w, int64_t h, int quads, uint64_t seed) {
+    if (quads < 1 || quads > 46340) return NULL;
+    orc_scene* sc = (orc_scene*)calloc(1, sizeof(orc_scene));
+    int mchk = orc_add_material(sc, readme_checker());
+    int64_t nv = (int64_t)(quads + 1) * (quads + 1), nt = 2 * (int64_t)quads * quads;
+    sc->mesh_p = (float*)malloc(sizeof(float) * 3 * (size_t)nv);
+    sc->mesh_idx = (int32_t*)malloc(sizeof(int32_t) * 3 * (size_t)nt);
+    for (int64_t j = 0; j <= quads; j++)
+        for (int64_t i = 0; i <= quads; i++) {
+            double x = -100.0 + 300.0 * (double)i / (double)quads, z = -100.0 + 300.0 * (double)j / (double)quads;
+            float* v = sc->mesh_p + 3 * (j * (quads + 1) + i);
+            v[0] = (float)x;
+            v[1] = (float)hf_height(seed, x, z);
+            v[2] = (float)z;
+        }
+    int32_t* t = sc->mesh_idx;
+    for (int64_t j = 0; j < quads; j++)
+        for (int64_t i = 0; i < quads; i++) {
+            int32_t a = (int32_t)(j * (quads + 1) + i), b = a + 1, c = a + (quads + 1), d = c + 1;
+            *t++ = a; *t++ = c; *t++ = b;   /* (i, j), (i, j+1), (i+1, j) */
+            *t++ = b; *t++ = c; *t++ = d;   /* (i+1, j), (i, j+1), (i+1, j+1) */
+        }
+    memset(&sc->mesh, 0, sizeof(sc->mesh));
+    sc->mesh.n_vertices = (int32_t)nv;
+    sc->mesh.n_triangles = (int32_t)nt;
+    sc->mesh.material = mchk;
+    sc->mesh.reverse_orientation = 0;
+    sc->mesh.p = sc->mesh_p;
+    sc->mesh.indices = sc->mesh_idx;
+    sc->n_meshes = 1;
+    readme_lights_camera(sc, w, h);
+    orc_scene_finalize(sc, 2);   /* no analytic primitive: no nodes */
+    /* world bound: the union of the triangles' vertices (bounds.go:54-66 Union) */
+    for (int64_t k = 0; k < 3 * nt; k++) {
+        const float* v = sc->mesh_p + 3 * (int64_t)sc->mesh_idx[k];
+        for (int a = 0; a < 3; a++) {
+            double x = (double)v[a];
+            sc->world_min[a] = k == 0 ? x : go_min(sc->world_min[a], x);
+            sc->world_max[a] = k == 0 ? x : go_max(sc->world_max[a], x);
+        }
+    }
+    v3 mn = V3(sc->world_min[0], sc->world_min[1], sc->world_min[2]);
+    v3 mx = V3(sc->world_max[0], sc->world_max[1], sc->world_max[2]);
+    v3 center = v_divs(v_add(mn, mx), 2.0);   /* bounds.go:105-112 BoundingSphere */
+    double radius = 0;
+    if (center.x >= mn.x && center.x <= mx.x && center.y >= mn.y && center.y <= mx.y && center.z >= mn.z &&
+        center.z <= mx.z)
+        radius = v_dist(center, mx);
+    for (int i = 0; i < sc->n_lights; i++)
+        if (sc->lights[i].type == PBRT_LIGHT_DISTANT) sc->lights[i].world_radius = radius;
     return sc;
 }
 
@@ -598,8 +741,17 @@ void orc_scene_desc(orc_scene* sc, pbrt_scene_desc* d) {
     d->nodes = sc->nodes; d->lights = sc->lights;
     d->camera = sc->camera; d->film = sc->film;
     for (int k = 0; k < 3; k++) { d->world_min[k] = sc->world_min[k]; d->world_max[k] = sc->world_max[k]; }
+    if (sc->n_meshes) {
+        d->n_meshes = 1;
+        d->meshes = &sc->mesh;
+    }
 }
-void orc_scene_free(orc_scene* sc) { free(sc); }
+void orc_scene_free(orc_scene* sc) {
+    if (!sc) return;
+    free(sc->mesh_p);
+    free(sc->mesh_idx);
+    free(sc);
+}
 
 /* bvh.go:163-175 PartitionPrimitiveInfoAt with bvh_test.go's centroid-x
  * predicate (mode 0, dim 0) on (prim, cx) records; for tests/ */

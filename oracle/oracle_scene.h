@@ -20,6 +20,10 @@ typedef struct {
     pbrt_camera_desc camera;
     pbrt_film_desc film;
     double world_min[3], world_max[3];
+    int n_meshes;                 /* extension: the height field (0 or 1) */
+    pbrt_mesh_desc mesh;
+    float* mesh_p;
+    int32_t* mesh_idx;
 } orc_scene;
 
 pbrt_matrix4x4 orc_m_mul(const pbrt_matrix4x4* m, const pbrt_matrix4x4* o);
@@ -37,6 +41,8 @@ int orc_add_material(orc_scene* sc, pbrt_material_desc m);
 int orc_scene_finalize(orc_scene* sc, int max_prims);
 orc_scene* orc_scene_readme(int64_t w, int64_t h);
 orc_scene* orc_scene_cornell(int64_t w, int64_t h);
+orc_scene* orc_scene_heightfield(int64_t w, int64_t h, int quads, uint64_t seed);
+orc_scene* orc_scene_readme_glass(int64_t w, int64_t h, int special, int mirror);
 void orc_scene_desc(orc_scene* sc, pbrt_scene_desc* d);
 void orc_scene_free(orc_scene* sc);
 

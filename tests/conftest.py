@@ -26,6 +26,15 @@ def _ensure_built():
 _ensure_built()
 
 
+@pytest.fixture(autouse=True)
+def _no_schedule_cache(monkeypatch):
+    """Every context a test creates learns its own schedule: the process-wide
+    schedule cache (render.hip, on by default) would otherwise hand one test's
+    measured order to the next test's fresh context and change which frames
+    split. tests/test_gpu_schedule_cache.py turns it back on."""
+    monkeypatch.setenv("PBRT_CI_ORDER_CACHE", "0")
+
+
 @pytest.fixture(scope="session")
 def oracle():
     import oracle_lib

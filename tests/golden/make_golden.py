@@ -136,11 +136,14 @@ MAT_CASES = {
     "materials_48x32_s4x4_path": (lambda: scenes.material_scene("both", 48, 32), dict(spp_x=4, spp_y=4)),
     "materials_48x32_s3x3_oren20_path6": (lambda: scenes.material_scene("matte", 48, 32, sigma=20.0),
                                           dict(spp_x=3, spp_y=3, max_depth=6)),
-    "readme_glass_64x48_s3x3_direct5": (lambda: G.Scene.readme_glass(64, 48, mirror=True),
+    # the oracle's own construction of server.go:67-91's glass sphere + a mirror
+    # (oracle_scene.c orc_scene_readme_glass), independent of the product's builder
+    "readme_glass_64x48_s3x3_direct5": (lambda: O.OracleScene.readme_glass(64, 48, mirror=True),
                                         dict(spp_x=3, spp_y=3, integrator=abi.PBRT_INTEGRATOR_DIRECT_LIGHTING,
                                              max_depth=5)),
     "mesh_glass_48x32_s2x2_path": (lambda: scenes.mesh_material_scene("glass", 48, 32), dict(spp_x=2, spp_y=2)),
-    "heightfield_q64_48x32_s2x2_path": (lambda: G.Scene.heightfield(48, 32, quads=64), dict(spp_x=2, spp_y=2)),
+    # the oracle's own height-field generator (oracle_scene.c orc_scene_heightfield)
+    "heightfield_q64_48x32_s2x2_path": (lambda: O.OracleScene.heightfield(48, 32, quads=64), dict(spp_x=2, spp_y=2)),
 }
 # config G (README + server.go:67-91's glass sphere + a mirror, 1920x1080,
 # Stratified(8,8), Path(10)): the 4x4 tiles of pixels x 1216..1279, y 768..831,
@@ -150,7 +153,7 @@ CROP_G = dict(w=1920, h=1080, tx0=76, ty0=48, n=4, render=dict(spp_x=8, spp_y=8)
 
 def crop_g():
     c = CROP_G
-    sc = G.Scene.readme_glass(c["w"], c["h"], mirror=True)
+    sc = O.OracleScene.readme_glass(c["w"], c["h"], mirror=True)
     ntx = (c["w"] + 15) // 16
     acc = None
     paths = 0

@@ -95,6 +95,10 @@ def _bind(L):
         L.oracle_scene_readme.restype = C.c_void_p
         L.oracle_scene_cornell.argtypes = [C.c_int64, C.c_int64]
         L.oracle_scene_cornell.restype = C.c_void_p
+        L.oracle_scene_heightfield.argtypes = [C.c_int64, C.c_int64, C.c_int, C.c_uint64]
+        L.oracle_scene_heightfield.restype = C.c_void_p
+        L.oracle_scene_readme_glass.argtypes = [C.c_int64, C.c_int64, C.c_int, C.c_int]
+        L.oracle_scene_readme_glass.restype = C.c_void_p
         L.oracle_scene_add_shape.argtypes = [C.c_void_p, P(abi.ShapeDesc)]
         L.oracle_scene_add_material.argtypes = [C.c_void_p, P(abi.MaterialDesc)]
         L.oracle_scene_add_primitive.argtypes = [C.c_void_p, P(abi.PrimitiveDesc)]
@@ -137,6 +141,21 @@ class OracleScene:
     @classmethod
     def cornell(cls, w, h):
         return cls(lib().oracle_scene_cornell(w, h))
+
+    @classmethod
+    def heightfield(cls, w, h, quads=707, seed=1):
+        """The height-field extension scene (configs D/E) from the oracle's own
+        generator (oracle_scene.c orc_scene_heightfield)."""
+        hnd = lib().oracle_scene_heightfield(w, h, quads, seed)
+        if not hnd:
+            raise ValueError("quads out of range")
+        return cls(hnd)
+
+    @classmethod
+    def readme_glass(cls, w, h, special="glass", mirror=True):
+        """server.go:67-91's glass sphere (+ a mirror) on the README scene, built
+        by the oracle's own constructor (oracle_scene.c orc_scene_readme_glass)."""
+        return cls(lib().oracle_scene_readme_glass(w, h, 1 if special == "glass" else 0, 1 if mirror else 0))
 
     def order(self):
         out = (C.c_int32 * self.desc.n_prims)()

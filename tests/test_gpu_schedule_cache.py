@@ -1,0 +1,77 @@
+"""The process-wide schedule cache (render.hip, sched_cache_*).
+
+internal/render/server.go:29-164 builds a fresh scene, integrator and renderer
+for every request. A fresh context therefore starts from the schedule another
+context measured on the same scene content and configuration, instead of the
+cold-frame probe. Only the schedule changes: every frame of every context is
+the oracle's, bit for bit.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import pbrtgpu as G
+from pbrtgpu import abi
+
+pytestmark = pytest.mark.gpu
+
+
+def same_bits(a, b):
+    return np.array_equal(np.ascontiguousarray(a).view(np.uint64), np.ascontiguousarray(b).view(np.uint64))
+
+
+def oracle_film(scene, rd):
+    rc, film, _ = O.render(scene.desc, rd, threads=min(16, os.cpu_count() or 1))
+    assert rc == 0
+    return film
+
+
+def test_fresh_context_starts_from_another_contexts_schedule(monkeypatch):
+    monkeypatch.setenv("PBRT_CI_ORDER_CACHE", "1")
+    G.schedule_cache_clear()
+    rd = abi.render_desc(8, 8)
+    scene = G.Scene.readme(320, 192)
+    want = oracle_film(scene, rd)
+    with G.Renderer(scene) as a:   # the first request of the process: probe, then its own measurement
+        for frame, src in enumerate(["probe", "learned"]):
+            film, st = a.render(rd)
+            assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
+            assert a.schedule_source() == src, frame
+            assert same_bits(film, want), frame
+    # a later request: a new scene object with the same content, a new context
+    scene2 = G.Scene.readme(320, 192)
+    with G.Renderer(scene2) as b:
+        for frame, src in enumerate(["cached", "learned"]):
+            film, _ = b.render(rd)
+            assert b.schedule_source() == src, frame
+            assert same_bits(film, want), frame
+    # other content or another configuration: no match
+    with G.Renderer(G.Scene.readme(320, 176)) as c:
+        c.render(rd)
+        assert c.schedule_source() == "probe"
+    rd_shard = abi.render_desc(8, 8, tile_begin=1, tile_stride=2)
+    with G.Renderer(scene2) as d:
+        film, _ = d.render(rd_shard)
+        assert d.schedule_source() == "probe"
+        assert same_bits(film, oracle_film(scene2, rd_shard))
+    G.schedule_cache_clear()
+    with G.Renderer(scene2) as e:
+        e.render(rd)
+        assert e.schedule_source() == "probe"
+
+
+def test_schedule_cache_off(monkeypatch):
+    monkeypatch.setenv("PBRT_CI_ORDER_CACHE", "1")
+    G.schedule_cache_clear()
+    rd = abi.render_desc(4, 4)
+    scene = G.Scene.readme(160, 96)
+    with G.Renderer(scene) as a:
+        a.render(rd)
+        a.render(rd)
+    monkeypatch.setenv("PBRT_CI_ORDER_CACHE", "0")
+    with G.Renderer(scene) as b:
+        b.render(rd)
+        assert b.schedule_source() == "probe"
+    G.schedule_cache_clear()

@@ -31,7 +31,7 @@ for step in "$@"; do
   bench=*)
     spec=${step#bench=}; cfg=${spec%%,*}; extra=""
     [[ "$spec" == *,* ]] && extra=$(echo "${spec#*,}" | tr ',' ' ')
-    timeout -k 10 500 python bench.py --config $cfg --no-cpu-baseline --no-side-mode $extra > $OUT/bench_$cfg.json 2> $OUT/bench_$cfg.err || { echo "bench $cfg failed"; tail -20 $OUT/bench_$cfg.err; exit 1; } ;;
+    timeout -k 10 500 python bench.py --config $cfg --no-cpu-baseline --no-side-mode --no-rpc $extra > $OUT/bench_$cfg.json 2> $OUT/bench_$cfg.err || { echo "bench $cfg failed"; tail -20 $OUT/bench_$cfg.err; exit 1; } ;;
   benchfull=*)
     cfg=${step#benchfull=}
     timeout -k 10 600 python bench.py --config $cfg > $OUT/benchfull_$cfg.json 2> $OUT/benchfull_$cfg.err || { echo "bench $cfg failed"; tail -20 $OUT/benchfull_$cfg.err; exit 1; } ;;
@@ -44,11 +44,11 @@ for step in "$@"; do
     PBRT_GPU_LIB=go-pbrt_amd/lib/exp/libpbrt_gpu_$lib.so timeout -k 10 300 python tools/phase_stats.py --scene $scn > $OUT/phase_${lib}_$scn.txt 2>&1 || { echo "phase $lib failed"; tail -20 $OUT/phase_${lib}_$scn.txt; exit 1; } ;;
   libbench=*)   # libbench=<variant>,<cfg>: bench.py --config <cfg> with lib/exp/libpbrt_gpu_<variant>.so
     spec=${step#libbench=}; v=${spec%%,*}; cfg=${spec#*,}
-    PBRT_GPU_LIB=go-pbrt_amd/lib/exp/libpbrt_gpu_$v.so timeout -k 10 400 python bench.py --config $cfg --no-cpu-baseline --no-side-mode --steps 2 > $OUT/bench_${cfg}_$v.json 2> $OUT/bench_${cfg}_$v.err || { echo "bench $cfg $v failed"; tail -20 $OUT/bench_${cfg}_$v.err; exit 1; } ;;
+    PBRT_GPU_LIB=go-pbrt_amd/lib/exp/libpbrt_gpu_$v.so timeout -k 10 400 python bench.py --config $cfg --no-cpu-baseline --no-side-mode --no-rpc --steps 2 > $OUT/bench_${cfg}_$v.json 2> $OUT/bench_${cfg}_$v.err || { echo "bench $cfg $v failed"; tail -20 $OUT/bench_${cfg}_$v.err; exit 1; } ;;
   envbench=*)   # envbench=VAR=VALUE,<cfg>[,args]: bench.py --config <cfg> (no CPU baseline / side mode) with VAR=VALUE
     spec=${step#envbench=}; kv=${spec%%,*}; rest=${spec#*,}; cfg=${rest%%,*}; extra=""
     [[ "$rest" == *,* ]] && extra=$(echo "${rest#*,}" | tr ',' ' ')
-    env $(echo "$kv" | tr '+' ' ') timeout -k 10 500 python bench.py --config $cfg --no-cpu-baseline --no-side-mode $extra > $OUT/bench_${cfg}_${kv}.json 2> $OUT/bench_${cfg}_${kv}.err || { echo "bench $cfg $kv failed"; tail -20 $OUT/bench_${cfg}_${kv}.err; exit 1; } ;;
+    env $(echo "$kv" | tr '+' ' ') timeout -k 10 500 python bench.py --config $cfg --no-cpu-baseline --no-side-mode --no-rpc $extra > $OUT/bench_${cfg}_${kv}.json 2> $OUT/bench_${cfg}_${kv}.err || { echo "bench $cfg $kv failed"; tail -20 $OUT/bench_${cfg}_${kv}.err; exit 1; } ;;
   py=*)   # py=<tools script>[~args]: python tools/<script>.py args ('~' separates; commas stay), output to <script>_<args>.txt
     spec=${step#py=}; scr=${spec%%~*}; args=""
     [[ "$spec" == *~* ]] && args=$(echo "${spec#*~}" | tr '~' ' ')

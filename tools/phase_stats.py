@@ -1,9 +1,16 @@
 """Render one frame and print the wave kernel's phase counters (diagnostics).
 
     python tools/phase_stats.py [--width W --height H --spp S --kernel auto|serial]
+                                [--scene cornell --max-depth 8 --tile-stride 16]
+
+With the diagnostics build (make diag) it also prints, per pixel, the chain
+steps, the candidate trajectories issued and the on-chain ones (the on-chain
+D histogram's total), and the count of on-chain draw counts above the tail
+cap's bound dmax (k_chain.h; must be 0).
 """
 import argparse
 import ctypes as C
+import json
 import os
 import sys
 import time
@@ -16,6 +23,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--width", type=int, default=1920)
 ap.add_argument("--height", type=int, default=1080)
 ap.add_argument("--spp", type=int, default=8)
+ap.add_argument("--max-depth", type=int, default=10)
+ap.add_argument("--tile-stride", type=int, default=1, help="render every k-th tile only (an evenly spread sample)")
 ap.add_argument("--kernel", default="auto")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--occupancy", type=int, default=0)
@@ -27,22 +36,31 @@ scene = {"readme": G.Scene.readme, "readme_glass": G.Scene.readme_glass, "cornel
     a.width, a.height)
 names = ["paths", "camera_samples", "closest_rays", "shadow_rays", "any_panic", "windows",
          "cyc_start_pixel", "cyc_issue_first_scatter", "cyc_traversal", "cyc_hit_processing",
-         "cyc_barrier_walk", "cyc_5", "cyc_6", "cyc_7"]
+         "cyc_barrier_walk", "issued", "d_over_dmax", "cyc_7"]
 with G.Renderer(scene, kernel=a.kernel, occupancy=a.occupancy, lanes_per_wave=a.tiles_per_wave) as r:
-    rd = abi.render_desc(a.spp, a.spp)
+    rd = abi.render_desc(a.spp, a.spp, max_depth=a.max_depth, tile_stride=a.tile_stride)
     for i in range(a.reps):
         t0 = time.perf_counter()
         r.render_async(rd)
         st = r.synchronize()
         dt = time.perf_counter() - t0
-        out = (C.c_uint64 * 32)()
-        n = G.lib().pbrt_gpu_counters(C.c_void_p(r.h), out, 32)
-        vals = dict(zip(names, list(out)[:n]))
-        tot = sum(vals[k] for k in names[6:13]) or 1
-        print(f"rep {i}: {dt * 1e3:.1f} ms kernel {st.kernel_ms:.1f} ms kernel={st.kernel} "
-              f"Mpaths/s={st.paths_traced / dt / 1e6:.2f}")
-        px = a.width * a.height
+        out = (C.c_uint64 * 78)()
+        n = G.lib().pbrt_gpu_counters(C.c_void_p(r.h), out, 78)
+        vals = dict(zip(names, list(out)[:14]))
+        dh = list(out)[14:n]
+        tot = sum(vals[k] for k in names[6:11]) or 1
+        print(f"rep {i}: {dt * 1e3:.1f} ms kernel {st.kernel_ms:.1f} ms chain {st.chain_ms:.1f} ms "
+              f"kernel={st.kernel} Mpaths/s={st.paths_traced / dt / 1e6:.2f}")
+        px = a.width * a.height / a.tile_stride   # pixels rendered (about, for a tile sample)
         print("  windows/pixel %.2f" % (vals["windows"] / px))
+        onchain = sum(dh)
+        if onchain:
+            print("  issued candidates/pixel %.1f, on-chain/pixel %.1f (%.1f%%), on-chain D above the tail "
+                  "cap's dmax: %d" % (vals["issued"] / px, onchain / px, 100.0 * onchain / max(vals["issued"], 1),
+                                      vals["d_over_dmax"]))
+            mean_d = sum((2 * b + 1) * c for b, c in enumerate(dh)) / onchain
+            print("  on-chain D histogram (bin = D // 2; mean D ~ %.1f): %s" % (
+                mean_d, json.dumps({2 * b: c for b, c in enumerate(dh) if c})))
         sc_ = (C.c_uint64 * 8)()
         G.lib().pbrt_gpu_step_cycles(sc_, 8, 1)
         tot_s = sum(sc_[:5])
@@ -54,5 +72,5 @@ with G.Renderer(scene, kernel=a.kernel, occupancy=a.occupancy, lanes_per_wave=a.
         if tt:   # the steptime build records the traversal regions on their own
             print("  closest-hit traversal: node walk %.1f%%, leaf tests %.1f%%, interaction %.1f%%" % tuple(
                 v / tt * 100 for v in sc_[5:8]))
-        for k in names[6:13]:
+        for k in names[6:11]:
             print(f"  {k:16s} {vals[k] / tot * 100:5.1f}%  {vals[k] / px:10.0f} cyc/pixel")
