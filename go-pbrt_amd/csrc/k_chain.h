@@ -54,6 +54,8 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
 #endif
     __shared__ CiGroup gs[kCiMaxGroups];
     __shared__ uint64_t sh_state;
+    __shared__ uint32_t sh_draws;   // StartPixel's draw count
+    __shared__ int sh_act;          // next-pixel speculation started this step
     __shared__ int wcnt[kW];
 #ifdef PBRT_CI_DIAG
     __shared__ uint32_t dh[64];   // on-chain D histogram of the block (diagnostics)
@@ -72,8 +74,39 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
     double* s1d = lay.s1d >= 0 ? (double*)(lds + lay.s1d) : nullptr;
     uint16_t* other = (uint16_t*)(lds + lay.other);
     uint32_t* vbuf = (uint32_t*)(lds + lay.vbuf);
-    RingEnt* ring = (RingEnt*)(lds + lay.ring) + (size_t)g * R;
-    ChainCache* pcs = (ChainCache*)(lds + lay.pcs);
+    // Next-pixel speculation (multi-wave Matte tiles, rp.ci_nps): once the
+    // current pixel's last sample has its offset, the lanes it leaves idle
+    // trace trajectories of the NEXT pixel from every offset its first sample
+    // can start at (a trajectory depends only on its offset's PCG32 state and
+    // the pixel's bounce-1 record), so the next pixel's chain
+    // starts on resolved entries instead of an empty pipeline. Each pixel
+    // parity has its own ring (not aliased with the StartPixel staging) and
+    // ChainCache; the next pixel's offset is only known after its StartPixel
+    // (draw count sh_draws), and every entry is exact for the pixel it was
+    // traced for, so the walk is unchanged.
+    constexpr bool kNps = kW > 1 && !kX;
+    const bool nps_on = kNps && rp.ci_nps != 0 && cstride == 1;
+    // speculation on the next pixel starts rp.ci_nps samples before the current
+    // pixel's end, once kNpsMinStats draw counts give the mean and spread
+    constexpr uint32_t kNpsMinStats = 16;
+    // the tile's on-chain draw-count statistics (Matte and mesh kernels): with
+    // them the current pixel's candidates stop zcap sigmas above the expected
+    // start of its last sample (next-pixel speculation: 3; PBRT_CI_SCAP otherwise).
+    // Not in the one-wave Matte builds: there the statistics cost registers
+    // (scratch 128 -> 140 B/lane) and idle lanes do not shorten a step of the
+    // VALU-bound walk
+    constexpr bool kStats = !kX && (kW > 1 || kDepth < 0);
+    // (mesh scenes default to 1.5 sigma: config D chain 535 -> 479 ms, flat from 1 to 2,
+    // profiles/r06/mesh_scap/)
+    const float zcap = nps_on ? 3.0f : rp.ci_scap >= 0 ? 0.1f * (float)rp.ci_scap : kDepth < 0 ? 1.5f : 0.0f;
+    // the ring of a pixel: per lane group, or (kNps) per pixel parity
+    auto ring_of = [&](int64_t pix) -> RingEnt* {
+        return (RingEnt*)(lds + lay.ring) + (size_t)(nps_on ? (int)(pix & 1) : g) * R;
+    };
+    auto rpar = [&](int64_t pix) -> int { return nps_on ? (int)(pix & 1) : 0; };
+    // (rb0 / rb1 by select, not an indexed array or a reference to the group's
+    // copy: either would put the copy in scratch)
+    ChainCache* pcs = (ChainCache*)(lds + lay.pcs);   // [2 * group + pixel parity]
     uint16_t* stack = stack_lds + tid;
     const int n = rp.spp, ndims = rp.ndims;
 #ifndef PBRT_CI_TAILCAP
@@ -94,7 +127,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
     const int64_t bs = blk * G + g;
     const uint64_t inc = pcg_inc_of((uint64_t)tile_of_slot(rp, slot_base + (bs < nslots_batch ? bs : 0)));
 #ifdef PBRT_CI_DIAG   // diagnostics build (make diag): steps, lane-0 phase clocks, on-chain D histogram
-    unsigned long long steps = 0;
+    unsigned long long steps = 0, busy = 0;
     unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     long long tprev = clock64();
     auto mark = [&](int k) {
@@ -113,7 +146,12 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
         CiGroup& s = gs[tid];
         s.pi = 0;
         s.kh = 1;
-        s.head = s.nxt = 0;
+        s.A = s.head = s.nxt = 0;
+        s.rb0 = s.rb1 = 0;
+        s.nb = s.nnx = 0;
+        s.nps = 0;
+        s.dcnt = 0;
+        s.dsum = s.dsq = 0.0f;
         s.reissue = 0;
         if (b < nslots_batch) {
             int64_t x0, y0, x1, y1;
@@ -136,6 +174,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
     uint64_t last_host_poll = t_begin;   // when this workgroup last read the host flag
     // lane trajectory state
     uint32_t off = kNoOff;
+    int opi = -1;   // the pixel the lane's candidate belongs to
     // kX: the trajectory's throughput, etaScale and start state live in LDS
     // (the BSDFX bounce needs their registers; 0 B of scratch)
 #ifdef PBRT_CI_LDS_STATE   // experiment: the Matte chain too
@@ -185,15 +224,19 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
                 const int64_t px = x0 + pi % (x1 - x0), py = y0 + pi / (x1 - x0);
                 double* gs1d = wb.s1d + rec * wb.s1d_stride;
                 double* sp = s1d ? s1d : gs1d;
-                const uint64_t S1 = start_pixel_wave<kSpWin>(rp, J, gs[q].S, incq, sp, other, vbuf, &sh_state);
+                const uint64_t S1 = start_pixel_wave<kSpWin>(rp, J, gs[q].S, incq, sp, other, vbuf, &sh_state, &sh_draws);
                 if (s1d)
                     for (int idx = tid; idx < ndims * n; idx += kT) gs1d[idx] = s1d[idx];
                 // the first traced sample's camera time value (read before the ring
                 // clear: with one tile per workgroup the StartPixel staging aliases the ring)
                 const double time_u = sp[1 < n ? 1 : 0];
                 __syncthreads();
-                RingEnt* rq = (RingEnt*)(lds + lay.ring) + (size_t)q * R;
-                for (uint32_t i = (uint32_t)tid; i < R; i += kT) rq[i].tag = kNoOff;
+                // next-pixel speculation already filled this pixel's ring (kNps)
+                const bool spec_ran = nps_on && gs[q].nps != 0;
+                if (!spec_ran) {
+                    RingEnt* rq = nps_on ? ring_of(pi) : (RingEnt*)(lds + lay.ring) + (size_t)q * R;
+                    for (uint32_t i = (uint32_t)tid; i < R; i += kT) rq[i].tag = kNoOff;
+                }
                 // bounce 1 (camera ray, first hit, BSDF) was computed for every
                 // pixel record by k_wf_primary; only the ray time needs StartPixel
                 PixelRec& pr = wb.prec[rec];
@@ -208,14 +251,23 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
                 if (tid == 0 && gs[q].phase == 0) {
                     if (hit0)   // the camera ray's time (Get1D after pFilm, pLens) of the pixel's first traced sample
                         pr.si.time = camera_ray(cam, (double)px, (double)py, time_u, V2{0.0, 0.0}).time;
-                    pcs[q].si = pr.si;
-                    pcs[q].b = pr.b;
-                    if constexpr (kX) pcs[q].x = pr.x;
-                    pcs[q].wo = pr.wo;
-                    pcs[q].hit = hit0;
+                    ChainCache& pq = pcs[2 * q + rpar(pi)];
+                    pq.si = pr.si;
+                    pq.b = pr.b;
+                    if constexpr (kX) pq.x = pr.x;
+                    pq.wo = pr.wo;
+                    pq.hit = hit0;
                     CiGroup& s = gs[q];
                     s.S = S1;
-                    s.head = s.nxt = 0;
+                    s.A += sh_draws;   // the first traced sample starts after StartPixel's draws
+                    s.head = s.A;
+                    // (a first sample below the speculation's base: dense issue from the head)
+                    s.nxt = (spec_ran && s.A >= s.nb) ? max(s.nnx, s.A) : s.A;
+                    if (!spec_ran) {
+                        if (rpar(pi)) s.rb1 = s.A;
+                        else s.rb0 = s.A;
+                    }
+                    s.nps = 0;
                     s.kh = 1;
                     s.reissue = 0;
                     wb.tile_npx[bq] = (int32_t)(pi + 1);
@@ -225,7 +277,10 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
                         s.phase = 1;
                     } else {   // no traced bounce: every sample is black and draws only its
                         // CameraSample's PCG32 values (n_dims < 2: pLens; c_camera)
-                        if (ndims < 2) s.S = pcg_advance(J, S1, incq, (uint64_t)(n - 1) * camera_draws(ndims));
+                        if (ndims < 2) {
+                            s.S = pcg_advance(J, S1, incq, (uint64_t)(n - 1) * camera_draws(ndims));
+                            s.A += (uint32_t)(n - 1) * camera_draws(ndims);
+                        }
                         s.pi = pi + 1;
                         s.phase = s.pi < s.npx ? 0 : 2;
                     }
@@ -268,47 +323,71 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
 #if PBRT_CI_TAILCAP
             const uint32_t tail = sg.head + (uint32_t)(n - 1 - sg.kh) * dmax;
             const int capn = nx0 <= tail ? (int)((tail - nx0) / cs) + 1 : 0;
-            const int nspec = min(min(nidle - re, avail), capn);
+            int nspec = min(min(nidle - re, avail), capn);
+            if (kStats && zcap > 0.0f && sg.dcnt >= kNpsMinStats) {
+                // the current pixel's last sample starts near head + rem * mean: a cap
+                // zcap sigmas above it (the lanes beyond go to the next pixel, or idle)
+                const float rem = (float)(n - 1 - sg.kh);
+                const float mu = sg.dsum / (float)sg.dcnt;
+                const float sd = sqrtf(fmaxf(0.0f, sg.dsq / (float)sg.dcnt - mu * mu));
+                const uint32_t scap = sg.head + (uint32_t)(rem * mu + zcap * sd * sqrtf(rem));
+                nspec = min(nspec, nx0 <= scap ? (int)((scap - nx0) / cs) + 1 : 0);
+            }
 #else
             const int nspec = min(nidle - re, avail);
 #endif
+            // the lanes left: the next pixel's candidates (stride 1, within its ring's window)
+            int nspec1 = 0;
+            if (kNps && sg.phase == 1 && sg.nps) {
+                const int avail1 = sg.nnx < sg.nb + R ? (int)(sg.nb + R - sg.nnx) : 0;
+                nspec1 = max(0, min(nidle - re - max(nspec, 0), avail1));
+            }
             uint32_t o = kNoOff;
             bool exact = false;
+            int opix = (int)sg.pi;
             if (idle) {
                 if (re && rank == 0) {
                     o = sg.head;
                     exact = true;
                 } else {
                     rank -= re;
-                    if (rank < nspec) o = nx0 + cs * (uint32_t)rank;
+                    if (rank < nspec) {
+                        o = nx0 + cs * (uint32_t)rank;
+                    } else if (kNps && rank - nspec < nspec1) {
+                        o = sg.nnx + (uint32_t)(rank - nspec);
+                        opix = (int)sg.pi + 1;
+                    }
                 }
             }
             if (gl == 0 && sg.phase == 1) {
                 gs[g].nxt = nx0 + cs * (uint32_t)max(nspec, 0);
-                CI_DIAG(ph[5] += (unsigned long long)(max(nspec, 0) + re);)   // candidate trajectories issued
+                if (kNps) gs[g].nnx = sg.nnx + (uint32_t)nspec1;
+                CI_DIAG(ph[5] += (unsigned long long)(max(nspec, 0) + nspec1 + re);)   // candidate trajectories issued
+                CI_DIAG(ph[7] += (unsigned long long)nspec1;)   // of them next-pixel speculation
                 if (re) gs[g].reissue = 0;
             }
             if (o != kNoOff) {
                 off = o;
-                st0 = pcg_advance(J, sg.S, inc, (uint64_t)o);
+                opi = opix;
+                st0 = pcg_advance(J, sg.S, inc, (uint64_t)(o - sg.A));
                 c.rng.state = st0;
                 c.draws = 0;
                 c_camera(c, ndims);   // camera: Get2D pFilm, Get2D pLens, Get1D time
                 c.k = exact ? sg.kh : -1;
                 c.kdep = 0;
                 if constexpr (kX) {   // speculative: RR decisions on stratified values are recorded
-                    c.rri = (!exact && ss.rrb) ? (int)(off & (R - 1u)) : -1;
+                    c.rri = (!exact && ss.rrb) ? (int)((off - sg.rb0) & (R - 1u)) : -1;
                     c.rrn = 0;
                 }
                 beta = spec(1);
                 eta_scale = 1.0;
                 bounces = 1;
-                const ChainCache& pc = pcs[g];
+                const ChainCache& pc = pcs[2 * g + rpar(opi)];
                 const int r = traj_scatter<kX>(sc, pc.si, pc.b, pc.x, pc.wo, c, ss, beta, eta_scale, bounces, ray,
                                                rp.max_depth, rp.rr_threshold);
                 tracing = r == 0;
                 if (r != 0) {
-                    RingEnt& e = ring[off & (R - 1u)];
+                    RingEnt& e = ring_of(opi)[(off - (rpar(opi) ? sg.rb1 : sg.rb0)) & (R - 1u)];
                     e.st = st0;
                     e.d = ring_d<kX>(c, ss, r == 1 ? c.draws : (c.k >= 0 ? kBadExactD : kBadSpecD));
                     e.tag = off;
@@ -317,6 +396,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
             }
         }
         mark(1);
+        CI_DIAG(const unsigned long long tbusy = __ballot(tracing); if (lane == 0) busy += (unsigned long long)__popcll(tbusy);)
         // ---- (3) one bounce of every live trajectory
 #ifdef PBRT_CI_DENSE_WALK   // experiment build: the whole wave walks together (dense leaf tests)
         const bool dense = kDepth == 0 && sc.dense_ok && sc.use_lds_nodes;
@@ -352,7 +432,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
                 }
             }
             if (d != kNoOff) {
-                RingEnt& e = ring[off & (R - 1u)];
+                RingEnt& e = ring_of(opi)[(off - (rpar(opi) ? sg.rb1 : sg.rb0)) & (R - 1u)];
                 e.st = st0;
                 e.d = ring_d<kX>(c, ss, d);
                 e.tag = off;
@@ -371,15 +451,17 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
                 if (host) last_host_poll = now;
                 if (cancel_requested(sc, host)) s.phase = 2;
             }
+            RingEnt* rcur = ring_of(s.pi);
+            const uint32_t rbase = rpar(s.pi) ? s.rb1 : s.rb0;
             for (; s.phase == 1;) {
-                RingEnt& e = ring[s.head & (R - 1u)];
+                RingEnt& e = rcur[(s.head - rbase) & (R - 1u)];
                 if (e.tag != s.head) break;
                 uint32_t d = e.d;
                 if (kX && d < kBadExactD && (d & kRrFlag)) {
                     // the trajectory survived RR decisions on stratified values of
                     // the then unknown sample index: with k = kh the first one whose
                     // value is below its q ends the path there
-                    const RrBranches& b = ss.rrb[s.head & (R - 1u)];
+                    const RrBranches& b = ss.rrb[(s.head - rbase) & (R - 1u)];
                     d = (d & kRrTailBad) == kRrTailBad ? kBadSpecD : (d & kRrTailBad);
                     for (uint32_t i = 0; i < b.n; i++) {
                         const uint32_t cd = b.cd[i];
@@ -404,24 +486,100 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
                 // the tail cap's bound (dmax per sample): an on-chain D above it would
                 // only slow the chain, never change a result; counted so tests can pin it
                 CI_DIAG(if (d > dmax) ph[6]++;)
+                if (kStats) {   // the tile's draw-count statistics
+                    s.dcnt++;
+                    s.dsum += (float)d;
+                    s.dsq += (float)d * (float)d;
+                }
                 s.kh++;
                 s.head += d;
                 if (s.kh >= n) {   // every sample of the pixel has its offset; the next StartPixel starts here
-                    s.S = pcg_advance(J, s.S, inc, (uint64_t)s.head);
+                    s.S = pcg_advance(J, s.S, inc, (uint64_t)(s.head - s.A));
+                    s.A = s.head;
                     s.pi++;
                     s.phase = s.pi < s.npx ? 0 : 2;
                     break;
                 }
             }
             if (s.nxt < s.head || (cs == 2u && ((s.nxt ^ s.head) & 1u))) s.nxt = s.head;
-            gs[g] = s;
+            // speculate on the next pixel: when the last sample has its offset (its
+            // first traced sample then starts at least StartPixel's events past this
+            // one), or, with the tile's draw-count statistics, from rp.ci_nps samples
+            // before the end (base: 3 sigma below the expected end; a first sample
+            // below it only wastes the speculation, the switch then issues from the head)
+            int act = 0;
+            const int left = n - s.kh;   // samples whose draw counts are still to come, the head's included
+            const bool stats = s.dcnt >= kNpsMinStats;
+            if (nps_on && s.phase == 1 && !s.nps && (left == 1 || (stats && left <= rp.ci_nps)) &&
+                s.pi + 1 < s.npx) {
+                const PixelRec& pn = wb.prec[rec + 1];
+                if (pn.hit && !pn.panic0) {
+                    float lo = 0.0f;
+                    if (left > 1) {
+                        const float mu = s.dsum / (float)s.dcnt;
+                        const float sd = sqrtf(fmaxf(0.0f, s.dsq / (float)s.dcnt - mu * mu));
+                        lo = fmaxf(0.0f, (float)left * mu - 3.0f * sd * sqrtf((float)left));
+                    }
+                    s.nps = 1;
+                    s.nb = s.head + (uint32_t)lo + (uint32_t)rp.sp_events;
+                    s.nnx = s.nb;
+                    if (rpar(s.pi + 1)) s.rb1 = s.nb;
+                    else s.rb0 = s.nb;
+                    act = 1;
+                }
+            }
+            if (kNps) sh_act = act;
+            // write back what the walk changes (a whole-struct store kept the
+            // untouched fields of the copy in scratch)
+            CiGroup& gw = gs[g];
+            gw.S = s.S;
+            gw.A = s.A;
+            gw.pi = s.pi;
+            gw.head = s.head;
+            gw.nxt = s.nxt;
+            gw.kh = s.kh;
+            gw.phase = s.phase;
+            gw.reissue = s.reissue;
+            if (kStats) {
+                gw.dcnt = s.dcnt;
+                gw.dsum = s.dsum;
+                gw.dsq = s.dsq;
+            }
+            if (kNps) {
+                gw.nps = s.nps;
+                gw.nb = s.nb;
+                gw.nnx = s.nnx;
+                gw.rb0 = s.rb0;
+                gw.rb1 = s.rb1;
+            }
         }
+        if (kNps && tid == 0 && !(gl == 0 && sg.phase == 1)) sh_act = 0;
         __syncthreads();
+        if (kNps && sh_act) {   // the next pixel's ring (its parity's: the pixel before this one's) and ChainCache
+            const CiGroup s3 = gs[g];
+            RingEnt* rn = ring_of(s3.pi + 1);
+            for (uint32_t i = (uint32_t)tid; i < R; i += kT) rn[i].tag = kNoOff;
+            if (tid == 0) {
+                const PixelRec& pn = wb.prec[rec + 1];
+                ChainCache& pc = pcs[2 * g + rpar(s3.pi + 1)];
+                pc.si = pn.si;
+                pc.b = pn.b;
+                pc.wo = pn.wo;
+                pc.hit = pn.hit;
+            }
+        }
         // ---- (5) drop candidates the chain has left behind
         if (off != kNoOff) {
             const CiGroup s2 = gs[g];
-            if (s2.phase != 1 || off < s2.head || (cs == 2u && ((off ^ s2.head) & 1u)) || s2.pi != sg.pi ||
-                (PBRT_CI_TAILCAP && off > s2.head + (uint32_t)(n - 1 - s2.kh) * dmax)) {
+            bool keep = false;
+            if (opi == s2.pi && s2.phase == 1)   // the current pixel
+                keep = !(off < s2.head || (cs == 2u && ((off ^ s2.head) & 1u)) ||
+                         (PBRT_CI_TAILCAP && off > s2.head + (uint32_t)(n - 1 - s2.kh) * dmax));
+            else if (kNps && opi == s2.pi && s2.phase == 0)   // speculated for the pixel whose StartPixel is next
+                keep = s2.nps != 0;
+            else if (kNps && opi == s2.pi + 1 && s2.phase == 1)   // the next pixel's speculation
+                keep = s2.nps != 0;
+            if (!keep) {
                 off = kNoOff;
                 tracing = false;
             }
@@ -434,7 +592,9 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
     if (tid == 0) {
         atomicAdd(&ctr->windows, steps);
         for (int k = 0; k < 8; k++) atomicAdd(&ctr->phase[k], ph[k]);
+        atomicAdd(&ctr->nps_issued, ph[7]);
     }
+    if (lane == 0) atomicAdd(&ctr->busy, busy);
 #endif
 #undef CI_DIAG
     if (prog) {   // every thread's writes of this tile (records, sample states) reach L2 first

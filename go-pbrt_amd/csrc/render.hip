@@ -68,6 +68,11 @@ struct Knobs {
     bool ci_probe = true;      // PBRT_CI_PROBE=0
     bool ci_order_cache = true;// PBRT_CI_ORDER_CACHE=0
     bool sp_window = true;     // PBRT_SP_WINDOW=0: the lane-0 StartPixel replay instead of the windowed one
+    int ci_scap = -1;          // PBRT_CI_SCAP=Z: k_chain_ci's statistical speculation cap at Z/10 sigmas (0: off;
+                               // -1: the kernel's default, 1.5 sigma for mesh scenes; multi-wave tiles with
+                               // next-pixel speculation always use 3)
+    int ci_nps = 8;            // PBRT_CI_NPS=K: next-pixel speculation in multi-wave k_chain_ci tiles from K
+                               // samples before a pixel's end (0: off)
     int paths_overlap = 5;     // PBRT_PATHS_OVERLAP=K: a split frame's path stage runs in K chunks of the
                                // tiles in their chains' completion order, each released when its tiles'
                                // chains have ended (render_enqueue; 0: off, the path stage after the chains)
@@ -102,6 +107,8 @@ struct Knobs {
         if (const char* e = getenv("PBRT_CI_PROBE")) k.ci_probe = atoi(e) != 0;
         if (const char* e = getenv("PBRT_CI_ORDER_CACHE")) k.ci_order_cache = atoi(e) != 0;
         if (const char* e = getenv("PBRT_SP_WINDOW")) k.sp_window = atoi(e) != 0;
+        if (const char* e = getenv("PBRT_CI_NPS")) k.ci_nps = std::max(0, atoi(e));
+        if (const char* e = getenv("PBRT_CI_SCAP")) k.ci_scap = std::max(-1, atoi(e));
         if (const char* e = getenv("PBRT_PATHS_OVERLAP")) k.paths_overlap = std::min(std::max(0, atoi(e)), 16);
         if (const char* e = getenv("PBRT_PATHS_S1D")) k.paths_s1d_lds = std::strcmp(e, "lds") == 0;
         if (const char* e = getenv("PBRT_PATHS_CI")) {
@@ -689,17 +696,23 @@ bool wave_eligible(const pbrt_gpu_ctx* c, const pbrt_render_desc* rd, const Rend
 // tile per workgroup (G == 1) the StartPixel staging aliases the offset ring:
 // a group starts a pixel only after its chain has dropped every candidate,
 // so the two are never live together (config C, 256 spp: 19 KB of staging).
-ChainLayout ci_layout(const ChainLayout& base, int w, int G, unsigned& lds_bytes) {
+// Multi-wave Matte tiles (nps: k_chain_ci's next-pixel speculation) keep
+// trajectories of the next pixel in flight through its StartPixel: two rings
+// (one per pixel parity) after the staging.
+ChainLayout ci_layout(const ChainLayout& base, int w, int G, unsigned& lds_bytes, bool nps = false) {
     ChainLayout l = base;
-    if (G == 1) {
+    if (nps) {
+        l.ring = (base.staging + 15) & ~15;
+        lds_bytes = (unsigned)(l.ring + 2 * w * kCiRingBytes);
+    } else if (G == 1) {
         l.ring = 0;
         lds_bytes = (unsigned)std::max(base.staging, w * kCiRingBytes);
     } else {
         lds_bytes = (unsigned)(base.total + (w - 1) * kCiRingBytes);
     }
-    // then one ChainCache per lane group (only the groups in use: G, not kCiMaxGroups)
+    // then two ChainCache per lane group (pixel parities; only the groups in use: G, not kCiMaxGroups)
     l.pcs = (int)((lds_bytes + 15u) & ~15u);
-    lds_bytes = (unsigned)l.pcs + (unsigned)(G * sizeof(ChainCache));
+    lds_bytes = (unsigned)l.pcs + (unsigned)(2 * G * sizeof(ChainCache));
     l.total = (int)lds_bytes;
     return l;
 }
@@ -990,6 +1003,8 @@ int prepare(pbrt_gpu_ctx* c, const pbrt_render_desc* rd) {
     rp.lanes_per_wave = c->lanes_per_wave;
     rp.flags = rd->flags;
     rp.mode = rd->mode;
+    rp.ci_nps = 0;   // set per k_chain_ci launch (launch_ci)
+    rp.ci_scap = c->knobs.ci_scap;
     pbrt_distribution_desc& dist = c->host_dist;
     std::memset(&dist, 0, sizeof(dist));
     if (rd->integrator == PBRT_INTEGRATOR_PATH) {
@@ -1318,11 +1333,18 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                         c->ticks_n = nb;
                     }
                     // one launch of n workgroups, workgroup b on slot ord[b] (identity if null)
+                    bool split_launch = false;   // launch_ci's launch is the heavy half of a split
                     auto launch_ci = [&](int w, int64_t n, const uint32_t* ord, hipStream_t st, uint32_t* prog) {
                         if (w > 1) {   // one tile per workgroup of w waves; the ring grows with the lanes
                             const int ring = w * kCiRingBytes / (int)sizeof(RingEnt);
                             unsigned lds = 0;
-                            const ChainLayout lw = ci_layout(c->lay_ci, w, 1, lds);
+                            // next-pixel speculation (k_chain_ci kNps: Matte, stride 1) for launches of
+                            // multi-wave tiles only: not for the heavy launch of a split, where
+                            // its two rings' LDS cost the light tiles beside it (1/4 shard of B
+                            // 132 -> 145 ms; a 1/8 shard, no split: 131.5 -> 127.2 ms)
+                            RenderParams rpl = rp;
+                            rpl.ci_nps = (!kx && !split_launch && ci_stride(c, w) == 1) ? c->knobs.ci_nps : 0;
+                            const ChainLayout lw = ci_layout(c->lay_ci, w, 1, lds, rpl.ci_nps > 0);
                             // kX: LDS-staged trees only, at most 4 waves per tile (wave_eligible, ci_waves)
                             auto kern = kx ? (w == 2 ? k_chain_ci<2, 0, true> : k_chain_ci<4, 0, true>)
                                         : mesh_only ? (w == 2 ? k_chain_ci<2, -1> : w == 4 ? k_chain_ci<4, -1> : k_chain_ci<8, -1>)
@@ -1332,7 +1354,7 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                                            : (w == 2   ? (lds_nodes ? k_chain_ci<2> : k_chain_ci<2, 64>)
                                               : w == 4 ? (lds_nodes ? k_chain_ci<4> : k_chain_ci<4, 64>)
                                                        : (lds_nodes ? k_chain_ci<8> : k_chain_ci<8, 64>));
-                            hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3(kWave * w), lds, st, with_slot(sc, 2), rp, lw,
+                            hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3(kWave * w), lds, st, with_slot(sc, 2), rpl, lw,
                                                c->d_jump, c->wb, sb, nb, kWave * w, ring, c->d_ctr, ord, ticks,
                                                ci_stride(c, w), prog);
                         } else {
@@ -1417,7 +1439,9 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                         HIPCHK(c, hipMemsetAsync(c->d_prog, 0, 2 * sizeof(uint32_t), c->stream));
                         HIPCHK(c, hipMemsetAsync(c->d_prog + 2, 0xFF, sizeof(uint32_t) * (size_t)nb, c->stream));
                         HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
+                        split_launch = true;
                         launch_ci(ci_heavy_waves(c), heavy, order, c->stream, c->d_prog);
+                        split_launch = false;
                         HIPCHK(c, hipGetLastError());   // the gates below wait for these workgroups
                         HIPCHK(c, hipStreamWaitEvent(c->stream3, c->ev_split, 0));
                         hipLaunchKernelGGL(k_gate, dim3(1), dim3(kWave), 0, c->stream3, c->d_prog, (uint32_t)heavy,
@@ -1438,7 +1462,9 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                         c->ov_done = nb;
                     } else if (heavy > 0) {
                         HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
+                        split_launch = true;
                         launch_ci(ci_heavy_waves(c), heavy, order, c->stream, nullptr);
+                        split_launch = false;
                         HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
                         launch_ci(1, nb - heavy, order + heavy, c->stream2, nullptr);
                         HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
@@ -1873,7 +1899,8 @@ extern "C" int pbrt_gpu_counters(pbrt_gpu_ctx* c, uint64_t* out, int n) {
                                       (uint64_t)ctr.any_panic, ctr.windows, ctr.phase[0], ctr.phase[1],
                                       ctr.phase[2], ctr.phase[3], ctr.phase[4], ctr.phase[5],
                                       ctr.phase[6], ctr.phase[7]};
-    for (int i = 0; i < n && i < kNumCounters; i++) out[i] = i < 14 ? v[i] : (uint64_t)ctr.dhist[i - 14];
+    for (int i = 0; i < n && i < kNumCounters; i++)
+        out[i] = i < 14 ? v[i] : i < 78 ? (uint64_t)ctr.dhist[i - 14] : i == 78 ? ctr.busy : ctr.nps_issued;
     return kNumCounters;
 }
 

@@ -35,7 +35,9 @@ struct RenderParams {
     int32_t sp_events, sp_draws, sp_serial;   // wave kernel StartPixel: events, raw draws buffered
     int32_t mode;                             // PBRT_MODE_EXACT / _THROUGHPUT
     int32_t sp_window;                        // sp_serial without jitter: the windowed wave StartPixel
-    int32_t pad0;
+    int32_t ci_nps;                           // k_chain_ci multi-wave tiles: next-pixel speculation
+    int32_t ci_scap;                          // k_chain_ci statistical speculation cap, tenths of a sigma (0: off)
+    int32_t pad1;
 };
 
 struct PanicRec {
@@ -54,8 +56,10 @@ struct Counters {
     // lane-0 clock64 cycles in StartPixel / bounce 1 / chain / full paths / film add
     unsigned long long windows, phase[8];
     unsigned long long dhist[64];   // k_chain_ci diagnostics: on-chain draw counts D (bin D/2, last bin >= 126)
+    unsigned long long busy;        // k_chain_ci diagnostics: lane-steps spent tracing (lane utilisation)
+    unsigned long long nps_issued;  // k_chain_ci diagnostics: next-pixel speculation candidates issued
 };
-constexpr int kNumCounters = 6 + 8 + 64;
+constexpr int kNumCounters = 6 + 8 + 64 + 2;
 
 __device__ __forceinline__ void tile_bounds(const RenderParams& rp, int64_t tile, int64_t& x0, int64_t& y0,
                                             int64_t& x1, int64_t& y1) {
@@ -239,7 +243,7 @@ __host__ __device__ inline int64_t sp_vbuf_bytes(const RenderParams& rp) {
 // chain's main loop, config B 314 -> 340 ms)
 template <bool kWin = true>
 __device__ uint64_t start_pixel_wave(const RenderParams& rp, const PcgJump& J, uint64_t S, uint64_t inc, double* s1d,
-                                     uint16_t* other, uint32_t* vbuf, uint64_t* sh_state) {
+                                     uint16_t* other, uint32_t* vbuf, uint64_t* sh_state, uint32_t* sh_draws = nullptr) {
     const int lane = threadIdx.x;
     const bool w0 = lane < kWave;
     const int n = rp.spp, ndims = rp.ndims;
@@ -329,7 +333,10 @@ __device__ uint64_t start_pixel_wave(const RenderParams& rp, const PcgJump& J, u
             __syncthreads();
             for (int idx = tid; idx < ndims * n; idx += nt)
                 s1d[idx] = gomath::min(((double)perm[idx] + 0.5) * inv_n, gomath::kOneMinusEpsilon);
-            if (tid == 0) *sh_state = pcg_advance(J, S, inc, (uint64_t)(E + R));
+            if (tid == 0) {
+                *sh_state = pcg_advance(J, S, inc, (uint64_t)(E + R));
+                if (sh_draws) *sh_draws = (uint32_t)(E + R);
+            }
             __syncthreads();
             return *sh_state;
         }
@@ -398,7 +405,10 @@ __device__ uint64_t start_pixel_wave(const RenderParams& rp, const PcgJump& J, u
                     samp[o] = a;
                 }
             }
-            if (lane == 0) *sh_state = pcg_advance(J, S, inc, (uint64_t)(E + R));
+            if (lane == 0) {
+                *sh_state = pcg_advance(J, S, inc, (uint64_t)(E + R));
+                if (sh_draws) *sh_draws = (uint32_t)(E + R);
+            }
         }
     }
     if (serial_sp || (rp.flags & PBRT_FLAG_SERIAL_START_PIXEL)) {
@@ -410,6 +420,15 @@ __device__ uint64_t start_pixel_wave(const RenderParams& rp, const PcgJump& J, u
             t.s1d = s1d;
             start_pixel(t);
             *sh_state = t.rng.state;
+            if (sh_draws) {   // its draw count: the events plus the rejections, found by stepping
+                uint64_t st = pcg_advance(J, S, inc, (uint64_t)rp.sp_events);
+                uint32_t k = (uint32_t)rp.sp_events;
+                while (st != t.rng.state) {
+                    st = st * 0x5851f42d4c957f2dULL + inc;
+                    k++;
+                }
+                *sh_draws = k;
+            }
         }
     }
     __syncthreads();
@@ -832,16 +851,26 @@ struct RingEnt {
     uint32_t d;     // its draw count D, or kBadSpecD / kBadExactD
     uint64_t st;    // PCG32 state at the offset
 };
+// Offsets are absolute: draws of the tile's PCG32 stream since the tile's
+// first pixel's StartPixel began (< 2^31 for any supported frame).
 struct CiGroup {
-    uint64_t S;     // PCG32 state at the current pixel's first sample (offset 0)
+    uint64_t S;     // PCG32 state at absolute offset A
     int64_t pi;     // current pixel (row-major index in the tile)
     int64_t npx;    // pixels of the tile
+    uint32_t A;     // absolute offset of S (the current pixel's first traced sample once it started)
     uint32_t head;  // offset of sample kh
     uint32_t nxt;   // next offset to issue (same parity as head)
     int kh;         // next sample without an offset
     int phase;      // 0 needs a pixel, 1 resolving offsets, 2 tile finished
     int reissue;    // the head must be re-run with its sample index known
-    int pad;
+    uint32_t rb0, rb1;   // ring base of the pixels of each parity: entry of offset o at (o - rb) & (R - 1)
+    // next-pixel speculation (multi-wave Matte tiles): trajectories of pixel
+    // pi + 1 from offsets nb, nb + 1, ... (nb: the lowest offset its first
+    // traced sample can start at), issued to lanes the current pixel leaves idle
+    uint32_t nb, nnx;   // its ring base and next offset to issue
+    int nps;            // active (pixel pi + 1's ring and ChainCache are loaded)
+    uint32_t dcnt;      // on-chain draw counts seen in the tile (kNps: their mean and spread set the
+    float dsum, dsq;    // current pixel's speculation cap and when the next pixel's starts)
 };
 
 }  // namespace pbrtk

@@ -51,8 +51,8 @@ def main():
                         _, st = r.render(rd)
                         if best is None or st.chain_ms < best:
                             best = st.chain_ms
-                            out = (C.c_uint64 * 32)()
-                            n = G.lib().pbrt_gpu_counters(C.c_void_p(r.h), out, 32)
+                            out = (C.c_uint64 * 80)()
+                            n = G.lib().pbrt_gpu_counters(C.c_void_p(r.h), out, 80)
                             vals = list(out)[:n]
                 rec = {"config": a.config, "env": a.env, "tile": t, "waves": w, "stride": cs, "chain_ms": best}
                 if vals and len(vals) >= 11 and sum(vals[6:11]) > 0:
@@ -60,8 +60,12 @@ def main():
                     tot = float(sum(ph))
                     rec["steps"] = vals[5]
                     rec["phase_share"] = {k: round(v / tot, 4) for k, v in zip(PHASES, ph)}
-                    if len(vals) >= 14:   # candidates issued; successor promotions / discards (PBRT_CI_SUCC)
-                        rec["issued"], rec["succ_promoted"], rec["succ_dropped"] = vals[11], vals[12], vals[13]
+                    rec["steps_per_pixel"] = vals[5] / 256.0
+                    rec["issued_per_pixel"] = vals[11] / 256.0
+                    rec["on_chain_per_pixel"] = sum(vals[14:78]) / 256.0
+                    if len(vals) >= 80:   # lane utilisation; next-pixel speculation candidates
+                        rec["lane_util"] = vals[78] / max(1, vals[5] * 64 * w)
+                        rec["nps_issued_per_pixel"] = vals[79] / 256.0
                 print(json.dumps(rec), flush=True)
 
 
