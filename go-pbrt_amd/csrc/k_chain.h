@@ -486,6 +486,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
                 // the tail cap's bound (dmax per sample): an on-chain D above it would
                 // only slow the chain, never change a result; counted so tests can pin it
                 CI_DIAG(if (d > dmax) ph[6]++;)
+                CI_DIAG(if (d & 1u) atomicAdd(&ctr->odd_d, 1ull);)
                 if (kStats) {   // the tile's draw-count statistics
                     s.dcnt++;
                     s.dsum += (float)d;

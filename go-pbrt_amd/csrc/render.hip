@@ -1900,7 +1900,8 @@ extern "C" int pbrt_gpu_counters(pbrt_gpu_ctx* c, uint64_t* out, int n) {
                                       ctr.phase[2], ctr.phase[3], ctr.phase[4], ctr.phase[5],
                                       ctr.phase[6], ctr.phase[7]};
     for (int i = 0; i < n && i < kNumCounters; i++)
-        out[i] = i < 14 ? v[i] : i < 78 ? (uint64_t)ctr.dhist[i - 14] : i == 78 ? ctr.busy : ctr.nps_issued;
+        out[i] = i < 14 ? v[i] : i < 78 ? (uint64_t)ctr.dhist[i - 14] : i == 78 ? ctr.busy : i == 79 ? ctr.nps_issued
+                                                                                                   : ctr.odd_d;
     return kNumCounters;
 }
 

@@ -58,8 +58,9 @@ struct Counters {
     unsigned long long dhist[64];   // k_chain_ci diagnostics: on-chain draw counts D (bin D/2, last bin >= 126)
     unsigned long long busy;        // k_chain_ci diagnostics: lane-steps spent tracing (lane utilisation)
     unsigned long long nps_issued;  // k_chain_ci diagnostics: next-pixel speculation candidates issued
+    unsigned long long odd_d;       // k_chain_ci diagnostics: on-chain draw counts that are odd (flip stride 2's parity)
 };
-constexpr int kNumCounters = 6 + 8 + 64 + 2;
+constexpr int kNumCounters = 6 + 8 + 64 + 3;
 
 __device__ __forceinline__ void tile_bounds(const RenderParams& rp, int64_t tile, int64_t& x0, int64_t& y0,
                                             int64_t& x1, int64_t& y1) {

@@ -72,7 +72,8 @@ int pbrt_gpu_probe(int device, int op, const double* in, size_t n, int in_stride
  * film add, StartPixel draws, chain walk, (spare); then 64 bins of the
  * continuous-issue chain's on-chain draw counts D (bin D/2, last bin >= 126),
  * then the chain's lane-steps spent tracing (utilisation = busy / (steps x
- * lanes)) and its next-pixel speculation candidates (diagnostics builds).
+ * lanes)), its next-pixel speculation candidates and its odd on-chain draw
+ * counts (diagnostics builds).
  * Returns the number of counters available. */
 struct pbrt_gpu_ctx;
 int pbrt_gpu_counters(struct pbrt_gpu_ctx* ctx, uint64_t* out, int n);

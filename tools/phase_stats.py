@@ -44,8 +44,8 @@ with G.Renderer(scene, kernel=a.kernel, occupancy=a.occupancy, lanes_per_wave=a.
         r.render_async(rd)
         st = r.synchronize()
         dt = time.perf_counter() - t0
-        out = (C.c_uint64 * 78)()
-        n = G.lib().pbrt_gpu_counters(C.c_void_p(r.h), out, 78)
+        out = (C.c_uint64 * 81)()
+        n = G.lib().pbrt_gpu_counters(C.c_void_p(r.h), out, 81)
         vals = dict(zip(names, list(out)[:14]))
         dh = list(out)[14:n]
         tot = sum(vals[k] for k in names[6:11]) or 1
@@ -53,6 +53,11 @@ with G.Renderer(scene, kernel=a.kernel, occupancy=a.occupancy, lanes_per_wave=a.
               f"kernel={st.kernel} Mpaths/s={st.paths_traced / dt / 1e6:.2f}")
         px = a.width * a.height / a.tile_stride   # pixels rendered (about, for a tile sample)
         print("  windows/pixel %.2f" % (vals["windows"] / px))
+        dh, busy, odd = dh[:64], (dh[64] if len(dh) > 64 else 0), (dh[66] if len(dh) > 66 else 0)
+        if odd:
+            print("  odd on-chain draw counts: %.1f%%" % (100.0 * odd / max(1, sum(dh))))
+        if busy and vals["windows"]:
+            print("  lane utilisation (lane-steps tracing / steps x 64) %.3f" % (busy / (vals["windows"] * 64.0)))
         onchain = sum(dh)
         if onchain:
             print("  issued candidates/pixel %.1f, on-chain/pixel %.1f (%.1f%%), on-chain D above the tail "

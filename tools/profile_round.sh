@@ -10,7 +10,7 @@ shift
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-side-mode $*"
+B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-side-mode --no-rpc $*"
 SQ1=SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_INSTS_VMEM,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_ACTIVE_INST_VALU
 SQ2=SQ_THREAD_CYCLES_VALU,SQ_WAIT_INST_ANY,SQ_INSTS_VALU_FMA_F64,SQ_INSTS_VALU_MUL_F64,SQ_INSTS_VALU_ADD_F64,SQ_INSTS_VALU_TRANS_F64,SQ_WAIT_ANY,SQ_ACTIVE_INST_ANY
 timeout -k 10 400 python3 bench.py $* > $OUT/bench.json 2> $OUT/bench.err &&
