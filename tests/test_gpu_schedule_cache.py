@@ -75,3 +75,27 @@ def test_schedule_cache_off(monkeypatch):
         b.render(rd)
         assert b.schedule_source() == "probe"
     G.schedule_cache_clear()
+
+
+def test_completion_driven_path_stage_ragged_tiles_and_mode_switch(monkeypatch):
+    """the completion-driven path stage launches k_paths_ci
+    over whole slots in completion order, ceil(ppt / P) groups per slot. With
+    tile size 13 (169 pixels: P = 8 does not divide it) and the one-GPU split
+    forced (one-wave tiles, 6 heavy tiles), the steady-state frames are the
+    oracle's bit for bit, also after a THROUGHPUT frame in between has
+    overwritten the wave buffers."""
+    monkeypatch.setenv("PBRT_CI_WAVES", "1")
+    monkeypatch.setenv("PBRT_CI_HEAVY", "6")
+    scene = G.Scene.readme(320, 240)
+    rd = abi.render_desc(4, 4, tile_size=13)
+    want = oracle_film(scene, rd)
+    with G.Renderer(scene) as r:
+        for frame, mode in enumerate(["exact", "exact", "throughput", "exact"]):
+            if mode == "throughput":
+                r.render(abi.render_desc(4, 4, tile_size=13, mode=abi.PBRT_MODE_THROUGHPUT))
+                continue
+            film, st = r.render(rd)
+            _, heavy = r.tile_ticks()
+            assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
+            assert (heavy > 0) == (frame > 0), (frame, heavy)
+            assert same_bits(film, want), frame

@@ -29,16 +29,21 @@ ap.add_argument("--kernel", default="auto")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--occupancy", type=int, default=0)
 ap.add_argument("--tiles-per-wave", type=int, default=0)
-ap.add_argument("--scene", default="readme", choices=["readme", "readme_glass", "cornell"])
+ap.add_argument("--scene", default="readme", choices=["readme", "readme_glass", "cornell", "heightfield"])
+ap.add_argument("--quads", type=int, default=707, help="height field cells per side (heightfield: 707 = config D, 2236 = E)")
+ap.add_argument("--tile-begin", type=int, default=0)
 a = ap.parse_args()
 
-scene = {"readme": G.Scene.readme, "readme_glass": G.Scene.readme_glass, "cornell": G.Scene.cornell}[a.scene](
-    a.width, a.height)
+if a.scene == "heightfield":
+    scene = G.Scene.heightfield(a.width, a.height, quads=a.quads, seed=1)
+else:
+    scene = {"readme": G.Scene.readme, "readme_glass": G.Scene.readme_glass, "cornell": G.Scene.cornell}[a.scene](
+        a.width, a.height)
 names = ["paths", "camera_samples", "closest_rays", "shadow_rays", "any_panic", "windows",
          "cyc_start_pixel", "cyc_issue_first_scatter", "cyc_traversal", "cyc_hit_processing",
          "cyc_barrier_walk", "issued", "d_over_dmax", "cyc_7"]
 with G.Renderer(scene, kernel=a.kernel, occupancy=a.occupancy, lanes_per_wave=a.tiles_per_wave) as r:
-    rd = abi.render_desc(a.spp, a.spp, max_depth=a.max_depth, tile_stride=a.tile_stride)
+    rd = abi.render_desc(a.spp, a.spp, max_depth=a.max_depth, tile_begin=a.tile_begin, tile_stride=a.tile_stride)
     for i in range(a.reps):
         t0 = time.perf_counter()
         r.render_async(rd)
