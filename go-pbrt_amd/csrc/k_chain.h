@@ -41,8 +41,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const uint64_t t_begin = wall_clock64();
     // the frame's chain progress record (completion-driven path stage, render.hip;
-    // null elsewhere): [0] workgroups started, [1] completions, [2 + i] the slot of
-    // the i-th completion
+    // null elsewhere; layout at kProgHead)
     if (prog && threadIdx.x == 0) __hip_atomic_fetch_add(&prog[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t cs = cstride == 1 ? 1u : 2u;   // candidate offsets head + cs * j
     constexpr int kT = kWave * kW;   // threads per workgroup (stack stride)
@@ -242,6 +241,8 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
                 PixelRec& pr = wb.prec[rec];
                 const int hit0 = pr.hit, panic0 = pr.panic0;
                 if (tid == 0) {   // pbrt_gpu_cancel: every group of the workgroup ends
+                    if (prog)   // the heartbeat k_gate tells running chains from undispatched ones by
+                        __hip_atomic_fetch_add(&prog[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     const uint64_t now = wall_clock64();
                     const bool host = now - last_host_poll >= 100000;   // 1 ms at 100 MHz
                     if (host) last_host_poll = now;
@@ -605,7 +606,7 @@ __global__ __launch_bounds__(kWave * kW) __attribute__((amdgpu_waves_per_eu(kEu 
     if (tid == 0) {
         if (prog && G == 1 && bs < nslots_batch) {   // publish the tile for the path stage
             const uint32_t pos = __hip_atomic_fetch_add(&prog[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&prog[2 + pos], (uint32_t)bs, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&prog[kProgHead + pos], (uint32_t)bs, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (ticks && G == 1 && bs < nslots_batch) {
             const uint64_t t_end = wall_clock64();

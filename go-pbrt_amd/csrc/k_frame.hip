@@ -588,16 +588,22 @@ __global__ __launch_bounds__(kWave) void k_tile_cost(DevScene sc, RenderParams r
 }
 
 // One wave that holds its stream's next launch back until the chain stage's
-// progress record (k_chain_ci's `prog`) allows it (the completion-driven path
-// stage, render.hip):
+// progress record (k_chain_ci's `prog`, layout at kProgHead) allows it (the
+// completion-driven path stage, render.hip):
 //   b == e: until at least `b` chain workgroups have started (every one of them
 //           has been dispatched);
 //   b <  e: until the completion list's entries [b, e) are all written (those
 //           tiles' chains have ended and their records are visible).
 // Progress-driven, not timed: the chains waited for are queued before the gate
-// and always run to their end (a cancelled chain ends early, but ends). Only a
-// bug could stall the record; 60 s without progress ends the wait and flags the
-// frame (Counters.gate_stall), and the path launches skip unwritten entries.
+// and always run to their end (a cancelled chain ends early, but ends). The wait
+// needs the chains to run beside it, which a dispatcher that serialises kernels
+// across streams does not allow (rocprofv3 counter collection does: measured,
+// DESIGN §3.3); there no chain starts a pixel and the record stands still. So
+// 1 s in which no workgroup starts, no pixel starts and no listed tile ends
+// ends the wait and flags the frame (Counters.gate_stall; every later gate of
+// the frame then opens at once), and the host renders the frame again with the
+// path stage after the chains (pbrt_gpu_synchronize). A running frame starts a
+// pixel every few microseconds (config B: ~522k pixels in ~300 ms).
 __global__ __launch_bounds__(kWave) void k_gate(const uint32_t* __restrict__ prog, uint32_t b, uint32_t e,
                                                 Counters* __restrict__ ctr) {
     const int lane = threadIdx.x;
@@ -605,15 +611,15 @@ __global__ __launch_bounds__(kWave) void k_gate(const uint32_t* __restrict__ pro
     uint32_t seen = 0xFFFFFFFFu;
     uint64_t t_prog = wall_clock64();
     for (;;) {
-        uint32_t v;
+        if (__hip_atomic_load(&ctr->gate_stall, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+        const uint32_t started = __hip_atomic_load(&prog[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
         if (b == e) {
-            v = __hip_atomic_load(&prog[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            if (v >= b) return;
+            if (started >= b) return;
         } else {
             for (;;) {   // advance over written entries, 64 at a time
                 const uint32_t i = cur + (uint32_t)lane;
-                const bool ok = i >= e || __hip_atomic_load(&prog[2 + i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) !=
-                                              kNoSlot;
+                const bool ok = i >= e || __hip_atomic_load(&prog[kProgHead + i], __ATOMIC_ACQUIRE,
+                                                            __HIP_MEMORY_SCOPE_AGENT) != kNoSlot;
                 const unsigned long long bad = __ballot(!ok);
                 if (bad) {
                     cur += (uint32_t)__builtin_ctzll(bad);
@@ -622,13 +628,13 @@ __global__ __launch_bounds__(kWave) void k_gate(const uint32_t* __restrict__ pro
                 cur += kWave;
                 if (cur >= e) return;
             }
-            v = cur;
         }
+        const uint32_t v = started + cur + __hip_atomic_load(&prog[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint64_t now = wall_clock64();
         if (v != seen) {
             seen = v;
             t_prog = now;
-        } else if (now - t_prog > 6000000000ull) {   // 60 s at 100 MHz without progress
+        } else if (now - t_prog > 100000000ull) {   // 1 s at 100 MHz without progress
             if (lane == 0) atomicExch(&ctr->gate_stall, 1);
             return;
         }

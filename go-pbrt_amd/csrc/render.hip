@@ -76,6 +76,9 @@ struct Knobs {
     int paths_overlap = 5;     // PBRT_PATHS_OVERLAP=K: a split frame's path stage runs in K chunks of the
                                // tiles in their chains' completion order, each released when its tiles'
                                // chains have ended (render_enqueue; 0: off, the path stage after the chains)
+    bool gate_hold = false;    // PBRT_GATE_HOLD=1 (tests): the light chain launch waits for the path stage,
+                               // as a dispatcher that serialises kernels across streams may order them;
+                               // k_gate's stall exit and the re-render recover the frame
     bool paths_s1d_lds = false;// PBRT_PATHS_S1D=lds
     int paths_ci = -1;         // PBRT_PATHS_CI = 0, 2, 4, 8 (-1: auto)
     int paths_wf = -1;         // PBRT_PATHS_WF = 0 / 1 (-1: mesh scenes)
@@ -110,6 +113,7 @@ struct Knobs {
         if (const char* e = getenv("PBRT_CI_NPS")) k.ci_nps = std::max(0, atoi(e));
         if (const char* e = getenv("PBRT_CI_SCAP")) k.ci_scap = std::max(-1, atoi(e));
         if (const char* e = getenv("PBRT_PATHS_OVERLAP")) k.paths_overlap = std::min(std::max(0, atoi(e)), 16);
+        if (const char* e = getenv("PBRT_GATE_HOLD")) k.gate_hold = atoi(e) != 0;
         if (const char* e = getenv("PBRT_PATHS_S1D")) k.paths_s1d_lds = std::strcmp(e, "lds") == 0;
         if (const char* e = getenv("PBRT_PATHS_CI")) {
             const int v = atoi(e);
@@ -139,12 +143,19 @@ struct pbrt_gpu_ctx {
     hipEvent_t ev_split = nullptr, ev_join = nullptr;
     // PBRT_PATHS_OVERLAP: a high-priority stream for the light chain launch, the
     // events of the completion-driven path stage, and k_chain_ci's progress record
-    // ([0] workgroups started, [1] completions, [2 ..] completion list)
+    // (layout at kProgHead)
     hipStream_t stream3 = nullptr;
     hipEvent_t ev_l2 = nullptr, ev_p1 = nullptr;
     int64_t ov_done = 0;                 // slots whose path stage was launched beside the chains
     uint32_t* d_prog = nullptr;
     int64_t prog_cap = 0;
+    // a frame whose k_gate saw the chains stand still (a dispatcher that serialises
+    // kernels across streams) is rendered again without the overlap; two such
+    // frames in a row turn the overlap off for the context
+    pbrt_render_desc last_rd{};
+    double* last_film_device = nullptr;
+    int ov_stalls = 0;
+    bool ov_retry = false;
     MeshBuild mesh;                      // triangle meshes + their LBVH (extension)
     int64_t heavy_k = 0;                 // slots at the front of h_slot_order that get 4 waves
     int ci_wps = 2;                      // waves/SIMD of the last one-wave k_chain_ci launch (3 or 2)
@@ -1194,6 +1205,8 @@ int pbrt_gpu_render_async_into(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, doub
         c->cancel_req = false;
         __atomic_store_n(c->h_cancel, 0, __ATOMIC_SEQ_CST);
     }
+    if (rd) c->last_rd = *rd;   // kept for a re-render (pbrt_gpu_synchronize)
+    c->last_film_device = film_device;
     const int rc = render_enqueue(c, rd, film_device);
     if (rc != PBRT_OK) {   // nothing was launched (or the launch failed): no render is in flight
         std::lock_guard<std::mutex> lk(c->cancel_mu);
@@ -1420,7 +1433,8 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                     //    chains run and takes the slots they free once no chain workgroup waits.
                     // Progress-driven, not timed (it replaces round 5's timed wait); only the
                     // schedule changes, never a result.
-                    const bool overlap = heavy > 0 && c->knobs.paths_overlap > 0 && paths_ci_exact && learned;
+                    const bool overlap = heavy > 0 && c->knobs.paths_overlap > 0 && paths_ci_exact && learned &&
+                                         !c->ov_retry && c->ov_stalls < 2;
                     if (overlap && !c->stream3) {   // created on first use
                         int least = 0, greatest = 0;
                         HIPCHK(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -1428,36 +1442,47 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                         HIPCHK(c, hipEventCreateWithFlags(&c->ev_l2, hipEventDisableTiming));
                         HIPCHK(c, hipEventCreateWithFlags(&c->ev_p1, hipEventDisableTiming));
                     }
-                    if (overlap && c->prog_cap < nb + 2) {
+                    if (overlap && c->prog_cap < nb + kProgHead) {
                         if (c->d_prog) (void)hipFree(c->d_prog);
                         c->d_prog = nullptr;
                         c->prog_cap = 0;
-                        HIPCHK(c, hipMalloc((void**)&c->d_prog, sizeof(uint32_t) * (size_t)(nb + 2)));
-                        c->prog_cap = nb + 2;
+                        HIPCHK(c, hipMalloc((void**)&c->d_prog, sizeof(uint32_t) * (size_t)(nb + kProgHead)));
+                        c->prog_cap = nb + kProgHead;
                     }
                     if (overlap) {
-                        HIPCHK(c, hipMemsetAsync(c->d_prog, 0, 2 * sizeof(uint32_t), c->stream));
-                        HIPCHK(c, hipMemsetAsync(c->d_prog + 2, 0xFF, sizeof(uint32_t) * (size_t)nb, c->stream));
+                        HIPCHK(c, hipMemsetAsync(c->d_prog, 0, kProgHead * sizeof(uint32_t), c->stream));
+                        HIPCHK(c, hipMemsetAsync(c->d_prog + kProgHead, 0xFF, sizeof(uint32_t) * (size_t)nb, c->stream));
                         HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
                         split_launch = true;
                         launch_ci(ci_heavy_waves(c), heavy, order, c->stream, c->d_prog);
                         split_launch = false;
                         HIPCHK(c, hipGetLastError());   // the gates below wait for these workgroups
-                        HIPCHK(c, hipStreamWaitEvent(c->stream3, c->ev_split, 0));
-                        hipLaunchKernelGGL(k_gate, dim3(1), dim3(kWave), 0, c->stream3, c->d_prog, (uint32_t)heavy,
-                                           (uint32_t)heavy, c->d_ctr);
-                        launch_ci(1, nb - heavy, order + heavy, c->stream3, c->d_prog);
-                        HIPCHK(c, hipGetLastError());
-                        HIPCHK(c, hipEventRecord(c->ev_l2, c->stream3));
-                        HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
-                        for (int64_t s0 = 0, j = 0; s0 < nb; j++) {
-                            const int64_t e0 = j + 1 >= c->knobs.paths_overlap ? nb : s0 + std::max<int64_t>(1, (nb - s0) / 2);
-                            hipLaunchKernelGGL(k_gate, dim3(1), dim3(kWave), 0, c->stream2, c->d_prog, (uint32_t)s0,
-                                               (uint32_t)e0, c->d_ctr);
-                            launch_paths(c->d_prog + 2 + s0, e0 - s0, c->stream2);
-                            s0 = e0;
-                        }
-                        HIPCHK(c, hipEventRecord(c->ev_p1, c->stream2));
+                        auto light = [&]() -> int {
+                            HIPCHK(c, hipStreamWaitEvent(c->stream3, c->knobs.gate_hold ? c->ev_p1 : c->ev_split, 0));
+                            hipLaunchKernelGGL(k_gate, dim3(1), dim3(kWave), 0, c->stream3, c->d_prog,
+                                               (uint32_t)heavy, (uint32_t)heavy, c->d_ctr);
+                            launch_ci(1, nb - heavy, order + heavy, c->stream3, c->d_prog);
+                            HIPCHK(c, hipGetLastError());
+                            HIPCHK(c, hipEventRecord(c->ev_l2, c->stream3));
+                            return PBRT_OK;
+                        };
+                        auto paths = [&]() -> int {
+                            HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
+                            for (int64_t s0 = 0, j = 0; s0 < nb; j++) {
+                                const int64_t e0 = j + 1 >= c->knobs.paths_overlap ? nb
+                                                                                  : s0 + std::max<int64_t>(1, (nb - s0) / 2);
+                                hipLaunchKernelGGL(k_gate, dim3(1), dim3(kWave), 0, c->stream2, c->d_prog,
+                                                   (uint32_t)s0, (uint32_t)e0, c->d_ctr);
+                                launch_paths(c->d_prog + kProgHead + s0, e0 - s0, c->stream2);
+                                s0 = e0;
+                            }
+                            HIPCHK(c, hipEventRecord(c->ev_p1, c->stream2));
+                            return PBRT_OK;
+                        };
+                        const int r1 = c->knobs.gate_hold ? paths() : light();
+                        if (r1 != PBRT_OK) return r1;
+                        const int r2 = c->knobs.gate_hold ? light() : paths();
+                        if (r2 != PBRT_OK) return r2;
                         HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_l2, 0));
                         c->ov_done = nb;
                     } else if (heavy > 0) {
@@ -1574,6 +1599,24 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
     }
     Counters ctr;
     HIPCHK(c, hipMemcpy(&ctr, c->d_ctr, sizeof(ctr), hipMemcpyDeviceToHost));
+    if (ctr.gate_stall) {
+        // the completion-driven path stage's gates saw the chains stand still
+        // (k_gate): the film misses path work. Render the frame again with the path
+        // stage after the chains; the chains replay the same streams, so the
+        // result is the one an overlapped frame gives.
+        if (++c->ov_stalls == 2)
+            std::fprintf(stderr, "pbrt: k_gate stalled twice (kernels serialised across streams, e.g. by a "
+                                 "counter-collecting profiler): the path stage now runs after the chains\n");
+        c->ov_retry = true;
+        const int rr = render_enqueue(c, &c->last_rd, c->last_film_device);
+        c->ov_retry = false;
+        if (rr != PBRT_OK) return rr;
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipMemcpy(&ctr, c->d_ctr, sizeof(ctr), hipMemcpyDeviceToHost));
+        if (ctr.gate_stall) return set_err(c, PBRT_E_HIP, "k_gate stalled without the overlap");
+    } else if (c->ov_done > 0) {
+        c->ov_stalls = 0;
+    }
     float ms = 0, ms_merge = 0;
     (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
     (void)hipEventElapsedTime(&ms_merge, c->ev1, c->ev2);
@@ -1628,7 +1671,6 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
         c->order_key = c->ticks_key;
         if (ci_order_cache(c)) sched_cache_put(c, c->ticks_key, c->h_slot_order, c->heavy_k);
     }
-    if (ctr.gate_stall) rc = set_err(c, PBRT_E_HIP, "k_gate: the chain progress record stalled (60 s)");
     if (ctr.any_panic) {
         std::vector<PanicRec> pr((size_t)c->rp.n_slots);
         HIPCHK(c, hipMemcpy(pr.data(), c->d_panics, sizeof(PanicRec) * pr.size(), hipMemcpyDeviceToHost));

@@ -51,7 +51,7 @@ struct PanicRec {
 struct Counters {
     unsigned long long paths, camera_samples, closest_rays, shadow_rays;
     int32_t any_panic;
-    int32_t gate_stall;   // a k_gate wait ended without the progress it waited for (never in a correct run)
+    int32_t gate_stall;   // a k_gate wait saw no chain progress for 1 s (serialised dispatch): the frame is rendered again
     // wave kernel diagnostics (pbrt_gpu_counters): speculation windows, and
     // lane-0 clock64 cycles in StartPixel / bounce 1 / chain / full paths / film add
     unsigned long long windows, phase[8];
@@ -845,6 +845,9 @@ constexpr double kCostPixel = 150.0;   // one StartPixel ~ this many trajectory 
 #endif
 constexpr uint32_t kNoOff = 0xFFFFFFFFu;
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;   // an unwritten entry of k_chain_ci's completion list
+// k_chain_ci's progress record: [0] workgroups started, [1] completions, [2] pixels
+// started (a heartbeat), [kProgHead + i] the slot of the i-th completion
+constexpr int kProgHead = 3;
 constexpr uint32_t kBadSpecD = 0xFFFFFFFEu;   // speculative lane could not resolve D
 constexpr uint32_t kBadExactD = 0xFFFFFFFDu;  // the exact head's trajectory panics
 struct RingEnt {

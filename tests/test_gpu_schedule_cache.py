@@ -99,3 +99,26 @@ def test_completion_driven_path_stage_ragged_tiles_and_mode_switch(monkeypatch):
             assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
             assert (heavy > 0) == (frame > 0), (frame, heavy)
             assert same_bits(film, want), frame
+
+
+def test_gate_stall_renders_the_frame_again(monkeypatch, capfd):
+    """A dispatcher that serialises kernels across streams (rocprofv3 counter
+    collection does) never runs the chains beside the k_gate waiting for them.
+    PBRT_GATE_HOLD=1 builds that order on purpose: the light chain launch waits
+    for the whole path stage. k_gate sees no chain progress for 1 s, opens every
+    gate of the frame, and pbrt_gpu_synchronize renders the frame again with the
+    path stage after the chains; after two such frames the context keeps the
+    overlap off. Every frame is the oracle's, bit for bit."""
+    monkeypatch.setenv("PBRT_CI_WAVES", "1")
+    monkeypatch.setenv("PBRT_CI_HEAVY", "6")
+    monkeypatch.setenv("PBRT_GATE_HOLD", "1")
+    scene = G.Scene.readme(320, 240)
+    rd = abi.render_desc(4, 4)
+    want = oracle_film(scene, rd)
+    with G.Renderer(scene) as r:
+        for frame in range(4):
+            film, st = r.render(rd)
+            assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
+            assert same_bits(film, want), frame
+            err = capfd.readouterr().err
+            assert ("k_gate stalled twice" in err) == (frame == 2), (frame, err)
