@@ -76,6 +76,9 @@ struct Knobs {
     int paths_overlap = 5;     // PBRT_PATHS_OVERLAP=K: a split frame's path stage runs in K chunks of the
                                // tiles in their chains' completion order, each released when its tiles'
                                // chains have ended (render_enqueue; 0: off, the path stage after the chains)
+    bool paths_overlap_all = true;    // PBRT_PATHS_OVERLAP_ALL=0: the completion-driven path stage only for
+                               // split frames (measured on: C 5056 -> 4603 ms, G 495 -> 472 ms, the
+                               // N=8 shards' max 128.6 -> 119.7 ms)
     bool gate_hold = false;    // PBRT_GATE_HOLD=1 (tests): the light chain launch waits for the path stage,
                                // as a dispatcher that serialises kernels across streams may order them;
                                // k_gate's stall exit and the re-render recover the frame
@@ -113,6 +116,7 @@ struct Knobs {
         if (const char* e = getenv("PBRT_CI_NPS")) k.ci_nps = std::max(0, atoi(e));
         if (const char* e = getenv("PBRT_CI_SCAP")) k.ci_scap = std::max(-1, atoi(e));
         if (const char* e = getenv("PBRT_PATHS_OVERLAP")) k.paths_overlap = std::min(std::max(0, atoi(e)), 16);
+        if (const char* e = getenv("PBRT_PATHS_OVERLAP_ALL")) k.paths_overlap_all = atoi(e) != 0;
         if (const char* e = getenv("PBRT_GATE_HOLD")) k.gate_hold = atoi(e) != 0;
         if (const char* e = getenv("PBRT_PATHS_S1D")) k.paths_s1d_lds = std::strcmp(e, "lds") == 0;
         if (const char* e = getenv("PBRT_PATHS_CI")) {
@@ -1433,26 +1437,54 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                     //    chains run and takes the slots they free once no chain workgroup waits.
                     // Progress-driven, not timed (it replaces round 5's timed wait); only the
                     // schedule changes, never a result.
-                    const bool overlap = heavy > 0 && c->knobs.paths_overlap > 0 && paths_ci_exact && learned &&
-                                         !c->ov_retry && c->ov_stalls < 2;
-                    if (overlap && !c->stream3) {   // created on first use
+                    const bool ov_ok = c->knobs.paths_overlap > 0 && paths_ci_exact && learned && !c->ov_retry &&
+                                       c->ov_stalls < 2;
+                    const bool overlap = heavy > 0 && ov_ok;
+                    // no split: the one chain launch on stream3 (its workgroups win the slots the
+                    // path chunks also wait for); the completion list needs one tile per workgroup
+                    const bool overlap1 = heavy == 0 && ov_ok && c->knobs.paths_overlap_all && (kw > 1 || G == 1);
+                    if ((overlap || overlap1) && !c->stream3) {   // created on first use
                         int least = 0, greatest = 0;
                         HIPCHK(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
                         HIPCHK(c, hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, greatest));
                         HIPCHK(c, hipEventCreateWithFlags(&c->ev_l2, hipEventDisableTiming));
                         HIPCHK(c, hipEventCreateWithFlags(&c->ev_p1, hipEventDisableTiming));
                     }
-                    if (overlap && c->prog_cap < nb + kProgHead) {
+                    if ((overlap || overlap1) && c->prog_cap < nb + kProgHead) {
                         if (c->d_prog) (void)hipFree(c->d_prog);
                         c->d_prog = nullptr;
                         c->prog_cap = 0;
                         HIPCHK(c, hipMalloc((void**)&c->d_prog, sizeof(uint32_t) * (size_t)(nb + kProgHead)));
                         c->prog_cap = nb + kProgHead;
                     }
-                    if (overlap) {
+                    auto paths = [&]() -> int {   // the path chunks on stream2, each behind its k_gate
+                        HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
+                        for (int64_t s0 = 0, j = 0; s0 < nb; j++) {
+                            const int64_t e0 = j + 1 >= c->knobs.paths_overlap ? nb
+                                                                              : s0 + std::max<int64_t>(1, (nb - s0) / 2);
+                            hipLaunchKernelGGL(k_gate, dim3(1), dim3(kWave), 0, c->stream2, c->d_prog, (uint32_t)s0,
+                                               (uint32_t)e0, c->d_ctr);
+                            launch_paths(c->d_prog + kProgHead + s0, e0 - s0, c->stream2);
+                            s0 = e0;
+                        }
+                        HIPCHK(c, hipEventRecord(c->ev_p1, c->stream2));
+                        return PBRT_OK;
+                    };
+                    if (overlap || overlap1) {
                         HIPCHK(c, hipMemsetAsync(c->d_prog, 0, kProgHead * sizeof(uint32_t), c->stream));
                         HIPCHK(c, hipMemsetAsync(c->d_prog + kProgHead, 0xFF, sizeof(uint32_t) * (size_t)nb, c->stream));
                         HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
+                    }
+                    if (overlap1) {
+                        HIPCHK(c, hipStreamWaitEvent(c->stream3, c->ev_split, 0));
+                        launch_ci(kw, nb, order, c->stream3, c->d_prog);
+                        HIPCHK(c, hipGetLastError());
+                        HIPCHK(c, hipEventRecord(c->ev_l2, c->stream3));
+                        const int r = paths();
+                        if (r != PBRT_OK) return r;
+                        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_l2, 0));
+                        c->ov_done = nb;
+                    } else if (overlap) {
                         split_launch = true;
                         launch_ci(ci_heavy_waves(c), heavy, order, c->stream, c->d_prog);
                         split_launch = false;
@@ -1464,19 +1496,6 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                             launch_ci(1, nb - heavy, order + heavy, c->stream3, c->d_prog);
                             HIPCHK(c, hipGetLastError());
                             HIPCHK(c, hipEventRecord(c->ev_l2, c->stream3));
-                            return PBRT_OK;
-                        };
-                        auto paths = [&]() -> int {
-                            HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
-                            for (int64_t s0 = 0, j = 0; s0 < nb; j++) {
-                                const int64_t e0 = j + 1 >= c->knobs.paths_overlap ? nb
-                                                                                  : s0 + std::max<int64_t>(1, (nb - s0) / 2);
-                                hipLaunchKernelGGL(k_gate, dim3(1), dim3(kWave), 0, c->stream2, c->d_prog,
-                                                   (uint32_t)s0, (uint32_t)e0, c->d_ctr);
-                                launch_paths(c->d_prog + kProgHead + s0, e0 - s0, c->stream2);
-                                s0 = e0;
-                            }
-                            HIPCHK(c, hipEventRecord(c->ev_p1, c->stream2));
                             return PBRT_OK;
                         };
                         const int r1 = c->knobs.gate_hold ? paths() : light();
@@ -2005,6 +2024,11 @@ extern "C" int64_t pbrt_gpu_tile_ticks(pbrt_gpu_ctx* c, uint32_t* out, int64_t n
 extern "C" void pbrt_gpu_schedule_cache_clear(void) {
     std::lock_guard<std::mutex> lk(g_sched_mu);
     g_sched.clear();
+}
+
+extern "C" int64_t pbrt_gpu_overlap_slots(pbrt_gpu_ctx* c) {
+    if (!c) return -PBRT_E_INVALID;
+    return c->ov_done;
 }
 
 extern "C" int pbrt_gpu_schedule_source(pbrt_gpu_ctx* c) {

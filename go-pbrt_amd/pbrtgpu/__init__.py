@@ -72,6 +72,8 @@ def lib():
     L.pbrt_gpu_counters.argtypes = [C.c_void_p, P(C.c_uint64), C.c_int]
     L.pbrt_gpu_schedule_source.argtypes = [C.c_void_p]
     L.pbrt_gpu_schedule_cache_clear.argtypes = []
+    L.pbrt_gpu_overlap_slots.argtypes = [C.c_void_p]
+    L.pbrt_gpu_overlap_slots.restype = C.c_int64
     L.pbrt_gpu_schedule_cache_clear.restype = None
     for name in ("pbrt_translate", "pbrt_scale"):
         getattr(L, name).argtypes = [d, d, d, T]
@@ -462,6 +464,11 @@ class Renderer:
         (cold-frame estimate), 'learned' (this context's previous frame) or 'cached'
         (the process-wide cache: another context's frame of the same scene and configuration)."""
         return self.SCHEDULE_SOURCES[lib().pbrt_gpu_schedule_source(self.h)]
+
+    def overlap_slots(self):
+        """Slots of the last EXACT frame whose path stage ran completion-driven
+        (pbrt_gpu_overlap_slots; 0: after the chain stage)."""
+        return lib().pbrt_gpu_overlap_slots(self.h)
 
     def counters(self):
         """pbrt_gpu_counters of the last render (include/pbrt_diag.h order)."""

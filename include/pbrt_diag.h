@@ -103,6 +103,10 @@ int pbrt_gpu_schedule_source(struct pbrt_gpu_ctx* ctx);
  * starts from the probe again). PBRT_CI_ORDER_CACHE=0 disables the cache for
  * contexts created while it is set. */
 void pbrt_gpu_schedule_cache_clear(void);
+/* Slots of the last EXACT frame (its last batch) whose path stage ran
+ * completion-driven, released tile by tile as their chains ended
+ * (PBRT_PATHS_OVERLAP); 0: the path stage ran after the chain stage. */
+int64_t pbrt_gpu_overlap_slots(struct pbrt_gpu_ctx* ctx);
 
 /* Cold-frame schedule estimate of the last EXACT frame, if that frame ran
  * render.hip's k_tile_cost probe (a fresh context or a new configuration):

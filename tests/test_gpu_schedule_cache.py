@@ -120,5 +120,33 @@ def test_gate_stall_renders_the_frame_again(monkeypatch, capfd):
             film, st = r.render(rd)
             assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
             assert same_bits(film, want), frame
+            assert r.overlap_slots() == 0, frame   # the re-render (and the probe frame) ran without it
             err = capfd.readouterr().err
             assert ("k_gate stalled twice" in err) == (frame == 2), (frame, err)
+
+
+@pytest.mark.parametrize("overlap_all", ["1", "0"])
+def test_completion_driven_path_stage_without_split(monkeypatch, overlap_all):
+    """Frames without a heavy/light split (no tile heavy enough, or a shard of
+    multi-wave tiles) run the completion-driven path stage too
+    (PBRT_PATHS_OVERLAP_ALL, default on): one chain launch, the path chunks
+    released by its completion list. Ragged 13-pixel tiles, one and two waves
+    per tile; every frame is the oracle's, bit for bit, with the stage on and
+    off."""
+    monkeypatch.setenv("PBRT_PATHS_OVERLAP_ALL", overlap_all)
+    monkeypatch.setenv("PBRT_CI_SPLIT", "0")
+    scene = G.Scene.readme(320, 240)
+    for waves in ("1", "2"):
+        monkeypatch.setenv("PBRT_CI_WAVES", waves)
+        rd = abi.render_desc(4, 4, tile_size=13, tile_begin=1, tile_stride=3)
+        want = oracle_film(scene, rd)
+        with G.Renderer(scene) as r:
+            for frame in range(3):
+                film, st = r.render(rd)
+                _, heavy = r.tile_ticks()
+                assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
+                assert heavy == 0, (waves, frame, heavy)
+                # frame 0 is the probe's (no completion-driven stage before a learned schedule)
+                assert r.overlap_slots() == (st.tiles_rendered if frame > 0 and overlap_all == "1" else 0), \
+                    (waves, frame)
+                assert same_bits(film, want), (waves, frame)
