@@ -60,6 +60,11 @@ struct Knobs {
     int ci_waves = 0;          // PBRT_CI_WAVES = 1, 2, 4, 8 (0: by tile count)
     int ci_stride = 0;         // PBRT_CI_STRIDE = 1, 2 (0: 2 at one wave per tile, else 1)
     int ci_heavy_waves = 4;    // PBRT_CI_HEAVY_WAVES = 4, 8
+    bool ci_light_kw = false;  // PBRT_CI_LIGHT_KW=1: a multi-wave shard's split runs its light tiles at the
+                               // shard's waves per tile (not 1), the heavy ones at PBRT_CI_HEAVY_WAVES
+    int ci_split8 = 32;        // PBRT_CI_SPLIT8=K: a learned multi-wave Matte shard that fits the wave slots
+                               // (no split otherwise: 1/8 of B) runs its K heaviest tiles (at most 1/16 of
+                               // them) at 8 waves beside the rest at its waves per tile; 0: off
     int ci_eu = 0;             // PBRT_CI_EU = 2 / 3: the one-wave Matte chain's build (waves/SIMD its registers
                                // are budgeted for); 0: by the workgroup's LDS (ci_eu3_fits)
     int64_t ci_heavy = -1;     // PBRT_CI_HEAVY = K forces the heavy tile count (tests)
@@ -105,6 +110,8 @@ struct Knobs {
             if (v == 1 || v == 2) k.ci_stride = v;
         }
         if (const char* e = getenv("PBRT_CI_HEAVY_WAVES")) k.ci_heavy_waves = atoi(e) == 8 ? 8 : 4;
+        if (const char* e = getenv("PBRT_CI_LIGHT_KW")) k.ci_light_kw = atoi(e) != 0;
+        if (const char* e = getenv("PBRT_CI_SPLIT8")) k.ci_split8 = std::max(0, atoi(e));
         if (const char* e = getenv("PBRT_CI_EU")) k.ci_eu = (atoi(e) == 2 || atoi(e) == 3) ? atoi(e) : 0;
         if (const char* e = getenv("PBRT_CI_HEAVY")) k.ci_heavy = (int64_t)atoll(e);
         if (const char* e = getenv("PBRT_CI_SPLIT")) k.ci_split = atoi(e) != 0;
@@ -1351,6 +1358,11 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                     }
                     // one launch of n workgroups, workgroup b on slot ord[b] (identity if null)
                     bool split_launch = false;   // launch_ci's launch is the heavy half of a split
+                    // waves per tile of a split's light launch
+                    // (set below, before any launch_ci call)
+                    bool light_kw = kw > 1 && c->knobs.ci_light_kw;
+                    int light_w = light_kw ? kw : 1;
+                    int heavy_w = ci_heavy_waves(c);
                     auto launch_ci = [&](int w, int64_t n, const uint32_t* ord, hipStream_t st, uint32_t* prog) {
                         if (w > 1) {   // one tile per workgroup of w waves; the ring grows with the lanes
                             const int ring = w * kCiRingBytes / (int)sizeof(RingEnt);
@@ -1360,7 +1372,7 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                             // its two rings' LDS cost the light tiles beside it (1/4 shard of B
                             // 132 -> 145 ms; a 1/8 shard, no split: 131.5 -> 127.2 ms)
                             RenderParams rpl = rp;
-                            rpl.ci_nps = (!kx && !split_launch && ci_stride(c, w) == 1) ? c->knobs.ci_nps : 0;
+                            rpl.ci_nps = (!kx && (!split_launch || light_kw) && ci_stride(c, w) == 1) ? c->knobs.ci_nps : 0;
                             const ChainLayout lw = ci_layout(c->lay_ci, w, 1, lds, rpl.ci_nps > 0);
                             // kX: LDS-staged trees only, at most 4 waves per tile (wave_eligible, ci_waves)
                             auto kern = kx ? (w == 2 ? k_chain_ci<2, 0, true> : k_chain_ci<4, 0, true>)
@@ -1419,11 +1431,22 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                                         ? std::min<int64_t>(c->heavy_k, nb) : 0;
                     if (ci_heavy_override(c) >= 0 && learned && G == 1)   // tests and experiments force the split
                         heavy = std::min<int64_t>(ci_heavy_override(c), nb);
+                    // a multi-wave Matte shard that fits the wave slots (1/8 of B: 1020 tiles at 4 waves)
+                    // is bound by its heaviest tiles' pixel-serial chains: those at 8 waves, the
+                    // rest at kw, next-pixel speculation in both (the N=8 shards' max 121.9 ->
+                    // ~107 ms with 32; 4-32 within a few ms; all tiles at 8 waves: 178 ms)
+                    if (heavy == 0 && ci_heavy_override(c) < 0 && learned && G == 1 && kw > 1 && nb <= c->n_simd &&
+                        !kx && !mesh_only && ci_split_enabled(c) && c->knobs.ci_split8 > 0) {
+                        heavy = std::min<int64_t>(c->knobs.ci_split8, nb / 16);
+                        light_kw = true;
+                        light_w = kw;
+                        heavy_w = 8;
+                    }
                     if (heavy >= nb) heavy = 0;   // nothing left for the light launch: one launch at kw
                     c->last_heavy = heavy;
                     if (ticks) {   // label every slot with the waves it actually runs at
-                        c->h_slot_kw.assign((size_t)nb, (uint8_t)(heavy > 0 ? 1 : kw));
-                        for (int64_t i = 0; i < heavy; i++) c->h_slot_kw[c->h_slot_order[(size_t)i]] = (uint8_t)ci_heavy_waves(c);
+                        c->h_slot_kw.assign((size_t)nb, (uint8_t)(heavy > 0 ? light_w : kw));
+                        for (int64_t i = 0; i < heavy; i++) c->h_slot_kw[c->h_slot_order[(size_t)i]] = (uint8_t)heavy_w;
                     }
                     // PBRT_PATHS_OVERLAP (a learned split, G == 1): the completion-driven path stage.
                     //  - the heavy launch on the main stream (normal priority);
@@ -1486,14 +1509,14 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                         c->ov_done = nb;
                     } else if (overlap) {
                         split_launch = true;
-                        launch_ci(ci_heavy_waves(c), heavy, order, c->stream, c->d_prog);
+                        launch_ci(heavy_w, heavy, order, c->stream, c->d_prog);
                         split_launch = false;
                         HIPCHK(c, hipGetLastError());   // the gates below wait for these workgroups
                         auto light = [&]() -> int {
                             HIPCHK(c, hipStreamWaitEvent(c->stream3, c->knobs.gate_hold ? c->ev_p1 : c->ev_split, 0));
                             hipLaunchKernelGGL(k_gate, dim3(1), dim3(kWave), 0, c->stream3, c->d_prog,
                                                (uint32_t)heavy, (uint32_t)heavy, c->d_ctr);
-                            launch_ci(1, nb - heavy, order + heavy, c->stream3, c->d_prog);
+                            launch_ci(light_w, nb - heavy, order + heavy, c->stream3, c->d_prog);
                             HIPCHK(c, hipGetLastError());
                             HIPCHK(c, hipEventRecord(c->ev_l2, c->stream3));
                             return PBRT_OK;
@@ -1507,10 +1530,10 @@ int render_enqueue(pbrt_gpu_ctx* c, const pbrt_render_desc* rd, double* film_dev
                     } else if (heavy > 0) {
                         HIPCHK(c, hipEventRecord(c->ev_split, c->stream));
                         split_launch = true;
-                        launch_ci(ci_heavy_waves(c), heavy, order, c->stream, nullptr);
+                        launch_ci(heavy_w, heavy, order, c->stream, nullptr);
                         split_launch = false;
                         HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split, 0));
-                        launch_ci(1, nb - heavy, order + heavy, c->stream2, nullptr);
+                        launch_ci(light_w, nb - heavy, order + heavy, c->stream2, nullptr);
                         HIPCHK(c, hipEventRecord(c->ev_join, c->stream2));
                         HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
                     } else {
