@@ -150,3 +150,23 @@ def test_completion_driven_path_stage_without_split(monkeypatch, overlap_all):
                 assert r.overlap_slots() == (st.tiles_rendered if frame > 0 and overlap_all == "1" else 0), \
                     (waves, frame)
                 assert same_bits(film, want), (waves, frame)
+
+
+def test_multiwave_shard_heavy_tiles_at_8_waves(monkeypatch):
+    """A learned multi-wave Matte shard that fits the wave slots (as 1/8 of B
+    does) runs its heaviest tiles, min(PBRT_CI_SPLIT8, slots / 16), at 8 waves
+    beside the rest at its own waves per tile; off with PBRT_CI_SPLIT8=0. Every
+    frame is the oracle's, bit for bit."""
+    monkeypatch.setenv("PBRT_CI_WAVES", "4")
+    scene = G.Scene.readme(320, 240)
+    rd = abi.render_desc(4, 4, tile_begin=2, tile_stride=3)   # 100 of the 300 tiles
+    want = oracle_film(scene, rd)
+    for k, expect in (("32", 100 // 16), ("0", 0)):
+        monkeypatch.setenv("PBRT_CI_SPLIT8", k)
+        with G.Renderer(scene) as r:
+            for frame in range(3):
+                film, st = r.render(rd)
+                _, heavy = r.tile_ticks()
+                assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
+                assert heavy == (expect if frame > 0 else 0), (k, frame, heavy)
+                assert same_bits(film, want), (k, frame)
