@@ -170,3 +170,19 @@ def test_multiwave_shard_heavy_tiles_at_8_waves(monkeypatch):
                 assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
                 assert heavy == (expect if frame > 0 else 0), (k, frame, heavy)
                 assert same_bits(film, want), (k, frame)
+
+
+def test_completion_driven_path_stage_over_several_batches(monkeypatch):
+    """A frame split into several tile batches (a small wave-buffer budget):
+    each batch runs its own chain and path stage, the next batch only after
+    both. Three frames of one context, each the oracle's bit for bit."""
+    monkeypatch.setenv("PBRT_WAVE_BUFFER_GB", "0.02")
+    scene = G.Scene.readme(320, 240)
+    rd = abi.render_desc(4, 4)
+    want = oracle_film(scene, rd)
+    with G.Renderer(scene) as r:
+        for frame in range(3):
+            film, st = r.render(rd)
+            assert st.kernel == abi.PBRT_KERNEL_WAVE_CI
+            assert st.batches > 1, st.batches
+            assert same_bits(film, want), frame
