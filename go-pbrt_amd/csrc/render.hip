@@ -1708,15 +1708,11 @@ int pbrt_gpu_synchronize(pbrt_gpu_ctx* c, pbrt_gpu_stats* stats) {
         const double thr = 0.7 * sum / ((double)c->ci_wps * (double)c->n_simd);
         int64_t k = 0;
         while (k < (int64_t)t.size() && cost[c->h_slot_order[(size_t)k]] > thr) k++;
-        // at most a quarter of the wave slots; when the tiles outnumber the one-wave
-        // slots (one GPU, 1/2 shards), whose light launch then fills the GPU longer than
-        // the heavy tiles take, at most 1/16 of them for the Matte chain (1/2 of B:
-        // 216 -> 202 ms with 64 against 256) and 1/8 for the mesh chain (E's rank-0
-        // shard: 9.14 / 8.84 / 10.00 s at 64 / 128 / 256); 1/4 of B: best at 256,
-        // 126-129 ms against 131-142 at 128-384
-        const int64_t cap = (int64_t)t.size() > (int64_t)c->ci_wps * c->n_simd
-                                ? (mesh_only_scene(c) ? c->n_simd / 8 : c->n_simd / 16)
-                                : c->n_simd / 4;
+        // at most a quarter of the wave slots; at most 1/16 of them when the tiles
+        // outnumber the one-wave slots (one GPU, 1/2 shards), whose light launch then
+        // fills the GPU longer than the heavy tiles take (1/2 of B: 216 -> 202 ms with
+        // 64 against 256; 1/4 of B: best at 256, 126-129 ms against 131-142 at 128-384)
+        const int64_t cap = (int64_t)t.size() > (int64_t)c->ci_wps * c->n_simd ? c->n_simd / 16 : c->n_simd / 4;
         c->heavy_k = std::min<int64_t>(k, cap);
         if (ci_heavy_override(c) >= 0) c->heavy_k = ci_heavy_override(c);
         c->order_key = c->ticks_key;
